@@ -1,0 +1,305 @@
+// ============================================================================
+//  CPU ORACLE — TEST INFRASTRUCTURE ONLY.
+//
+//  This is a from-scratch, plain-C++ restatement of the RNS-CKKS arithmetic
+//  and of the rank-sort hot path of oksuman/FHE-Sorting.  It exists so that
+//  tests/, __graft_entry__.smoke() and bench.py's `cpu_baseline` leg can check
+//  (and time) the MI355X engine in fhe-sorting_amd/.  Nothing in the product
+//  library links, loads or calls this code.
+//
+//  What it follows (reference = /root/reference, read-only):
+//    * DirectSort<N>::{getSizeParameters, constructRank, vecRotsOpt,
+//      blindRotationOptN, rotationIndexCheckN, sort}
+//                                   src/sort_algo.h:87-201, 326-366, 368-506,
+//                                   561-584, 658-750, 752-774
+//    * Comparison::{compare, indicator}        src/comparison.cpp:4-40
+//    * compositeSign<3|4>, sign()             src/sign.cpp:9-185, 635-651
+//    * Decomposer / RotationComposer          src/rotation.h:30-233
+//    * Sinc<N>::doubled_sinc (coefficient recipe, generated offline)
+//                                              src/comparison.h:57-78,
+//                                              utils/generate_cheb_doubled_coeffs.cpp:14-36
+//  The lattice arithmetic underneath (EvalMult, EvalRotate, rescale,
+//  EvalChebyshevSeriesPS ...) lives in OpenFHE in the reference, which is
+//  neither vendored nor installed here.  It is restated from the published
+//  RNS-CKKS algorithms (HYBRID key switching, dnum digits, FLEXIBLEAUTO-style
+//  exact per-level scale factors); see DESIGN.md §3 for the exact spec that
+//  both this oracle and the GPU engine implement.
+//
+//  Parity status: bit-exact GPU<->oracle on identical keys/inputs; oracle vs
+//  OpenFHE itself is "parity unpinned" (OpenFHE absent).  The oracle is pinned
+//  by big-integer golden vectors (NTT, basis conversion, automorphism) and by
+//  the reference's own test tolerances (SignTest, CompareTest, DecomposeTest,
+//  DirectSortTest ...), see tests/.
+// ============================================================================
+#pragma once
+
+#include <cstdint>
+#include <cstddef>
+#include <functional>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+namespace oracle {
+
+using u64 = uint64_t;
+using i64 = int64_t;
+using u128 = unsigned __int128;
+using i128 = __int128;
+
+// ---------------------------------------------------------------- modular ---
+struct Modulus {
+    u64 q = 0;
+    int k = 0;     // bit length of q
+    u64 mu = 0;    // floor(2^(2k) / q)
+    Modulus() = default;
+    explicit Modulus(u64 q_);
+};
+
+u64 mod_reduce128(u128 z, const Modulus &m);   // z < q^2
+u64 mod_mul(u64 a, u64 b, const Modulus &m);
+u64 mod_pow(u64 a, u64 e, const Modulus &m);
+u64 mod_inv(u64 a, const Modulus &m);
+inline u64 mod_add(u64 a, u64 b, u64 q) { u64 r = a + b; return r >= q ? r - q : r; }
+inline u64 mod_sub(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
+inline u64 shoup_pre(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
+inline u64 mul_shoup(u64 a, u64 w, u64 wp, u64 q) {
+    u64 hi = (u64)(((u128)a * wp) >> 64);
+    u64 r = a * w - hi * q;
+    return r >= q ? r - q : r;
+}
+u64 signed_to_mod(i64 v, u64 q);
+u64 i128_to_mod(i128 v, u64 q);
+bool is_prime(u64 n);
+
+// ---------------------------------------------------------------- params ----
+struct Params {
+    int logN = 0;
+    size_t n = 0;
+    int L = 0;          // multiplicative depth: L+1 Q primes
+    int dnum = 3;       // key-switching digits (at the top level)
+    int alpha = 0;      // limbs per digit = ceil((L+1)/dnum)
+    int K = 0;          // number of special P primes
+    int scale_bits = 40;
+    int first_bits = 60;
+    std::vector<u64> primes;     // Q primes (L+1) followed by P primes (K)
+    std::vector<double> delta;   // canonical scale at level 0..L
+    size_t nq() const { return (size_t)L + 1; }
+    size_t nall() const { return primes.size(); }
+    size_t limbs_at(int level) const { return (size_t)(L + 1 - level); }
+};
+
+Params make_params(int logN, int L, int scale_bits, int first_bits, int dnum);
+
+// ------------------------------------------------------------------ NTT -----
+struct NTTTable {
+    Modulus mod;
+    u64 psi = 0;
+    std::vector<u64> fwd, fwd_shoup;   // psi^{brev(k)}
+    std::vector<u64> inv, inv_shoup;   // psi^{-brev(k)}
+    u64 ninv = 0, ninv_shoup = 0;
+};
+NTTTable make_ntt_table(u64 q, int logN);
+void ntt_forward(u64 *a, const NTTTable &t, size_t n);
+void ntt_inverse(u64 *a, const NTTTable &t, size_t n);
+// NTT-domain automorphism X -> X^g: out[k] = in[perm[k]]
+std::vector<uint32_t> automorphism_perm(int logN, u64 g);
+u64 galois_for_rotation(int logN, long k);
+
+// ---------------------------------------------------------------- PRNG ------
+// Sampling spec shared (by restatement, not by code) with the GPU engine's
+// host-side key generation: DESIGN.md §3.5.
+struct SplitMix64 {
+    u64 s;
+    SplitMix64(u64 seed, u64 tag);
+    u64 next();
+};
+u64 sample_uniform_mod(SplitMix64 &g, u64 q);
+int sample_ternary(SplitMix64 &g);
+int sample_cbd(SplitMix64 &g);
+
+// --------------------------------------------------------------- objects ----
+struct Plaintext {
+    std::vector<u64> m;   // [limbs][n], NTT form
+    int level = 0;
+    int slots = 0;
+    double scale = 0;
+    size_t limbs = 0;
+};
+
+struct Ciphertext {
+    std::vector<u64> c;   // [2][limbs][n], NTT form
+    int level = 0;
+    int slots = 0;
+    double scale = 0;
+    size_t limbs = 0;
+    u64 *poly(int i, size_t n) { return c.data() + (size_t)i * limbs * n; }
+    const u64 *poly(int i, size_t n) const { return c.data() + (size_t)i * limbs * n; }
+};
+using CtPtr = std::shared_ptr<Ciphertext>;
+
+struct SwitchKey {
+    // per digit j: b_j, a_j over all Q and P primes, NTT form: [digit][2][nall][n]
+    std::vector<u64> data;
+    int digits = 0;
+};
+
+struct OpCounters {
+    u64 hmult = 0;      // relinearised ct x ct products
+    u64 keyswitch = 0;  // every hybrid key switch (relin + rotation)
+    u64 rotations = 0;  // keyed automorphisms
+    u64 rescale = 0;
+    u64 ptmult = 0;
+    u64 constmult = 0;
+};
+
+class Context {
+  public:
+    Context(const Params &p, u64 seed);
+    const Params P;
+    std::vector<NTTTable> tab;      // per prime (Q then P)
+    u64 seed;
+
+    // keys
+    std::vector<i64> s_coeff;       // ternary secret
+    std::vector<u64> s_ntt;         // [nall][n]
+    std::vector<u64> pk;            // [2][nq][n]
+    SwitchKey relin;
+    std::map<u64, SwitchKey> rotkeys;  // galois element -> key
+    u64 enc_counter = 0;
+    OpCounters ctr;
+
+    void keygen();
+    void gen_rotation_keys(const std::vector<int> &rot);
+    void gen_switch_key(const std::vector<u64> &sprime_ntt, SwitchKey &out, u64 tag);
+    bool has_rotation_key(long k) const;
+
+    // encode / decode
+    Plaintext encode(const std::vector<double> &v, int slots, int level) const;
+    std::vector<double> decode(const std::vector<u64> &m0_coeff_limb0, int slots, double scale) const;
+    CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
+    CtPtr encrypt_pt(const Plaintext &pt);
+    std::vector<double> decrypt(const Ciphertext &ct);
+
+    // ------------------------------------------------------------ ops -----
+    CtPtr clone(const Ciphertext &a) const;
+    CtPtr add(const Ciphertext &a, const Ciphertext &b);
+    CtPtr sub(const Ciphertext &a, const Ciphertext &b);
+    void add_inplace(CtPtr &acc, const Ciphertext &b);  // acc may be null => copy
+    CtPtr negate(const Ciphertext &a) const;
+    CtPtr add_plain(const Ciphertext &a, const Plaintext &p) const;
+    CtPtr sub_plain(const Ciphertext &a, const Plaintext &p) const;   // a - p
+    CtPtr plain_sub(const Plaintext &p, const Ciphertext &a) const;   // p - a
+    CtPtr add_const(const Ciphertext &a, double c) const;
+    CtPtr mul_int(const Ciphertext &a, i64 k) const;                 // no rescale
+    CtPtr mul_const(const Ciphertext &a, double c);                  // -> level+1
+    CtPtr mul_const_to(const Ciphertext &a, double c, int target);   // -> target (> a.level)
+    CtPtr mul_plain(const Ciphertext &a, const Plaintext &p);        // -> level+1
+    CtPtr mul(const Ciphertext &a, const Ciphertext &b);             // relin + rescale
+    CtPtr square(const Ciphertext &a);
+    CtPtr rotate(const Ciphertext &a, long k);                       // keyed rotation
+    std::vector<CtPtr> rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks);
+    CtPtr rescale(const Ciphertext &a);                              // drop last prime
+    CtPtr drop_to(const Ciphertext &a, int level) const;             // discard limbs
+    CtPtr level_adjust(const Ciphertext &a, int target);             // scalar-1 + rescale
+    void match_levels(CtPtr &a, CtPtr &b);
+    // sum_i K_i * x_i at level (target-1), then rescale (PS linear sums)
+    CtPtr linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c,
+                        int target);
+    CtPtr trivial_const(double c, int level, int slots) const;
+    CtPtr zero_like(int level, int slots) const;
+
+    // ---------------------------------------------------- kernel-level ----
+    // (exposed for golden-vector / parity tests)
+    void modup(const u64 *d_ntt, size_t ell, std::vector<u64> &ext) const;   // ext [digits][ell+K][n]
+    void keyswitch_core(const std::vector<u64> &ext, size_t ell, const SwitchKey &key,
+                        const std::vector<uint32_t> *perm, std::vector<u64> &out01) const;
+    void moddown(const u64 *in_ext_poly, size_t ell, u64 *out_q) const; // in: [ell+K][n] NTT
+
+    double delta(int level) const { return P.delta[level]; }
+
+  private:
+    void rescale_poly(const u64 *in, size_t ell, u64 *out) const;
+};
+
+// ------------------------------------------------------- algorithms ---------
+enum class SignFunc { CompositeSign = 0, SignumPolycircuit = 1, Tanh = 2, NaiveDiscrete = 3 };
+struct SignConfig {
+    int n = 3, dg = 0, df = 0;
+};
+
+CtPtr cheb_series_ps(Context &cc, const Ciphertext &x, const std::vector<double> &coeffs,
+                     double a, double b);
+CtPtr composite_sign(Context &cc, const Ciphertext &x, const SignConfig &cfg);
+CtPtr sign(Context &cc, const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+CtPtr compare(Context &cc, const Ciphertext &a, const Ciphertext &b, SignFunc f,
+              const SignConfig &cfg);
+CtPtr indicator(Context &cc, const Ciphertext &x, double c, SignFunc f, const SignConfig &cfg);
+
+enum class DecomposeAlgo { NAF = 0, BNAF = 1, BINARY = 2 };
+struct Step {
+    int value;
+    int stepSize;
+};
+class Decomposer {
+  public:
+    Decomposer(int N, std::vector<int> rot);
+    std::vector<Step> decompose(int rotation, int wrapN, DecomposeAlgo algo) const;
+    int N;
+    std::vector<int> rotIndices;
+    int maxDecomposed;
+};
+
+class RotationComposer {
+  public:
+    RotationComposer(Context &cc, int N, const std::vector<int> &rotIndices,
+                     DecomposeAlgo algo = DecomposeAlgo::BINARY);
+    CtPtr rotate(const Ciphertext &in, int rotation);
+    Context &cc;
+    Decomposer dec;
+    DecomposeAlgo algo;
+    std::set<int> avail;
+};
+
+struct SortShape {
+    int N, num_partition, num_batch, num_slots, np;
+};
+void direct_sort_size_parameters(int N, int &multDepth, std::vector<int> &rotations);
+SortShape rank_shape(int N, int max_batch);
+SortShape check_shape(int N, int max_batch);
+
+// Reduction hook for sharded runs: sums the ciphertext limbs over ranks in place
+// (u64 add), the callee leaves values < world*q; caller reduces mod q.
+using CtAllReduce = std::function<void(u64 *data, size_t count)>;
+
+class DirectSort {
+  public:
+    DirectSort(Context &cc, int N, const std::vector<int> &rotIndices);
+    CtPtr constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+    CtPtr rotationIndexCheckN(const Ciphertext &rank, const Ciphertext &x);
+    CtPtr sort(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+    // sharding over ranks (batch b handled iff b % world == rank)
+    int shard_rank = 0, shard_world = 1;
+    CtAllReduce allreduce;
+
+    Context &cc;
+    int N;
+    RotationComposer rot;
+    int max_batch;
+    const std::vector<double> *sinc_coeffs = nullptr;
+
+  private:
+    CtPtr vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np,
+                     int is);
+    CtPtr blindRotationOptN(const std::vector<CtPtr> &masked, int num_slots, int np, int ib,
+                            int num_partition);
+    void reduce_partial(CtPtr &acc, int level, int slots);
+};
+
+// Doubled-sinc Chebyshev coefficients (generated offline, data file).
+const std::vector<double> &doubled_sinc_coefficients(int N);
+void set_coefficient_dir(const std::string &dir);
+
+}  // namespace oracle
