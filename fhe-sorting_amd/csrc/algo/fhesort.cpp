@@ -1,0 +1,574 @@
+// Rank-sort comparator hot path on the MI355X engine (see fhesort.hpp).
+//
+// The operation sequences here are the spec that the CPU
+// oracle restates; GPU results are bit-identical to it.  Reference call sites
+// replaced (file:line in oksuman/FHE-Sorting):
+//   src/sign.cpp:9-60 (g_3/f_3), :62-158 (g_4/f_4), :160-185 (compositeSign),
+//   :635-651 (sign); src/comparison.cpp:4-40; src/rotation.h:54-233;
+//   src/sort_algo.h:326-366 (vecRotsOpt), :368-506 (constructRank),
+//   :561-584 (blindRotationOptN), :658-750 (rotationIndexCheckN), :752-774.
+#include "fhesort.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <fstream>
+#include <mutex>
+#include <stdexcept>
+#include <tuple>
+
+namespace fhe {
+
+// ===================================================== Chebyshev (PS) ======
+namespace {
+
+int ceil_log2(long x) {
+    int r = 0;
+    while ((1L << r) < x) ++r;
+    return r;
+}
+void trim_zeros(std::vector<double> &a) {
+    while (a.size() > 1 && a.back() == 0.0) a.pop_back();
+}
+
+// Leaves are sum_{i<=B} a_i T_i (depth log2(B)+1); a node p = q T_G + r with
+// G a power of two; capacity at depth D is 2^D - B, so a degree-d series
+// costs ceil(log2(d+1)) levels.
+struct PSEval {
+    Engine &cc;
+    int B = 1, beta = 1, D = 1;
+    std::map<int, CtPtr> T;
+
+    PSEval(Engine &c, const Ciphertext &x, int d) : cc(c) {
+        D = std::max(1, ceil_log2((long)d + 1));
+        const long bmax = (1L << D) - d;
+        const double lim = std::sqrt(2.0 * d);
+        long b = 1;
+        while (b * 2 <= bmax && (double)(b * 2) <= lim) b *= 2;
+        B = (int)b;
+        beta = ceil_log2(B) + 1;
+        T[1] = cc.clone(x);
+    }
+    void build_baby() {
+        for (int i = 2; i <= B; ++i) {
+            const int a = 1 << (ceil_log2(i) - 1), b = i - a;
+            CtPtr t = (a == b) ? cc.square(*T[a]) : cc.mul(*T[a], *T[b]);
+            t = cc.add(*t, *t);
+            t = (a == b) ? cc.add_const(*t, -1.0) : cc.sub(*t, *T[a - b]);
+            T[i] = t;
+        }
+    }
+    const Ciphertext &giant(int G) {
+        auto it = T.find(G);
+        if (it != T.end()) return *it->second;
+        const Ciphertext &h = giant(G / 2);
+        CtPtr t = cc.square(h);
+        t = cc.add(*t, *t);
+        T[G] = cc.add_const(*t, -1.0);
+        return *T[G];
+    }
+    CtPtr leaf(const std::vector<double> &a, int target) {
+        std::vector<const Ciphertext *> xs;
+        std::vector<double> cs;
+        for (size_t i = 1; i < a.size(); ++i)
+            if (a[i] != 0.0) {
+                xs.push_back(T.at((int)i).get());
+                cs.push_back(a[i]);
+            }
+        CtPtr r = xs.empty() ? cc.trivial_const(0.0, target, T[1]->slots) : cc.linear_sum_to(xs, cs, target);
+        if (a[0] != 0.0) r = cc.add_const(*r, a[0]);
+        return r;
+    }
+    CtPtr eval(std::vector<double> a, int target) {
+        trim_zeros(a);
+        const int d = (int)a.size() - 1;
+        if (d <= B) return leaf(a, target);
+        int Dpp = beta + 1;
+        while ((1L << Dpp) - B < d) ++Dpp;
+        int G = 1 << (Dpp - 1);
+        while (G > d) G >>= 1;
+        std::vector<double> q(d - G + 1), r(a.begin(), a.begin() + G);
+        q[0] = a[G];
+        for (int j = 1; j <= d - G; ++j) {
+            q[j] = 2.0 * a[G + j];
+            r[G - j] -= a[G + j];
+        }
+        CtPtr qv = eval(q, target - 1);
+        CtPtr prod = cc.mul(*qv, giant(G));
+        trim_zeros(r);
+        if (r.size() == 1 && r[0] == 0.0) return prod;
+        CtPtr rv = eval(r, target);
+        return cc.add(*prod, *rv);
+    }
+};
+
+}  // namespace
+
+CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<double> &coeffs, double a,
+                            double b) {
+    std::vector<double> c(coeffs);
+    trim_zeros(c);
+    if (c.empty()) throw std::invalid_argument("evalChebyshevSeriesPS: empty coefficients");
+    CtPtr x = cc.clone(x0);
+    if (!(a == -1.0 && b == 1.0)) {
+        x = cc.mul_const(*x, 2.0 / (b - a));
+        x = cc.add_const(*x, -(a + b) / (b - a));
+    }
+    std::vector<double> s(c);
+    s[0] = c[0] / 2.0;
+    const int d = (int)s.size() - 1;
+    if (d == 0) return cc.add_const(*cc.trivial_const(0.0, x->level, x->slots), s[0]);
+    PSEval ev(cc, *x, d);
+    ev.build_baby();
+    return ev.eval(s, x->level + ev.D);
+}
+
+// ====================================================== composite sign =====
+namespace {
+
+CtPtr odd7(Engine &cc, const Ciphertext &x, double c1, double c3, double c5, double c7) {
+    const int l = x.level;
+    CtPtr x2 = cc.square(x);
+    CtPtr x4 = cc.square(*x2);
+    CtPtr t3 = cc.mul(*cc.mul_const(x, c3), *x2);
+    CtPtr t7 = cc.mul(*cc.mul_const(x, c7), *x2);
+    CtPtr u = cc.add(*cc.mul_const_to(x, c5, l + 2), *t7);
+    CtPtr v = cc.mul(*u, *x4);
+    CtPtr y = cc.add(*cc.mul_const_to(x, c1, l + 3), *cc.level_adjust(*t3, l + 3));
+    return cc.add(*y, *v);
+}
+// g_3 = (4589x - 16577x^3 + 25614x^5 - 12860x^7)/2^10       (src/sign.cpp:15-36)
+CtPtr g3(Engine &cc, const Ciphertext &x) {
+    return odd7(cc, x, 4589.0 / 1024.0, -16577.0 / 1024.0, 25614.0 / 1024.0, -12860.0 / 1024.0);
+}
+// f_3 = (35x - 35x^3 + 21x^5 - 5x^7)/2^4                    (src/sign.cpp:38-59)
+CtPtr f3(Engine &cc, const Ciphertext &x) { return odd7(cc, x, 35.0 / 16.0, -35.0 / 16.0, 21.0 / 16.0, -5.0 / 16.0); }
+
+// g_4: degree-27 Chebyshev series on [-1, 1]                  (src/sign.cpp:66-77)
+const std::vector<double> &g4_coeffs() {
+    static const std::vector<double> c = {
+        0.0, 1.077117252745569,    0.0, -0.36166113998402755, 0.0, 0.2137420717859748,
+        0.0, -0.15635204788780485, 0.0, 0.11749645501187332,  0.0, -0.10074154666447852,
+        0.0, 0.08002086947825496,  0.0, -0.07533558758484624, 0.0, 0.059514472116534836,
+        0.0, -0.06146663712787884, 0.0, 0.04570084927999001,  0.0, -0.05403683682999072,
+        0.0, 0.03364293851188723,  0.0, -0.054459493266273494};
+    return c;
+}
+CtPtr g4(Engine &cc, const Ciphertext &x) { return evalChebyshevSeriesPS(cc, x, g4_coeffs(), -1.0, 1.0); }
+
+// f_4: odd degree-15 polynomial                               (src/sign.cpp:79-157)
+CtPtr f4(Engine &cc, const Ciphertext &x) {
+    const double c1 = 3.14208984375, c3 = -7.33154296875, c5 = 13.19677734375, c7 = -15.71044921875,
+                 c9 = 12.21923828125, c11 = -5.99853515625, c13 = 1.69189453125, c15 = -0.20947265625;
+    const int l = x.level;
+    CtPtr x2 = cc.square(x);
+    CtPtr x4 = cc.square(*x2);
+    CtPtr x8 = cc.square(*x4);
+    CtPtr c3x3 = cc.mul(*cc.mul_const(x, c3), *x2);
+    CtPtr c7x3 = cc.mul(*cc.mul_const(x, c7), *x2);
+    CtPtr c11x3 = cc.mul(*cc.mul_const(x, c11), *x2);
+    CtPtr c15x3 = cc.mul(*cc.mul_const(x, c15), *x2);
+    CtPtr v1 = cc.mul(*cc.add(*cc.mul_const_to(x, c5, l + 2), *c7x3), *x4);
+    CtPtr bt = cc.add(*cc.mul_const_to(x, c9, l + 2), *c11x3);
+    CtPtr w = cc.mul(*cc.add(*cc.mul_const_to(x, c13, l + 2), *c15x3), *x4);
+    CtPtr tmp1 = cc.add(*cc.level_adjust(*bt, l + 3), *w);
+    CtPtr z = cc.mul(*tmp1, *x8);
+    CtPtr y = cc.add(*cc.mul_const_to(x, c1, l + 4), *cc.level_adjust(*c3x3, l + 4));
+    y = cc.add(*y, *cc.level_adjust(*v1, l + 4));
+    return cc.add(*y, *z);
+}
+
+}  // namespace
+
+CtPtr compositeSignN(Engine &cc, const Ciphertext &x, int n, const SignConfig &cfg) {
+    if (n != 3 && n != 4) throw std::invalid_argument("compositeSign: n must be 3 or 4");
+    auto g = [&](const Ciphertext &v) { return n == 3 ? g3(cc, v) : g4(cc, v); };
+    auto f = [&](const Ciphertext &v) { return n == 3 ? f3(cc, v) : f4(cc, v); };
+    CtPtr y = g(x);  // applied once even when dg == 0 (src/sign.cpp:173)
+    for (int i = 1; i < cfg.compos.dg; ++i) y = g(*y);
+    for (int i = 0; i < cfg.compos.df; ++i) y = f(*y);
+    return y;
+}
+
+CtPtr sign(const Ciphertext &x, Engine &cc, SignFunc func, const SignConfig &cfg) {
+    if (func != SignFunc::CompositeSign)
+        throw std::invalid_argument("sign: only SignFunc::CompositeSign is implemented on the GPU path");
+    return compositeSignN(cc, x, cfg.compos.n, cfg);
+}
+
+CtPtr Comparison::compare(Engine &cc, const Ciphertext &a, const Ciphertext &b, SignFunc f, const SignConfig &cfg) {
+    CtPtr diff = cc.sub(a, b);
+    CtPtr s = sign(*diff, cc, f, cfg);
+    return cc.mul_const(*cc.add_const(*s, 1.0), 0.5);
+}
+
+CtPtr Comparison::indicator(Engine &cc, const Ciphertext &x, double c, SignFunc f, const SignConfig &cfg) {
+    CtPtr d1 = cc.add_const(x, c);
+    CtPtr d2 = cc.add_const(x, -c);
+    CtPtr s1 = sign(*d1, cc, f, cfg);
+    CtPtr s2 = sign(*d2, cc, f, cfg);
+    CtPtr c1 = cc.mul_const(*cc.add_const(*s1, 1.0), 0.5);
+    CtPtr c2 = cc.mul_const(*cc.add_const(*s2, 1.0), 0.5);
+    CtPtr om = cc.add_const(*cc.negate(*c2), 1.0);
+    return cc.mul(*c1, *om);
+}
+
+// ================================================ Decomposer / composer =====
+DecomposerN::DecomposerN(int N_, std::vector<int> rot) : N(N_), maxDecomposed(0), rotIndices(std::move(rot)) {
+    if (rotIndices.empty()) throw std::invalid_argument("Decomposer: empty rotation index set");
+    std::sort(rotIndices.begin(), rotIndices.end());
+    int step = 1;
+    for (int idx : rotIndices) {
+        if (step == idx / 2) maxDecomposed += idx;
+        step = idx;
+    }
+}
+
+std::vector<Step> DecomposerN::decompose(int rotation, int wrapN, DecomposeAlgo algo) const {
+    std::vector<Step> steps;
+    const int largest = rotIndices.back();
+    while (rotation >= largest) {
+        steps.push_back({1, largest});
+        rotation -= largest;
+    }
+    if (!rotation) return steps;
+    while (rotation > maxDecomposed) {
+        const int legal = *(std::lower_bound(rotIndices.begin(), rotIndices.end(), rotation) - 1);
+        steps.push_back({1, legal});
+        rotation -= legal;
+    }
+    if (!rotation) return steps;
+    std::vector<Step> rem;
+    if (algo == DecomposeAlgo::BINARY) {
+        for (int i = 30; i >= 0; --i) {
+            const int s = 1 << i;
+            if (s < N && (rotation & s)) rem.push_back({1, s});
+        }
+    } else if (algo == DecomposeAlgo::NAF) {
+        int r = rotation, i = 0;
+        while (r != 0) {
+            if (r & 1) {
+                const int z = (r & 2) ? -1 : 1;
+                const int s = z * (1 << i);
+                if (s == -N / 2)
+                    rem.push_back({-z, -s});
+                else
+                    rem.push_back({z, s});
+                r -= z;
+            }
+            r >>= 1;
+            ++i;
+        }
+        std::reverse(rem.begin(), rem.end());
+    } else {
+        std::vector<int> digits;
+        int Kk = rotation;
+        while (Kk != 0) {
+            int ki = Kk % 2;
+            Kk = (Kk - ki) / 2;
+            if (ki > 1 || (ki == 1 && (Kk % 2) >= 1)) {
+                ki -= 2;
+                Kk += 1;
+            }
+            digits.push_back(ki);
+        }
+        for (size_t i = 0; i < digits.size(); ++i)
+            if (digits[i] != 0) rem.push_back({digits[i], (int)((long)digits[i] * (1L << i))});
+        std::reverse(rem.begin(), rem.end());
+    }
+    steps.insert(steps.end(), rem.begin(), rem.end());
+    steps.erase(std::remove_if(steps.begin(), steps.end(), [wrapN](const Step &s) { return s.stepSize % wrapN == 0; }),
+                steps.end());
+    return steps;
+}
+
+RotationComposerN::RotationComposerN(Engine &c, int N, const std::vector<int> &rotIndices, DecomposeAlgo a)
+    : cc(c), dec(N, rotIndices), algo(a), avail(rotIndices.begin(), rotIndices.end()) {}
+
+CtPtr RotationComposerN::rotate(const Ciphertext &in, int rotation) {
+    if (rotation % in.slots == 0) return cc.clone(in);
+    if (avail.count(rotation)) return cc.rotate(in, rotation);
+    CtPtr r = cc.clone(in);
+    for (const Step &s : dec.decompose(rotation, in.slots, algo)) r = cc.rotate(*r, s.stepSize);
+    return r;
+}
+
+std::vector<CtPtr> RotationComposerN::rotateMany(const Ciphertext &in, const std::vector<int> &rotations) {
+    std::vector<CtPtr> out(rotations.size());
+    std::vector<long> keyed;
+    std::vector<size_t> where;
+    for (size_t i = 0; i < rotations.size(); ++i) {
+        const int r = rotations[i];
+        if (r % in.slots == 0)
+            out[i] = cc.clone(in);
+        else if (avail.count(r)) {
+            keyed.push_back(r);
+            where.push_back(i);
+        } else
+            out[i] = rotate(in, r);
+    }
+    if (!keyed.empty()) {
+        auto h = cc.rotate_hoisted(in, keyed);  // one ModUp shared by all keyed rotations
+        for (size_t i = 0; i < h.size(); ++i) out[where[i]] = h[i];
+    }
+    return out;
+}
+
+// ============================================================ DirectSort ===
+void directSortSizeParameters(int N, int &multDepth, std::vector<int> &r) {
+    // restated from src/sort_algo.h:87-201 (depth, rotation-key set per N)
+    switch (N) {
+    case 4: multDepth = 23; r = {1, 2, 4, 8, 16}; break;
+    case 8: multDepth = 24; r = {1, 2, 4, 6, 8, 16, 32, 64}; break;
+    case 16: multDepth = 25; r = {1, 2, 3, 4, 8, 12, 16, 32, 64, 128, 256}; break;
+    case 32: multDepth = 28; r = {1, 2, 3, 4, 8, 12, 16, 20, 24, 28, 32, 64, 128, 256, 512, 1024}; break;
+    case 64:
+        multDepth = 29;
+        r = {1, 2, 3, 4, 5, 6, 7, 8, 16, 24, 32, 40, 48, 56, 64, 128, 256, 512, 1024, 2048, 4096};
+        break;
+    case 128:
+        multDepth = 30;
+        r = {1, 2, 3, 4, 5, 6, 7, 8, 16, 24, 32, 40, 48, 56, 64, 72, 80, 88, 96, 104, 112, 120, 128, 256, 512, 1024,
+             2048, 4096, 8192, 16384};
+        break;
+    case 256: {
+        multDepth = 34;
+        r.clear();
+        for (int i = 1; i <= 16; ++i) r.push_back(i);
+        for (int i = 24; i <= 128; i += 8) r.push_back(i);
+        for (int i = 129; i <= 135; ++i) r.push_back(i);
+        for (int i = 144; i <= 256; i += 16) r.push_back(i);
+        for (int i = 512; i <= 32768; i *= 2) r.push_back(i);
+        break;
+    }
+    case 512: {
+        multDepth = 35;
+        r.clear();
+        for (int i = 1; i <= 16; ++i) r.push_back(i);
+        for (int i = 24; i <= 64; i += 8) r.push_back(i);
+        for (int b = 64; b <= 448; b += 64) {
+            for (int i = 1; i <= 7; ++i) r.push_back(b + i);
+            for (int i = b + 16; i <= b + 64; i += 16) r.push_back(i);
+        }
+        for (int i = 1024; i <= 32768; i *= 2) r.push_back(i);
+        std::sort(r.begin(), r.end());
+        r.erase(std::unique(r.begin(), r.end()), r.end());
+        break;
+    }
+    case 1024: {
+        multDepth = 39;
+        r.clear();
+        for (int i = 1; i <= 35; ++i) r.push_back(i);
+        for (int b = 64; b <= 992; b += 32)
+            for (int i = 0; i <= 3; ++i) r.push_back(b + i);
+        for (int i = 1024; i <= 32768; i *= 2) r.push_back(i);
+        break;
+    }
+    default: throw std::invalid_argument("DirectSort::getSizeParameters: unsupported N");
+    }
+}
+
+static int rank_np(int N, int P) {  // src/sort_algo.h:383-416
+    switch (N) {
+    case 4: case 8: return std::min(2, P);
+    case 16: case 32: return std::min(4, P);
+    case 64: case 128: return std::min(8, P);
+    case 256: case 512: return std::min(16, P);
+    case 1024: case 2048: return std::min(32, P);
+    default: return 1;
+    }
+}
+static int check_np(int N) {  // src/sort_algo.h:670-703
+    switch (N) {
+    case 4: case 8: return 2;
+    case 16: case 32: return 4;
+    case 64: case 128: return 8;
+    case 256: return 16;
+    case 512: case 1024: return 8;
+    default: return 4;
+    }
+}
+SortShape rankShape(int N, int max_batch) {
+    SortShape s;
+    s.N = N;
+    s.num_partition = std::min(N, max_batch / N);
+    if (s.num_partition < 1) throw std::invalid_argument("DirectSort: N*N exceeds ring capacity");
+    s.num_batch = N / s.num_partition;
+    s.num_slots = N * s.num_partition;
+    s.np = rank_np(N, s.num_partition);
+    return s;
+}
+SortShape checkShape(int N, int max_batch) {
+    SortShape s = rankShape(N, max_batch);
+    s.np = check_np(N);
+    return s;
+}
+
+namespace {
+std::vector<double> mask_vector(int num_slots, int N, int k) {  // src/sort_algo.h:206-233
+    std::vector<double> v(num_slots, 0.0);
+    for (int i = k * N; i < (k + 1) * N; ++i) v[i] = 1.0;
+    return v;
+}
+std::vector<double> vector_rotate(std::vector<double> v, int r) {  // src/sort_algo.h:289-306
+    const int n = (int)v.size();
+    if (r > 0)
+        std::rotate(v.begin(), v.begin() + r, v.end());
+    else if (r < 0)
+        std::rotate(v.begin(), v.begin() + (r + n), v.end());
+    return v;
+}
+std::vector<double> checking_vector(int num_slots, int N, int k) {  // src/sort_algo.h:272-286
+    std::vector<double> v(num_slots);
+    int idx = 0, cur = k;
+    while (idx < num_slots) {
+        for (int i = 0; i < N && idx < num_slots; ++i) v[idx++] = cur;
+        cur = (cur + 1) % N;
+    }
+    return v;
+}
+}  // namespace
+
+DirectSortN::DirectSortN(Engine &c, int N_, const std::vector<int> &rotIndices)
+    : cc(c), N(N_), rot(c, N_, rotIndices), max_batch((int)(c.n() / 2)) {}
+
+// kind 0: mask_vector(k) rotated by `r` (vector_rotate); kind 1: checking vector(k)
+const Plaintext &DirectSortN::mask(int kind, int num_slots, int k, int r, int level) {
+    auto key = std::make_tuple(kind, num_slots, k, r, level);
+    auto it = mask_cache.find(key);
+    if (it != mask_cache.end()) return *it->second;
+    std::vector<double> v = kind == 0 ? vector_rotate(mask_vector(num_slots, N, k), r) : checking_vector(num_slots, N, k);
+    PtPtr p = cc.encode(v, num_slots, level);
+    mask_cache[key] = p;
+    return *p;
+}
+
+void DirectSortN::reducePartial(CtPtr &acc, int slots) {
+    if (shard_world <= 1) return;
+    if (!allreduce) throw std::runtime_error("DirectSort: sharded run without an allreduce hook");
+    auto hdr = cc.alloc_u64(2);
+    u64 h[2] = {acc ? (u64)(acc->level + 1) : 0, acc ? 1ULL : 0ULL};
+    cc.h2d(hdr.ptr, h, 2);
+    allreduce(hdr.ptr, 2);
+    cc.d2h(h, hdr.ptr, 2);
+    if (h[1] == 0) throw std::runtime_error("DirectSort: no shard produced a partial");
+    const int level = (int)(h[0] / h[1]) - 1;
+    if (!acc) acc = cc.zero_like(level, slots);
+    allreduce(acc->data, 2 * acc->limbs * cc.n());
+    cc.reduce_after_allreduce(*acc);
+}
+
+CtPtr DirectSortN::vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is) {
+    CtPtr result;
+    for (int j = 0; j < num_partition / np; ++j) {
+        CtPtr Tj;
+        for (int i = 0; i < np; ++i) {
+            const Plaintext &pm = mask(0, num_slots, np * j + i, -is * num_partition - j * np, baby[i]->level);
+            cc.add_inplace(Tj, *cc.mul_plain(*baby[i], pm));
+        }
+        CtPtr o = rot.rotate(*Tj, is * num_partition + j * np);
+        cc.add_inplace(result, *o);
+    }
+    return result;
+}
+
+CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg) {
+    const SortShape s = rankShape(N, max_batch);
+    std::vector<int> idx(s.np);
+    for (int i = 0; i < s.np; ++i) idx[i] = i;
+    std::vector<CtPtr> baby = rot.rotateMany(x, idx);
+    for (auto &b : baby) b->slots = s.num_slots;
+    Comparison comp;
+    CtPtr rank;
+    for (int b = 0; b < s.num_batch; ++b) {
+        if (b % shard_world != shard_rank) continue;
+        CtPtr shifted = vecRotsOpt(baby, s.num_partition, s.num_slots, s.np, b);
+        CtPtr dup = cc.clone(x);
+        dup->slots = s.num_slots;
+        CtPtr c = comp.compare(cc, *dup, *shifted, f, cfg);
+        cc.add_inplace(rank, *c);
+    }
+    reducePartial(rank, s.num_slots);
+    for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)
+        rank = cc.add(*rank, *rot.rotate(*rank, s.num_slots / (1 << i)));
+    rank->slots = N;
+    return cc.add_const(*rank, -0.5);
+}
+
+CtPtr DirectSortN::blindRotationOptN(const std::vector<CtPtr> &mi, int num_slots, int np, int ib, int num_partition) {
+    CtPtr result;
+    for (int i = 0; i < (num_slots / N) / np; ++i) {
+        CtPtr tmp;
+        for (int j = 0; j < np; ++j) {
+            const Plaintext &pm = mask(0, num_slots, np * i + j, j, mi[j]->level);
+            cc.add_inplace(tmp, *cc.mul_plain(*mi[j], pm));
+        }
+        tmp = rot.rotate(*tmp, ib * num_partition + i * np);
+        cc.add_inplace(result, *tmp);
+    }
+    return result;
+}
+
+CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext &x) {
+    const SortShape s = checkShape(N, max_batch);
+    std::vector<double> idx(N);
+    for (int i = 0; i < N; ++i) idx[i] = (double)i;
+    PtPtr idxpt = cc.encode(idx, N, rank.level);
+    CtPtr imr = cc.plain_sub(*idxpt, rank);
+    imr->slots = s.num_slots;
+    CtPtr xs = cc.clone(x);
+    xs->slots = s.num_slots;
+    const std::vector<double> &coeffs = sincCoefficients();
+    std::vector<int> ridx(s.np);
+    for (int i = 0; i < s.np; ++i) ridx[i] = i;
+    CtPtr out;
+    for (int b = 0; b < s.num_batch; ++b) {
+        if (b % shard_world != shard_rank) continue;
+        const Plaintext &chk = mask(1, s.num_slots, b * s.num_partition, 0, imr->level);
+        CtPtr ri = cc.sub_plain(*imr, chk);
+        ri = cc.mul_const(*ri, 1.0 / N / 2);
+        ri = evalChebyshevSeriesPS(cc, *ri, coeffs, -1.0, 1.0);
+        CtPtr masked = cc.mul(*ri, *xs);
+        std::vector<CtPtr> mi = rot.rotateMany(*masked, ridx);
+        CtPtr r = blindRotationOptN(mi, s.num_slots, s.np, b, s.num_partition);
+        cc.add_inplace(out, *r);
+    }
+    reducePartial(out, s.num_slots);
+    for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)
+        out = cc.add(*out, *rot.rotate(*out, s.num_slots / (1 << i)));
+    out->slots = N;
+    return out;
+}
+
+CtPtr DirectSortN::sort(const Ciphertext &x, SignFunc f, const SignConfig &cfg) {
+    CtPtr rank = constructRank(x, f, cfg);
+    return rotationIndexCheckN(*rank, x);
+}
+
+// ================================================== coefficient tables =====
+namespace {
+std::string g_dir = "fhe-sorting_amd/data";
+std::map<int, std::vector<double>> g_cache;
+std::mutex g_mu;
+}  // namespace
+void setCoefficientDir(const std::string &dir) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_dir = dir;
+    g_cache.clear();
+}
+const std::vector<double> &doubledSincCoefficients(int N) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(N);
+    if (it != g_cache.end()) return it->second;
+    const std::string path = g_dir + "/doubled_sinc_" + std::to_string(N) + ".f64";
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("missing coefficient file " + path);
+    f.seekg(0, std::ios::end);
+    const size_t bytes = (size_t)f.tellg();
+    f.seekg(0);
+    std::vector<double> v(bytes / 8);
+    f.read(reinterpret_cast<char *>(v.data()), (std::streamsize)bytes);
+    return g_cache[N] = std::move(v);
+}
+const std::vector<double> &DirectSortN::sincCoefficients() const { return doubledSincCoefficients(N); }
+
+}  // namespace fhe

@@ -1,0 +1,141 @@
+// C++ call surface of the rank-sort comparator hot path, MI355X edition.
+//
+// Mirrors the reference's interface (names, argument meaning, error
+// behaviour) so a caller of oksuman/FHE-Sorting finds the same entry points:
+//   enum SignFunc, CompositeSignConfig, SignConfig      src/sign.h:6-32
+//   compositeSign<n>(), sign()                          src/sign.h:35-41
+//   Comparison::compare / indicator                     src/comparison.h:81-101
+//   DecomposeAlgo, Step, Decomposer<N>                  src/rotation.h:12-166
+//   RotationComposer<N>::rotate                         src/rotation.h:193-233
+//   DirectSort<N>::{getSizeParameters, constructRank,
+//                   rotationIndexCheckN, sort}          src/sort_algo.h:61-774
+// Every operation executes on the GPU through fhe::Engine (engine.hpp); the
+// templates are thin wrappers over runtime-N implementations.
+#pragma once
+#include <functional>
+#include <map>
+#include <set>
+#include <vector>
+
+#include "../engine/engine.hpp"
+
+namespace fhe {
+
+enum class SignFunc { CompositeSign = 0, SignumPolycircuit = 1, Tanh = 2, NaiveDiscrete = 3 };
+
+struct CompositeSignConfig {
+    int n, dg, df;
+    CompositeSignConfig(int n_, int dg_, int df_) : n(n_), dg(dg_), df(df_) {}
+};
+struct SignConfig {
+    CompositeSignConfig compos{0, 0, 0};
+    int multDepth = 100;  // src/sign.h:27-28: no bootstrapping on this path
+    SignConfig() = default;
+    explicit SignConfig(CompositeSignConfig c) : compos(c) {}
+    SignConfig(CompositeSignConfig c, int depth) : compos(c), multDepth(depth) {}
+};
+
+// Chebyshev series sum c_0/2 + sum_{i>=1} c_i T_i((2x-a-b)/(b-a)), depth-optimal
+// Paterson-Stockmeyer; replaces OpenFHE EvalChebyshevSeriesPS.
+CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x, const std::vector<double> &coeffs, double a,
+                            double b);
+
+CtPtr compositeSignN(Engine &cc, const Ciphertext &x, int n, const SignConfig &cfg);
+template <int n>
+CtPtr compositeSign(const Ciphertext &x, Engine &cc, const SignConfig &cfg) {
+    return compositeSignN(cc, x, n, cfg);
+}
+CtPtr sign(const Ciphertext &x, Engine &cc, SignFunc func, const SignConfig &cfg);
+
+class Comparison {
+  public:
+    CtPtr compare(Engine &cc, const Ciphertext &a, const Ciphertext &b, SignFunc f, const SignConfig &cfg);
+    CtPtr indicator(Engine &cc, const Ciphertext &x, double c, SignFunc f, const SignConfig &cfg);
+};
+
+enum class DecomposeAlgo { NAF = 0, BNAF = 1, BINARY = 2 };
+struct Step {
+    int value;
+    int stepSize;
+};
+
+class DecomposerN {
+  public:
+    DecomposerN(int N, std::vector<int> rot);
+    std::vector<Step> decompose(int rotation, int wrapN, DecomposeAlgo algo) const;
+    const std::vector<int> &getRotIndices() const { return rotIndices; }
+    int N, maxDecomposed;
+    std::vector<int> rotIndices;
+};
+template <int SIZE>
+class Decomposer : public DecomposerN {
+  public:
+    explicit Decomposer(std::vector<int> rot) : DecomposerN(SIZE, std::move(rot)) {}
+};
+
+class RotationComposerN {
+  public:
+    RotationComposerN(Engine &cc, int N, const std::vector<int> &rotIndices,
+                      DecomposeAlgo algo = DecomposeAlgo::BINARY);
+    CtPtr rotate(const Ciphertext &in, int rotation);
+    // several rotations of one input; single keyed steps share one ModUp
+    std::vector<CtPtr> rotateMany(const Ciphertext &in, const std::vector<int> &rotations);
+    Engine &cc;
+    DecomposerN dec;
+    DecomposeAlgo algo;
+    std::set<int> avail;
+};
+template <int SIZE>
+class RotationComposer : public RotationComposerN {
+  public:
+    RotationComposer(Engine &cc, const std::vector<int> &rot, DecomposeAlgo a = DecomposeAlgo::BINARY)
+        : RotationComposerN(cc, SIZE, rot, a) {}
+};
+
+struct SortShape {
+    int N, num_partition, num_batch, num_slots, np;
+};
+void directSortSizeParameters(int N, int &multDepth, std::vector<int> &rotations);
+SortShape rankShape(int N, int max_batch);
+SortShape checkShape(int N, int max_batch);
+
+// Sums a ciphertext's u64 limbs over ranks in place (device pointer, count
+// u64); the engine reduces mod q afterwards.  nullptr = single rank.
+using CtAllReduce = std::function<void(u64 *dev_data, size_t count)>;
+
+class DirectSortN {
+  public:
+    DirectSortN(Engine &cc, int N, const std::vector<int> &rotIndices);
+    CtPtr constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+    CtPtr rotationIndexCheckN(const Ciphertext &rank, const Ciphertext &x);
+    CtPtr sort(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+    const std::vector<double> &sincCoefficients() const;
+
+    int shard_rank = 0, shard_world = 1;
+    CtAllReduce allreduce;
+    Engine &cc;
+    int N;
+    RotationComposerN rot;
+    int max_batch;
+
+  private:
+    CtPtr vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is);
+    CtPtr blindRotationOptN(const std::vector<CtPtr> &masked, int num_slots, int np, int ib, int num_partition);
+    void reducePartial(CtPtr &acc, int slots);
+    const Plaintext &mask(int kind, int num_slots, int k, int rot, int level);
+    std::map<std::tuple<int, int, int, int, int>, PtPtr> mask_cache;
+};
+template <int SIZE>
+class DirectSort : public DirectSortN {
+  public:
+    DirectSort(Engine &cc, const std::vector<int> &rot) : DirectSortN(cc, SIZE, rot) {}
+    static void getSizeParameters(int &multDepth, std::vector<int> &rotations) {
+        directSortSizeParameters(SIZE, multDepth, rotations);
+    }
+};
+
+// coefficient tables (generated offline by data/gen_doubled_sinc.py)
+void setCoefficientDir(const std::string &dir);
+const std::vector<double> &doubledSincCoefficients(int N);
+
+}  // namespace fhe

@@ -1,0 +1,368 @@
+// extern "C" boundary of the MI355X engine (declarations: include/fhe_gpu.h).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+
+#include "../../../include/fhe_gpu.h"
+#include "../algo/fhesort.hpp"
+#include "../engine/engine.hpp"
+
+using namespace fhe;
+
+struct fhe_ctx {
+    std::unique_ptr<Engine> eng;
+    ncclComm_t comm = nullptr;
+    int rank = 0, world = 1;
+};
+struct fhe_ct {
+    CtPtr p;
+};
+struct fhe_pt {
+    PtPtr p;
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <class F>
+int guard(F &&f) {
+    try {
+        f();
+        return FHE_OK;
+    } catch (const NoKeyError &e) {
+        g_err = e.what();
+        return FHE_ENOKEY;
+    } catch (const std::invalid_argument &e) {
+        g_err = e.what();
+        return FHE_EINVAL;
+    } catch (const std::out_of_range &e) {
+        g_err = e.what();
+        return FHE_EINVAL;
+    } catch (const std::bad_alloc &e) {
+        g_err = e.what();
+        return FHE_ENOMEM;
+    } catch (const std::runtime_error &e) {
+        g_err = e.what();
+        const std::string m = e.what();
+        if (m.find("no levels left") != std::string::npos) return FHE_EDEPTH;
+        if (m.find("HIP error") != std::string::npos) return FHE_EHIP;
+        return FHE_EINTERNAL;
+    } catch (...) {
+        g_err = "unknown error";
+        return FHE_EINTERNAL;
+    }
+}
+inline fhe_ct *wrap(CtPtr p) { return new fhe_ct{std::move(p)}; }
+SignConfig cfgof(int n, int dg, int df) { return SignConfig(CompositeSignConfig(n, dg, df)); }
+#define NEED(x)                                                   \
+    do {                                                          \
+        if (!(x)) throw std::invalid_argument("null argument: " #x); \
+    } while (0)
+}  // namespace
+
+extern "C" {
+
+const char *fhe_last_error(void) { return g_err.c_str(); }
+
+int fhe_ctx_create(const fhe_params *p, int device, fhe_ctx **out) {
+    return guard([&] {
+        NEED(p);
+        NEED(out);
+        auto c = std::make_unique<fhe_ctx>();
+        c->eng = std::make_unique<Engine>(p->log_n, p->mult_depth, p->scale_bits, p->first_bits, p->dnum, device,
+                                          p->seed);
+        *out = c.release();
+    });
+}
+int fhe_ctx_destroy(fhe_ctx *ctx) {
+    return guard([&] {
+        if (!ctx) return;
+        if (ctx->comm) ncclCommDestroy(ctx->comm);
+        delete ctx;
+    });
+}
+int fhe_ctx_info(fhe_ctx *ctx, int *nq, int *K, int *alpha, uint64_t *primes, double *deltas) {
+    return guard([&] {
+        NEED(ctx);
+        const auto &P = ctx->eng->params();
+        if (nq) *nq = (int)P.nq();
+        if (K) *K = P.K;
+        if (alpha) *alpha = P.alpha;
+        if (primes) std::memcpy(primes, P.primes.data(), P.primes.size() * 8);
+        if (deltas) std::memcpy(deltas, P.delta.data(), P.delta.size() * 8);
+    });
+}
+int fhe_set_coeff_dir(const char *dir) {
+    return guard([&] {
+        NEED(dir);
+        setCoefficientDir(dir);
+    });
+}
+
+int fhe_keygen(fhe_ctx *ctx) { return guard([&] { ctx->eng->keygen(); }); }
+int fhe_gen_rotation_keys(fhe_ctx *ctx, const int32_t *idx, int n) {
+    return guard([&] { ctx->eng->gen_rotation_keys(std::vector<int>(idx, idx + n)); });
+}
+int fhe_ctx_load_secret(fhe_ctx *ctx, const uint64_t *s) { return guard([&] { ctx->eng->load_secret(s); }); }
+int fhe_ctx_load_public(fhe_ctx *ctx, const uint64_t *pk) { return guard([&] { ctx->eng->load_public(pk); }); }
+int fhe_ctx_load_keys(fhe_ctx *ctx, const uint64_t *relin, const int32_t *rot_idx, const uint64_t *const *rot_keys,
+                      int nrot) {
+    return guard([&] {
+        if (relin) ctx->eng->load_relin(relin);
+        for (int i = 0; i < nrot; ++i) ctx->eng->load_rotation(rot_idx[i], rot_keys[i]);
+    });
+}
+uint64_t fhe_key_bytes(fhe_ctx *ctx) { return ctx ? ctx->eng->key_bytes() : 0; }
+
+int fhe_encrypt(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->encrypt(std::vector<double>(v, v + len), slots, level)); });
+}
+int fhe_decrypt(fhe_ctx *ctx, const fhe_ct *ct, double *out) {
+    return guard([&] {
+        auto v = ctx->eng->decrypt(*ct->p);
+        std::memcpy(out, v.data(), v.size() * 8);
+    });
+}
+int fhe_ct_upload(fhe_ctx *ctx, const uint64_t *h, int limbs, int level, int slots, double scale, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->upload(h, (size_t)limbs, level, slots, scale)); });
+}
+int fhe_ct_download(fhe_ctx *ctx, const fhe_ct *ct, uint64_t *h) {
+    return guard([&] { ctx->eng->download(*ct->p, h); });
+}
+int fhe_ct_info(const fhe_ct *ct, int *level, int *slots, double *scale, int *limbs) {
+    return guard([&] {
+        NEED(ct);
+        if (level) *level = ct->p->level;
+        if (slots) *slots = ct->p->slots;
+        if (scale) *scale = ct->p->scale;
+        if (limbs) *limbs = (int)ct->p->limbs;
+    });
+}
+int fhe_ct_set_slots(fhe_ct *ct, int slots) {
+    return guard([&] {
+        NEED(ct);
+        ct->p->slots = slots;
+    });
+}
+int fhe_ct_free(fhe_ct *ct) {
+    delete ct;
+    return FHE_OK;
+}
+int fhe_pt_encode(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_pt **out) {
+    return guard([&] { *out = new fhe_pt{ctx->eng->encode(std::vector<double>(v, v + len), slots, level)}; });
+}
+int fhe_pt_upload(fhe_ctx *ctx, const uint64_t *h, int limbs, int level, int slots, double scale, fhe_pt **out) {
+    return guard([&] { *out = new fhe_pt{ctx->eng->upload_pt(h, (size_t)limbs, level, slots, scale)}; });
+}
+int fhe_pt_free(fhe_pt *pt) {
+    delete pt;
+    return FHE_OK;
+}
+
+#define OP1(name, expr) \
+    int name(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out) { return guard([&] { *out = wrap(expr); }); }
+OP1(fhe_negate, ctx->eng->negate(*a->p))
+OP1(fhe_rescale, ctx->eng->rescale(*a->p))
+OP1(fhe_square_relin, ctx->eng->square(*a->p))
+int fhe_add(fhe_ctx *ctx, const fhe_ct *a, const fhe_ct *b, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->add(*a->p, *b->p)); });
+}
+int fhe_sub(fhe_ctx *ctx, const fhe_ct *a, const fhe_ct *b, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->sub(*a->p, *b->p)); });
+}
+int fhe_mul_relin(fhe_ctx *ctx, const fhe_ct *a, const fhe_ct *b, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->mul(*a->p, *b->p)); });
+}
+int fhe_add_const(fhe_ctx *ctx, const fhe_ct *a, double c, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->add_const(*a->p, c)); });
+}
+int fhe_mul_const(fhe_ctx *ctx, const fhe_ct *a, double c, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->mul_const(*a->p, c)); });
+}
+int fhe_mul_const_to(fhe_ctx *ctx, const fhe_ct *a, double c, int t, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->mul_const_to(*a->p, c, t)); });
+}
+int fhe_mul_int(fhe_ctx *ctx, const fhe_ct *a, int64_t k, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->mul_int(*a->p, k)); });
+}
+int fhe_level_adjust(fhe_ctx *ctx, const fhe_ct *a, int t, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->level_adjust(*a->p, t)); });
+}
+int fhe_mul_plain(fhe_ctx *ctx, const fhe_ct *a, const fhe_pt *p, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->mul_plain(*a->p, *p->p)); });
+}
+int fhe_add_plain(fhe_ctx *ctx, const fhe_ct *a, const fhe_pt *p, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->add_plain(*a->p, *p->p)); });
+}
+int fhe_rotate(fhe_ctx *ctx, const fhe_ct *a, int k, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->rotate(*a->p, k)); });
+}
+int fhe_rotate_hoisted(fhe_ctx *ctx, const fhe_ct *a, const int32_t *ks, int m, fhe_ct **outs) {
+    return guard([&] {
+        auto v = ctx->eng->rotate_hoisted(*a->p, std::vector<long>(ks, ks + m));
+        for (int i = 0; i < m; ++i) outs[i] = wrap(v[i]);
+    });
+}
+int fhe_linear_sum_to(fhe_ctx *ctx, const fhe_ct *const *xs, const double *c, int m, int t, fhe_ct **out) {
+    return guard([&] {
+        std::vector<const Ciphertext *> v;
+        for (int i = 0; i < m; ++i) v.push_back(xs[i]->p.get());
+        *out = wrap(ctx->eng->linear_sum_to(v, std::vector<double>(c, c + m), t));
+    });
+}
+int fhe_cheb_ps(fhe_ctx *ctx, const fhe_ct *a, const double *coeffs, int nc, double lo, double hi, fhe_ct **out) {
+    return guard([&] {
+        *out = wrap(evalChebyshevSeriesPS(*ctx->eng, *a->p, std::vector<double>(coeffs, coeffs + nc), lo, hi));
+    });
+}
+int fhe_sign_composite(fhe_ctx *ctx, const fhe_ct *x, int n, int dg, int df, fhe_ct **out) {
+    return guard([&] { *out = wrap(sign(*x->p, *ctx->eng, SignFunc::CompositeSign, cfgof(n, dg, df))); });
+}
+int fhe_compare(fhe_ctx *ctx, const fhe_ct *a, const fhe_ct *b, int n, int dg, int df, fhe_ct **out) {
+    return guard([&] {
+        Comparison c;
+        *out = wrap(c.compare(*ctx->eng, *a->p, *b->p, SignFunc::CompositeSign, cfgof(n, dg, df)));
+    });
+}
+int fhe_indicator(fhe_ctx *ctx, const fhe_ct *x, double k, int n, int dg, int df, fhe_ct **out) {
+    return guard([&] {
+        Comparison c;
+        *out = wrap(c.indicator(*ctx->eng, *x->p, k, SignFunc::CompositeSign, cfgof(n, dg, df)));
+    });
+}
+int fhe_compose_rotate(fhe_ctx *ctx, const fhe_ct *a, int N, const int32_t *rots, int nrot, int algo, int rotation,
+                       fhe_ct **out) {
+    return guard([&] {
+        RotationComposerN rc(*ctx->eng, N, std::vector<int>(rots, rots + nrot), (DecomposeAlgo)algo);
+        *out = wrap(rc.rotate(*a->p, rotation));
+    });
+}
+int fhe_decompose(int N, const int32_t *rots, int nrot, int rotation, int wrap_n, int algo, int32_t *values,
+                  int32_t *sizes, int max_steps) {
+    int count = -1;
+    int rc = guard([&] {
+        DecomposerN d(N, std::vector<int>(rots, rots + nrot));
+        auto s = d.decompose(rotation, wrap_n, (DecomposeAlgo)algo);
+        count = (int)s.size();
+        for (int i = 0; i < count && i < max_steps; ++i) {
+            values[i] = s[i].value;
+            sizes[i] = s[i].stepSize;
+        }
+    });
+    return rc == FHE_OK ? count : -rc;
+}
+int fhe_size_parameters(int N, int *depth, int32_t *rots, int max_rots) {
+    int count = -1;
+    int rc = guard([&] {
+        std::vector<int> r;
+        directSortSizeParameters(N, *depth, r);
+        count = (int)r.size();
+        for (int i = 0; i < count && i < max_rots; ++i) rots[i] = r[i];
+    });
+    return rc == FHE_OK ? count : -rc;
+}
+
+int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, const int32_t *rots, int nrot, int n,
+                    int dg, int df, int mode, int shard_rank, int shard_world, fhe_allreduce_fn fn, void *user,
+                    fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(x);
+        DirectSortN ds(*ctx->eng, N, std::vector<int>(rots, rots + nrot));
+        ds.shard_rank = shard_rank;
+        ds.shard_world = shard_world;
+        if (fn) {
+            ds.allreduce = [fn, user](u64 *d, size_t c) { fn(d, (uint64_t)c, user); };
+        } else if (shard_world > 1) {
+            if (!ctx->comm) throw std::runtime_error("sharded sort needs fhe_comm_init or an allreduce hook");
+            ncclComm_t comm = ctx->comm;
+            hipStream_t st = static_cast<hipStream_t>(ctx->eng->stream_handle());
+            ds.allreduce = [comm, st](u64 *d, size_t c) {
+                if (ncclAllReduce(d, d, c, ncclUint64, ncclSum, comm, st) != ncclSuccess)
+                    throw std::runtime_error("HIP error: ncclAllReduce failed");
+            };
+        }
+        const SignConfig cfg = cfgof(n, dg, df);
+        if (mode == 1)
+            *out = wrap(ds.constructRank(*x->p, SignFunc::CompositeSign, cfg));
+        else if (mode == 2) {
+            NEED(rank);
+            *out = wrap(ds.rotationIndexCheckN(*rank->p, *x->p));
+        } else
+            *out = wrap(ds.sort(*x->p, SignFunc::CompositeSign, cfg));
+    });
+}
+
+int fhe_comm_get_unique_id(uint8_t id[128]) {
+    return guard([&] {
+        ncclUniqueId u;
+        if (ncclGetUniqueId(&u) != ncclSuccess) throw std::runtime_error("HIP error: ncclGetUniqueId failed");
+        static_assert(sizeof(u) == 128, "ncclUniqueId size");
+        std::memcpy(id, &u, 128);
+    });
+}
+int fhe_comm_init(fhe_ctx *ctx, const uint8_t id[128], int rank, int world) {
+    return guard([&] {
+        ncclUniqueId u;
+        std::memcpy(&u, id, 128);
+        if (hipSetDevice(ctx->eng->device()) != hipSuccess) throw std::runtime_error("HIP error: hipSetDevice");
+        if (ncclCommInitRank(&ctx->comm, world, u, rank) != ncclSuccess)
+            throw std::runtime_error("HIP error: ncclCommInitRank failed");
+        ctx->rank = rank;
+        ctx->world = world;
+    });
+}
+int fhe_comm_destroy(fhe_ctx *ctx) {
+    return guard([&] {
+        if (ctx->comm) ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    });
+}
+int fhe_ct_allreduce(fhe_ctx *ctx, fhe_ct *ct) {
+    if (!ctx || !ctx->comm) {
+        g_err = "fhe_ct_allreduce: no communicator";
+        return FHE_ENOCOMM;
+    }
+    return guard([&] {
+        hipStream_t st = static_cast<hipStream_t>(ctx->eng->stream_handle());
+        const size_t cnt = 2 * ct->p->limbs * ctx->eng->n();
+        if (ncclAllReduce(ct->p->data, ct->p->data, cnt, ncclUint64, ncclSum, ctx->comm, st) != ncclSuccess)
+            throw std::runtime_error("HIP error: ncclAllReduce failed");
+        ctx->eng->reduce_after_allreduce(*ct->p);
+    });
+}
+
+int fhe_ntt(fhe_ctx *ctx, uint64_t *h, int prime_index, int limbs, int inverse) {
+    return guard([&] { ctx->eng->ntt_host(h, prime_index, limbs, inverse != 0); });
+}
+int fhe_modup(fhe_ctx *ctx, const uint64_t *d, int ell, uint64_t *ext) {
+    return guard([&] { ctx->eng->modup_host(d, (size_t)ell, ext); });
+}
+int fhe_moddown(fhe_ctx *ctx, const uint64_t *in, int ell, uint64_t *out) {
+    return guard([&] { ctx->eng->moddown_host(in, (size_t)ell, out); });
+}
+int fhe_automorph(fhe_ctx *ctx, const uint64_t *in, int limbs, uint64_t g, uint64_t *out) {
+    return guard([&] { ctx->eng->automorph_host(in, (size_t)limbs, g, out); });
+}
+int fhe_counters(fhe_ctx *ctx, uint64_t out[6]) {
+    return guard([&] {
+        const auto &c = ctx->eng->ctr;
+        out[0] = c.hmult;
+        out[1] = c.keyswitch;
+        out[2] = c.rotations;
+        out[3] = c.rescale;
+        out[4] = c.ptmult;
+        out[5] = c.constmult;
+    });
+}
+int fhe_reset_counters(fhe_ctx *ctx) {
+    return guard([&] { ctx->eng->ctr = Counters(); });
+}
+int fhe_sync(fhe_ctx *ctx) { return guard([&] { ctx->eng->sync(); }); }
+void *fhe_stream(fhe_ctx *ctx) { return ctx ? ctx->eng->stream_handle() : nullptr; }
+
+}  // extern "C"

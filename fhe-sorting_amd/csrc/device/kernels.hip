@@ -1,0 +1,649 @@
+// gfx950 kernels for the RNS-CKKS ciphertext-op engine.
+//
+// Everything here is 64-bit integer modular arithmetic (no MFMA: the hot path
+// is HBM/VALU-bound integer work).  Design notes:
+//   * NTT (n = 2^logN, 12 <= logN <= 17) is split into two LDS-staged passes
+//     n = R1 x R2 ("column" pass over the top k1 index bits, "row" pass over
+//     the low k2 bits); each pass keeps a 32 KiB tile in LDS and runs all its
+//     radix-2 stages there, so a limb crosses HBM twice per transform.
+//     Column tiles are C >= 8 adjacent columns wide, so every global access is
+//     a >= 64 B contiguous segment per row.
+//   * element-wise kernels move 16 B per lane (ulonglong2) and are launched
+//     3-D: x = coefficient blocks, y = limb (prime), z = polynomial segment.
+//   * basis conversions (ModUp / ModDown) hold the source residues of one
+//     coefficient in registers and emit a chunk of target limbs per thread;
+//     every constant multiply is a Shoup multiply with a precomputed
+//     companion.
+#include "kernels.hpp"
+
+namespace fhe {
+namespace dev {
+
+namespace {
+
+constexpr int TILE = 4096;  // u64 elements per LDS tile (32 KiB)
+constexpr int NT = 256;     // threads per block
+constexpr int MAXSRC = 16;  // max limbs per digit / special primes held in registers
+constexpr int TCH = 8;      // target limbs per thread in basis conversions
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+
+// ----------------------------------------------------------------- NTT ----
+__global__ __launch_bounds__(NT) void k_ntt_fwd_cols(u64 *data, size_t seg, const int *pmap, int logN, int k1,
+                                                     int C, NttTables T) {
+    __shared__ u64 tile[TILE];
+    const int R1 = 1 << k1, k2 = logN - k1, R2 = 1 << k2;
+    const size_t n = (size_t)1 << logN;
+    const int limb = blockIdx.y;
+    const int p = pmap ? pmap[limb] : limb;
+    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n;
+    const int lo0 = blockIdx.x * C;
+    const u64 q = T.mods[p].q;
+    const u64 *tw = T.fwd + (size_t)p * n, *tws = T.fwd_s + (size_t)p * n;
+    const int lgC = __builtin_ctz(C);
+    for (int idx = lane_id(); idx < C * R1; idx += NT) {
+        const int r = idx >> lgC, c = idx & (C - 1);
+        tile[idx] = a[(size_t)r * R2 + lo0 + c];
+    }
+    __syncthreads();
+    for (int s = 0; s < k1; ++s) {
+        const int lgt = k1 - 1 - s;
+        const int t = 1 << lgt;
+        for (int b = lane_id(); b < (C * R1) >> 1; b += NT) {
+            const int c = b & (C - 1), pp = b >> lgC;
+            const int g = pp >> lgt, o = pp & (t - 1);
+            const int r0 = (g << (lgt + 1)) + o;
+            const u64 W = tw[(1 << s) + g], Wp = tws[(1 << s) + g];
+            const int i0 = (r0 << lgC) + c, i1 = ((r0 + t) << lgC) + c;
+            const u64 U = tile[i0];
+            const u64 V = mul_shoup(tile[i1], W, Wp, q);
+            tile[i0] = add_mod(U, V, q);
+            tile[i1] = sub_mod(U, V, q);
+        }
+        __syncthreads();
+    }
+    for (int idx = lane_id(); idx < C * R1; idx += NT) {
+        const int r = idx >> lgC, c = idx & (C - 1);
+        a[(size_t)r * R2 + lo0 + c] = tile[idx];
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_ntt_fwd_rows(u64 *data, size_t seg, const int *pmap, int logN, int k1,
+                                                     int ROWS, NttTables T) {
+    __shared__ u64 tile[TILE];
+    const int k2 = logN - k1, R2 = 1 << k2;
+    const size_t n = (size_t)1 << logN;
+    const int limb = blockIdx.y;
+    const int p = pmap ? pmap[limb] : limb;
+    const int row0 = blockIdx.x * ROWS;
+    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n + (size_t)row0 * R2;
+    const u64 q = T.mods[p].q;
+    const u64 *tw = T.fwd + (size_t)p * n, *tws = T.fwd_s + (size_t)p * n;
+    const int cnt = ROWS * R2;
+    for (int idx = lane_id(); idx < cnt; idx += NT) tile[idx] = a[idx];
+    __syncthreads();
+    for (int sl = 0; sl < k2; ++sl) {
+        const int s = k1 + sl;
+        const int lgt = k2 - 1 - sl;
+        const int t = 1 << lgt;
+        for (int b = lane_id(); b < cnt >> 1; b += NT) {
+            const int row = b >> (k2 - 1), pp = b & ((R2 >> 1) - 1);
+            const int g = pp >> lgt, o = pp & (t - 1);
+            const int c0 = (g << (lgt + 1)) + o;
+            const int widx = (1 << s) + ((row0 + row) << sl) + g;
+            const u64 W = tw[widx], Wp = tws[widx];
+            const int i0 = row * R2 + c0, i1 = i0 + t;
+            const u64 U = tile[i0];
+            const u64 V = mul_shoup(tile[i1], W, Wp, q);
+            tile[i0] = add_mod(U, V, q);
+            tile[i1] = sub_mod(U, V, q);
+        }
+        __syncthreads();
+    }
+    for (int idx = lane_id(); idx < cnt; idx += NT) a[idx] = tile[idx];
+}
+
+__global__ __launch_bounds__(NT) void k_ntt_inv_rows(u64 *data, size_t seg, const int *pmap, int logN, int k1,
+                                                     int ROWS, NttTables T) {
+    __shared__ u64 tile[TILE];
+    const int k2 = logN - k1, R2 = 1 << k2;
+    const size_t n = (size_t)1 << logN;
+    const int limb = blockIdx.y;
+    const int p = pmap ? pmap[limb] : limb;
+    const int row0 = blockIdx.x * ROWS;
+    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n + (size_t)row0 * R2;
+    const u64 q = T.mods[p].q;
+    const u64 *tw = T.inv + (size_t)p * n, *tws = T.inv_s + (size_t)p * n;
+    const int cnt = ROWS * R2;
+    for (int idx = lane_id(); idx < cnt; idx += NT) tile[idx] = a[idx];
+    __syncthreads();
+    for (int sl = 0; sl < k2; ++sl) {
+        const int lgt = sl;  // tt = 2^sl
+        const int t = 1 << lgt;
+        const size_t m = n >> (sl + 1);
+        for (int b = lane_id(); b < cnt >> 1; b += NT) {
+            const int row = b >> (k2 - 1), pp = b & ((R2 >> 1) - 1);
+            const int g = pp >> lgt, o = pp & (t - 1);
+            const int c0 = (g << (lgt + 1)) + o;
+            const size_t i = ((size_t)(row0 + row) << (k2 - 1 - sl)) + g;
+            const u64 W = tw[m + i], Wp = tws[m + i];
+            const int i0 = row * R2 + c0, i1 = i0 + t;
+            const u64 U = tile[i0], V = tile[i1];
+            tile[i0] = add_mod(U, V, q);
+            tile[i1] = mul_shoup(sub_mod(U, V, q), W, Wp, q);
+        }
+        __syncthreads();
+    }
+    for (int idx = lane_id(); idx < cnt; idx += NT) a[idx] = tile[idx];
+}
+
+__global__ __launch_bounds__(NT) void k_ntt_inv_cols(u64 *data, size_t seg, const int *pmap, int logN, int k1,
+                                                     int C, NttTables T) {
+    __shared__ u64 tile[TILE];
+    const int R1 = 1 << k1, k2 = logN - k1, R2 = 1 << k2;
+    const size_t n = (size_t)1 << logN;
+    const int limb = blockIdx.y;
+    const int p = pmap ? pmap[limb] : limb;
+    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n;
+    const int lo0 = blockIdx.x * C;
+    const u64 q = T.mods[p].q;
+    const u64 *tw = T.inv + (size_t)p * n, *tws = T.inv_s + (size_t)p * n;
+    const int lgC = __builtin_ctz(C);
+    for (int idx = lane_id(); idx < C * R1; idx += NT) {
+        const int r = idx >> lgC, c = idx & (C - 1);
+        tile[idx] = a[(size_t)r * R2 + lo0 + c];
+    }
+    __syncthreads();
+    for (int sc = 0; sc < k1; ++sc) {
+        const int lgt = sc;
+        const int t = 1 << lgt;
+        const size_t m = n >> (k2 + sc + 1);
+        for (int b = lane_id(); b < (C * R1) >> 1; b += NT) {
+            const int c = b & (C - 1), pp = b >> lgC;
+            const int g = pp >> lgt, o = pp & (t - 1);
+            const int r0 = (g << (lgt + 1)) + o;
+            const u64 W = tw[m + g], Wp = tws[m + g];
+            const int i0 = (r0 << lgC) + c, i1 = ((r0 + t) << lgC) + c;
+            const u64 U = tile[i0], V = tile[i1];
+            tile[i0] = add_mod(U, V, q);
+            tile[i1] = mul_shoup(sub_mod(U, V, q), W, Wp, q);
+        }
+        __syncthreads();
+    }
+    const u64 ni = T.ninv[p], nis = T.ninv_s[p];
+    for (int idx = lane_id(); idx < C * R1; idx += NT) {
+        const int r = idx >> lgC, c = idx & (C - 1);
+        a[(size_t)r * R2 + lo0 + c] = mul_shoup(tile[idx], ni, nis, q);
+    }
+}
+
+// --------------------------------------------------------- element-wise ----
+// grid: x = n / (2 NT), y = limb, z = segment; 2 coefficients per lane
+#define EW_PROLOGUE                                                           \
+    const size_t n = (size_t)1 << logN;                                       \
+    const int l = blockIdx.y;                                                 \
+    const size_t off = (size_t)blockIdx.z * seg + (size_t)l * n;              \
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;             \
+    if (k >= n) return;                                                       \
+    const u64 q = mods[l].q;
+
+__global__ __launch_bounds__(NT) void k_add(u64 *out, const u64 *a, const u64 *b, size_t seg, const Mod *mods,
+                                            int logN) {
+    EW_PROLOGUE
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
+    const ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(b + off + k);
+    ulonglong2 r;
+    r.x = add_mod(x.x, y.x, q);
+    r.y = add_mod(x.y, y.y, q);
+    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+}
+__global__ __launch_bounds__(NT) void k_sub(u64 *out, const u64 *a, const u64 *b, size_t seg, const Mod *mods,
+                                            int logN) {
+    EW_PROLOGUE
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
+    const ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(b + off + k);
+    ulonglong2 r;
+    r.x = sub_mod(x.x, y.x, q);
+    r.y = sub_mod(x.y, y.y, q);
+    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+}
+__global__ __launch_bounds__(NT) void k_neg(u64 *out, const u64 *a, size_t seg, const Mod *mods, int logN) {
+    EW_PROLOGUE
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
+    ulonglong2 r;
+    r.x = sub_mod(0, x.x, q);
+    r.y = sub_mod(0, x.y, q);
+    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+}
+__device__ __forceinline__ u64 smod(int64_t v, const Mod &m) {
+    if (v >= 0) return reduce64((u64)v, m);
+    const u64 r = reduce64((u64)0 - (u64)v, m);
+    return r ? m.q - r : 0;
+}
+__global__ __launch_bounds__(NT) void k_mul_scalar(u64 *out, const u64 *a, int64_t K, size_t seg, const Mod *mods,
+                                                   int logN) {
+    EW_PROLOGUE
+    const Mod m = mods[l];
+    const u64 w = smod(K, m);
+    (void)q;
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
+    ulonglong2 r;
+    r.x = mul_barrett(x.x, w, m);
+    r.y = mul_barrett(x.y, w, m);
+    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+}
+__global__ __launch_bounds__(NT) void k_add_scalar(u64 *out, const u64 *a, int64_t K, size_t seg, const Mod *mods,
+                                                   int logN) {
+    EW_PROLOGUE
+    const u64 w = smod(K, mods[l]);
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
+    ulonglong2 r;
+    r.x = add_mod(x.x, w, q);
+    r.y = add_mod(x.y, w, q);
+    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+}
+__global__ __launch_bounds__(NT) void k_mul_plain(u64 *out, const u64 *a, const u64 *p, size_t seg,
+                                                  const Mod *mods, int logN) {
+    EW_PROLOGUE
+    const Mod m = mods[l];
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
+    const ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(p + (size_t)l * n + k);
+    ulonglong2 r;
+    r.x = mul_barrett(x.x, y.x, m);
+    r.y = mul_barrett(x.y, y.y, m);
+    (void)q;
+    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+}
+// a, b: [2][limbs][n]; d: [3][limbs][n]  (seg = limbs * n)
+__global__ __launch_bounds__(NT) void k_tensor(u64 *d, const u64 *a, const u64 *b, size_t seg, const Mod *mods,
+                                               int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const Mod m = mods[l];
+    const size_t o = (size_t)l * n + k;
+    const ulonglong2 a0 = *reinterpret_cast<const ulonglong2 *>(a + o);
+    const ulonglong2 a1 = *reinterpret_cast<const ulonglong2 *>(a + seg + o);
+    const ulonglong2 b0 = *reinterpret_cast<const ulonglong2 *>(b + o);
+    const ulonglong2 b1 = *reinterpret_cast<const ulonglong2 *>(b + seg + o);
+    ulonglong2 d0, d1, d2;
+    d0.x = mul_barrett(a0.x, b0.x, m);
+    d0.y = mul_barrett(a0.y, b0.y, m);
+    d1.x = add_mod(mul_barrett(a0.x, b1.x, m), mul_barrett(a1.x, b0.x, m), m.q);
+    d1.y = add_mod(mul_barrett(a0.y, b1.y, m), mul_barrett(a1.y, b0.y, m), m.q);
+    d2.x = mul_barrett(a1.x, b1.x, m);
+    d2.y = mul_barrett(a1.y, b1.y, m);
+    *reinterpret_cast<ulonglong2 *>(d + o) = d0;
+    *reinterpret_cast<ulonglong2 *>(d + seg + o) = d1;
+    *reinterpret_cast<ulonglong2 *>(d + 2 * seg + o) = d2;
+}
+constexpr int LIN_MAX = 32;
+struct LinArgs {
+    const u64 *x[LIN_MAX];
+    int64_t K[LIN_MAX];
+    int m, accumulate;
+    size_t xseg;
+};
+__global__ __launch_bounds__(NT) void k_linear_sum(u64 *out, LinArgs A, size_t seg, const Mod *mods, int logN) {
+    EW_PROLOGUE
+    const Mod md = mods[l];
+    u64 r0 = 0, r1 = 0;
+    if (A.accumulate) {
+        const ulonglong2 o = *reinterpret_cast<const ulonglong2 *>(out + off + k);
+        r0 = o.x;
+        r1 = o.y;
+    }
+    const size_t xo = (size_t)blockIdx.z * A.xseg + (size_t)l * n + k;
+    for (int i = 0; i < A.m; ++i) {
+        const u64 w = smod(A.K[i], md);
+        const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(A.x[i] + xo);
+        r0 = add_mod(r0, mul_barrett(x.x, w, md), q);
+        r1 = add_mod(r1, mul_barrett(x.y, w, md), q);
+    }
+    ulonglong2 r;
+    r.x = r0;
+    r.y = r1;
+    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+}
+__global__ __launch_bounds__(NT) void k_permute(u64 *out, const u64 *in, const uint32_t *perm, size_t seg,
+                                                int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t off = (size_t)blockIdx.z * seg + (size_t)blockIdx.y * n;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    out[off + k] = in[off + perm[k]];
+}
+__global__ __launch_bounds__(NT) void k_signed_to_rns(u64 *out, const int64_t *coef, const int *pmap,
+                                                      const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const Mod m = mods[pmap ? pmap[l] : l];
+    const int64_t v = coef[k];
+    u64 r;
+    if (v >= 0) {
+        r = reduce64((u64)v, m);
+    } else {
+        r = reduce64((u64)(-v), m);
+        r = r ? m.q - r : 0;
+    }
+    out[(size_t)l * n + k] = r;
+}
+__global__ __launch_bounds__(NT) void k_reduce(u64 *x, size_t seg, const Mod *mods, int logN) {
+    EW_PROLOGUE
+    const Mod m = mods[l];
+    ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(x + off + k);
+    v.x = reduce64(v.x, m);
+    v.y = reduce64(v.y, m);
+    (void)q;
+    *reinterpret_cast<ulonglong2 *>(x + off + k) = v;
+}
+
+// ------------------------------------------------------------ keyswitch ----
+struct ModUpArgs {
+    const u64 *qhinv[8], *qhinv_s[8], *qhat[8], *qhat_s[8];
+    int lo[8], hi[8];
+};
+
+// grid: x = n / NT, y = target chunks of TCH, z = digit
+__global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef, int W, ModUpArgs A,
+                                                      const int *pmap_ext, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const int j = blockIdx.z;
+    const int lo = A.lo[j], hi = A.hi[j], a = hi - lo;
+    const int t0 = blockIdx.y * TCH;
+    bool any = false;
+    for (int t = t0; t < t0 + TCH && t < W; ++t) any |= !(t >= lo && t < hi);
+    if (!any) return;
+    u64 y[MAXSRC];
+#pragma unroll
+    for (int i = 0; i < MAXSRC; ++i) {
+        if (i < a) {
+            const u64 qi = mods[lo + i].q;
+            y[i] = mul_shoup(coef[(size_t)(lo + i) * n + k], A.qhinv[j][i], A.qhinv_s[j][i], qi);
+        }
+    }
+    for (int t = t0; t < t0 + TCH && t < W; ++t) {
+        if (t >= lo && t < hi) continue;
+        const u64 qt = mods[pmap_ext[t]].q;
+        u64 acc = 0;
+#pragma unroll
+        for (int i = 0; i < MAXSRC; ++i) {
+            if (i < a) {
+                const size_t ti = (size_t)i * W + t;
+                acc = add_mod(acc, mul_shoup(y[i], A.qhat[j][ti], A.qhat_s[j][ti], qt), qt);
+            }
+        }
+        ext[((size_t)j * W + t) * n + k] = acc;
+    }
+}
+
+// grid: x = n / NT, y = W targets
+__global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
+                                                 int ell, int W, int nall, int alpha, int digits,
+                                                 const uint32_t *perm, const int *pmap_ext, const Mod *mods,
+                                                 int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const int t = blockIdx.y;
+    const int pt = pmap_ext[t];
+    const Mod m = mods[pt];
+    const size_t kk = perm ? perm[k] : k;
+    u64 a0 = 0, a1 = 0;
+    for (int j = 0; j < digits; ++j) {
+        const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
+        const u64 x = (t >= lo && t < hi) ? dntt[(size_t)t * n + kk] : ext[((size_t)j * W + t) * n + kk];
+        const u64 kb = key[(((size_t)j * 2 + 0) * nall + pt) * n + k];
+        const u64 ka = key[(((size_t)j * 2 + 1) * nall + pt) * n + k];
+        a0 = add_mod(a0, mul_barrett(x, kb, m), m.q);
+        a1 = add_mod(a1, mul_barrett(x, ka, m), m.q);
+    }
+    acc[(size_t)t * n + k] = a0;
+    acc[((size_t)W + t) * n + k] = a1;
+}
+
+// grid: x = n / NT, y = ceil(ell / TCH), z = segment
+__global__ __launch_bounds__(NT) void k_moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq,
+                                                        size_t seg_in, size_t seg_out, const u64 *phinv,
+                                                        const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
+                                                        const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const u64 *src = pc + (size_t)blockIdx.z * seg_in;
+    u64 *dst = conv + (size_t)blockIdx.z * seg_out;
+    u64 v[MAXSRC];
+#pragma unroll
+    for (int i = 0; i < MAXSRC; ++i)
+        if (i < K) v[i] = mul_shoup(src[(size_t)i * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+    const int i0 = blockIdx.y * TCH;
+    for (int i = i0; i < i0 + TCH && i < ell; ++i) {
+        const u64 qi = mods[i].q;
+        u64 acc = 0;
+#pragma unroll
+        for (int kk = 0; kk < MAXSRC; ++kk)
+            if (kk < K) {
+                const size_t ix = (size_t)kk * nq + i;
+                acc = add_mod(acc, mul_shoup(v[kk], phat[ix], phat_s[ix], qi), qi);
+            }
+        dst[(size_t)i * n + k] = acc;
+    }
+}
+
+// grid: x = n / (2 NT), y = limb i < ell, z = segment
+__global__ __launch_bounds__(NT) void k_moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add,
+                                                       int add_segs, size_t seg_out, size_t seg_acc, size_t seg_add,
+                                                       const u64 *pinv, const u64 *pinv_s, const Mod *mods,
+                                                       int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y, s = blockIdx.z;
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const u64 q = mods[l].q, w = pinv[l], wp = pinv_s[l];
+    const size_t lo = (size_t)l * n + k;
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(acc + (size_t)s * seg_acc + lo);
+    const ulonglong2 c = *reinterpret_cast<const ulonglong2 *>(conv + (size_t)s * seg_out + lo);
+    ulonglong2 r;
+    r.x = mul_shoup(sub_mod(x.x, c.x, q), w, wp, q);
+    r.y = mul_shoup(sub_mod(x.y, c.y, q), w, wp, q);
+    if (add && s < add_segs) {
+        const ulonglong2 d = *reinterpret_cast<const ulonglong2 *>(add + (size_t)s * seg_add + lo);
+        r.x = add_mod(r.x, d.x, q);
+        r.y = add_mod(r.y, d.y, q);
+    }
+    *reinterpret_cast<ulonglong2 *>(out + (size_t)s * seg_out + lo) = r;
+}
+
+// -------------------------------------------------------------- rescale ----
+// grid: x = n / NT, y = i < ell-1, z = segment
+__global__ __launch_bounds__(NT) void k_rescale_prep(u64 *tmp, const u64 *last, int ell, size_t seg_last,
+                                                     size_t seg_tmp, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const int i = blockIdx.y, s = blockIdx.z;
+    const u64 ql = mods[ell - 1].q;
+    const Mod mi = mods[i];
+    const u64 c = last[(size_t)s * seg_last + k];
+    u64 v = reduce64(c, mi);
+    if (c > (ql >> 1)) v = sub_mod(v, reduce64(ql, mi), mi.q);
+    tmp[(size_t)s * seg_tmp + (size_t)i * n + k] = v;
+}
+__global__ __launch_bounds__(NT) void k_rescale_finish(u64 *out, const u64 *in, const u64 *tmp, size_t seg_out,
+                                                       size_t seg_in, size_t seg_tmp, const u64 *qlinv,
+                                                       const u64 *qlinv_s, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y, s = blockIdx.z;
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const u64 q = mods[l].q, w = qlinv[l], wp = qlinv_s[l];
+    const size_t lo = (size_t)l * n + k;
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(in + (size_t)s * seg_in + lo);
+    const ulonglong2 t = *reinterpret_cast<const ulonglong2 *>(tmp + (size_t)s * seg_tmp + lo);
+    ulonglong2 r;
+    r.x = mul_shoup(sub_mod(x.x, t.x, q), w, wp, q);
+    r.y = mul_shoup(sub_mod(x.y, t.y, q), w, wp, q);
+    *reinterpret_cast<ulonglong2 *>(out + (size_t)s * seg_out + lo) = r;
+}
+
+inline dim3 ew_grid(int logN, int limbs, int segs) {
+    const size_t n = (size_t)1 << logN;
+    return dim3((unsigned)((n / 2 + NT - 1) / NT), (unsigned)limbs, (unsigned)segs);
+}
+inline dim3 pt_grid(int logN, int y, int z) {
+    const size_t n = (size_t)1 << logN;
+    return dim3((unsigned)((n + NT - 1) / NT), (unsigned)y, (unsigned)z);
+}
+inline void split(int logN, int &k1, int &C, int &ROWS) {
+    k1 = (logN + 1) / 2;
+    const int k2 = logN - k1;
+    C = std::min(1 << k2, TILE >> k1);
+    ROWS = std::min(1 << k1, TILE >> k2);
+}
+
+}  // namespace
+
+// ============================================================ wrappers =====
+void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    int k1, C, ROWS;
+    split(T.logN, k1, C, ROWS);
+    const int k2 = T.logN - k1;
+    hipLaunchKernelGGL(k_ntt_fwd_cols, dim3((1 << k2) / C, limbs, segs), dim3(NT), 0, st, data, seg, pmap, T.logN, k1,
+                       C, T);
+    hipLaunchKernelGGL(k_ntt_fwd_rows, dim3((1 << k1) / ROWS, limbs, segs), dim3(NT), 0, st, data, seg, pmap, T.logN,
+                       k1, ROWS, T);
+}
+void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    int k1, C, ROWS;
+    split(T.logN, k1, C, ROWS);
+    const int k2 = T.logN - k1;
+    hipLaunchKernelGGL(k_ntt_inv_rows, dim3((1 << k1) / ROWS, limbs, segs), dim3(NT), 0, st, data, seg, pmap, T.logN,
+                       k1, ROWS, T);
+    hipLaunchKernelGGL(k_ntt_inv_cols, dim3((1 << k2) / C, limbs, segs), dim3(NT), 0, st, data, seg, pmap, T.logN, k1,
+                       C, T);
+}
+
+void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+            hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_add, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, b, seg, mods, logN);
+}
+void ew_sub(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+            hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_sub, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, b, seg, mods, logN);
+}
+void ew_neg(u64 *out, const u64 *a, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_neg, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, seg, mods, logN);
+}
+void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+                   hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_mul_scalar, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, K, seg, mods, logN);
+}
+void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_add_scalar, ew_grid(logN, limbs, 1), dim3(NT), 0, st, out, a, K, (size_t)0, mods, logN);
+}
+void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, size_t seg, const Mod *mods,
+                  int logN, hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_mul_plain, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, p, seg, mods, logN);
+}
+void ew_tensor(u64 *d, const u64 *a, const u64 *b, int limbs, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0) return;
+    const size_t seg = (size_t)limbs << logN;
+    hipLaunchKernelGGL(k_tensor, ew_grid(logN, limbs, 1), dim3(NT), 0, st, d, a, b, seg, mods, logN);
+}
+void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
+                   size_t xseg, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0) return;
+    for (int base = 0; base < m || (m == 0 && base == 0); base += LIN_MAX) {
+        LinArgs A{};
+        A.m = std::min(LIN_MAX, m - base);
+        A.accumulate = base > 0;
+        A.xseg = xseg;
+        for (int i = 0; i < A.m; ++i) {
+            A.x[i] = xs[base + i];
+            A.K[i] = K[base + i];
+        }
+        hipLaunchKernelGGL(k_linear_sum, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, A, seg, mods, logN);
+        if (m == 0) break;
+    }
+}
+void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, size_t seg, int logN,
+                hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_permute, pt_grid(logN, limbs, segs), dim3(NT), 0, st, out, in, perm, seg, logN);
+}
+void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap, const Mod *mods, int logN,
+                      hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_signed_to_rns, pt_grid(logN, limbs, 1), dim3(NT), 0, st, out, coef, pmap, mods, logN);
+}
+void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0) return;
+    hipLaunchKernelGGL(k_reduce, ew_grid(logN, limbs, segs), dim3(NT), 0, st, x, seg, mods, logN);
+}
+
+void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, const int *pmap_ext,
+                   const u64 *tabs, const size_t *tab_off, const Mod *mods, int logN, hipStream_t st) {
+    const int W = ell + K;
+    ModUpArgs A{};
+    for (int j = 0; j < digits; ++j) {
+        const int lo = j * alpha, hi = std::min((j + 1) * alpha, ell), a = hi - lo;
+        const u64 *base = tabs + tab_off[j];
+        A.qhinv[j] = base;
+        A.qhinv_s[j] = base + a;
+        A.qhat[j] = base + 2 * a;
+        A.qhat_s[j] = base + 2 * a + (size_t)a * W;
+        A.lo[j] = lo;
+        A.hi[j] = hi;
+    }
+    hipLaunchKernelGGL(k_modup_convert, pt_grid(logN, (W + TCH - 1) / TCH, digits), dim3(NT), 0, st, ext, coef, W, A,
+                       pmap_ext, mods, logN);
+}
+void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
+              int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
+              hipStream_t st) {
+    (void)nq;
+    const int W = ell + K;
+    hipLaunchKernelGGL(k_ks_inner, pt_grid(logN, W, 1), dim3(NT), 0, st, acc, ext, dntt, key, ell, W, nall, alpha,
+                       digits, perm, pmap_ext, mods, logN);
+}
+void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
+                     const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s, const Mod *mods,
+                     int logN, hipStream_t st) {
+    hipLaunchKernelGGL(k_moddown_convert, pt_grid(logN, (ell + TCH - 1) / TCH, segs), dim3(NT), 0, st, conv, pc, ell,
+                       K, nq, seg_in, seg_out, phinv, phinv_s, phat, phat_s, mods, logN);
+}
+void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int add_segs, int ell, int segs,
+                    size_t seg_out, size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s,
+                    const Mod *mods, int logN, hipStream_t st) {
+    hipLaunchKernelGGL(k_moddown_finish, ew_grid(logN, ell, segs), dim3(NT), 0, st, out, acc, conv, add, add_segs,
+                       seg_out, seg_acc, seg_add, pinv, pinv_s, mods, logN);
+}
+void rescale_prep(u64 *tmp, const u64 *last, int ell, int segs, size_t seg_last, size_t seg_tmp, const Mod *mods,
+                  int logN, hipStream_t st) {
+    if (ell <= 1) return;
+    hipLaunchKernelGGL(k_rescale_prep, pt_grid(logN, ell - 1, segs), dim3(NT), 0, st, tmp, last, ell, seg_last,
+                       seg_tmp, mods, logN);
+}
+void rescale_finish(u64 *out, const u64 *in, const u64 *tmp, int ell, int segs, size_t seg_out, size_t seg_in,
+                    size_t seg_tmp, const u64 *qlinv, const u64 *qlinv_s, const Mod *mods, int logN,
+                    hipStream_t st) {
+    if (ell <= 1) return;
+    hipLaunchKernelGGL(k_rescale_finish, ew_grid(logN, ell - 1, segs), dim3(NT), 0, st, out, in, tmp, seg_out, seg_in,
+                       seg_tmp, qlinv, qlinv_s, mods, logN);
+}
+
+}  // namespace dev
+}  // namespace fhe

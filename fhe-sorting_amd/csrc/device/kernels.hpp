@@ -1,0 +1,94 @@
+// Launch wrappers for the gfx950 kernels (kernels.hip).  All pointers are
+// device pointers; every launch is asynchronous on `st`.
+//
+// Conventions:
+//   * a "poly array" is [segments][limbs][n] u64, segment stride `seg`
+//     elements; limb l of a Q-basis object uses prime index l.
+//   * a "prime map" (pmap) gives the prime index of each limb of a batch when
+//     the limbs are not Q primes 0..ell-1 (extended Q u P basis).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+#include "modmath.hpp"
+
+namespace fhe {
+namespace dev {
+
+struct NttTables {
+    const u64 *fwd, *fwd_s;    // [nprimes][n] psi^brev(k) and Shoup companions
+    const u64 *inv, *inv_s;    // [nprimes][n] psi^-brev(k)
+    const u64 *ninv, *ninv_s;  // [nprimes]
+    const Mod *mods;           // [nprimes]
+    int logN;
+};
+
+// forward / inverse negacyclic NTT of `limbs` limbs x `segs` segments
+void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
+                 hipStream_t st);
+void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
+                 hipStream_t st);
+
+// element-wise, Q basis (limb l <-> prime l); out may alias inputs
+void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+            hipStream_t st);
+void ew_sub(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+            hipStream_t st);
+void ew_neg(u64 *out, const u64 *a, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st);
+// out = a * (K mod q_l)   (K: signed integer constant, reduced in-kernel)
+void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+                   hipStream_t st);
+// out = a + (K mod q_l)   (one segment)
+void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, const Mod *mods, int logN, hipStream_t st);
+// out[s] = a[s] * p  (p: one [limbs][n] plaintext, Barrett)
+void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, size_t seg, const Mod *mods,
+                  int logN, hipStream_t st);
+// d0 = a0 b0, d1 = a0 b1 + a1 b0, d2 = a1 b1   (a, b: [2][limbs][n]; d: [3][limbs][n])
+void ew_tensor(u64 *d, const u64 *a, const u64 *b, int limbs, const Mod *mods, int logN, hipStream_t st);
+// out = sum_i (K_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride)
+void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
+                   size_t xseg, const Mod *mods, int logN, hipStream_t st);
+// out[l][k] = in[l][perm[k]]
+void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, size_t seg, int logN,
+                hipStream_t st);
+// out[l][k] = coef[k] mod q_{pmap[l]} (signed 64-bit coefficients)
+void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap, const Mod *mods, int logN,
+                      hipStream_t st);
+
+// ---------------------------------------------------------------- keyswitch
+struct ModUpTab {
+    const u64 *qhinv, *qhinv_s;  // [alpha]        (digit source primes)
+    const u64 *qhat, *qhat_s;    // [alpha][W]     (W = ell + K targets)
+};
+// ext[j][t][k] for every digit j and target t not in digit j (coefficient in, NTT NOT applied)
+void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, const int *pmap_ext,
+                   const u64 *tabs /* packed, see engine */, const size_t *tab_off, const Mod *mods, int logN,
+                   hipStream_t st);
+// acc0/acc1 [W][n]: sum_j ext_j * key_j   (own-digit limbs read from dntt)
+void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
+              int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
+              hipStream_t st);
+// conv[s][i][k] = sum_k' (pc[s][k'] * phinv_k') * phat[k'][i] mod q_i  for i < ell
+void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out,
+                     int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
+                     const Mod *mods, int logN, hipStream_t st);
+// out[s][i] = (acc[s][i] - conv[s][i]) * Pinv_i (+ add[s][i] for s < add_segs)
+void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int add_segs, int ell, int segs,
+                    size_t seg_out, size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s,
+                    const Mod *mods, int logN, hipStream_t st);
+
+// ------------------------------------------------------------------ rescale
+// tmp[s][i][k] = centred(last[s][k]) mod q_i for i < ell-1
+void rescale_prep(u64 *tmp, const u64 *last, int ell, int segs, size_t seg_last, size_t seg_tmp, const Mod *mods,
+                  int logN, hipStream_t st);
+// out[s][i] = (in[s][i] - tmp[s][i]) * qlinv_i
+void rescale_finish(u64 *out, const u64 *in, const u64 *tmp, int ell, int segs, size_t seg_out, size_t seg_in,
+                    size_t seg_tmp, const u64 *qlinv, const u64 *qlinv_s, const Mod *mods, int logN,
+                    hipStream_t st);
+
+// u64 all-reduce fix-up: x mod q_l per limb
+void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st);
+
+}  // namespace dev
+}  // namespace fhe

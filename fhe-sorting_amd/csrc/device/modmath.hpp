@@ -1,0 +1,68 @@
+// 64-bit modular arithmetic for gfx950 (CDNA4) — pure integer VALU work.
+//
+// Residues are u64 < q < 2^61.  CDNA4 has no 64x64->128 multiply; hipcc
+// lowers a*b (low half) to v_mul_lo_u32/v_mul_hi_u32/v_mad_u64_u32 sequences
+// and __umul64hi to the matching high-half sequence.  Two reduction flavours:
+//   * Shoup  (one operand is a precomputed constant w, w' = floor(w 2^64 / q)):
+//            1 mulhi + 2 mullo, valid for ANY a < 2^64, result < 2q before the
+//            final conditional subtraction.
+//   * Barrett (both operands variable, a,b < q): mu = floor(2^(2k)/q), k = bitlen(q).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace fhe {
+namespace dev {
+
+using u64 = uint64_t;
+
+struct Mod {
+    u64 q;
+    u64 mu;     // floor(2^(2k) / q)
+    int k;      // bit length of q
+    int pad;
+};
+
+__device__ __forceinline__ u64 mulhi(u64 a, u64 b) { return __umul64hi(a, b); }
+
+__device__ __forceinline__ u64 add_mod(u64 a, u64 b, u64 q) {
+    u64 r = a + b;
+    return r >= q ? r - q : r;
+}
+__device__ __forceinline__ u64 sub_mod(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
+
+__device__ __forceinline__ u64 mul_shoup(u64 a, u64 w, u64 wp, u64 q) {
+    u64 hi = mulhi(a, wp);
+    u64 r = a * w - hi * q;
+    return r >= q ? r - q : r;
+}
+// lazy Shoup: result in [0, 2q)
+__device__ __forceinline__ u64 mul_shoup_lazy(u64 a, u64 w, u64 wp, u64 q) {
+    return a * w - mulhi(a, wp) * q;
+}
+
+__device__ __forceinline__ u64 mul_barrett(u64 a, u64 b, const Mod &m) {
+    const u64 lo = a * b, hi = mulhi(a, b);
+    const u64 t = (hi << (65 - m.k)) | (lo >> (m.k - 1));       // z >> (k-1)
+    const u64 plo = t * m.mu, phi = mulhi(t, m.mu);
+    const u64 qh = (phi << (63 - m.k)) | (plo >> (m.k + 1));     // (t*mu) >> (k+1)
+    u64 r = lo - qh * m.q;
+    if (r >= m.q) r -= m.q;
+    if (r >= m.q) r -= m.q;
+    return r;
+}
+
+// reduce an arbitrary u64 (< 2^64) modulo q (q >= 2^32 assumed by callers)
+__device__ __forceinline__ u64 reduce64(u64 a, const Mod &m) {
+    // Barrett with z = a < 2^64 <= q^2 since q >= 2^32
+    const u64 t = (m.k - 1 >= 64) ? 0 : (a >> (m.k - 1));
+    const u64 plo = t * m.mu, phi = mulhi(t, m.mu);
+    const u64 qh = (phi << (63 - m.k)) | (plo >> (m.k + 1));
+    u64 r = a - qh * m.q;
+    if (r >= m.q) r -= m.q;
+    if (r >= m.q) r -= m.q;
+    return r;
+}
+
+}  // namespace dev
+}  // namespace fhe

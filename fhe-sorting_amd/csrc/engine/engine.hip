@@ -1,0 +1,853 @@
+// MI355X RNS-CKKS engine: device residency, tables, keys and op orchestration.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+
+#include "../device/kernels.hpp"
+#include "engine.hpp"
+
+#define HIP_OK(x)                                                                                     \
+    do {                                                                                              \
+        hipError_t _e = (x);                                                                          \
+        if (_e != hipSuccess)                                                                         \
+            throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " +    \
+                                     __FILE__ + ":" + std::to_string(__LINE__));                      \
+    } while (0)
+
+namespace fhe {
+
+using dev::Mod;
+
+// ================================================================ pool ====
+struct Pool {
+    std::mutex mu;
+    std::multimap<size_t, void *> free_list;
+    size_t live = 0, cached = 0;
+    int device = 0;
+    void *get(size_t bytes) {
+        bytes = (bytes + 255) & ~(size_t)255;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            auto it = free_list.find(bytes);
+            if (it != free_list.end()) {
+                void *p = it->second;
+                free_list.erase(it);
+                cached -= bytes;
+                live += bytes;
+                return p;
+            }
+        }
+        void *p = nullptr;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            trim();
+            HIP_OK(hipMalloc(&p, bytes));
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        live += bytes;
+        return p;
+    }
+    void put(void *p, size_t bytes) {
+        bytes = (bytes + 255) & ~(size_t)255;
+        std::lock_guard<std::mutex> lk(mu);
+        free_list.emplace(bytes, p);
+        live -= bytes;
+        cached += bytes;
+    }
+    void trim() {
+        std::lock_guard<std::mutex> lk(mu);
+        (void)hipDeviceSynchronize();
+        for (auto &kv : free_list) (void)hipFree(kv.second);
+        free_list.clear();
+        cached = 0;
+    }
+    ~Pool() {
+        for (auto &kv : free_list) (void)hipFree(kv.second);
+    }
+};
+
+struct DevMem {
+    std::shared_ptr<Pool> pool;
+    void *p = nullptr;
+    size_t bytes = 0;
+    ~DevMem() {
+        if (p) pool->put(p, bytes);
+    }
+};
+
+// ================================================================ impl ====
+struct Engine::Impl {
+    host::Params P;
+    host::LevelTables LT;
+    int device = 0;
+    hipStream_t st = nullptr;
+    std::shared_ptr<Pool> pool;
+    u64 seed = 0;
+    u64 enc_counter = 0;
+
+    // static device tables
+    std::vector<std::shared_ptr<DevMem>> keep;
+    Mod *mods = nullptr;
+    dev::NttTables T{};
+    int *extmap = nullptr;   // [nq+1][nq+K]
+    u64 *modup_tab = nullptr;  // packed ModUp tables
+    u64 *phinv = nullptr, *phinv_s = nullptr, *phat = nullptr, *phat_s = nullptr, *pinv = nullptr, *pinv_s = nullptr;
+    u64 *qlinv = nullptr, *qlinv_s = nullptr;
+
+    // keys
+    std::shared_ptr<DevMem> s_ntt, pk, relin;
+    std::map<u64, std::shared_ptr<DevMem>> rotkeys;
+    std::map<u64, std::shared_ptr<DevMem>> perms;
+    int key_digits = 0;
+
+    std::shared_ptr<DevMem> alloc(size_t bytes) {
+        auto m = std::make_shared<DevMem>();
+        m->pool = pool;
+        m->p = pool->get(bytes);
+        m->bytes = bytes;
+        return m;
+    }
+    template <class T>
+    T *upload_static(const std::vector<T> &v) {
+        auto m = alloc(std::max<size_t>(v.size(), 1) * sizeof(T));
+        HIP_OK(hipMemcpy(m->p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+        keep.push_back(m);
+        return static_cast<T *>(m->p);
+    }
+    size_t n() const { return P.n; }
+    size_t wmax() const { return P.nq() + P.K; }
+    const int *ext(size_t ell) const { return extmap + ell * wmax(); }
+    const uint32_t *perm(u64 g) {
+        auto it = perms.find(g);
+        if (it != perms.end()) return static_cast<const uint32_t *>(it->second->p);
+        auto v = host::automorphism_perm(P.logN, g);
+        auto m = alloc(v.size() * 4);
+        HIP_OK(hipMemcpyAsync(m->p, v.data(), v.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_OK(hipStreamSynchronize(st));
+        perms[g] = m;
+        return static_cast<const uint32_t *>(m->p);
+    }
+
+    // ------------------------------------------------------- key switch --
+    // ext[j][t] (NTT form) for all digits of d ([ell][n], NTT form)
+    std::shared_ptr<DevMem> modup(const u64 *d, size_t ell) {
+        const size_t nn = n(), K = (size_t)P.K, W = ell + K;
+        const int digits = P.digits_at(ell);
+        auto coef = alloc(ell * nn * 8);
+        u64 *c = static_cast<u64 *>(coef->p);
+        HIP_OK(hipMemcpyAsync(c, d, ell * nn * 8, hipMemcpyDeviceToDevice, st));
+        dev::ntt_inverse(c, (int)ell, 1, 0, nullptr, T, st);
+        auto extm = alloc((size_t)digits * W * nn * 8);
+        u64 *e = static_cast<u64 *>(extm->p);
+        dev::modup_convert(e, c, (int)ell, P.K, P.alpha, digits, ext(ell), modup_tab, LT.modup_off[ell].data(), mods,
+                           P.logN, st);
+        for (int j = 0; j < digits; ++j) {
+            const size_t lo = (size_t)j * P.alpha, hi = std::min(ell, (size_t)(j + 1) * P.alpha);
+            u64 *ej = e + (size_t)j * W * nn;
+            dev::ntt_forward(ej, (int)lo, 1, 0, ext(ell), T, st);
+            dev::ntt_forward(ej + hi * nn, (int)(W - hi), 1, 0, ext(ell) + hi, T, st);
+        }
+        return extm;
+    }
+    // out[2][ell][n] = ModDown(sum_j ext_j * key_j) (+ add for the first add_segs segments)
+    void ks_apply(const u64 *e, const u64 *d, size_t ell, const u64 *key, const uint32_t *pm, u64 *out,
+                  const u64 *add, int add_segs, size_t add_seg) {
+        const size_t nn = n(), K = (size_t)P.K, W = ell + K;
+        const int digits = P.digits_at(ell);
+        auto accm = alloc(2 * W * nn * 8);
+        u64 *acc = static_cast<u64 *>(accm->p);
+        dev::ks_inner(acc, e, d, key, (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha, digits, pm, ext(ell), mods,
+                      P.logN, st);
+        // ModDown of both accumulators
+        dev::ntt_inverse(acc + ell * nn, (int)K, 2, W * nn, ext(ell) + ell, T, st);
+        auto convm = alloc(2 * ell * nn * 8);
+        u64 *conv = static_cast<u64 *>(convm->p);
+        dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, 2, phinv, phinv_s,
+                             phat, phat_s, mods, P.logN, st);
+        dev::ntt_forward(conv, (int)ell, 2, ell * nn, nullptr, T, st);
+        dev::moddown_finish(out, acc, conv, add, add_segs, (int)ell, 2, ell * nn, W * nn, add_seg, pinv, pinv_s, mods,
+                            P.logN, st);
+    }
+    // out [2][ell-1][n] from in [2][ell][n] with input segment stride seg_in
+    void rescale(const u64 *in, size_t ell, size_t seg_in, u64 *out) {
+        const size_t nn = n();
+        auto lastm = alloc(2 * nn * 8);
+        u64 *last = static_cast<u64 *>(lastm->p);
+        HIP_OK(hipMemcpy2DAsync(last, nn * 8, in + (ell - 1) * nn, seg_in * 8, nn * 8, 2, hipMemcpyDeviceToDevice, st));
+        dev::ntt_inverse(last, 1, 2, nn, ext(ell) + (ell - 1), T, st);
+        auto tmpm = alloc(2 * (ell - 1) * nn * 8);
+        u64 *tmp = static_cast<u64 *>(tmpm->p);
+        dev::rescale_prep(tmp, last, (int)ell, 2, nn, (ell - 1) * nn, mods, P.logN, st);
+        dev::ntt_forward(tmp, (int)(ell - 1), 2, (ell - 1) * nn, nullptr, T, st);
+        dev::rescale_finish(out, in, tmp, (int)ell, 2, (ell - 1) * nn, seg_in, (ell - 1) * nn,
+                            qlinv + ell * P.nq(), qlinv_s + ell * P.nq(), mods, P.logN, st);
+    }
+};
+
+// ============================================================== engine ====
+Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int device, u64 seed)
+    : impl(new Impl) {
+    auto &I = *impl;
+    I.device = device;
+    I.seed = seed;
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipStreamCreateWithFlags(&I.st, hipStreamNonBlocking));
+    I.pool = std::make_shared<Pool>();
+    I.pool->device = device;
+    I.P = host::make_params(logN, L, scale_bits, first_bits, dnum);
+    I.LT = host::make_level_tables(I.P);
+    const size_t nall = I.P.nall(), n = I.P.n;
+    std::vector<Mod> mods(nall);
+    for (size_t i = 0; i < nall; ++i) {
+        host::Modulus m(I.P.primes[i]);
+        mods[i] = Mod{m.q, m.mu, m.k, 0};
+    }
+    I.mods = I.upload_static(mods);
+    std::vector<u64> fwd(nall * n), fwd_s(nall * n), inv(nall * n), inv_s(nall * n), ninv(nall), ninv_s(nall);
+    {
+        std::vector<std::thread> th;
+        const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        for (unsigned w = 0; w < nt; ++w)
+            th.emplace_back([&, w]() {
+                for (size_t i = w; i < nall; i += nt) {
+                    auto t = host::make_ntt_table(I.P.primes[i], logN);
+                    std::copy(t.fwd.begin(), t.fwd.end(), fwd.begin() + i * n);
+                    std::copy(t.fwd_s.begin(), t.fwd_s.end(), fwd_s.begin() + i * n);
+                    std::copy(t.inv.begin(), t.inv.end(), inv.begin() + i * n);
+                    std::copy(t.inv_s.begin(), t.inv_s.end(), inv_s.begin() + i * n);
+                    ninv[i] = t.ninv;
+                    ninv_s[i] = t.ninv_s;
+                }
+            });
+        for (auto &t : th) t.join();
+    }
+    I.T.fwd = I.upload_static(fwd);
+    I.T.fwd_s = I.upload_static(fwd_s);
+    I.T.inv = I.upload_static(inv);
+    I.T.inv_s = I.upload_static(inv_s);
+    I.T.ninv = I.upload_static(ninv);
+    I.T.ninv_s = I.upload_static(ninv_s);
+    I.T.mods = I.mods;
+    I.T.logN = logN;
+    I.extmap = I.upload_static(I.LT.extmap);
+    I.modup_tab = I.upload_static(I.LT.modup);
+    I.phinv = I.upload_static(I.LT.phinv);
+    I.phinv_s = I.upload_static(I.LT.phinv_s);
+    I.phat = I.upload_static(I.LT.phat);
+    I.phat_s = I.upload_static(I.LT.phat_s);
+    I.pinv = I.upload_static(I.LT.pinv);
+    I.pinv_s = I.upload_static(I.LT.pinv_s);
+    I.qlinv = I.upload_static(I.LT.qlinv);
+    I.qlinv_s = I.upload_static(I.LT.qlinv_s);
+    I.key_digits = I.P.digits_at(I.P.nq());
+}
+
+Engine::~Engine() {
+    if (impl && impl->st) {
+        (void)hipStreamSynchronize(impl->st);
+        impl->rotkeys.clear();
+        impl->perms.clear();
+        impl->relin.reset();
+        impl->pk.reset();
+        impl->s_ntt.reset();
+        impl->keep.clear();
+        (void)hipStreamDestroy(impl->st);
+    }
+}
+
+const host::Params &Engine::params() const { return impl->P; }
+size_t Engine::n() const { return impl->P.n; }
+double Engine::delta(int level) const { return impl->P.delta[level]; }
+void Engine::sync() { HIP_OK(hipStreamSynchronize(impl->st)); }
+Engine::DevBuf Engine::alloc_u64(size_t count) {
+    DevBuf b;
+    b.mem = impl->alloc(std::max<size_t>(count, 1) * 8);
+    b.ptr = static_cast<u64 *>(b.mem->p);
+    return b;
+}
+void Engine::h2d(u64 *dst, const u64 *src, size_t count) {
+    HIP_OK(hipMemcpyAsync(dst, src, count * 8, hipMemcpyHostToDevice, impl->st));
+    HIP_OK(hipStreamSynchronize(impl->st));
+}
+void Engine::d2h(u64 *dst, const u64 *src, size_t count) {
+    HIP_OK(hipMemcpyAsync(dst, src, count * 8, hipMemcpyDeviceToHost, impl->st));
+    HIP_OK(hipStreamSynchronize(impl->st));
+}
+void *Engine::stream_handle() { return impl->st; }
+int Engine::device() const { return impl->device; }
+
+CtPtr Engine::new_ct(int level, int slots, double scale, size_t limbs) {
+    auto c = std::make_shared<Ciphertext>();
+    c->mem = impl->alloc(2 * limbs * n() * 8);
+    c->data = static_cast<u64 *>(c->mem->p);
+    c->level = level;
+    c->slots = slots;
+    c->scale = scale;
+    c->limbs = limbs;
+    return c;
+}
+
+// ================================================================ keys ====
+namespace {
+std::vector<int64_t> sample_coeffs(u64 seed, u64 tag, size_t n, bool ternary) {
+    host::SplitMix64 g(seed, tag);
+    std::vector<int64_t> v(n);
+    for (size_t k = 0; k < n; ++k) v[k] = ternary ? host::sample_ternary(g) : host::sample_cbd(g);
+    return v;
+}
+}  // namespace
+
+void Engine::keygen() {
+    auto &I = *impl;
+    const size_t n = I.n(), nall = I.P.nall(), nq = I.P.nq();
+    // secret over every prime
+    auto s = sample_coeffs(I.seed, host::tags::secret, n, true);
+    auto coef = I.alloc(n * 8);
+    HIP_OK(hipMemcpyAsync(coef->p, s.data(), n * 8, hipMemcpyHostToDevice, I.st));
+    I.s_ntt = I.alloc(nall * n * 8);
+    u64 *S = static_cast<u64 *>(I.s_ntt->p);
+    dev::ew_signed_to_rns(S, static_cast<int64_t *>(coef->p), (int)nall, nullptr, I.mods, I.P.logN, I.st);
+    dev::ntt_forward(S, (int)nall, 1, 0, nullptr, I.T, I.st);
+    // public key
+    std::vector<u64> a(nq * n);
+    {
+        host::SplitMix64 g(I.seed, host::tags::pk_a);
+        for (size_t l = 0; l < nq; ++l)
+            for (size_t k = 0; k < n; ++k) a[l * n + k] = host::sample_uniform_mod(g, I.P.primes[l]);
+    }
+    auto e = sample_coeffs(I.seed, host::tags::pk_e, n, false);
+    I.pk = I.alloc(2 * nq * n * 8);
+    u64 *pk = static_cast<u64 *>(I.pk->p);
+    HIP_OK(hipMemcpyAsync(pk + nq * n, a.data(), nq * n * 8, hipMemcpyHostToDevice, I.st));
+    auto ec = I.alloc(n * 8);
+    HIP_OK(hipMemcpyAsync(ec->p, e.data(), n * 8, hipMemcpyHostToDevice, I.st));
+    auto tmp = I.alloc(nq * n * 8);
+    u64 *t = static_cast<u64 *>(tmp->p);
+    dev::ew_signed_to_rns(pk, static_cast<int64_t *>(ec->p), (int)nq, nullptr, I.mods, I.P.logN, I.st);
+    dev::ntt_forward(pk, (int)nq, 1, 0, nullptr, I.T, I.st);
+    dev::ew_mul_plain(t, pk + nq * n, S, (int)nq, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_sub(pk, pk, t, (int)nq, 1, 0, I.mods, I.P.logN, I.st);
+    HIP_OK(hipStreamSynchronize(I.st));
+    // relinearisation key: s' = s^2
+    auto s2 = I.alloc(nq * n * 8);
+    dev::ew_mul_plain(static_cast<u64 *>(s2->p), S, S, (int)nq, 1, 0, I.mods, I.P.logN, I.st);
+    I.relin = I.alloc((size_t)I.key_digits * 2 * nall * n * 8);
+    // (key material generated by the shared helper below)
+    extern void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out);
+    gen_switch_key_impl(I, static_cast<u64 *>(s2->p), 0, static_cast<u64 *>(I.relin->p));
+    HIP_OK(hipStreamSynchronize(I.st));
+}
+
+void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out) {
+    const size_t n = I.n(), nall = I.P.nall(), nq = I.P.nq();
+    const u64 *S = static_cast<const u64 *>(I.s_ntt->p);
+    const int digits = I.key_digits;
+    // P mod q_i
+    std::vector<int64_t> Pmod(nq);
+    for (size_t i = 0; i < nq; ++i) {
+        host::Modulus mi(I.P.primes[i]);
+        u64 acc = 1 % mi.q;
+        for (int k = 0; k < I.P.K; ++k) acc = host::mulmod(acc, I.P.primes[nq + k] % mi.q, mi);
+        Pmod[i] = (int64_t)acc;
+    }
+    // sample every digit's (a_j, e_j) on host threads, then combine on the GPU
+    std::vector<std::vector<u64>> A(digits);
+    std::vector<std::vector<int64_t>> E(digits);
+    {
+        std::vector<std::thread> th;
+        for (int j = 0; j < digits; ++j)
+            th.emplace_back([&, j]() {
+                host::SplitMix64 ga(I.seed, host::tags::swk_a(kid, j));
+                A[j].resize(nall * n);
+                for (size_t l = 0; l < nall; ++l)
+                    for (size_t k = 0; k < n; ++k) A[j][l * n + k] = host::sample_uniform_mod(ga, I.P.primes[l]);
+                host::SplitMix64 ge(I.seed, host::tags::swk_e(kid, j));
+                E[j].resize(n);
+                for (size_t k = 0; k < n; ++k) E[j][k] = host::sample_cbd(ge);
+            });
+        for (auto &t : th) t.join();
+    }
+    auto ec = I.alloc(n * 8);
+    auto tmpm = I.alloc(nall * n * 8);
+    u64 *tmp = static_cast<u64 *>(tmpm->p);
+    for (int j = 0; j < digits; ++j) {
+        u64 *bj = out + ((size_t)j * 2 + 0) * nall * n;
+        u64 *aj = out + ((size_t)j * 2 + 1) * nall * n;
+        HIP_OK(hipMemcpyAsync(aj, A[j].data(), nall * n * 8, hipMemcpyHostToDevice, I.st));
+        HIP_OK(hipMemcpyAsync(ec->p, E[j].data(), n * 8, hipMemcpyHostToDevice, I.st));
+        dev::ew_signed_to_rns(bj, static_cast<int64_t *>(ec->p), (int)nall, nullptr, I.mods, I.P.logN, I.st);
+        dev::ntt_forward(bj, (int)nall, 1, 0, nullptr, I.T, I.st);
+        dev::ew_mul_plain(tmp, aj, S, (int)nall, 1, 0, I.mods, I.P.logN, I.st);
+        dev::ew_sub(bj, bj, tmp, (int)nall, 1, 0, I.mods, I.P.logN, I.st);
+        const size_t lo = (size_t)j * I.P.alpha, hi = std::min(nq, (size_t)(j + 1) * I.P.alpha);
+        for (size_t i = lo; i < hi; ++i) {
+            dev::ew_mul_scalar(tmp, sp + i * n, Pmod[i], 1, 1, 0, I.mods + i, I.P.logN, I.st);
+            dev::ew_add(bj + i * n, bj + i * n, tmp, 1, 1, 0, I.mods + i, I.P.logN, I.st);
+        }
+        HIP_OK(hipStreamSynchronize(I.st));  // host buffers A[j], E[j] go out of scope after the loop
+    }
+}
+
+void Engine::gen_rotation_keys(const std::vector<int> &rot) {
+    auto &I = *impl;
+    const size_t n = I.n(), nq = I.P.nq(), nall = I.P.nall();
+    if (!I.s_ntt) throw std::runtime_error("gen_rotation_keys: no secret key (call keygen)");
+    auto sp = I.alloc(nq * n * 8);
+    for (int k : rot) {
+        const u64 g = host::galois_for_rotation(I.P.logN, k);
+        if (g == 1 || I.rotkeys.count(g)) continue;
+        dev::ew_permute(static_cast<u64 *>(sp->p), static_cast<const u64 *>(I.s_ntt->p), I.perm(g), (int)nq, 1, 0,
+                        I.P.logN, I.st);
+        auto key = I.alloc((size_t)I.key_digits * 2 * nall * n * 8);
+        gen_switch_key_impl(I, static_cast<u64 *>(sp->p), g, static_cast<u64 *>(key->p));
+        I.rotkeys[g] = key;
+    }
+    HIP_OK(hipStreamSynchronize(I.st));
+}
+
+void Engine::load_secret(const u64 *s) {
+    auto &I = *impl;
+    const size_t bytes = I.P.nall() * I.n() * 8;
+    I.s_ntt = I.alloc(bytes);
+    HIP_OK(hipMemcpy(I.s_ntt->p, s, bytes, hipMemcpyHostToDevice));
+}
+void Engine::load_public(const u64 *pk) {
+    auto &I = *impl;
+    const size_t bytes = 2 * I.P.nq() * I.n() * 8;
+    I.pk = I.alloc(bytes);
+    HIP_OK(hipMemcpy(I.pk->p, pk, bytes, hipMemcpyHostToDevice));
+}
+void Engine::load_relin(const u64 *key) {
+    auto &I = *impl;
+    const size_t bytes = (size_t)I.key_digits * 2 * I.P.nall() * I.n() * 8;
+    I.relin = I.alloc(bytes);
+    HIP_OK(hipMemcpy(I.relin->p, key, bytes, hipMemcpyHostToDevice));
+}
+void Engine::load_rotation(long k, const u64 *key) {
+    auto &I = *impl;
+    const size_t bytes = (size_t)I.key_digits * 2 * I.P.nall() * I.n() * 8;
+    const u64 g = host::galois_for_rotation(I.P.logN, k);
+    auto m = I.alloc(bytes);
+    HIP_OK(hipMemcpy(m->p, key, bytes, hipMemcpyHostToDevice));
+    I.rotkeys[g] = m;
+}
+bool Engine::has_rotation_key(long k) const {
+    return impl->rotkeys.count(host::galois_for_rotation(impl->P.logN, k)) > 0;
+}
+size_t Engine::key_bytes() const {
+    size_t b = impl->relin ? impl->relin->bytes : 0;
+    for (auto &kv : impl->rotkeys) b += kv.second->bytes;
+    return b;
+}
+
+// ==================================================== encode / encrypt ====
+PtPtr Engine::encode(const std::vector<double> &v, int slots, int level) {
+    auto &I = *impl;
+    const size_t n = I.n(), ell = I.P.limbs_at(level);
+    auto coef = host::encode_coeffs(v, n, slots, I.P.delta[level]);
+    auto cm = I.alloc(n * 8);
+    HIP_OK(hipMemcpyAsync(cm->p, coef.data(), n * 8, hipMemcpyHostToDevice, I.st));
+    auto pt = std::make_shared<Plaintext>();
+    pt->mem = I.alloc(ell * n * 8);
+    pt->data = static_cast<u64 *>(pt->mem->p);
+    pt->level = level;
+    pt->slots = slots;
+    pt->scale = I.P.delta[level];
+    pt->limbs = ell;
+    dev::ew_signed_to_rns(pt->data, static_cast<int64_t *>(cm->p), (int)ell, nullptr, I.mods, I.P.logN, I.st);
+    dev::ntt_forward(pt->data, (int)ell, 1, 0, nullptr, I.T, I.st);
+    HIP_OK(hipStreamSynchronize(I.st));  // `coef` (pageable host) must outlive the copy
+    return pt;
+}
+
+CtPtr Engine::encrypt_pt(const Plaintext &pt) {
+    auto &I = *impl;
+    if (!I.pk) throw std::runtime_error("encrypt: no public key");
+    const size_t n = I.n(), nq = I.P.nq(), ell = pt.limbs;
+    const u64 c = I.enc_counter++;
+    std::vector<int64_t> smp(3 * n);
+    {
+        auto v = sample_coeffs(I.seed, host::tags::enc_v(c), n, true);
+        auto e0 = sample_coeffs(I.seed, host::tags::enc_e0(c), n, false);
+        auto e1 = sample_coeffs(I.seed, host::tags::enc_e1(c), n, false);
+        std::copy(v.begin(), v.end(), smp.begin());
+        std::copy(e0.begin(), e0.end(), smp.begin() + n);
+        std::copy(e1.begin(), e1.end(), smp.begin() + 2 * n);
+    }
+    auto sm = I.alloc(3 * n * 8);
+    HIP_OK(hipMemcpyAsync(sm->p, smp.data(), 3 * n * 8, hipMemcpyHostToDevice, I.st));
+    auto rm = I.alloc(3 * ell * n * 8);
+    u64 *r = static_cast<u64 *>(rm->p);
+    for (int i = 0; i < 3; ++i)
+        dev::ew_signed_to_rns(r + i * ell * n, static_cast<int64_t *>(sm->p) + i * n, (int)ell, nullptr, I.mods,
+                              I.P.logN, I.st);
+    dev::ntt_forward(r, (int)ell, 3, ell * n, nullptr, I.T, I.st);
+    auto ct = new_ct(pt.level, pt.slots, pt.scale, ell);
+    const u64 *pk = static_cast<const u64 *>(I.pk->p);
+    u64 *c0 = ct->data, *c1 = ct->data + ell * n;
+    dev::ew_mul_plain(c0, r, pk, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_add(c0, c0, r + ell * n, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_add(c0, c0, pt.data, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_mul_plain(c1, r, pk + nq * n, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_add(c1, c1, r + 2 * ell * n, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
+    HIP_OK(hipStreamSynchronize(I.st));
+    return ct;
+}
+
+CtPtr Engine::encrypt(const std::vector<double> &v, int slots, int level) {
+    return encrypt_pt(*encode(v, slots, level));
+}
+
+std::vector<double> Engine::decrypt(const Ciphertext &ct) {
+    auto &I = *impl;
+    if (!I.s_ntt) throw std::runtime_error("decrypt: no secret key");
+    const size_t n = I.n();
+    auto mm = I.alloc(n * 8);
+    u64 *m = static_cast<u64 *>(mm->p);
+    dev::ew_mul_plain(m, ct.data + ct.limbs * n, static_cast<const u64 *>(I.s_ntt->p), 1, 1, 0, I.mods, I.P.logN,
+                      I.st);
+    dev::ew_add(m, m, ct.data, 1, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ntt_inverse(m, 1, 1, 0, nullptr, I.T, I.st);
+    std::vector<u64> h(n);
+    HIP_OK(hipMemcpyAsync(h.data(), m, n * 8, hipMemcpyDeviceToHost, I.st));
+    HIP_OK(hipStreamSynchronize(I.st));
+    return host::decode_coeffs(h.data(), n, I.P.primes[0], ct.slots, ct.scale);
+}
+
+CtPtr Engine::upload(const u64 *h, size_t limbs, int level, int slots, double scale) {
+    auto ct = new_ct(level, slots, scale, limbs);
+    HIP_OK(hipMemcpyAsync(ct->data, h, 2 * limbs * n() * 8, hipMemcpyHostToDevice, impl->st));
+    HIP_OK(hipStreamSynchronize(impl->st));
+    return ct;
+}
+void Engine::download(const Ciphertext &ct, u64 *h) {
+    HIP_OK(hipMemcpyAsync(h, ct.data, 2 * ct.limbs * n() * 8, hipMemcpyDeviceToHost, impl->st));
+    HIP_OK(hipStreamSynchronize(impl->st));
+}
+PtPtr Engine::upload_pt(const u64 *h, size_t limbs, int level, int slots, double scale) {
+    auto pt = std::make_shared<Plaintext>();
+    pt->mem = impl->alloc(limbs * n() * 8);
+    pt->data = static_cast<u64 *>(pt->mem->p);
+    pt->level = level;
+    pt->slots = slots;
+    pt->scale = scale;
+    pt->limbs = limbs;
+    HIP_OK(hipMemcpyAsync(pt->data, h, limbs * n() * 8, hipMemcpyHostToDevice, impl->st));
+    HIP_OK(hipStreamSynchronize(impl->st));
+    return pt;
+}
+
+// ================================================================= ops ====
+#define LOGN impl->P.logN
+#define MODS impl->mods
+#define ST impl->st
+
+CtPtr Engine::clone(const Ciphertext &a) {
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs);
+    HIP_OK(hipMemcpyAsync(r->data, a.data, 2 * a.limbs * n() * 8, hipMemcpyDeviceToDevice, ST));
+    return r;
+}
+
+CtPtr Engine::drop_to(const Ciphertext &a, int level) {
+    if (level < a.level) throw std::invalid_argument("drop_to: cannot raise level");
+    const size_t ell = impl->P.limbs_at(level), nn = n();
+    auto r = new_ct(level, a.slots, a.scale, ell);
+    HIP_OK(hipMemcpy2DAsync(r->data, ell * nn * 8, a.data, a.limbs * nn * 8, ell * nn * 8, 2,
+                            hipMemcpyDeviceToDevice, ST));
+    return r;
+}
+
+void Engine::match_levels(CtPtr &a, CtPtr &b) {
+    if (a->level < b->level)
+        a = level_adjust(*a, b->level);
+    else if (b->level < a->level)
+        b = level_adjust(*b, a->level);
+}
+
+CtPtr Engine::add(const Ciphertext &a0, const Ciphertext &b0) {
+    auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
+    match_levels(a, b);
+    auto r = new_ct(a->level, a->slots, a->scale, a->limbs);
+    dev::ew_add(r->data, a->data, b->data, (int)a->limbs, 2, a->limbs * n(), MODS, LOGN, ST);
+    return r;
+}
+CtPtr Engine::sub(const Ciphertext &a0, const Ciphertext &b0) {
+    auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
+    match_levels(a, b);
+    auto r = new_ct(a->level, a->slots, a->scale, a->limbs);
+    dev::ew_sub(r->data, a->data, b->data, (int)a->limbs, 2, a->limbs * n(), MODS, LOGN, ST);
+    return r;
+}
+void Engine::add_inplace(CtPtr &acc, const Ciphertext &b) {
+    if (!acc) {
+        acc = clone(b);
+        return;
+    }
+    if (acc->level == b.level && acc.use_count() == 1) {
+        dev::ew_add(acc->data, acc->data, b.data, (int)b.limbs, 2, b.limbs * n(), MODS, LOGN, ST);
+        return;
+    }
+    acc = add(*acc, b);
+}
+CtPtr Engine::negate(const Ciphertext &a) {
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs);
+    dev::ew_neg(r->data, a.data, (int)a.limbs, 2, a.limbs * n(), MODS, LOGN, ST);
+    return r;
+}
+CtPtr Engine::add_plain(const Ciphertext &a, const Plaintext &p) {
+    if (p.level != a.level) throw std::invalid_argument("add_plain: level mismatch");
+    auto r = clone(a);
+    dev::ew_add(r->data, r->data, p.data, (int)a.limbs, 1, 0, MODS, LOGN, ST);
+    return r;
+}
+CtPtr Engine::sub_plain(const Ciphertext &a, const Plaintext &p) {
+    if (p.level != a.level) throw std::invalid_argument("sub_plain: level mismatch");
+    auto r = clone(a);
+    dev::ew_sub(r->data, r->data, p.data, (int)a.limbs, 1, 0, MODS, LOGN, ST);
+    return r;
+}
+CtPtr Engine::plain_sub(const Plaintext &p, const Ciphertext &a) {
+    if (p.level != a.level) throw std::invalid_argument("plain_sub: level mismatch");
+    auto r = negate(a);
+    dev::ew_add(r->data, r->data, p.data, (int)a.limbs, 1, 0, MODS, LOGN, ST);
+    return r;
+}
+CtPtr Engine::add_const(const Ciphertext &a, double c) {
+    auto r = clone(a);
+    const i64 K = host::const_at_scale(c, a.scale);
+    dev::ew_add_scalar(r->data, r->data, K, (int)a.limbs, MODS, LOGN, ST);
+    return r;
+}
+CtPtr Engine::mul_int(const Ciphertext &a, i64 K) {
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs);
+    dev::ew_mul_scalar(r->data, a.data, K, (int)a.limbs, 2, a.limbs * n(), MODS, LOGN, ST);
+    return r;
+}
+CtPtr Engine::mul_const_to(const Ciphertext &a, double c, int target) {
+    auto &I = *impl;
+    if (target <= a.level) throw std::invalid_argument("mul_const_to: target must exceed level");
+    if (target > I.P.L) throw std::runtime_error("mul_const_to: no levels left");
+    ctr.constmult++;
+    ctr.rescale++;
+    const size_t nn = n(), ell = I.P.limbs_at(target - 1);
+    const i64 K = host::const_to_target(c, I.P.delta[target], I.P.primes[I.P.L - target + 1], a.scale);
+    auto tm = I.alloc(2 * ell * nn * 8);
+    u64 *t = static_cast<u64 *>(tm->p);
+    // multiply the (dropped) input: each segment is read with the input's own stride
+    dev::ew_mul_scalar(t, a.data, K, (int)ell, 1, 0, MODS, LOGN, ST);
+    dev::ew_mul_scalar(t + ell * nn, a.data + a.limbs * nn, K, (int)ell, 1, 0, MODS, LOGN, ST);
+    auto r = new_ct(target, a.slots, I.P.delta[target], ell - 1);
+    I.rescale(t, ell, ell * nn, r->data);
+    return r;
+}
+CtPtr Engine::mul_const(const Ciphertext &a, double c) { return mul_const_to(a, c, a.level + 1); }
+CtPtr Engine::level_adjust(const Ciphertext &a, int target) {
+    if (target == a.level) return clone(a);
+    return mul_const_to(a, 1.0, target);
+}
+CtPtr Engine::rescale(const Ciphertext &a) {
+    auto &I = *impl;
+    if (a.level >= I.P.L) throw std::runtime_error("rescale: no levels left");
+    ctr.rescale++;
+    auto r = new_ct(a.level + 1, a.slots, a.scale / (double)I.P.primes[a.limbs - 1], a.limbs - 1);
+    I.rescale(a.data, a.limbs, a.limbs * n(), r->data);
+    return r;
+}
+CtPtr Engine::mul_plain(const Ciphertext &a, const Plaintext &p) {
+    auto &I = *impl;
+    if (p.level != a.level) throw std::invalid_argument("mul_plain: level mismatch");
+    if (a.level >= I.P.L) throw std::runtime_error("mul_plain: no levels left");
+    ctr.ptmult++;
+    ctr.rescale++;
+    const size_t nn = n(), ell = a.limbs;
+    auto tm = I.alloc(2 * ell * nn * 8);
+    u64 *t = static_cast<u64 *>(tm->p);
+    dev::ew_mul_plain(t, a.data, p.data, (int)ell, 2, ell * nn, MODS, LOGN, ST);
+    auto r = new_ct(a.level + 1, a.slots, I.P.delta[a.level + 1], ell - 1);
+    I.rescale(t, ell, ell * nn, r->data);
+    return r;
+}
+
+CtPtr Engine::mul(const Ciphertext &a0, const Ciphertext &b0) {
+    auto &I = *impl;
+    auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
+    match_levels(a, b);
+    if (a->level >= I.P.L) throw std::runtime_error("mul: no levels left");
+    if (!I.relin) throw std::runtime_error("mul: no relinearisation key");
+    ctr.hmult++;
+    ctr.keyswitch++;
+    ctr.rescale++;
+    const size_t nn = n(), ell = a->limbs;
+    auto dm = I.alloc(3 * ell * nn * 8);
+    u64 *d = static_cast<u64 *>(dm->p);
+    dev::ew_tensor(d, a->data, b->data, (int)ell, MODS, LOGN, ST);
+    auto extm = I.modup(d + 2 * ell * nn, ell);
+    auto tm = I.alloc(2 * ell * nn * 8);
+    u64 *t = static_cast<u64 *>(tm->p);
+    I.ks_apply(static_cast<u64 *>(extm->p), d + 2 * ell * nn, ell, static_cast<u64 *>(I.relin->p), nullptr, t, d, 2,
+               ell * nn);
+    auto r = new_ct(a->level + 1, a->slots, I.P.delta[a->level + 1], ell - 1);
+    I.rescale(t, ell, ell * nn, r->data);
+    return r;
+}
+CtPtr Engine::square(const Ciphertext &a) { return mul(a, a); }
+
+std::vector<CtPtr> Engine::rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks) {
+    auto &I = *impl;
+    const size_t nn = n(), ell = a.limbs;
+    std::vector<CtPtr> outs;
+    std::shared_ptr<DevMem> extm;
+    for (long k : ks) {
+        const u64 g = host::galois_for_rotation(I.P.logN, k);
+        if (g == 1) {
+            outs.push_back(clone(a));
+            continue;
+        }
+        auto it = I.rotkeys.find(g);
+        if (it == I.rotkeys.end()) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
+        if (!extm) extm = I.modup(a.data + ell * nn, ell);
+        ctr.keyswitch++;
+        ctr.rotations++;
+        const uint32_t *pm = I.perm(g);
+        auto c0m = I.alloc(ell * nn * 8);
+        u64 *c0p = static_cast<u64 *>(c0m->p);
+        dev::ew_permute(c0p, a.data, pm, (int)ell, 1, 0, LOGN, ST);
+        auto r = new_ct(a.level, a.slots, a.scale, ell);
+        I.ks_apply(static_cast<u64 *>(extm->p), a.data + ell * nn, ell, static_cast<u64 *>(it->second->p), pm,
+                   r->data, c0p, 1, ell * nn);
+        outs.push_back(r);
+    }
+    return outs;
+}
+CtPtr Engine::rotate(const Ciphertext &a, long k) { return rotate_hoisted(a, {k})[0]; }
+
+CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c, int target) {
+    auto &I = *impl;
+    if (target > I.P.L) throw std::runtime_error("linear_sum_to: no levels left");
+    const size_t nn = n(), ell = I.P.limbs_at(target - 1);
+    const double qd = (double)I.P.primes[I.P.L - target + 1];
+    auto tm = I.alloc(2 * ell * nn * 8);
+    u64 *t = static_cast<u64 *>(tm->p);
+    std::vector<const u64 *> ptr0, ptr1;
+    std::vector<int64_t> K;
+    // group inputs by their limb count (segment stride) so each launch has one xseg
+    std::map<size_t, std::vector<size_t>> by_limbs;
+    for (size_t i = 0; i < xs.size(); ++i) {
+        if (xs[i]->level > target - 1) throw std::invalid_argument("linear_sum_to: input level too high");
+        by_limbs[xs[i]->limbs].push_back(i);
+    }
+    ctr.constmult += xs.size();
+    bool first = true;
+    for (auto &kv : by_limbs) {
+        std::vector<const u64 *> p;
+        std::vector<int64_t> k;
+        for (size_t i : kv.second) {
+            p.push_back(xs[i]->data);
+            k.push_back(host::const_to_target(c[i], I.P.delta[target], (u64)qd, xs[i]->scale));
+        }
+        // accumulate: first group writes, later groups add
+        if (first) {
+            dev::ew_linear_sum(t, p.data(), k.data(), (int)p.size(), (int)ell, 2, ell * nn, kv.first * nn, MODS, LOGN,
+                               ST);
+            first = false;
+        } else {
+            auto sm = I.alloc(2 * ell * nn * 8);
+            u64 *s = static_cast<u64 *>(sm->p);
+            dev::ew_linear_sum(s, p.data(), k.data(), (int)p.size(), (int)ell, 2, ell * nn, kv.first * nn, MODS, LOGN,
+                               ST);
+            dev::ew_add(t, t, s, (int)ell, 2, ell * nn, MODS, LOGN, ST);
+        }
+    }
+    if (first) HIP_OK(hipMemsetAsync(t, 0, 2 * ell * nn * 8, ST));
+    ctr.rescale++;
+    auto r = new_ct(target, xs.empty() ? 0 : xs[0]->slots, I.P.delta[target], ell - 1);
+    I.rescale(t, ell, ell * nn, r->data);
+    return r;
+}
+
+CtPtr Engine::trivial_const(double c, int level, int slots) {
+    auto r = zero_like(level, slots);
+    const i64 K = host::const_at_scale(c, impl->P.delta[level]);
+    dev::ew_add_scalar(r->data, r->data, K, (int)r->limbs, MODS, LOGN, ST);
+    return r;
+}
+CtPtr Engine::zero_like(int level, int slots) {
+    const size_t ell = impl->P.limbs_at(level);
+    auto r = new_ct(level, slots, impl->P.delta[level], ell);
+    HIP_OK(hipMemsetAsync(r->data, 0, 2 * ell * n() * 8, ST));
+    return r;
+}
+void Engine::reduce_after_allreduce(Ciphertext &ct) {
+    dev::ew_reduce(ct.data, (int)ct.limbs, 2, ct.limbs * n(), MODS, LOGN, ST);
+}
+
+// =================================================== kernel-level (tests) ==
+void Engine::ntt_host(u64 *data, int prime_index, int limbs, bool inverse) {
+    auto &I = *impl;
+    const size_t nn = n();
+    auto m = I.alloc((size_t)limbs * nn * 8);
+    u64 *d = static_cast<u64 *>(m->p);
+    std::vector<int> pm(limbs);
+    for (int i = 0; i < limbs; ++i) pm[i] = prime_index + i;
+    auto pmm = I.alloc(limbs * sizeof(int));
+    HIP_OK(hipMemcpyAsync(pmm->p, pm.data(), limbs * sizeof(int), hipMemcpyHostToDevice, ST));
+    HIP_OK(hipMemcpyAsync(d, data, (size_t)limbs * nn * 8, hipMemcpyHostToDevice, ST));
+    if (inverse)
+        dev::ntt_inverse(d, limbs, 1, 0, static_cast<int *>(pmm->p), I.T, ST);
+    else
+        dev::ntt_forward(d, limbs, 1, 0, static_cast<int *>(pmm->p), I.T, ST);
+    HIP_OK(hipMemcpyAsync(data, d, (size_t)limbs * nn * 8, hipMemcpyDeviceToHost, ST));
+    HIP_OK(hipStreamSynchronize(ST));
+}
+void Engine::modup_host(const u64 *d, size_t ell, u64 *ext) {
+    auto &I = *impl;
+    const size_t nn = n(), W = ell + I.P.K;
+    const int digits = I.P.digits_at(ell);
+    auto dm = I.alloc(ell * nn * 8);
+    HIP_OK(hipMemcpyAsync(dm->p, d, ell * nn * 8, hipMemcpyHostToDevice, ST));
+    auto e = I.modup(static_cast<u64 *>(dm->p), ell);
+    // own-digit limbs are not materialised on the device: fill them from d
+    u64 *ep = static_cast<u64 *>(e->p);
+    for (int j = 0; j < digits; ++j) {
+        const size_t lo = (size_t)j * I.P.alpha, hi = std::min(ell, (size_t)(j + 1) * I.P.alpha);
+        HIP_OK(hipMemcpyAsync(ep + ((size_t)j * W + lo) * nn, static_cast<u64 *>(dm->p) + lo * nn,
+                              (hi - lo) * nn * 8, hipMemcpyDeviceToDevice, ST));
+    }
+    HIP_OK(hipMemcpyAsync(ext, ep, (size_t)digits * W * nn * 8, hipMemcpyDeviceToHost, ST));
+    HIP_OK(hipStreamSynchronize(ST));
+}
+void Engine::moddown_host(const u64 *in, size_t ell, u64 *out) {
+    auto &I = *impl;
+    const size_t nn = n(), K = I.P.K, W = ell + K;
+    auto im = I.alloc(W * nn * 8);
+    u64 *x = static_cast<u64 *>(im->p);
+    HIP_OK(hipMemcpyAsync(x, in, W * nn * 8, hipMemcpyHostToDevice, ST));
+    dev::ntt_inverse(x + ell * nn, (int)K, 1, 0, I.ext(ell) + ell, I.T, ST);
+    auto cm = I.alloc(ell * nn * 8);
+    u64 *conv = static_cast<u64 *>(cm->p);
+    dev::moddown_convert(conv, x + ell * nn, (int)ell, (int)K, (int)I.P.nq(), W * nn, ell * nn, 1, I.phinv,
+                         I.phinv_s, I.phat, I.phat_s, MODS, LOGN, ST);
+    dev::ntt_forward(conv, (int)ell, 1, 0, nullptr, I.T, ST);
+    auto om = I.alloc(ell * nn * 8);
+    dev::moddown_finish(static_cast<u64 *>(om->p), x, conv, nullptr, 0, (int)ell, 1, ell * nn, W * nn, 0, I.pinv,
+                        I.pinv_s, MODS, LOGN, ST);
+    HIP_OK(hipMemcpyAsync(out, om->p, ell * nn * 8, hipMemcpyDeviceToHost, ST));
+    HIP_OK(hipStreamSynchronize(ST));
+}
+void Engine::automorph_host(const u64 *in, size_t limbs, u64 g, u64 *out) {
+    auto &I = *impl;
+    const size_t nn = n();
+    auto im = I.alloc(limbs * nn * 8), om = I.alloc(limbs * nn * 8);
+    HIP_OK(hipMemcpyAsync(im->p, in, limbs * nn * 8, hipMemcpyHostToDevice, ST));
+    dev::ew_permute(static_cast<u64 *>(om->p), static_cast<u64 *>(im->p), I.perm(g), (int)limbs, 1, 0, LOGN, ST);
+    HIP_OK(hipMemcpyAsync(out, om->p, limbs * nn * 8, hipMemcpyDeviceToHost, ST));
+    HIP_OK(hipStreamSynchronize(ST));
+}
+
+}  // namespace fhe

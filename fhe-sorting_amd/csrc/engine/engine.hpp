@@ -1,0 +1,147 @@
+// MI355X RNS-CKKS ciphertext-op engine — host-side C++ interface.
+//
+// One Engine per GPU (one process per GPU).  Ciphertexts live in HBM for
+// their whole life: [2][limbs][n] u64 in NTT (evaluation) form.  Every op is
+// enqueued on the engine's HIP stream; nothing synchronises the host except
+// downloads/decryption.  The op set and its semantics (levels, canonical
+// scales, rounding of constants) are the spec of DESIGN.md §3, which the CPU
+// oracle (oracle/) restates independently; results are bit-identical.
+//
+// The reference reaches these operations through OpenFHE's CryptoContext
+// (EvalAdd/EvalSub/EvalMult/EvalSquare/EvalMultAndRelinearize/EvalRotate/
+// EvalFastRotation/EvalChebyshevSeriesPS, called from src/sign.cpp,
+// src/comparison.cpp, src/rotation.h and src/sort_algo.h).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../host/hostmath.hpp"
+
+namespace fhe {
+
+using u64 = uint64_t;
+using i64 = int64_t;
+
+struct DevMem;  // pooled device allocation (engine.hip)
+
+struct Ciphertext {
+    std::shared_ptr<DevMem> mem;
+    u64 *data = nullptr;  // [2][limbs][n]
+    int level = 0;
+    int slots = 0;
+    double scale = 0;
+    size_t limbs = 0;
+};
+using CtPtr = std::shared_ptr<Ciphertext>;
+
+struct Plaintext {
+    std::shared_ptr<DevMem> mem;
+    u64 *data = nullptr;  // [limbs][n]
+    int level = 0;
+    int slots = 0;
+    double scale = 0;
+    size_t limbs = 0;
+};
+using PtPtr = std::shared_ptr<Plaintext>;
+
+struct Counters {
+    u64 hmult = 0, keyswitch = 0, rotations = 0, rescale = 0, ptmult = 0, constmult = 0;
+};
+
+class Engine {
+  public:
+    Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int device, u64 seed);
+    ~Engine();
+    Engine(const Engine &) = delete;
+    Engine &operator=(const Engine &) = delete;
+
+    const host::Params &params() const;
+    size_t n() const;
+    double delta(int level) const;
+
+    // ------------------------------------------------------------ keys ---
+    void keygen();
+    void gen_rotation_keys(const std::vector<int> &rot);
+    void load_secret(const u64 *s_ntt);           // [nall][n]
+    void load_public(const u64 *pk);              // [2][nq][n]
+    void load_relin(const u64 *key);              // [digits][2][nall][n]
+    void load_rotation(long k, const u64 *key);   // [digits][2][nall][n]
+    bool has_rotation_key(long k) const;
+    size_t key_bytes() const;
+
+    // ------------------------------------------------- encode / encrypt ---
+    PtPtr encode(const std::vector<double> &v, int slots, int level);
+    CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
+    CtPtr encrypt_pt(const Plaintext &pt);
+    std::vector<double> decrypt(const Ciphertext &ct);
+    CtPtr upload(const u64 *host, size_t limbs, int level, int slots, double scale);
+    void download(const Ciphertext &ct, u64 *host);
+    PtPtr upload_pt(const u64 *host, size_t limbs, int level, int slots, double scale);
+
+    // -------------------------------------------------------------- ops ---
+    CtPtr clone(const Ciphertext &a);
+    CtPtr add(const Ciphertext &a, const Ciphertext &b);
+    CtPtr sub(const Ciphertext &a, const Ciphertext &b);
+    void add_inplace(CtPtr &acc, const Ciphertext &b);
+    CtPtr negate(const Ciphertext &a);
+    CtPtr add_plain(const Ciphertext &a, const Plaintext &p);
+    CtPtr sub_plain(const Ciphertext &a, const Plaintext &p);
+    CtPtr plain_sub(const Plaintext &p, const Ciphertext &a);
+    CtPtr add_const(const Ciphertext &a, double c);
+    CtPtr mul_int(const Ciphertext &a, i64 k);
+    CtPtr mul_const(const Ciphertext &a, double c);
+    CtPtr mul_const_to(const Ciphertext &a, double c, int target);
+    CtPtr level_adjust(const Ciphertext &a, int target);
+    void match_levels(CtPtr &a, CtPtr &b);
+    CtPtr mul_plain(const Ciphertext &a, const Plaintext &p);
+    CtPtr mul(const Ciphertext &a, const Ciphertext &b);
+    CtPtr square(const Ciphertext &a);
+    CtPtr rotate(const Ciphertext &a, long k);
+    std::vector<CtPtr> rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks);
+    CtPtr rescale(const Ciphertext &a);
+    CtPtr drop_to(const Ciphertext &a, int level);
+    CtPtr linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c, int target);
+    CtPtr trivial_const(double c, int level, int slots);
+    CtPtr zero_like(int level, int slots);
+    // sum over ranks already done into ct (u64 add, no reduction): reduce mod q
+    void reduce_after_allreduce(Ciphertext &ct);
+
+    // ---------------------------------------------- kernel-level access ---
+    // host in/out, for parity tests
+    void ntt_host(u64 *data, int prime_index, int limbs, bool inverse);
+    void modup_host(const u64 *d, size_t ell, u64 *ext);          // ext [digits][ell+K][n] NTT
+    void moddown_host(const u64 *in, size_t ell, u64 *out);        // in [ell+K][n] -> [ell][n]
+    void automorph_host(const u64 *in, size_t limbs, u64 g, u64 *out);
+
+    // small device scratch (for collectives / headers); copies are synchronous
+    struct DevBuf {
+        std::shared_ptr<DevMem> mem;
+        u64 *ptr = nullptr;
+    };
+    DevBuf alloc_u64(size_t count);
+    void h2d(u64 *dst, const u64 *src, size_t count);
+    void d2h(u64 *dst, const u64 *src, size_t count);
+
+    void sync();
+    void *stream_handle();   // hipStream_t
+    int device() const;
+    Counters ctr;
+
+    struct Impl;
+    std::unique_ptr<Impl> impl;
+
+  private:
+    CtPtr new_ct(int level, int slots, double scale, size_t limbs);
+};
+
+// Raised on a rotation index with no key (the reference's OpenFHE raises on
+// EvalRotate with a missing key).
+struct NoKeyError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+}  // namespace fhe

@@ -1,0 +1,422 @@
+// Host-side precomputation for the MI355X RNS-CKKS engine (see hostmath.hpp).
+#include "hostmath.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <mutex>
+#include <set>
+#include <stdexcept>
+
+namespace fhe {
+namespace host {
+
+// ------------------------------------------------------------ arithmetic --
+Modulus::Modulus(u64 q_) : q(q_) {
+    k = 64 - __builtin_clzll(q);
+    mu = (u64)(((u128)1 << (2 * k)) / q);
+}
+u64 mulmod(u64 a, u64 b, const Modulus &m) {
+    const u128 z = (u128)a * b;
+    const u64 t = (u64)(z >> (m.k - 1));
+    const u64 qh = (u64)(((u128)t * m.mu) >> (m.k + 1));
+    u64 r = (u64)z - qh * m.q;
+    while (r >= m.q) r -= m.q;
+    return r;
+}
+u64 powmod(u64 a, u64 e, const Modulus &m) {
+    u64 r = 1 % m.q;
+    a %= m.q;
+    for (; e; e >>= 1) {
+        if (e & 1) r = mulmod(r, a, m);
+        a = mulmod(a, a, m);
+    }
+    return r;
+}
+u64 invmod(u64 a, const Modulus &m) { return powmod(a, m.q - 2, m); }
+u64 shoup(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
+u64 to_mod(i64 v, u64 q) {
+    if (v >= 0) return (u64)v % q;
+    const u64 r = (u64)(-(v + 1)) % q;
+    const u64 s = (r + 1) % q;
+    return s ? q - s : 0;
+}
+bool is_prime(u64 n) {
+    if (n < 2) return false;
+    static const u64 bases[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+    for (u64 p : bases)
+        if (n % p == 0) return n == p;
+    u64 d = n - 1;
+    int s = 0;
+    for (; !(d & 1); d >>= 1) ++s;
+    auto pw = [n](u64 b, u64 e) {
+        u128 r = 1, x = b % n;
+        for (; e; e >>= 1) {
+            if (e & 1) r = r * x % n;
+            x = x * x % n;
+        }
+        return (u64)r;
+    };
+    for (u64 a : bases) {
+        u64 x = pw(a, d);
+        if (x == 1 || x == n - 1) continue;
+        bool witness = true;
+        for (int r = 1; r < s && witness; ++r) {
+            x = (u64)((u128)x * x % n);
+            if (x == n - 1) witness = false;
+        }
+        if (witness) return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- params --
+Params make_params(int logN, int L, int scale_bits, int first_bits, int dnum) {
+    if (logN < 4 || logN > 17) throw std::invalid_argument("logN out of range [4,17]");
+    if (scale_bits < 20 || scale_bits > 58 || first_bits > 61 || first_bits <= scale_bits)
+        throw std::invalid_argument("unsupported modulus sizes");
+    Params P;
+    P.logN = logN;
+    P.n = (size_t)1 << logN;
+    P.L = L;
+    P.dnum = dnum;
+    P.scale_bits = scale_bits;
+    P.first_bits = first_bits;
+    const u64 m2 = 2 * (u64)P.n;
+    std::set<u64> used;
+    std::vector<u64> q(L + 1);
+    // q_0: largest NTT prime below 2^first_bits
+    u64 c = ((((u64)1 << first_bits) - 1) / m2) * m2 + 1;
+    if (c >= ((u64)1 << first_bits)) c -= m2;
+    while (!is_prime(c)) c -= m2;
+    q[0] = c;
+    used.insert(c);
+    // q_L .. q_1: greedy closest primes keep Delta_l == 2^scale_bits (no drift)
+    auto nearest = [&](double target) {
+        const u64 t = (u64)target;
+        u64 lo = (t / m2) * m2 + 1;
+        if (lo > t) lo -= m2;
+        u64 hi = lo + m2;
+        for (;;) {
+            const bool below = (double)(t - lo) <= (double)(hi - t);
+            const u64 cand = below ? lo : hi;
+            if (is_prime(cand) && !used.count(cand)) return cand;
+            if (below)
+                lo -= m2;
+            else
+                hi += m2;
+        }
+    };
+    if (L >= 1) {
+        double d = std::ldexp(1.0, scale_bits);
+        q[L] = nearest(d);
+        used.insert(q[L]);
+        d = (double)q[L];
+        for (int l = 0; l + 1 < L; ++l) {
+            d = d * d / (double)q[L - l];
+            q[L - l - 1] = nearest(d);
+            used.insert(q[L - l - 1]);
+        }
+    }
+    P.alpha = (L + 1 + dnum - 1) / dnum;
+    double maxbits = 0;
+    for (int j = 0; j * P.alpha < L + 1; ++j) {
+        double b = 0;
+        for (int i = j * P.alpha; i < std::min((j + 1) * P.alpha, L + 1); ++i) b += std::log2((double)q[i]);
+        maxbits = std::max(maxbits, b);
+    }
+    P.K = (int)std::ceil(maxbits / 60.0);
+    u64 p = q[0];
+    for (int k = 0; k < P.K; ++k) {
+        do {
+            p -= m2;
+        } while (!is_prime(p) || used.count(p));
+        q.push_back(p);
+        used.insert(p);
+    }
+    P.primes = q;
+    P.delta.resize(L + 1);
+    P.delta[0] = (double)q[L];
+    for (int l = 0; l < L; ++l) P.delta[l + 1] = P.delta[l] * P.delta[l] / (double)q[L - l];
+    return P;
+}
+
+// ------------------------------------------------------------------- NTT --
+static uint32_t brev(uint32_t x, int bits) {
+    uint32_t r = 0;
+    for (int i = 0; i < bits; ++i, x >>= 1) r = (r << 1) | (x & 1);
+    return r;
+}
+NttTable make_ntt_table(u64 q, int logN) {
+    const Modulus m(q);
+    const size_t n = (size_t)1 << logN;
+    NttTable t;
+    u64 g = 2;
+    while (powmod(g, (q - 1) / 2, m) != q - 1) ++g;  // smallest non-residue
+    t.psi = powmod(g, (q - 1) / (2 * n), m);
+    const u64 psii = invmod(t.psi, m);
+    std::vector<u64> pw(n), pwi(n);
+    pw[0] = pwi[0] = 1;
+    for (size_t i = 1; i < n; ++i) {
+        pw[i] = mulmod(pw[i - 1], t.psi, m);
+        pwi[i] = mulmod(pwi[i - 1], psii, m);
+    }
+    t.fwd.resize(n);
+    t.fwd_s.resize(n);
+    t.inv.resize(n);
+    t.inv_s.resize(n);
+    for (size_t k = 0; k < n; ++k) {
+        const uint32_t r = brev((uint32_t)k, logN);
+        t.fwd[k] = pw[r];
+        t.inv[k] = pwi[r];
+        t.fwd_s[k] = shoup(t.fwd[k], q);
+        t.inv_s[k] = shoup(t.inv[k], q);
+    }
+    t.ninv = invmod(n % q, m);
+    t.ninv_s = shoup(t.ninv, q);
+    return t;
+}
+std::vector<uint32_t> automorphism_perm(int logN, u64 g) {
+    const size_t n = (size_t)1 << logN;
+    const u64 m2 = 2 * (u64)n;
+    std::vector<uint32_t> perm(n);
+    for (size_t k = 0; k < n; ++k) {
+        const u64 i = brev((uint32_t)k, logN);
+        const u64 e = ((2 * i + 1) * g) % m2;
+        perm[k] = brev((uint32_t)((e - 1) / 2), logN);
+    }
+    return perm;
+}
+u64 galois_for_rotation(int logN, long k) {
+    const long half = 1L << (logN - 1);
+    const long r = ((k % half) + half) % half;
+    const u64 m2 = (u64)1 << (logN + 1);
+    u64 g = 1;
+    for (long i = 0; i < r; ++i) g = g * 5 % m2;
+    return g;
+}
+
+// --------------------------------------------------------------- encoder --
+namespace {
+using cd = std::complex<double>;
+struct Emb {
+    std::vector<cd> ksi;
+    std::vector<u64> rot;
+};
+const Emb &emb_tables(size_t n) {
+    static std::mutex mu;
+    static std::map<size_t, Emb> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(n);
+    if (it != cache.end()) return it->second;
+    Emb e;
+    const size_t M = 2 * n;
+    e.ksi.resize(M + 1);
+    for (size_t k = 0; k <= M; ++k) {
+        const double ang = 2.0 * M_PI * (double)k / (double)M;
+        e.ksi[k] = cd(std::cos(ang), std::sin(ang));
+    }
+    e.rot.resize(n / 2);
+    u64 g = 1;
+    for (size_t j = 0; j < n / 2; ++j, g = g * 5 % M) e.rot[j] = g;
+    return cache[n] = std::move(e);
+}
+void bit_reverse(std::vector<cd> &v) {
+    const size_t n = v.size();
+    for (size_t i = 1, j = 0; i < n; ++i) {
+        size_t bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) std::swap(v[i], v[j]);
+    }
+}
+// inverse special FFT: slot values -> (real, imag) coefficient halves
+void special_ifft(std::vector<cd> &v, const Emb &E, size_t n) {
+    const size_t S = v.size(), M = 2 * n;
+    for (size_t len = S; len >= 1; len >>= 1) {
+        for (size_t i = 0; i < S; i += len) {
+            const size_t h = len >> 1, lq = len << 2, gap = M / lq;
+            for (size_t j = 0; j < h; ++j) {
+                const size_t idx = (lq - (E.rot[j] % lq)) * gap;
+                cd u = v[i + j] + v[i + j + h];
+                cd w = v[i + j] - v[i + j + h];
+                w *= E.ksi[idx];
+                v[i + j] = u;
+                v[i + j + h] = w;
+            }
+        }
+    }
+    bit_reverse(v);
+    for (auto &x : v) x /= (double)S;
+}
+void special_fft(std::vector<cd> &v, const Emb &E, size_t n) {
+    const size_t S = v.size(), M = 2 * n;
+    bit_reverse(v);
+    for (size_t len = 2; len <= S; len <<= 1) {
+        for (size_t i = 0; i < S; i += len) {
+            const size_t h = len >> 1, lq = len << 2, gap = M / lq;
+            for (size_t j = 0; j < h; ++j) {
+                const size_t idx = (E.rot[j] % lq) * gap;
+                cd u = v[i + j];
+                cd w = v[i + j + h];
+                w *= E.ksi[idx];
+                v[i + j] = u + w;
+                v[i + j + h] = u - w;
+            }
+        }
+    }
+}
+}  // namespace
+
+std::vector<i64> encode_coeffs(const std::vector<double> &v, size_t n, int slots, double scale) {
+    if (slots <= 0 || (slots & (slots - 1)) || (size_t)slots > n / 2)
+        throw std::invalid_argument("encode: slots must be a power of two <= n/2");
+    const Emb &E = emb_tables(n);
+    std::vector<cd> z(slots, cd(0, 0));
+    for (size_t i = 0; i < v.size() && i < (size_t)slots; ++i) z[i] = cd(v[i], 0);
+    special_ifft(z, E, n);
+    const size_t gap = n / (2 * (size_t)slots);
+    std::vector<i64> coef(n, 0);
+    for (size_t i = 0; i < (size_t)slots; ++i) {
+        coef[i * gap] = std::llround(z[i].real() * scale);
+        coef[i * gap + n / 2] = std::llround(z[i].imag() * scale);
+    }
+    return coef;
+}
+
+std::vector<double> decode_coeffs(const u64 *m0, size_t n, u64 q0, int slots, double scale) {
+    const Emb &E = emb_tables(n);
+    const size_t gap = n / (2 * (size_t)slots);
+    auto centred = [q0](u64 x) { return x > q0 / 2 ? -(double)(q0 - x) : (double)x; };
+    std::vector<cd> z(slots);
+    for (size_t i = 0; i < (size_t)slots; ++i)
+        z[i] = cd(centred(m0[i * gap]) / scale, centred(m0[i * gap + n / 2]) / scale);
+    special_fft(z, E, n);
+    std::vector<double> out(slots);
+    for (size_t i = 0; i < (size_t)slots; ++i) out[i] = z[i].real();
+    return out;
+}
+
+i64 const_to_target(double c, double delta_target, u64 q_dropped, double scale_in) {
+    return std::llround(c * delta_target * (double)q_dropped / scale_in);
+}
+i64 const_at_scale(double c, double scale) { return std::llround(c * scale); }
+
+// -------------------------------------------------------------- sampling --
+SplitMix64::SplitMix64(u64 seed, u64 tag) : s(seed ^ (tag * 0xD1B54A32D192ED03ULL)) { next(); }
+u64 SplitMix64::next() {
+    s += 0x9E3779B97F4A7C15ULL;
+    u64 z = s;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+u64 sample_uniform_mod(SplitMix64 &g, u64 q) {
+    const int bits = 64 - __builtin_clzll(q);
+    for (;;) {
+        const u64 r = g.next() >> (64 - bits);
+        if (r < q) return r;
+    }
+}
+int sample_ternary(SplitMix64 &g) {
+    const u64 r = g.next() % 3;
+    return r == 0 ? 0 : (r == 1 ? 1 : -1);
+}
+int sample_cbd(SplitMix64 &g) {
+    const u64 m = (1ULL << 21) - 1;
+    const u64 a = g.next(), b = g.next();
+    return __builtin_popcountll(a & m) - __builtin_popcountll(b & m);
+}
+
+// ---------------------------------------------------------- level tables --
+LevelTables make_level_tables(const Params &P) {
+    LevelTables T;
+    const size_t nq = P.nq(), K = (size_t)P.K, alpha = (size_t)P.alpha;
+    std::vector<Modulus> mods;
+    for (u64 q : P.primes) mods.emplace_back(q);
+    // prime maps
+    const size_t Wmax = nq + K;
+    T.extmap.assign((nq + 1) * Wmax, 0);
+    for (size_t ell = 1; ell <= nq; ++ell) {
+        for (size_t t = 0; t < ell; ++t) T.extmap[ell * Wmax + t] = (int)t;
+        for (size_t k = 0; k < K; ++k) T.extmap[ell * Wmax + ell + k] = (int)(nq + k);
+    }
+    // ModUp
+    T.modup_off.assign(nq + 1, {});
+    for (size_t ell = 1; ell <= nq; ++ell) {
+        const size_t W = ell + K;
+        const size_t digits = (ell + alpha - 1) / alpha;
+        for (size_t j = 0; j < digits; ++j) {
+            const size_t lo = j * alpha, hi = std::min(ell, (j + 1) * alpha), a = hi - lo;
+            T.modup_off[ell].push_back(T.modup.size());
+            std::vector<u64> qhinv(a), qhinv_s(a), qhat(a * W, 0), qhat_s(a * W, 0);
+            for (size_t i = lo; i < hi; ++i) {
+                u64 prod = 1;
+                for (size_t s = lo; s < hi; ++s)
+                    if (s != i) prod = mulmod(prod, P.primes[s] % P.primes[i], mods[i]);
+                qhinv[i - lo] = invmod(prod, mods[i]);
+                qhinv_s[i - lo] = shoup(qhinv[i - lo], P.primes[i]);
+            }
+            for (size_t t = 0; t < W; ++t) {
+                if (t >= lo && t < hi) continue;
+                const size_t pt = t < ell ? t : nq + (t - ell);
+                const Modulus &mt = mods[pt];
+                for (size_t i = lo; i < hi; ++i) {
+                    u64 prod = 1;
+                    for (size_t s = lo; s < hi; ++s)
+                        if (s != i) prod = mulmod(prod, P.primes[s] % mt.q, mt);
+                    qhat[(i - lo) * W + t] = prod;
+                    qhat_s[(i - lo) * W + t] = shoup(prod, mt.q);
+                }
+            }
+            T.modup.insert(T.modup.end(), qhinv.begin(), qhinv.end());
+            T.modup.insert(T.modup.end(), qhinv_s.begin(), qhinv_s.end());
+            T.modup.insert(T.modup.end(), qhat.begin(), qhat.end());
+            T.modup.insert(T.modup.end(), qhat_s.begin(), qhat_s.end());
+        }
+    }
+    // ModDown
+    T.phinv.resize(K);
+    T.phinv_s.resize(K);
+    T.phat.assign(K * nq, 0);
+    T.phat_s.assign(K * nq, 0);
+    T.pinv.resize(nq);
+    T.pinv_s.resize(nq);
+    for (size_t k = 0; k < K; ++k) {
+        const Modulus &mk = mods[nq + k];
+        u64 prod = 1;
+        for (size_t s = 0; s < K; ++s)
+            if (s != k) prod = mulmod(prod, P.primes[nq + s] % mk.q, mk);
+        T.phinv[k] = invmod(prod, mk);
+        T.phinv_s[k] = shoup(T.phinv[k], mk.q);
+    }
+    for (size_t i = 0; i < nq; ++i) {
+        const Modulus &mi = mods[i];
+        u64 Pm = 1;
+        for (size_t k = 0; k < K; ++k) {
+            u64 prod = 1;
+            for (size_t s = 0; s < K; ++s)
+                if (s != k) prod = mulmod(prod, P.primes[nq + s] % mi.q, mi);
+            T.phat[k * nq + i] = prod;
+            T.phat_s[k * nq + i] = shoup(prod, mi.q);
+            Pm = mulmod(Pm, P.primes[nq + k] % mi.q, mi);
+        }
+        T.pinv[i] = invmod(Pm, mi);
+        T.pinv_s[i] = shoup(T.pinv[i], mi.q);
+    }
+    // Rescale
+    T.qlinv.assign((nq + 1) * nq, 0);
+    T.qlinv_s.assign((nq + 1) * nq, 0);
+    for (size_t ell = 2; ell <= nq; ++ell) {
+        const u64 ql = P.primes[ell - 1];
+        for (size_t i = 0; i + 1 < ell; ++i) {
+            const u64 v = invmod(ql % P.primes[i], mods[i]);
+            T.qlinv[ell * nq + i] = v;
+            T.qlinv_s[ell * nq + i] = shoup(v, P.primes[i]);
+        }
+    }
+    return T;
+}
+
+}  // namespace host
+}  // namespace fhe

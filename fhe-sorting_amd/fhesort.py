@@ -1,0 +1,406 @@
+"""Python binding of the MI355X engine (lib/libfhesort.so, C ABI in
+include/fhe_gpu.h).
+
+This is the host-side handle the tests and bench.py use.  There is no CPU
+fallback: if the HIP library is missing or no GPU is visible, constructing a
+Context raises.  Method names mirror the reference API where one exists
+(compare, indicator, sign_composite, direct_sort, ...).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'lib', 'libfhesort.so')
+COEFF_DIR = os.path.join(HERE, 'data')
+HEADER = os.path.join(os.path.dirname(HERE), 'include', 'fhe_gpu.h')
+
+FHE_OK, FHE_EINVAL, FHE_ENOKEY, FHE_EDEPTH, FHE_EHIP, FHE_ENOMEM, FHE_EINTERNAL, FHE_ENOCOMM = range(8)
+NAF, BNAF, BINARY = 0, 1, 2
+
+
+class FheError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f'fhe error {code}: {msg}')
+        self.code = code
+
+
+class NoKeyError(FheError):
+    pass
+
+
+class Params(C.Structure):
+    _fields_ = [('log_n', C.c_int), ('mult_depth', C.c_int), ('scale_bits', C.c_int), ('first_bits', C.c_int),
+                ('dnum', C.c_int), ('seed', C.c_uint64)]
+
+
+_lib = None
+vp, ip, dp, u64p = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_uint64)
+PP = C.POINTER(C.c_void_p)
+ALLREDUCE_FN = C.CFUNCTYPE(None, C.POINTER(C.c_uint64), C.c_uint64, C.c_void_p)
+
+_SIGS = {
+    'fhe_last_error': (C.c_char_p, []),
+    'fhe_ctx_create': (C.c_int, [C.POINTER(Params), C.c_int, PP]),
+    'fhe_ctx_destroy': (C.c_int, [vp]),
+    'fhe_ctx_info': (C.c_int, [vp, ip, ip, ip, u64p, dp]),
+    'fhe_set_coeff_dir': (C.c_int, [C.c_char_p]),
+    'fhe_keygen': (C.c_int, [vp]),
+    'fhe_gen_rotation_keys': (C.c_int, [vp, ip, C.c_int]),
+    'fhe_ctx_load_secret': (C.c_int, [vp, u64p]),
+    'fhe_ctx_load_public': (C.c_int, [vp, u64p]),
+    'fhe_ctx_load_keys': (C.c_int, [vp, u64p, ip, C.POINTER(u64p), C.c_int]),
+    'fhe_key_bytes': (C.c_uint64, [vp]),
+    'fhe_encrypt': (C.c_int, [vp, dp, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_decrypt': (C.c_int, [vp, vp, dp]),
+    'fhe_ct_upload': (C.c_int, [vp, u64p, C.c_int, C.c_int, C.c_int, C.c_double, PP]),
+    'fhe_ct_download': (C.c_int, [vp, vp, u64p]),
+    'fhe_ct_info': (C.c_int, [vp, ip, ip, dp, ip]),
+    'fhe_ct_set_slots': (C.c_int, [vp, C.c_int]),
+    'fhe_ct_free': (C.c_int, [vp]),
+    'fhe_pt_encode': (C.c_int, [vp, dp, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_pt_upload': (C.c_int, [vp, u64p, C.c_int, C.c_int, C.c_int, C.c_double, PP]),
+    'fhe_pt_free': (C.c_int, [vp]),
+    'fhe_add': (C.c_int, [vp, vp, vp, PP]),
+    'fhe_sub': (C.c_int, [vp, vp, vp, PP]),
+    'fhe_negate': (C.c_int, [vp, vp, PP]),
+    'fhe_add_const': (C.c_int, [vp, vp, C.c_double, PP]),
+    'fhe_mul_const': (C.c_int, [vp, vp, C.c_double, PP]),
+    'fhe_mul_const_to': (C.c_int, [vp, vp, C.c_double, C.c_int, PP]),
+    'fhe_mul_int': (C.c_int, [vp, vp, C.c_int64, PP]),
+    'fhe_level_adjust': (C.c_int, [vp, vp, C.c_int, PP]),
+    'fhe_rescale': (C.c_int, [vp, vp, PP]),
+    'fhe_mul_plain': (C.c_int, [vp, vp, vp, PP]),
+    'fhe_add_plain': (C.c_int, [vp, vp, vp, PP]),
+    'fhe_mul_relin': (C.c_int, [vp, vp, vp, PP]),
+    'fhe_square_relin': (C.c_int, [vp, vp, PP]),
+    'fhe_rotate': (C.c_int, [vp, vp, C.c_int, PP]),
+    'fhe_rotate_hoisted': (C.c_int, [vp, vp, ip, C.c_int, PP]),
+    'fhe_linear_sum_to': (C.c_int, [vp, PP, dp, C.c_int, C.c_int, PP]),
+    'fhe_cheb_ps': (C.c_int, [vp, vp, dp, C.c_int, C.c_double, C.c_double, PP]),
+    'fhe_sign_composite': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_compare': (C.c_int, [vp, vp, vp, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_indicator': (C.c_int, [vp, vp, C.c_double, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_compose_rotate': (C.c_int, [vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_decompose': (C.c_int, [C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip, C.c_int]),
+    'fhe_size_parameters': (C.c_int, [C.c_int, ip, ip, C.c_int]),
+    'fhe_direct_sort': (C.c_int, [vp, vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.c_int, vp, vp, PP]),
+    'fhe_comm_get_unique_id': (C.c_int, [C.POINTER(C.c_uint8)]),
+    'fhe_comm_init': (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
+    'fhe_comm_destroy': (C.c_int, [vp]),
+    'fhe_ct_allreduce': (C.c_int, [vp, vp]),
+    'fhe_ntt': (C.c_int, [vp, u64p, C.c_int, C.c_int, C.c_int]),
+    'fhe_modup': (C.c_int, [vp, u64p, C.c_int, u64p]),
+    'fhe_moddown': (C.c_int, [vp, u64p, C.c_int, u64p]),
+    'fhe_automorph': (C.c_int, [vp, u64p, C.c_int, C.c_uint64, u64p]),
+    'fhe_counters': (C.c_int, [vp, u64p]),
+    'fhe_reset_counters': (C.c_int, [vp]),
+    'fhe_sync': (C.c_int, [vp]),
+    'fhe_stream': (vp, [vp]),
+}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'MI355X engine library missing: {LIB_PATH} (run __graft_entry__.build())')
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        L.fhe_set_coeff_dir(COEFF_DIR.encode())
+        _lib = L
+    return _lib
+
+
+def _chk(rc):
+    if rc != FHE_OK:
+        msg = lib().fhe_last_error().decode()
+        if rc == FHE_ENOKEY:
+            raise NoKeyError(rc, msg)
+        raise FheError(rc, msg)
+
+
+def _u64(a):
+    return a.ctypes.data_as(u64p)
+
+
+def _dbl(a):
+    return a.ctypes.data_as(dp)
+
+
+def _int(a):
+    return a.ctypes.data_as(ip)
+
+
+class Ct:
+    def __init__(self, ctx, h):
+        self.ctx, self.h = ctx, h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().fhe_ct_free(self.h)
+        except Exception:
+            pass
+
+    def info(self):
+        lv, sl, lm, sc = C.c_int(), C.c_int(), C.c_int(), C.c_double()
+        _chk(lib().fhe_ct_info(self.h, C.byref(lv), C.byref(sl), C.byref(sc), C.byref(lm)))
+        return dict(level=lv.value, slots=sl.value, scale=sc.value, limbs=lm.value)
+
+    @property
+    def level(self):
+        return self.info()['level']
+
+    @property
+    def slots(self):
+        return self.info()['slots']
+
+    def set_slots(self, s):
+        _chk(lib().fhe_ct_set_slots(self.h, s))
+
+    def data(self):
+        inf = self.info()
+        out = np.empty((2, inf['limbs'], self.ctx.n), dtype=np.uint64)
+        _chk(lib().fhe_ct_download(self.ctx.h, self.h, _u64(out)))
+        return out
+
+    def decrypt(self):
+        return self.ctx.decrypt(self)
+
+
+class Pt:
+    def __init__(self, ctx, h):
+        self.ctx, self.h = ctx, h
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().fhe_pt_free(self.h)
+        except Exception:
+            pass
+
+
+class Context:
+    """One engine on one GPU (`device`)."""
+
+    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, device=0, keygen=True):
+        self.logN, self.n, self.L = logN, 1 << logN, L
+        p = Params(logN, L, scale_bits, first_bits, dnum, seed)
+        h = C.c_void_p()
+        _chk(lib().fhe_ctx_create(C.byref(p), device, C.byref(h)))
+        self.h = h
+        nq, K, alpha = C.c_int(), C.c_int(), C.c_int()
+        _chk(lib().fhe_ctx_info(self.h, C.byref(nq), C.byref(K), C.byref(alpha), None, None))
+        self.nq, self.K, self.alpha = nq.value, K.value, alpha.value
+        self.primes = np.empty(self.nq + self.K, dtype=np.uint64)
+        self.delta = np.empty(L + 1)
+        _chk(lib().fhe_ctx_info(self.h, None, None, None, _u64(self.primes), _dbl(self.delta)))
+        if keygen:
+            self.keygen()
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().fhe_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def digits(self):
+        return (self.nq + self.alpha - 1) // self.alpha
+
+    def _new(self, fn, *args):
+        out = C.c_void_p()
+        _chk(fn(self.h, *args, C.byref(out)))
+        return Ct(self, out.value)
+
+    # keys ---------------------------------------------------------------
+    def keygen(self):
+        _chk(lib().fhe_keygen(self.h))
+
+    def gen_rotation_keys(self, rots):
+        r = np.asarray(rots, dtype=np.int32)
+        _chk(lib().fhe_gen_rotation_keys(self.h, _int(r), len(r)))
+
+    def load_keys_from(self, orc, rots=()):
+        """Upload the CPU oracle's secret/public/relin/rotation keys (parity tests)."""
+        s = np.ascontiguousarray(orc.secret_ntt())
+        _chk(lib().fhe_ctx_load_secret(self.h, _u64(s)))
+        pk = np.ascontiguousarray(orc.public_key())
+        _chk(lib().fhe_ctx_load_public(self.h, _u64(pk)))
+        rl = np.ascontiguousarray(orc.relin_key())
+        keys, idx = [], []
+        for k in rots:
+            g, key = orc.rot_key(k)
+            if g:
+                keys.append(np.ascontiguousarray(key))
+                idx.append(k)
+        arr = (u64p * max(1, len(keys)))(*[_u64(k) for k in keys])
+        ia = np.asarray(idx, dtype=np.int32)
+        _chk(lib().fhe_ctx_load_keys(self.h, _u64(rl), _int(ia), arr, len(keys)))
+
+    def key_bytes(self):
+        return lib().fhe_key_bytes(self.h)
+
+    # objects ------------------------------------------------------------
+    def encode(self, v, slots, level=0):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        out = C.c_void_p()
+        _chk(lib().fhe_pt_encode(self.h, _dbl(v), len(v), slots, level, C.byref(out)))
+        return Pt(self, out.value)
+
+    def upload_pt(self, data, level, slots, scale=None):
+        data = np.ascontiguousarray(data, dtype=np.uint64)
+        scale = self.delta[level] if scale is None else scale
+        out = C.c_void_p()
+        _chk(lib().fhe_pt_upload(self.h, _u64(data), data.shape[0], level, slots, scale, C.byref(out)))
+        return Pt(self, out.value)
+
+    def encrypt(self, v, slots=None, level=0):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        return self._new(lib().fhe_encrypt, _dbl(v), len(v), slots or len(v), level)
+
+    def decrypt(self, ct):
+        out = np.empty(ct.slots)
+        _chk(lib().fhe_decrypt(self.h, ct.h, _dbl(out)))
+        return out
+
+    def upload(self, data, level, slots, scale=None):
+        data = np.ascontiguousarray(data, dtype=np.uint64)
+        scale = self.delta[level] if scale is None else scale
+        return self._new(lib().fhe_ct_upload, _u64(data), data.shape[1], level, slots, scale)
+
+    def from_oracle(self, oct):
+        inf = oct.info()
+        return self.upload(oct.data(), inf['level'], inf['slots'], inf['scale'])
+
+    # ops ----------------------------------------------------------------
+    def add(self, a, b): return self._new(lib().fhe_add, a.h, b.h)
+    def sub(self, a, b): return self._new(lib().fhe_sub, a.h, b.h)
+    def negate(self, a): return self._new(lib().fhe_negate, a.h)
+    def add_const(self, a, k): return self._new(lib().fhe_add_const, a.h, k)
+    def mul_const(self, a, k): return self._new(lib().fhe_mul_const, a.h, k)
+    def mul_const_to(self, a, k, t): return self._new(lib().fhe_mul_const_to, a.h, k, t)
+    def mul_int(self, a, k): return self._new(lib().fhe_mul_int, a.h, k)
+    def level_adjust(self, a, t): return self._new(lib().fhe_level_adjust, a.h, t)
+    def rescale(self, a): return self._new(lib().fhe_rescale, a.h)
+    def mul_plain(self, a, p): return self._new(lib().fhe_mul_plain, a.h, p.h)
+    def add_plain(self, a, p): return self._new(lib().fhe_add_plain, a.h, p.h)
+    def mul(self, a, b): return self._new(lib().fhe_mul_relin, a.h, b.h)
+    def square(self, a): return self._new(lib().fhe_square_relin, a.h)
+    def rotate(self, a, k): return self._new(lib().fhe_rotate, a.h, k)
+
+    def rotate_hoisted(self, a, ks):
+        ks = np.asarray(ks, dtype=np.int32)
+        outs = (C.c_void_p * len(ks))()
+        _chk(lib().fhe_rotate_hoisted(self.h, a.h, _int(ks), len(ks), outs))
+        return [Ct(self, outs[i]) for i in range(len(ks))]
+
+    def linear_sum_to(self, xs, cs, target):
+        arr = (C.c_void_p * len(xs))(*[x.h for x in xs])
+        cs = np.ascontiguousarray(cs, dtype=np.float64)
+        return self._new(lib().fhe_linear_sum_to, arr, _dbl(cs), len(xs), target)
+
+    def cheb(self, a, coeffs, lo=-1.0, hi=1.0):
+        c = np.ascontiguousarray(coeffs, dtype=np.float64)
+        return self._new(lib().fhe_cheb_ps, a.h, _dbl(c), len(c), lo, hi)
+
+    def sign(self, a, n, dg, df): return self._new(lib().fhe_sign_composite, a.h, n, dg, df)
+    def compare(self, a, b, n, dg, df): return self._new(lib().fhe_compare, a.h, b.h, n, dg, df)
+    def indicator(self, a, c, n, dg, df): return self._new(lib().fhe_indicator, a.h, c, n, dg, df)
+
+    def compose_rotate(self, a, N, rots, algo, rotation):
+        r = np.asarray(rots, dtype=np.int32)
+        return self._new(lib().fhe_compose_rotate, a.h, N, _int(r), len(r), algo, rotation)
+
+    def direct_sort(self, x, N, rots, cfg, mode=0, rank=None, shard=(0, 1), allreduce=None):
+        r = np.asarray(rots, dtype=np.int32)
+        cb = ALLREDUCE_FN(allreduce) if allreduce else None
+        self._cb = cb  # keep alive for the duration of the call
+        return self._new(lib().fhe_direct_sort, x.h, rank.h if rank is not None else None, N, _int(r), len(r),
+                         cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1],
+                         C.cast(cb, C.c_void_p) if cb else None, None)
+
+    # multi-GPU -----------------------------------------------------------
+    @staticmethod
+    def comm_unique_id():
+        buf = (C.c_uint8 * 128)()
+        _chk(lib().fhe_comm_get_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid, rank, world):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _chk(lib().fhe_comm_init(self.h, buf, rank, world))
+
+    def ct_allreduce(self, ct):
+        _chk(lib().fhe_ct_allreduce(self.h, ct.h))
+
+    # kernel level -------------------------------------------------------
+    def ntt(self, prime_index, data, inverse=False):
+        d = np.ascontiguousarray(data, dtype=np.uint64).copy()
+        limbs = 1 if d.ndim == 1 else d.shape[0]
+        _chk(lib().fhe_ntt(self.h, _u64(d), prime_index, limbs, 1 if inverse else 0))
+        return d
+
+    def modup(self, d):
+        d = np.ascontiguousarray(d, dtype=np.uint64)
+        ell = d.shape[0]
+        digits = (ell + self.alpha - 1) // self.alpha
+        out = np.empty((digits, ell + self.K, self.n), dtype=np.uint64)
+        _chk(lib().fhe_modup(self.h, _u64(d), ell, _u64(out)))
+        return out
+
+    def moddown(self, x):
+        x = np.ascontiguousarray(x, dtype=np.uint64)
+        ell = x.shape[0] - self.K
+        out = np.empty((ell, self.n), dtype=np.uint64)
+        _chk(lib().fhe_moddown(self.h, _u64(x), ell, _u64(out)))
+        return out
+
+    def automorph(self, x, g):
+        x = np.ascontiguousarray(x, dtype=np.uint64)
+        out = np.empty_like(x)
+        _chk(lib().fhe_automorph(self.h, _u64(x), x.shape[0], g, _u64(out)))
+        return out
+
+    def counters(self):
+        out = np.zeros(6, dtype=np.uint64)
+        _chk(lib().fhe_counters(self.h, _u64(out)))
+        return dict(zip(['hmult', 'keyswitch', 'rotations', 'rescale', 'ptmult', 'constmult'], map(int, out)))
+
+    def reset_counters(self):
+        _chk(lib().fhe_reset_counters(self.h))
+
+    def sync(self):
+        _chk(lib().fhe_sync(self.h))
+
+    def stream(self):
+        return lib().fhe_stream(self.h)
+
+
+def size_parameters(N):
+    d = C.c_int()
+    rots = np.zeros(512, dtype=np.int32)
+    m = lib().fhe_size_parameters(N, C.byref(d), _int(rots), 512)
+    if m < 0:
+        raise FheError(-m, lib().fhe_last_error().decode())
+    return d.value, [int(x) for x in rots[:m]]
+
+
+def decompose(N, rots, rotation, wrapN, algo):
+    r = np.asarray(rots, dtype=np.int32)
+    vals = np.zeros(128, dtype=np.int32)
+    sizes = np.zeros(128, dtype=np.int32)
+    m = lib().fhe_decompose(N, _int(r), len(r), rotation, wrapN, algo, _int(vals), _int(sizes), 128)
+    if m < 0:
+        raise FheError(-m, lib().fhe_last_error().decode())
+    return [(int(vals[i]), int(sizes[i])) for i in range(m)]

@@ -1,0 +1,176 @@
+/*
+ * fhe_gpu.h — C ABI of the MI355X RNS-CKKS ciphertext-op engine that runs the
+ * rank-sort / comparator hot path of oksuman/FHE-Sorting.
+ *
+ * Drop-in boundary.  In the reference every call below is a method of
+ * OpenFHE's CryptoContext<DCRTPoly> reached from the sort code; this header
+ * is what that code binds instead (C++ callers can also use the header-only
+ * mirror in fhe-sorting_amd/csrc/algo/fhesort.hpp).  Each entry point names
+ * the reference call site(s) it replaces.
+ *
+ * Rules: handles are opaque; every function returns an int status (FHE_OK =
+ * 0); no C++ exception crosses the ABI (fhe_last_error() has the message);
+ * results are new objects returned through **out and owned by the caller
+ * (free with fhe_ct_free / fhe_pt_free); one context per GPU, calls on one
+ * context must be serialised by the caller (the reference's OpenMP threads
+ * share one CryptoContext; here one process drives one GPU).  All arrays are
+ * host memory unless a name says `dev`.
+ */
+#ifndef FHE_GPU_H
+#define FHE_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    FHE_OK = 0,
+    FHE_EINVAL = 1,    /* bad argument / level mismatch / unsupported N */
+    FHE_ENOKEY = 2,    /* rotation index without a key (OpenFHE throws in EvalRotate) */
+    FHE_EDEPTH = 3,    /* no modulus levels left */
+    FHE_EHIP = 4,      /* HIP runtime error */
+    FHE_ENOMEM = 5,
+    FHE_EINTERNAL = 6,
+    FHE_ENOCOMM = 7    /* collective requested without fhe_comm_init */
+};
+
+typedef struct fhe_ctx fhe_ctx;
+typedef struct fhe_ct fhe_ct;
+typedef struct fhe_pt fhe_pt;
+
+/* CCParams<CryptoContextCKKSRNS> subset used by the sort path
+ * (tests/DirectSortTest.cpp:24-31; src/sort_algo.h:87-201) */
+typedef struct {
+    int log_n;       /* ring dimension 2^log_n (SetRingDim) */
+    int mult_depth;  /* SetMultiplicativeDepth: mult_depth+1 Q primes */
+    int scale_bits;  /* SetScalingModSize */
+    int first_bits;  /* first modulus size (OpenFHE default 60) */
+    int dnum;        /* hybrid key-switching digits (OpenFHE default 3) */
+    uint64_t seed;   /* seeds key generation and encryption randomness */
+} fhe_params;
+
+const char *fhe_last_error(void);
+
+/* ---------------------------------------------------------------- context */
+/* replaces GenCryptoContext(parameters) (tests/DirectSortTest.cpp:33) */
+int fhe_ctx_create(const fhe_params *p, int device, fhe_ctx **out);
+int fhe_ctx_destroy(fhe_ctx *ctx);
+/* primes: nq+K values; deltas: mult_depth+1 canonical scales */
+int fhe_ctx_info(fhe_ctx *ctx, int *nq, int *K, int *alpha, uint64_t *primes, double *deltas);
+/* directory holding doubled_sinc_<N>.f64 (generated_doubled_sinc_coeffs.h) */
+int fhe_set_coeff_dir(const char *dir);
+
+/* ------------------------------------------------------------------- keys */
+/* KeyGen + EvalMultKeyGen (tests/DirectSortTest.cpp:41-47), on the GPU */
+int fhe_keygen(fhe_ctx *ctx);
+/* EvalRotateKeyGen(sk, rotations) (tests/DirectSortTest.cpp:46) */
+int fhe_gen_rotation_keys(fhe_ctx *ctx, const int32_t *idx, int n);
+/* externally generated keys (identical layout to the CPU oracle):
+ * secret [nq+K][n] NTT, public [2][nq][n], key [digits][2][nq+K][n] */
+int fhe_ctx_load_secret(fhe_ctx *ctx, const uint64_t *s_ntt);
+int fhe_ctx_load_public(fhe_ctx *ctx, const uint64_t *pk);
+int fhe_ctx_load_keys(fhe_ctx *ctx, const uint64_t *relin, const int32_t *rot_idx,
+                      const uint64_t *const *rot_keys, int nrot);
+uint64_t fhe_key_bytes(fhe_ctx *ctx);
+
+/* ------------------------------------------------------ ciphertext / pt */
+/* Encryption::encryptInput = MakeCKKSPackedPlaintext + Encrypt (src/encryption.cpp:5-12) */
+int fhe_encrypt(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_ct **out);
+/* DebugEncryption::getPlaintext / Decrypt (src/encryption.cpp:14-27); out: slots values */
+int fhe_decrypt(fhe_ctx *ctx, const fhe_ct *ct, double *out);
+int fhe_ct_upload(fhe_ctx *ctx, const uint64_t *host, int limbs, int level, int slots, double scale,
+                  fhe_ct **out);
+int fhe_ct_download(fhe_ctx *ctx, const fhe_ct *ct, uint64_t *host); /* [2][limbs][n] */
+int fhe_ct_info(const fhe_ct *ct, int *level, int *slots, double *scale, int *limbs);
+/* Ciphertext::SetSlots (src/sort_algo.h:429,447,501) */
+int fhe_ct_set_slots(fhe_ct *ct, int slots);
+int fhe_ct_free(fhe_ct *ct);
+/* MakeCKKSPackedPlaintext(v, 1, level, nullptr, slots) (src/sort_algo.h:341,573) */
+int fhe_pt_encode(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_pt **out);
+int fhe_pt_upload(fhe_ctx *ctx, const uint64_t *host, int limbs, int level, int slots, double scale,
+                  fhe_pt **out);
+int fhe_pt_free(fhe_pt *pt);
+
+/* -------------------------------------------------------------------- ops */
+/* EvalAdd / EvalSub (src/comparison.cpp:13,19; src/sort_algo.h:454,495,504) */
+int fhe_add(fhe_ctx *ctx, const fhe_ct *a, const fhe_ct *b, fhe_ct **out);
+int fhe_sub(fhe_ctx *ctx, const fhe_ct *a, const fhe_ct *b, fhe_ct **out);
+int fhe_negate(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out);
+/* EvalAdd(ct, double) / EvalMult(ct, double) (src/comparison.cpp:19; src/sign.cpp:25-32) */
+int fhe_add_const(fhe_ctx *ctx, const fhe_ct *a, double c, fhe_ct **out);
+int fhe_mul_const(fhe_ctx *ctx, const fhe_ct *a, double c, fhe_ct **out);
+int fhe_mul_const_to(fhe_ctx *ctx, const fhe_ct *a, double c, int target_level, fhe_ct **out);
+int fhe_mul_int(fhe_ctx *ctx, const fhe_ct *a, int64_t k, fhe_ct **out);
+int fhe_level_adjust(fhe_ctx *ctx, const fhe_ct *a, int target_level, fhe_ct **out);
+int fhe_rescale(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out);
+/* EvalMult(ct, pt) (src/sort_algo.h:344,576) / EvalAdd(ct, pt) */
+int fhe_mul_plain(fhe_ctx *ctx, const fhe_ct *a, const fhe_pt *p, fhe_ct **out);
+int fhe_add_plain(fhe_ctx *ctx, const fhe_ct *a, const fhe_pt *p, fhe_ct **out);
+/* EvalMultAndRelinearize / EvalMult(ct,ct) / EvalSquare (src/sign.cpp:23-33; sort_algo.h:730) */
+int fhe_mul_relin(fhe_ctx *ctx, const fhe_ct *a, const fhe_ct *b, fhe_ct **out);
+int fhe_square_relin(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out);
+/* EvalRotate(ct, k) (src/rotation.h:224,231); FHE_ENOKEY if k has no key */
+int fhe_rotate(fhe_ctx *ctx, const fhe_ct *a, int k, fhe_ct **out);
+/* EvalFastRotationPrecompute + EvalFastRotation (src/rotation.h:281,342-346) */
+int fhe_rotate_hoisted(fhe_ctx *ctx, const fhe_ct *a, const int32_t *ks, int m, fhe_ct **outs);
+/* EvalLinearWSum-style sum_i c_i x_i rescaled to target_level */
+int fhe_linear_sum_to(fhe_ctx *ctx, const fhe_ct *const *xs, const double *c, int m, int target_level,
+                      fhe_ct **out);
+/* EvalChebyshevSeriesPS(ct, coeffs, a, b) (src/sort_algo.h:629,727; src/sign.cpp:76) */
+int fhe_cheb_ps(fhe_ctx *ctx, const fhe_ct *a, const double *coeffs, int ncoeffs, double lo, double hi,
+                fhe_ct **out);
+
+/* ---------------------------------------------------- comparator surface */
+/* compositeSign<n>(x, cc, SignConfig(CompositeSignConfig(n, dg, df))) (src/sign.cpp:160-185) */
+int fhe_sign_composite(fhe_ctx *ctx, const fhe_ct *x, int n, int dg, int df, fhe_ct **out);
+/* Comparison::compare(cc, a, b, CompositeSign, cfg) (src/comparison.cpp:4-22) */
+int fhe_compare(fhe_ctx *ctx, const fhe_ct *a, const fhe_ct *b, int n, int dg, int df, fhe_ct **out);
+/* Comparison::indicator(cc, x, c, CompositeSign, cfg) (src/comparison.cpp:24-40) */
+int fhe_indicator(fhe_ctx *ctx, const fhe_ct *x, double c, int n, int dg, int df, fhe_ct **out);
+/* RotationComposer<N>(cc, enc, rots, algo).rotate(ct, rotation) (src/rotation.h:205-233);
+ * algo: 0 NAF, 1 BNAF, 2 BINARY */
+int fhe_compose_rotate(fhe_ctx *ctx, const fhe_ct *a, int N, const int32_t *rots, int nrot, int algo,
+                       int rotation, fhe_ct **out);
+/* Decomposer<N>(rots).decompose(rotation, wrapN, algo) (src/rotation.h:54-102); returns #steps */
+int fhe_decompose(int N, const int32_t *rots, int nrot, int rotation, int wrap_n, int algo, int32_t *values,
+                  int32_t *sizes, int max_steps);
+
+/* -------------------------------------------------------------- rank sort */
+/* DirectSort<N>::getSizeParameters (src/sort_algo.h:87-201); returns #rotations */
+int fhe_size_parameters(int N, int *mult_depth, int32_t *rots, int max_rots);
+/* u64 sum of `count` device words over all ranks, in place (RCCL, MPI, ...) */
+typedef void (*fhe_allreduce_fn)(uint64_t *dev_data, uint64_t count, void *user);
+/* DirectSort<N>(cc, pk, rots, enc).{sort | constructRank | rotationIndexCheckN}
+ * (src/sort_algo.h:752-774 / 368-506 / 658-750); mode 0 sort, 1 rank, 2 index
+ * check (then `rank` is the rank ciphertext).  Batches b with b % world == rank
+ * run locally; partial ranks/outputs are summed with `allreduce` (or with the
+ * RCCL communicator of fhe_comm_init when allreduce == NULL and world > 1). */
+int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, const int32_t *rots, int nrot,
+                    int n, int dg, int df, int mode, int shard_rank, int shard_world, fhe_allreduce_fn allreduce,
+                    void *user, fhe_ct **out);
+
+/* ------------------------------------------------------ multi-GPU (RCCL) */
+int fhe_comm_get_unique_id(uint8_t id[128]);
+int fhe_comm_init(fhe_ctx *ctx, const uint8_t id[128], int rank, int world);
+int fhe_comm_destroy(fhe_ctx *ctx);
+/* sum the ciphertext over all ranks (RCCL all-reduce u64 + per-limb mod q) */
+int fhe_ct_allreduce(fhe_ctx *ctx, fhe_ct *ct);
+
+/* ---------------------------------------------- kernel-level (parity) */
+int fhe_ntt(fhe_ctx *ctx, uint64_t *host, int prime_index, int limbs, int inverse);
+int fhe_modup(fhe_ctx *ctx, const uint64_t *d, int ell, uint64_t *ext);
+int fhe_moddown(fhe_ctx *ctx, const uint64_t *in, int ell, uint64_t *out);
+int fhe_automorph(fhe_ctx *ctx, const uint64_t *in, int limbs, uint64_t galois, uint64_t *out);
+/* op counters: hmult, keyswitch, rotations, rescale, ptmult, constmult */
+int fhe_counters(fhe_ctx *ctx, uint64_t out[6]);
+int fhe_reset_counters(fhe_ctx *ctx);
+int fhe_sync(fhe_ctx *ctx);
+/* opaque hipStream_t of the context (for event timing by the caller) */
+void *fhe_stream(fhe_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FHE_GPU_H */

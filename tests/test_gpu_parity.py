@@ -1,0 +1,228 @@
+"""GPU parity: every engine op is bit-exact with the CPU oracle on identical
+keys and inputs, and decrypts within the reference tests' tolerances.
+
+All calls go through the C ABI (include/fhe_gpu.h) via fhesort.py.
+"""
+import numpy as np
+import pytest
+
+import fhesort as F
+import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+ROTS = [1, 2, 3, -1, -4, 5, 8, 16]
+
+
+@pytest.fixture(scope='module')
+def pair():
+    orc = O.Context(12, 12, 40, 60, 3, seed=5)
+    orc.gen_rotation_keys(ROTS)
+    gpu = F.Context(12, 12, 40, 60, 3, seed=5, keygen=False)
+    gpu.load_keys_from(orc, ROTS)
+    return orc, gpu
+
+
+def same(gct, oct_):
+    gi, oi = gct.info(), oct_.info()
+    assert gi['level'] == oi['level'] and gi['slots'] == oi['slots'] and gi['limbs'] == oi['limbs']
+    assert gi['scale'] == oi['scale']
+    gd, od = gct.data(), oct_.data()
+    assert gd.shape == od.shape
+    if not np.array_equal(gd, od):
+        bad = np.argwhere(gd != od)
+        raise AssertionError(f'{len(bad)} limb words differ, first at {bad[0].tolist()}')
+
+
+def test_params_identical(pair):
+    orc, gpu = pair
+    assert np.array_equal(orc.primes, gpu.primes)
+    assert np.array_equal(orc.delta, gpu.delta)
+
+
+@pytest.mark.parametrize('logN', [12, 13, 16])
+def test_ntt_matches_oracle(logN):
+    orc = O.Context(logN, 3, 40, 60, 3, seed=1, keygen=False)
+    gpu = F.Context(logN, 3, 40, 60, 3, seed=1, keygen=False)
+    rng = np.random.default_rng(logN)
+    for pi in range(len(orc.primes)):
+        q = int(orc.primes[pi])
+        x = rng.integers(0, q, size=orc.n, dtype=np.uint64)
+        f_o = orc.ntt(pi, x)
+        f_g = gpu.ntt(pi, x)
+        assert np.array_equal(f_o, f_g), f'forward NTT differs, prime {pi}'
+        assert np.array_equal(gpu.ntt(pi, f_g, inverse=True), x), 'inverse NTT does not round-trip'
+
+
+def test_ntt_batched_limbs():
+    gpu = F.Context(16, 6, 40, 60, 3, seed=1, keygen=False)
+    orc = O.Context(16, 6, 40, 60, 3, seed=1, keygen=False)
+    rng = np.random.default_rng(3)
+    x = np.stack([rng.integers(0, int(q), size=gpu.n, dtype=np.uint64) for q in gpu.primes[:5]])
+    g = gpu.ntt(0, x)
+    for i in range(5):
+        assert np.array_equal(g[i], orc.ntt(i, x[i]))
+
+
+def test_encrypt_decrypt_and_upload(pair):
+    orc, gpu = pair
+    x = np.linspace(-1, 1, 16)
+    c = orc.encrypt(x, 16)
+    g = gpu.from_oracle(c)
+    same(g, c)
+    assert np.max(np.abs(gpu.decrypt(g) - x)) < 1e-6
+
+
+def test_elementwise_ops(pair):
+    orc, gpu = pair
+    rng = np.random.default_rng(0)
+    a, b = rng.uniform(-1, 1, 8), rng.uniform(-1, 1, 8)
+    oa, ob = orc.encrypt(a, 8), orc.encrypt(b, 8)
+    ga, gb = gpu.from_oracle(oa), gpu.from_oracle(ob)
+    same(gpu.add(ga, gb), orc.add(oa, ob))
+    same(gpu.sub(ga, gb), orc.sub(oa, ob))
+    same(gpu.negate(ga), orc.negate(oa))
+    same(gpu.add_const(ga, 0.375), orc.add_const(oa, 0.375))
+    same(gpu.mul_int(ga, -3), orc.mul_int(oa, -3))
+    same(gpu.mul_const(ga, -2.5), orc.mul_const(oa, -2.5))
+    same(gpu.mul_const_to(ga, 1.25, 3), orc.mul_const_to(oa, 1.25, 3))
+    same(gpu.level_adjust(ga, 2), orc.level_adjust(oa, 2))
+    same(gpu.rescale(gpu.mul_int(ga, 7)), orc.rescale(orc.mul_int(oa, 7)))
+    p = orc.encode(b, 8, 0)
+    gp = gpu.upload_pt(p.data(), 0, 8)
+    same(gpu.mul_plain(ga, gp), orc.mul_plain(oa, p))
+    same(gpu.add_plain(ga, gp), orc.add_plain(oa, p))
+    # level mismatch is adjusted identically
+    m = orc.mul_const(oa, 0.5)
+    same(gpu.add(gpu.from_oracle(m), gb), orc.add(m, ob))
+
+
+def test_relinearised_products(pair):
+    orc, gpu = pair
+    rng = np.random.default_rng(1)
+    a, b = rng.uniform(-1, 1, 8), rng.uniform(-1, 1, 8)
+    oa, ob = orc.encrypt(a, 8), orc.encrypt(b, 8)
+    ga, gb = gpu.from_oracle(oa), gpu.from_oracle(ob)
+    om, gm = orc.mul(oa, ob), gpu.mul(ga, gb)
+    same(gm, om)
+    assert np.max(np.abs(gpu.decrypt(gm) - a * b)) < 1e-6
+    same(gpu.square(ga), orc.square(oa))
+    # chained products down the modulus chain
+    oc, gc = oa, ga
+    for _ in range(4):
+        oc, gc = orc.mul(oc, ob), gpu.mul(gc, gb)
+    same(gc, oc)
+
+
+def test_rotations(pair):
+    orc, gpu = pair
+    x = np.arange(16, dtype=float) / 16
+    ox = orc.encrypt(x, 16)
+    gx = gpu.from_oracle(ox)
+    for k in [1, 2, 3, -1, -4, 5, 8]:
+        gr = gpu.rotate(gx, k)
+        same(gr, orc.rotate(ox, k))
+        assert np.max(np.abs(gpu.decrypt(gr) - np.roll(x, -k))) < 1e-6
+    hs = gpu.rotate_hoisted(gx, [1, 2, 3, 0])
+    for h, k in zip(hs, [1, 2, 3, 0]):
+        same(h, orc.rotate(ox, k) if k else ox)
+    with pytest.raises(F.NoKeyError):
+        gpu.rotate(gx, 7)
+
+
+def test_modup_moddown(pair):
+    orc, gpu = pair
+    rng = np.random.default_rng(2)
+    for ell in (13, 9, 5, 1):
+        d = np.stack([rng.integers(0, int(q), size=orc.n, dtype=np.uint64) for q in orc.primes[:ell]])
+        eo, eg = orc.modup(d), gpu.modup(d)
+        assert np.array_equal(eo, eg), f'modup differs at ell={ell}'
+        x = np.stack([rng.integers(0, int(q), size=orc.n, dtype=np.uint64)
+                      for q in list(orc.primes[:ell]) + list(orc.primes[orc.nq:])])
+        assert np.array_equal(orc.moddown(x), gpu.moddown(x)), f'moddown differs at ell={ell}'
+
+
+def test_automorphism(pair):
+    orc, gpu = pair
+    rng = np.random.default_rng(4)
+    x = np.stack([rng.integers(0, int(q), size=orc.n, dtype=np.uint64) for q in orc.primes[:3]])
+    for k in (1, 5, -1):
+        g = O.galois(12, k)
+        perm = O.automorph_perm(12, g)
+        assert np.array_equal(gpu.automorph(x, g), x[:, perm])
+
+
+def test_linear_sum_mixed_levels(pair):
+    orc, gpu = pair
+    rng = np.random.default_rng(5)
+    xs = [orc.encrypt(rng.uniform(-1, 1, 8), 8) for _ in range(3)]
+    xs[1] = orc.mul_const(xs[1], 1.0)  # level 1
+    gx = [gpu.from_oracle(x) for x in xs]
+    cs = [0.25, -1.5, 3.0]
+    same(gpu.linear_sum_to(gx, cs, 3), orc.linear_sum_to(xs, cs, 3))
+
+
+@pytest.mark.parametrize('deg', [1, 3, 7, 27, 70])
+def test_chebyshev_ps(deg):
+    orc = O.Context(12, 10, 40, 60, 3, seed=9)
+    gpu = F.Context(12, 10, 40, 60, 3, seed=9, keygen=False)
+    gpu.load_keys_from(orc)
+    x = np.linspace(-1, 1, 16)
+    ox = orc.encrypt(x, 16)
+    c = np.random.default_rng(deg).normal(size=deg + 1) / (1 + np.arange(deg + 1))
+    oy = orc.cheb(ox, c)
+    gy = gpu.cheb(gpu.from_oracle(ox), c)
+    same(gy, oy)
+    ref = np.polynomial.chebyshev.chebval(x, np.concatenate([[c[0] / 2], c[1:]]))
+    assert np.max(np.abs(gpu.decrypt(gy) - ref)) < 1e-5
+
+
+def test_composite_sign_and_compare():
+    # tests/SignTest.cpp:41-80 and tests/CompareTest.cpp:43-63 (see test_oracle for tolerances)
+    orc = O.Context(12, 30, 40, 60, 3, seed=11)
+    gpu = F.Context(12, 30, 40, 60, 3, seed=11, keygen=False)
+    gpu.load_keys_from(orc)
+    x = np.array([0.5, -0.3, 0.1, -0.7, 0.0, 0.8, -0.9, 0.2])
+    ox = orc.encrypt(x, 8)
+    gx = gpu.from_oracle(ox)
+    same(gpu.sign(gx, 3, 0, 1), orc.sign(ox, 3, 0, 1))
+    a = orc.encrypt([0.1, 0.5, 0.3, 0.4], 4)
+    b = orc.encrypt([0.2, 0.4, 0.3, 0.3], 4)
+    gc = gpu.compare(gpu.from_oracle(a), gpu.from_oracle(b), 3, 3, 2)
+    same(gc, orc.compare(a, b, 3, 3, 2))
+    assert np.allclose(gpu.decrypt(gc), [0, 1, 0.5, 1], atol=0.1)
+    gi = gpu.indicator(gpu.from_oracle(a), 0.05, 3, 2, 1)
+    same(gi, orc.indicator(a, 0.05, 3, 2, 1))
+
+
+def test_keygen_and_encrypt_parity():
+    """GPU key generation + encryption == oracle's for the same seed (bit-exact)."""
+    orc = O.Context(12, 6, 40, 60, 3, seed=77)
+    orc.gen_rotation_keys([1, 3])
+    gpu = F.Context(12, 6, 40, 60, 3, seed=77)
+    gpu.gen_rotation_keys([1, 3])
+    x = np.linspace(-0.5, 0.5, 8)
+    oc, gc = orc.encrypt(x, 8), gpu.encrypt(x, 8)
+    same(gc, oc)
+    same(gpu.mul(gc, gc), orc.mul(oc, oc))
+    same(gpu.rotate(gc, 3), orc.rotate(oc, 3))
+    assert np.max(np.abs(orc.decrypt(orc.ct_from(gc.data(), 0, 8)) - x)) < 1e-6
+
+
+@pytest.mark.parametrize('N,cfg', [(4, (3, 2, 2)), (8, (3, 2, 2)), (16, (3, 2, 2))])
+def test_direct_sort_bit_exact(N, cfg):
+    depth, rots = O.size_parameters(N)
+    assert F.size_parameters(N) == (depth, rots)
+    orc = O.Context(12, depth, 40, 60, 3, seed=100 + N)
+    orc.gen_rotation_keys(rots)
+    gpu = F.Context(12, depth, 40, 60, 3, seed=100 + N, keygen=False)
+    gpu.load_keys_from(orc, rots)
+    x = np.random.default_rng(20250704).permutation(N) / N
+    ox = orc.encrypt(x, N)
+    gx = gpu.from_oracle(ox)
+    gout = gpu.direct_sort(gx, N, rots, cfg)
+    oout = orc.direct_sort(ox, N, rots, cfg)
+    same(gout, oout)
+    y = gpu.decrypt(gout)
+    assert np.max(np.abs(y - np.sort(x))) < 0.01
+    assert gout.level <= depth
