@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""Benchmark: encrypted rank sort (DirectSort) on MI355X.
+
+Workload (BASELINE.json metric): DirectSort of N=1024 reals at ring dimension
+2^16, multiplicative depth 39 (40 Q primes + 10 special primes, dnum=3),
+161 rotation keys, CompositeSign(3,5,2) -- the reference's DirectSortTest
+configuration for N=1024 (tests/DirectSortTest.cpp:104-112,
+src/sort_algo.h:147-165).  One step = one full sort() of an encrypted input
+already resident in HBM (constructRank + rotationIndexCheckN); keys, the
+input encryption and the public plaintext masks are produced before timing.
+
+Multi-GPU (torchrun, one process per GPU): the 32 comparator batches of
+constructRank and the 32 index-check batches of rotationIndexCheckN are
+sharded over ranks (batch b -> rank b % world); the partial ranks/outputs are
+summed by one RCCL all-reduce each (u64 sum + mod q) -- strong scaling.
+
+Output: one JSON line.  value = ciphertext-mults/s (relinearised ct x ct
+products, incl. those in the Chebyshev PS, summed over ranks / wall time);
+ms_per_step = sort wall time.  Also: roofline of the dominant kernel (HIP
+events on the engine stream) and the CPU-oracle baseline (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'fhe-sorting_amd'))
+
+import fhesort as F  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=2)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--n-sort', type=int, default=1024)
+    ap.add_argument('--log-n', type=int, default=16)
+    ap.add_argument('--seed', type=int, default=20250704)
+    ap.add_argument('--scale-bits', type=int, default=50,
+                    help='scaling-prime size; 40 (the reference) leaves the N>=128 sort noise-limited, DESIGN.md §6')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-sample-mults', type=int, default=0, help='override CPU sample size')
+    return ap.parse_args()
+
+
+def sign_cfg(N):  # tests/DirectSortTest.cpp:104-112
+    if N <= 16:
+        return (3, 2, 2)
+    if N <= 128:
+        return (3, 3, 2)
+    if N <= 512:
+        return (3, 4, 2)
+    return (3, 5, 2)
+
+
+class Dist:
+    def __init__(self, world):
+        self.world = world
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local = int(os.environ.get('LOCAL_RANK', '0'))
+        self.pg = None
+        if world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            dist.init_process_group('gloo', rank=self.rank, world_size=world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def bcast_bytes(self, b):
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def max(self, v):
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v):
+        if self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def device_sync(ctx):
+    ctx.sync()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def roofline(ctx, level_limbs):
+    """Time the dominant kernel with HIP events on the engine stream."""
+    r = F.time_kernel(ctx, 'ks_inner', level_limbs, iters=20)
+    achieved = r['bytes'] / (r['avg_ms'] * 1e-3) / 1e9
+    return {'kernel': r['name'], 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+            'avg_us': round(r['avg_ms'] * 1e3, 2), 'algorithmic_bytes': r['bytes'], 'limbs': level_limbs}
+
+
+def cpu_baseline(logN, depth, N, sample_mults, scale_bits):
+    """CPU oracle (this repo's C++ restatement, OpenMP) on a bounded sample of
+    the same workload: the comparator of one constructRank batch
+    (CompositeSign(3,5,2): 35 relinearised products at ring 2^logN, depth 39)."""
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import pyoracle as O
+    orc = O.Context(logN, depth, scale_bits, 60, 3, seed=7)
+    rng = np.random.default_rng(1)
+    a = orc.encrypt(rng.uniform(0, 1, N), N)
+    b = orc.encrypt(rng.uniform(0, 1, N), N)
+    cfg = sign_cfg(N)
+    orc.reset_counters()
+    t = time.perf_counter()
+    if sample_mults and sample_mults < 35:
+        x = orc.sub(a, b)
+        for _ in range(sample_mults):
+            x = orc.square(x)
+        sample = f'{sample_mults} chained relinearised squarings at ring 2^{logN}, depth {depth}'
+    else:
+        orc.compare(a, b, *cfg)
+        sample = (f'one constructRank comparator batch: Comparison::compare with CompositeSign{cfg} '
+                  f'at ring 2^{logN}, depth {depth}')
+    dt = time.perf_counter() - t
+    c = orc.counters()
+    return {'value': round(c['hmult'] / dt, 3), 'unit': 'ciphertext-mults/s', 'cores': O.lib().orc_num_threads(),
+            'kind': 'port', 'sample': sample, 'seconds': round(dt, 2), 'hmults': c['hmult']}
+
+
+def main():
+    a = parse()
+    d = Dist(a.gpus)
+    N, logN = a.n_sort, a.log_n
+    depth, rots = F.size_parameters(N)
+    cfg = sign_cfg(N)
+    t0 = time.time()
+    ctx = F.Context(logN, depth, a.scale_bits, 60, 3, seed=a.seed, device=d.local)
+    ctx.gen_rotation_keys(rots)
+    if d.world > 1:
+        uid = d.bcast_bytes(F.Context.comm_unique_id() if d.rank == 0 else None)
+        ctx.comm_init(uid, d.rank, d.world)
+    x = np.random.default_rng(a.seed).permutation(N) / N  # getVectorWithMinDiff(N, 0, 1, 1/N)
+    ct = ctx.encrypt(x, N)
+    setup_s = time.time() - t0
+    shard = (d.rank, d.world)
+
+    out = None
+    for _ in range(a.warmup):
+        out = ctx.direct_sort(ct, N, rots, cfg, shard=shard)
+    device_sync(ctx)
+    d.barrier()
+    ctx.reset_counters()
+    device_sync(ctx)
+    d.barrier()
+    t = time.perf_counter()
+    for _ in range(a.steps):
+        out = ctx.direct_sort(ct, N, rots, cfg, shard=shard)
+    device_sync(ctx)
+    d.barrier()
+    dt = time.perf_counter() - t
+    dt = d.max(dt)
+    cnt = ctx.counters()
+    hm_total = d.sum(cnt['hmult'])
+    ks_total = d.sum(cnt['keyswitch'])
+
+    res = None
+    if d.rank == 0:
+        y = ctx.decrypt(out)
+        max_err = float(np.max(np.abs(y - np.sort(x))))
+        ms = dt / a.steps * 1e3
+        res = {
+            'metric': 'encrypted sort seconds + ciphertext-mults/sec, N=1024 @ ringDim 2^16',
+            'value': round(hm_total / dt, 2),
+            'unit': 'ciphertext-mults/s',
+            'n_gpus': d.world,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': round(ms, 2),
+            'sort_seconds': round(ms / 1e3, 4),
+            'keyswitches_per_s': round(ks_total / dt, 2),
+            'higher_is_better': True,
+            'scaling': 'strong',
+            'vs_baseline': None,
+            'dtype': 'u64',
+            'data': 'synthetic: seeded permutation of {k/N}, keys and encryption from a seeded PRNG',
+            'config': {'workload': f'DirectSort N={N}, ringDim 2^{logN}, depth {depth}, scale 2^{a.scale_bits}, '
+                                   f'{len(rots)} rotation keys, CompositeSign{cfg}, dnum 3',
+                       'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'parallelism': f'batch-shard x{d.world}'},
+            'max_abs_err': max_err,
+            'output_level': out.level,
+            'hmult_per_sort': int(hm_total / a.steps),
+            'setup_s': round(setup_s, 1),
+        }
+        try:
+            res['roofline'] = roofline(ctx, depth + 1)
+        except Exception as e:  # never hide the main number
+            res['roofline'] = {'error': str(e)}
+        if d.world == 1 and not a.no_cpu_baseline:
+            try:
+                res['cpu_baseline'] = cpu_baseline(logN, depth, N, a.cpu_sample_mults, a.scale_bits)
+            except Exception as e:
+                res['cpu_baseline'] = {'error': str(e)}
+        print(json.dumps(res), flush=True)
+    d.barrier()
+
+
+if __name__ == '__main__':
+    main()

@@ -364,5 +364,11 @@ int fhe_reset_counters(fhe_ctx *ctx) {
 }
 int fhe_sync(fhe_ctx *ctx) { return guard([&] { ctx->eng->sync(); }); }
 void *fhe_stream(fhe_ctx *ctx) { return ctx ? ctx->eng->stream_handle() : nullptr; }
+int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double *avg_ms, double *bytes) {
+    return guard([&] {
+        NEED(name);
+        ctx->eng->time_kernel(name, (size_t)limbs, iters, *avg_ms, *bytes);
+    });
+}
 
 }  // extern "C"

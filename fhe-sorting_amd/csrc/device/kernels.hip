@@ -2,12 +2,7 @@
 //
 // Everything here is 64-bit integer modular arithmetic (no MFMA: the hot path
 // is HBM/VALU-bound integer work).  Design notes:
-//   * NTT (n = 2^logN, 12 <= logN <= 17) is split into two LDS-staged passes
-//     n = R1 x R2 ("column" pass over the top k1 index bits, "row" pass over
-//     the low k2 bits); each pass keeps a 32 KiB tile in LDS and runs all its
-//     radix-2 stages there, so a limb crosses HBM twice per transform.
-//     Column tiles are C >= 8 adjacent columns wide, so every global access is
-//     a >= 64 B contiguous segment per row.
+//   * the NTT lives in ntt.hip (register-blocked, two passes per transform).
 //   * element-wise kernels move 16 B per lane (ulonglong2) and are launched
 //     3-D: x = coefficient blocks, y = limb (prime), z = polynomial segment.
 //   * basis conversions (ModUp / ModDown) hold the source residues of one
@@ -21,161 +16,11 @@ namespace dev {
 
 namespace {
 
-constexpr int TILE = 4096;  // u64 elements per LDS tile (32 KiB)
 constexpr int NT = 256;     // threads per block
 constexpr int MAXSRC = 16;  // max limbs per digit / special primes held in registers
 constexpr int TCH = 8;      // target limbs per thread in basis conversions
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
-
-// ----------------------------------------------------------------- NTT ----
-__global__ __launch_bounds__(NT) void k_ntt_fwd_cols(u64 *data, size_t seg, const int *pmap, int logN, int k1,
-                                                     int C, NttTables T) {
-    __shared__ u64 tile[TILE];
-    const int R1 = 1 << k1, k2 = logN - k1, R2 = 1 << k2;
-    const size_t n = (size_t)1 << logN;
-    const int limb = blockIdx.y;
-    const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n;
-    const int lo0 = blockIdx.x * C;
-    const u64 q = T.mods[p].q;
-    const u64 *tw = T.fwd + (size_t)p * n, *tws = T.fwd_s + (size_t)p * n;
-    const int lgC = __builtin_ctz(C);
-    for (int idx = lane_id(); idx < C * R1; idx += NT) {
-        const int r = idx >> lgC, c = idx & (C - 1);
-        tile[idx] = a[(size_t)r * R2 + lo0 + c];
-    }
-    __syncthreads();
-    for (int s = 0; s < k1; ++s) {
-        const int lgt = k1 - 1 - s;
-        const int t = 1 << lgt;
-        for (int b = lane_id(); b < (C * R1) >> 1; b += NT) {
-            const int c = b & (C - 1), pp = b >> lgC;
-            const int g = pp >> lgt, o = pp & (t - 1);
-            const int r0 = (g << (lgt + 1)) + o;
-            const u64 W = tw[(1 << s) + g], Wp = tws[(1 << s) + g];
-            const int i0 = (r0 << lgC) + c, i1 = ((r0 + t) << lgC) + c;
-            const u64 U = tile[i0];
-            const u64 V = mul_shoup(tile[i1], W, Wp, q);
-            tile[i0] = add_mod(U, V, q);
-            tile[i1] = sub_mod(U, V, q);
-        }
-        __syncthreads();
-    }
-    for (int idx = lane_id(); idx < C * R1; idx += NT) {
-        const int r = idx >> lgC, c = idx & (C - 1);
-        a[(size_t)r * R2 + lo0 + c] = tile[idx];
-    }
-}
-
-__global__ __launch_bounds__(NT) void k_ntt_fwd_rows(u64 *data, size_t seg, const int *pmap, int logN, int k1,
-                                                     int ROWS, NttTables T) {
-    __shared__ u64 tile[TILE];
-    const int k2 = logN - k1, R2 = 1 << k2;
-    const size_t n = (size_t)1 << logN;
-    const int limb = blockIdx.y;
-    const int p = pmap ? pmap[limb] : limb;
-    const int row0 = blockIdx.x * ROWS;
-    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n + (size_t)row0 * R2;
-    const u64 q = T.mods[p].q;
-    const u64 *tw = T.fwd + (size_t)p * n, *tws = T.fwd_s + (size_t)p * n;
-    const int cnt = ROWS * R2;
-    for (int idx = lane_id(); idx < cnt; idx += NT) tile[idx] = a[idx];
-    __syncthreads();
-    for (int sl = 0; sl < k2; ++sl) {
-        const int s = k1 + sl;
-        const int lgt = k2 - 1 - sl;
-        const int t = 1 << lgt;
-        for (int b = lane_id(); b < cnt >> 1; b += NT) {
-            const int row = b >> (k2 - 1), pp = b & ((R2 >> 1) - 1);
-            const int g = pp >> lgt, o = pp & (t - 1);
-            const int c0 = (g << (lgt + 1)) + o;
-            const int widx = (1 << s) + ((row0 + row) << sl) + g;
-            const u64 W = tw[widx], Wp = tws[widx];
-            const int i0 = row * R2 + c0, i1 = i0 + t;
-            const u64 U = tile[i0];
-            const u64 V = mul_shoup(tile[i1], W, Wp, q);
-            tile[i0] = add_mod(U, V, q);
-            tile[i1] = sub_mod(U, V, q);
-        }
-        __syncthreads();
-    }
-    for (int idx = lane_id(); idx < cnt; idx += NT) a[idx] = tile[idx];
-}
-
-__global__ __launch_bounds__(NT) void k_ntt_inv_rows(u64 *data, size_t seg, const int *pmap, int logN, int k1,
-                                                     int ROWS, NttTables T) {
-    __shared__ u64 tile[TILE];
-    const int k2 = logN - k1, R2 = 1 << k2;
-    const size_t n = (size_t)1 << logN;
-    const int limb = blockIdx.y;
-    const int p = pmap ? pmap[limb] : limb;
-    const int row0 = blockIdx.x * ROWS;
-    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n + (size_t)row0 * R2;
-    const u64 q = T.mods[p].q;
-    const u64 *tw = T.inv + (size_t)p * n, *tws = T.inv_s + (size_t)p * n;
-    const int cnt = ROWS * R2;
-    for (int idx = lane_id(); idx < cnt; idx += NT) tile[idx] = a[idx];
-    __syncthreads();
-    for (int sl = 0; sl < k2; ++sl) {
-        const int lgt = sl;  // tt = 2^sl
-        const int t = 1 << lgt;
-        const size_t m = n >> (sl + 1);
-        for (int b = lane_id(); b < cnt >> 1; b += NT) {
-            const int row = b >> (k2 - 1), pp = b & ((R2 >> 1) - 1);
-            const int g = pp >> lgt, o = pp & (t - 1);
-            const int c0 = (g << (lgt + 1)) + o;
-            const size_t i = ((size_t)(row0 + row) << (k2 - 1 - sl)) + g;
-            const u64 W = tw[m + i], Wp = tws[m + i];
-            const int i0 = row * R2 + c0, i1 = i0 + t;
-            const u64 U = tile[i0], V = tile[i1];
-            tile[i0] = add_mod(U, V, q);
-            tile[i1] = mul_shoup(sub_mod(U, V, q), W, Wp, q);
-        }
-        __syncthreads();
-    }
-    for (int idx = lane_id(); idx < cnt; idx += NT) a[idx] = tile[idx];
-}
-
-__global__ __launch_bounds__(NT) void k_ntt_inv_cols(u64 *data, size_t seg, const int *pmap, int logN, int k1,
-                                                     int C, NttTables T) {
-    __shared__ u64 tile[TILE];
-    const int R1 = 1 << k1, k2 = logN - k1, R2 = 1 << k2;
-    const size_t n = (size_t)1 << logN;
-    const int limb = blockIdx.y;
-    const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n;
-    const int lo0 = blockIdx.x * C;
-    const u64 q = T.mods[p].q;
-    const u64 *tw = T.inv + (size_t)p * n, *tws = T.inv_s + (size_t)p * n;
-    const int lgC = __builtin_ctz(C);
-    for (int idx = lane_id(); idx < C * R1; idx += NT) {
-        const int r = idx >> lgC, c = idx & (C - 1);
-        tile[idx] = a[(size_t)r * R2 + lo0 + c];
-    }
-    __syncthreads();
-    for (int sc = 0; sc < k1; ++sc) {
-        const int lgt = sc;
-        const int t = 1 << lgt;
-        const size_t m = n >> (k2 + sc + 1);
-        for (int b = lane_id(); b < (C * R1) >> 1; b += NT) {
-            const int c = b & (C - 1), pp = b >> lgC;
-            const int g = pp >> lgt, o = pp & (t - 1);
-            const int r0 = (g << (lgt + 1)) + o;
-            const u64 W = tw[m + g], Wp = tws[m + g];
-            const int i0 = (r0 << lgC) + c, i1 = ((r0 + t) << lgC) + c;
-            const u64 U = tile[i0], V = tile[i1];
-            tile[i0] = add_mod(U, V, q);
-            tile[i1] = mul_shoup(sub_mod(U, V, q), W, Wp, q);
-        }
-        __syncthreads();
-    }
-    const u64 ni = T.ninv[p], nis = T.ninv_s[p];
-    for (int idx = lane_id(); idx < C * R1; idx += NT) {
-        const int r = idx >> lgC, c = idx & (C - 1);
-        a[(size_t)r * R2 + lo0 + c] = mul_shoup(tile[idx], ni, nis, q);
-    }
-}
 
 // --------------------------------------------------------- element-wise ----
 // grid: x = n / (2 NT), y = limb, z = segment; 2 coefficients per lane
@@ -499,37 +344,9 @@ inline dim3 pt_grid(int logN, int y, int z) {
     const size_t n = (size_t)1 << logN;
     return dim3((unsigned)((n + NT - 1) / NT), (unsigned)y, (unsigned)z);
 }
-inline void split(int logN, int &k1, int &C, int &ROWS) {
-    k1 = (logN + 1) / 2;
-    const int k2 = logN - k1;
-    C = std::min(1 << k2, TILE >> k1);
-    ROWS = std::min(1 << k1, TILE >> k2);
-}
-
 }  // namespace
 
 // ============================================================ wrappers =====
-void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
-    if (limbs <= 0 || segs <= 0) return;
-    int k1, C, ROWS;
-    split(T.logN, k1, C, ROWS);
-    const int k2 = T.logN - k1;
-    hipLaunchKernelGGL(k_ntt_fwd_cols, dim3((1 << k2) / C, limbs, segs), dim3(NT), 0, st, data, seg, pmap, T.logN, k1,
-                       C, T);
-    hipLaunchKernelGGL(k_ntt_fwd_rows, dim3((1 << k1) / ROWS, limbs, segs), dim3(NT), 0, st, data, seg, pmap, T.logN,
-                       k1, ROWS, T);
-}
-void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
-    if (limbs <= 0 || segs <= 0) return;
-    int k1, C, ROWS;
-    split(T.logN, k1, C, ROWS);
-    const int k2 = T.logN - k1;
-    hipLaunchKernelGGL(k_ntt_inv_rows, dim3((1 << k1) / ROWS, limbs, segs), dim3(NT), 0, st, data, seg, pmap, T.logN,
-                       k1, ROWS, T);
-    hipLaunchKernelGGL(k_ntt_inv_cols, dim3((1 << k2) / C, limbs, segs), dim3(NT), 0, st, data, seg, pmap, T.logN, k1,
-                       C, T);
-}
-
 void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
             hipStream_t st) {
     if (limbs <= 0) return;

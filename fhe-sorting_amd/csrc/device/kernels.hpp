@@ -17,8 +17,8 @@ namespace fhe {
 namespace dev {
 
 struct NttTables {
-    const u64 *fwd, *fwd_s;    // [nprimes][n] psi^brev(k) and Shoup companions
-    const u64 *inv, *inv_s;    // [nprimes][n] psi^-brev(k)
+    const ulonglong2 *fwd2;    // [nprimes][n] {psi^brev(k), Shoup companion}
+    const ulonglong2 *inv2;    // [nprimes][n] {psi^-brev(k), Shoup companion}
     const u64 *ninv, *ninv_s;  // [nprimes]
     const Mod *mods;           // [nprimes]
     int logN;

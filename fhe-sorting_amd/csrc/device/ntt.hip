@@ -1,0 +1,279 @@
+// Register-blocked negacyclic NTT for gfx950.
+//
+// n = 2^logN is split into a column pass over the top k1 index bits and a row
+// pass over the low k2 bits (k1 = ceil(logN/2)).  Each pass is a batch of
+// 2^PB-point transforms; one transform is owned by T = 2^(PB-EB) lanes that
+// each hold E = 2^EB coefficients in VGPRs:
+//   round 1: the E coefficients of a lane differ in the top EB index bits, so
+//            EB radix-2 stages run in registers with no LDS traffic;
+//   one LDS exchange (padded tile) re-deals the coefficients so that each lane
+//   owns 2^(PB-EB)-point groups differing in the low bits;
+//   round 2: the remaining PB-EB stages in registers.
+// A limb therefore crosses HBM twice per transform (one read + one write per
+// pass) and LDS once per pass.  Twiddles are psi^brev tables with Shoup
+// companions; round-1 twiddles of the column pass are wave-uniform.
+// The inverse runs the same machinery in Gentleman-Sande order (row pass first,
+// low bits first) and folds n^-1 into the final store.
+#include "kernels.hpp"
+
+namespace fhe {
+namespace dev {
+
+namespace {
+
+constexpr int NTB = 256;  // threads per block
+
+template <int PB>
+__device__ __forceinline__ int pad(int idx) {
+    return idx + (idx >> 4);  // one u64 of padding per 16 breaks power-of-two strides
+}
+
+// Harvey lazy forward CT butterfly: x, y in [0, 4q) -> x, y in [0, 4q)
+__device__ __forceinline__ void ct_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2) {
+    u64 u = x;
+    u = u >= q2 ? u - q2 : u;                        // [0, 2q)
+    const u64 v = mul_shoup_lazy(y, w.x, w.y, q2 >> 1);  // [0, 2q)
+    x = u + v;
+    y = u + q2 - v;
+}
+// lazy inverse GS butterfly: x, y in [0, 2q) -> x, y in [0, 2q)
+__device__ __forceinline__ void gs_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2) {
+    const u64 u = x, v = y;
+    u64 s = u + v;
+    x = s >= q2 ? s - q2 : s;
+    y = mul_shoup_lazy(u + q2 - v, w.x, w.y, q2 >> 1);
+}
+__device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0, q)
+    x = x >= q2 ? x - q2 : x;
+    return x >= q ? x - q : x;
+}
+
+// COLS: the transform index is a column `col`, element idx sits at idx * 2^k2 + col.
+// ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
+template <int PB, int EB, bool COLS>
+__global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const int *pmap, int logN, NttTables Tb) {
+    constexpr int E = 1 << EB;          // coefficients per lane
+    constexpr int RB = PB - EB;         // bits of round 2
+    constexpr int T = 1 << RB;          // lanes per transform
+    constexpr int NB = NTB / T;         // transforms per block
+    constexpr int G = E >> RB;          // round-2 groups per lane
+    constexpr int LEN = 1 << PB;
+    constexpr int STRIDE = LEN + (LEN >> 4);
+    __shared__ u64 tile[NB * STRIDE];
+
+    const size_t n = (size_t)1 << logN;
+    const int k2 = COLS ? logN - PB : 0;
+    const int limb = blockIdx.y;
+    const int p = pmap ? pmap[limb] : limb;
+    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n;
+    const u64 q = Tb.mods[p].q, q2 = 2 * q;
+    const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
+
+    int t, tr;  // lane within its transform, transform within the block
+    if (COLS) {
+        tr = threadIdx.x % NB;
+        t = threadIdx.x / NB;
+    } else {
+        tr = threadIdx.x / T;
+        t = threadIdx.x % T;
+    }
+    const size_t tid_global = (size_t)blockIdx.x * NB + tr;  // column or row index
+    const bool valid = tid_global < ((size_t)1 << (logN - PB));  // small rings: partial block
+    const int S0 = COLS ? 0 : logN - PB;                      // global stage of local stage 0
+
+    u64 x[E];
+    // ---- load, layout L1: idx = t + T * r
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int idx = t + T * r;
+        const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
+        x[r] = valid ? a[off] : 0;
+    }
+    // ---- round 1: local stages 0..EB-1
+#pragma unroll
+    for (int s = 0; s < EB; ++s) {
+        const int hb = EB - 1 - s;  // pair bit in r
+#pragma unroll
+        for (int r0 = 0; r0 < E; ++r0) {
+            if (r0 & (1 << hb)) continue;
+            const int idx0 = t + T * r0;
+            const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
+            const size_t wi = ((size_t)1 << (S0 + s)) + i;
+            ct_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2);
+        }
+    }
+    // ---- exchange through LDS: L1 -> L2 (idx = (t*G + g) * 2^RB + r)
+    u64 *tl = tile + tr * STRIDE;
+#pragma unroll
+    for (int r = 0; r < E; ++r) tl[pad<PB>(t + T * r)] = x[r];
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < T; ++r) x[g * T + r] = tl[pad<PB>((t * G + g) * T + r)];
+    // ---- round 2: local stages EB..PB-1 (pair bit PB-1-s < RB)
+#pragma unroll
+    for (int s = EB; s < PB; ++s) {
+        const int hb = PB - 1 - s;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r0 = 0; r0 < T; ++r0) {
+                if (r0 & (1 << hb)) continue;
+                const int idx0 = (t * G + g) * T + r0;
+                const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
+                const size_t wi = ((size_t)1 << (S0 + s)) + i;
+                ct_bfly(x[g * T + r0], x[g * T + r0 + (1 << hb)], tw[wi], q2);
+            }
+    }
+    // ---- store, layout L2
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < T; ++r) {
+            const int idx = (t * G + g) * T + r;
+            const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
+            if (valid) a[off] = COLS ? x[g * T + r] : canon4(x[g * T + r], q, q2);
+        }
+}
+
+// Inverse: global GS stage sg has pair distance 2^sg, twiddle psi^-brev(m + i),
+// m = n >> (sg + 1), i = j >> (sg + 1).  ROWS covers sg in [0, PB) (low bits),
+// COLS covers sg in [logN - PB, logN) and multiplies by n^-1 on the way out.
+template <int PB, int EB, bool COLS>
+__global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const int *pmap, int logN, NttTables Tb) {
+    constexpr int E = 1 << EB;
+    constexpr int RB = PB - EB;
+    constexpr int T = 1 << RB;
+    constexpr int NB = NTB / T;
+    constexpr int G = E >> RB;
+    constexpr int LEN = 1 << PB;
+    constexpr int STRIDE = LEN + (LEN >> 4);
+    __shared__ u64 tile[NB * STRIDE];
+
+    const size_t n = (size_t)1 << logN;
+    const int k2 = COLS ? logN - PB : 0;
+    const int limb = blockIdx.y;
+    const int p = pmap ? pmap[limb] : limb;
+    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n;
+    const u64 q = Tb.mods[p].q, q2 = 2 * q;
+    const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
+
+    int t, tr;
+    if (COLS) {
+        tr = threadIdx.x % NB;
+        t = threadIdx.x / NB;
+    } else {
+        tr = threadIdx.x / T;
+        t = threadIdx.x % T;
+    }
+    const size_t tid_global = (size_t)blockIdx.x * NB + tr;
+    const bool valid = tid_global < ((size_t)1 << (logN - PB));
+    const int SG0 = COLS ? logN - PB : 0;  // global GS stage of local stage 0
+
+    u64 x[E];
+    // ---- load, layout L2 (low bits within a lane group)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < T; ++r) {
+            const int idx = (t * G + g) * T + r;
+            const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
+            x[g * T + r] = valid ? a[off] : 0;
+        }
+    // ---- round A: local stages 0..RB-1 (pair bit s)
+#pragma unroll
+    for (int s = 0; s < RB; ++s) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r0 = 0; r0 < T; ++r0) {
+                if (r0 & (1 << s)) continue;
+                const int idx0 = (t * G + g) * T + r0;
+                const int sg = SG0 + s;
+                const size_t j = COLS ? 0 : tid_global * LEN;  // row offset (COLS: column bits vanish)
+                const size_t i = (j + (size_t)idx0 * (COLS ? ((size_t)1 << k2) : 1)) >> (sg + 1);
+                const size_t wi = (n >> (sg + 1)) + i;
+                gs_bfly(x[g * T + r0], x[g * T + r0 + (1 << s)], tw[wi], q2);
+            }
+    }
+    // ---- exchange L2 -> L1 (idx = t + T * r)
+    u64 *tl = tile + tr * STRIDE;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < T; ++r) tl[pad<PB>((t * G + g) * T + r)] = x[g * T + r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < E; ++r) x[r] = tl[pad<PB>(t + T * r)];
+    // ---- round B: local stages RB..PB-1 (pair bit s >= RB, i.e. bit s-RB of r)
+#pragma unroll
+    for (int s = RB; s < PB; ++s) {
+        const int hb = s - RB;
+#pragma unroll
+        for (int r0 = 0; r0 < E; ++r0) {
+            if (r0 & (1 << hb)) continue;
+            const int idx0 = t + T * r0;
+            const int sg = SG0 + s;
+            const size_t j = COLS ? 0 : tid_global * LEN;
+            const size_t i = (j + (size_t)idx0 * (COLS ? ((size_t)1 << k2) : 1)) >> (sg + 1);
+            const size_t wi = (n >> (sg + 1)) + i;
+            gs_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2);
+        }
+    }
+    // ---- store, layout L1 (COLS: times n^-1)
+    const u64 ni = Tb.ninv[p], nis = Tb.ninv_s[p];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int idx = t + T * r;
+        const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
+        if (valid) a[off] = COLS ? mul_shoup(x[r], ni, nis, q) : x[r];
+    }
+}
+
+template <int PB, int EB, bool COLS, bool FWD>
+void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
+    constexpr int NB = NTB >> (PB - EB);
+    const int count = 1 << (T.logN - PB);  // columns (COLS) or rows (ROWS)
+    const dim3 grid((unsigned)((count + NB - 1) / NB), (unsigned)limbs, (unsigned)segs);
+    if (FWD)
+        hipLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS>), grid, dim3(NTB), 0, st, data, seg, pmap, T.logN, T);
+    else
+        hipLaunchKernelGGL((k_ntt_inv<PB, EB, COLS>), grid, dim3(NTB), 0, st, data, seg, pmap, T.logN, T);
+}
+
+// pass bits -> (PB, EB): EB = ceil(PB / 2)
+template <bool COLS, bool FWD>
+void dispatch(int PB, u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
+              hipStream_t st) {
+    switch (PB) {
+    case 2: launch_pass<2, 1, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    case 3: launch_pass<3, 2, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    case 4: launch_pass<4, 2, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    case 5: launch_pass<5, 3, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    case 6: launch_pass<6, 3, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    case 7: launch_pass<7, 4, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    case 8: launch_pass<8, 4, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    case 9: launch_pass<9, 5, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    default: break;
+    }
+}
+
+}  // namespace
+
+void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
+    dispatch<true, true>(k1, data, limbs, segs, seg, pmap, T, st);
+    dispatch<false, true>(k2, data, limbs, segs, seg, pmap, T, st);
+}
+
+void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
+    dispatch<false, false>(k2, data, limbs, segs, seg, pmap, T, st);
+    dispatch<true, false>(k1, data, limbs, segs, seg, pmap, T, st);
+}
+
+}  // namespace dev
+}  // namespace fhe

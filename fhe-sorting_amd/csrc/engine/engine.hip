@@ -7,6 +7,7 @@
 #include <map>
 #include <mutex>
 #include <stdexcept>
+#include <functional>
 #include <thread>
 
 #include "../device/kernels.hpp"
@@ -209,7 +210,7 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
         mods[i] = Mod{m.q, m.mu, m.k, 0};
     }
     I.mods = I.upload_static(mods);
-    std::vector<u64> fwd(nall * n), fwd_s(nall * n), inv(nall * n), inv_s(nall * n), ninv(nall), ninv_s(nall);
+    std::vector<u64> fwd(2 * nall * n), inv(2 * nall * n), ninv(nall), ninv_s(nall);
     {
         std::vector<std::thread> th;
         const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -217,20 +218,20 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
             th.emplace_back([&, w]() {
                 for (size_t i = w; i < nall; i += nt) {
                     auto t = host::make_ntt_table(I.P.primes[i], logN);
-                    std::copy(t.fwd.begin(), t.fwd.end(), fwd.begin() + i * n);
-                    std::copy(t.fwd_s.begin(), t.fwd_s.end(), fwd_s.begin() + i * n);
-                    std::copy(t.inv.begin(), t.inv.end(), inv.begin() + i * n);
-                    std::copy(t.inv_s.begin(), t.inv_s.end(), inv_s.begin() + i * n);
+                    for (size_t k = 0; k < n; ++k) {  // interleaved {w, w'} pairs: one 16-B load
+                        fwd[2 * (i * n + k)] = t.fwd[k];
+                        fwd[2 * (i * n + k) + 1] = t.fwd_s[k];
+                        inv[2 * (i * n + k)] = t.inv[k];
+                        inv[2 * (i * n + k) + 1] = t.inv_s[k];
+                    }
                     ninv[i] = t.ninv;
                     ninv_s[i] = t.ninv_s;
                 }
             });
         for (auto &t : th) t.join();
     }
-    I.T.fwd = I.upload_static(fwd);
-    I.T.fwd_s = I.upload_static(fwd_s);
-    I.T.inv = I.upload_static(inv);
-    I.T.inv_s = I.upload_static(inv_s);
+    I.T.fwd2 = reinterpret_cast<const ulonglong2 *>(I.upload_static(fwd));
+    I.T.inv2 = reinterpret_cast<const ulonglong2 *>(I.upload_static(inv));
     I.T.ninv = I.upload_static(ninv);
     I.T.ninv_s = I.upload_static(ninv_s);
     I.T.mods = I.mods;
@@ -508,16 +509,18 @@ std::vector<double> Engine::decrypt(const Ciphertext &ct) {
     auto &I = *impl;
     if (!I.s_ntt) throw std::runtime_error("decrypt: no secret key");
     const size_t n = I.n();
-    auto mm = I.alloc(n * 8);
+    const int L2 = ct.limbs >= 2 ? 2 : 1;  // m = c0 + c1 s on the first one or two limbs
+    auto mm = I.alloc(L2 * n * 8);
     u64 *m = static_cast<u64 *>(mm->p);
-    dev::ew_mul_plain(m, ct.data + ct.limbs * n, static_cast<const u64 *>(I.s_ntt->p), 1, 1, 0, I.mods, I.P.logN,
+    dev::ew_mul_plain(m, ct.data + ct.limbs * n, static_cast<const u64 *>(I.s_ntt->p), L2, 1, 0, I.mods, I.P.logN,
                       I.st);
-    dev::ew_add(m, m, ct.data, 1, 1, 0, I.mods, I.P.logN, I.st);
-    dev::ntt_inverse(m, 1, 1, 0, nullptr, I.T, I.st);
-    std::vector<u64> h(n);
-    HIP_OK(hipMemcpyAsync(h.data(), m, n * 8, hipMemcpyDeviceToHost, I.st));
+    dev::ew_add(m, m, ct.data, L2, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ntt_inverse(m, L2, 1, 0, nullptr, I.T, I.st);
+    std::vector<u64> h(L2 * n);
+    HIP_OK(hipMemcpyAsync(h.data(), m, L2 * n * 8, hipMemcpyDeviceToHost, I.st));
     HIP_OK(hipStreamSynchronize(I.st));
-    return host::decode_coeffs(h.data(), n, I.P.primes[0], ct.slots, ct.scale);
+    return host::decode_coeffs(h.data(), L2 == 2 ? h.data() + n : nullptr, n, I.P.primes[0],
+                               L2 == 2 ? I.P.primes[1] : 0, ct.slots, ct.scale);
 }
 
 CtPtr Engine::upload(const u64 *h, size_t limbs, int level, int slots, double scale) {
@@ -848,6 +851,57 @@ void Engine::automorph_host(const u64 *in, size_t limbs, u64 g, u64 *out) {
     dev::ew_permute(static_cast<u64 *>(om->p), static_cast<u64 *>(im->p), I.perm(g), (int)limbs, 1, 0, LOGN, ST);
     HIP_OK(hipMemcpyAsync(out, om->p, limbs * nn * 8, hipMemcpyDeviceToHost, ST));
     HIP_OK(hipStreamSynchronize(ST));
+}
+
+void Engine::time_kernel(const std::string &name, size_t ell, int iters, double &avg_ms, double &bytes) {
+    auto &I = *impl;
+    const size_t nn = n(), K = (size_t)I.P.K, W = ell + K, B = nn * 8;
+    const int digits = I.P.digits_at(ell);
+    if (ell < 1 || ell > I.P.nq()) throw std::invalid_argument("time_kernel: bad limb count");
+    if (!I.relin) throw std::runtime_error("time_kernel: needs the relinearisation key");
+    // operands with random-looking contents (reduced residues)
+    auto dm = I.alloc(3 * ell * nn * 8);
+    auto em = I.alloc((size_t)digits * W * nn * 8);
+    auto am = I.alloc(2 * W * nn * 8);
+    u64 *d = static_cast<u64 *>(dm->p), *e = static_cast<u64 *>(em->p), *acc = static_cast<u64 *>(am->p);
+    HIP_OK(hipMemsetAsync(d, 0x11, 3 * ell * nn * 8, ST));
+    HIP_OK(hipMemsetAsync(e, 0x22, (size_t)digits * W * nn * 8, ST));
+    dev::ew_reduce(d, (int)ell, 3, ell * nn, MODS, LOGN, ST);
+    std::function<void()> launch;
+    if (name == "ks_inner") {
+        launch = [&] {
+            dev::ks_inner(acc, e, d, static_cast<u64 *>(I.relin->p), (int)ell, (int)K, (int)I.P.nq(), (int)I.P.nall(),
+                          I.P.alpha, digits, nullptr, I.ext(ell), MODS, LOGN, ST);
+        };
+        bytes = (double)((size_t)digits * W * 3 + 2 * W) * B;  // ext + key(b,a) read, 2 accumulators written
+    } else if (name == "ntt_fwd") {
+        launch = [&] { dev::ntt_forward(e, (int)W, digits, W * nn, I.ext(ell), I.T, ST); };
+        bytes = 2.0 * 2.0 * (double)(W * digits) * B;  // two passes, each reads + writes every limb
+    } else if (name == "modup_convert") {
+        launch = [&] {
+            dev::modup_convert(e, d, (int)ell, (int)K, I.P.alpha, digits, I.ext(ell), I.modup_tab,
+                               I.LT.modup_off[ell].data(), MODS, LOGN, ST);
+        };
+        bytes = (double)(ell + (size_t)digits * W - ell) * B;
+    } else if (name == "tensor") {
+        launch = [&] { dev::ew_tensor(d, acc, acc + ell * nn, (int)ell, MODS, LOGN, ST); };
+        bytes = 7.0 * (double)ell * B;
+    } else {
+        throw std::invalid_argument("time_kernel: unknown kernel " + name);
+    }
+    launch();  // warm
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, ST));
+    for (int i = 0; i < iters; ++i) launch();
+    HIP_OK(hipEventRecord(e1, ST));
+    HIP_OK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    avg_ms = (double)ms / iters;
 }
 
 }  // namespace fhe

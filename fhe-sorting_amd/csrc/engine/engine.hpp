@@ -116,6 +116,10 @@ class Engine {
     void modup_host(const u64 *d, size_t ell, u64 *ext);          // ext [digits][ell+K][n] NTT
     void moddown_host(const u64 *in, size_t ell, u64 *out);        // in [ell+K][n] -> [ell][n]
     void automorph_host(const u64 *in, size_t limbs, u64 g, u64 *out);
+    // time `iters` back-to-back launches of one kernel on the engine stream
+    // (HIP events), shaped like a key switch at `limbs` Q limbs; returns the
+    // average ms per launch and the algorithmic HBM bytes per launch.
+    void time_kernel(const std::string &name, size_t limbs, int iters, double &avg_ms, double &bytes);
 
     // small device scratch (for collectives / headers); copies are synchronous
     struct DevBuf {

@@ -284,13 +284,27 @@ std::vector<i64> encode_coeffs(const std::vector<double> &v, size_t n, int slots
     return coef;
 }
 
-std::vector<double> decode_coeffs(const u64 *m0, size_t n, u64 q0, int slots, double scale) {
+std::vector<double> decode_coeffs(const u64 *m0, const u64 *m1, size_t n, u64 q0, u64 q1, int slots,
+                                  double scale) {
     const Emb &E = emb_tables(n);
     const size_t gap = n / (2 * (size_t)slots);
-    auto centred = [q0](u64 x) { return x > q0 / 2 ? -(double)(q0 - x) : (double)x; };
+    // centred lift mod q0 (one limb) or mod q0*q1 (two limbs, CRT)
+    const Modulus M1(q1 ? q1 : 3);
+    const u64 q0inv = q1 ? invmod(q0 % q1, M1) : 0;
+    const u128 Q = (u128)q0 * (q1 ? q1 : 1);
+    auto centred = [&](size_t k) -> double {
+        if (!q1) {
+            const u64 x = m0[k];
+            return x > q0 / 2 ? -(double)(q0 - x) : (double)x;
+        }
+        const u64 a0 = m0[k], a1 = m1[k];
+        const u64 t = mulmod((a1 + q1 - a0 % q1) % q1, q0inv, M1);
+        const u128 x = (u128)a0 + (u128)q0 * t;
+        return x > Q / 2 ? -(double)(Q - x) : (double)x;
+    };
     std::vector<cd> z(slots);
     for (size_t i = 0; i < (size_t)slots; ++i)
-        z[i] = cd(centred(m0[i * gap]) / scale, centred(m0[i * gap + n / 2]) / scale);
+        z[i] = cd(centred(i * gap) / scale, centred(i * gap + n / 2) / scale);
     special_fft(z, E, n);
     std::vector<double> out(slots);
     for (size_t i = 0; i < (size_t)slots; ++i) out[i] = z[i].real();

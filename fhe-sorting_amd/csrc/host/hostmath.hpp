@@ -54,7 +54,9 @@ u64 galois_for_rotation(int logN, long k);
 
 // canonical embedding (special FFT, fp64) -> signed integer coefficients
 std::vector<i64> encode_coeffs(const std::vector<double> &v, size_t n, int slots, double scale);
-std::vector<double> decode_coeffs(const u64 *m0, size_t n, u64 q0, int slots, double scale);
+// m0 (and m1 when q1 != 0): message limbs in coefficient form; 2 limbs => CRT lift
+std::vector<double> decode_coeffs(const u64 *m0, const u64 *m1, size_t n, u64 q0, u64 q1, int slots,
+                                  double scale);
 
 // constants of the scale bookkeeping
 i64 const_to_target(double c, double delta_target, u64 q_dropped, double scale_in);

@@ -99,6 +99,7 @@ _SIGS = {
     'fhe_reset_counters': (C.c_int, [vp]),
     'fhe_sync': (C.c_int, [vp]),
     'fhe_stream': (vp, [vp]),
+    'fhe_time_kernel': (C.c_int, [vp, C.c_char_p, C.c_int, C.c_int, dp, dp]),
 }
 
 
@@ -385,6 +386,12 @@ class Context:
 
     def stream(self):
         return lib().fhe_stream(self.h)
+
+
+def time_kernel(ctx, name, limbs, iters=20):
+    ms, b = C.c_double(), C.c_double()
+    _chk(lib().fhe_time_kernel(ctx.h, name.encode(), limbs, iters, C.byref(ms), C.byref(b)))
+    return {'name': name, 'avg_ms': ms.value, 'bytes': b.value}
 
 
 def size_parameters(N):

@@ -169,6 +169,10 @@ int fhe_reset_counters(fhe_ctx *ctx);
 int fhe_sync(fhe_ctx *ctx);
 /* opaque hipStream_t of the context (for event timing by the caller) */
 void *fhe_stream(fhe_ctx *ctx);
+/* time `iters` launches of one hot kernel ("ks_inner", "ntt_fwd",
+ * "modup_convert", "tensor") with HIP events on the context stream, shaped as
+ * a key switch at `limbs` Q limbs: average ms and algorithmic bytes/launch */
+int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double *avg_ms, double *bytes);
 
 #ifdef __cplusplus
 }

@@ -179,6 +179,7 @@ class Context {
     // encode / decode
     Plaintext encode(const std::vector<double> &v, int slots, int level) const;
     std::vector<double> decode(const std::vector<u64> &m0_coeff_limb0, int slots, double scale) const;
+    std::vector<double> decode_real(const std::vector<double> &m_coeff, int slots, double scale) const;
     CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
     CtPtr encrypt_pt(const Plaintext &pt);
     std::vector<double> decrypt(const Ciphertext &ct);

@@ -564,13 +564,40 @@ CtPtr Context::encrypt(const std::vector<double> &v, int slots, int level) {
 }
 
 std::vector<double> Context::decrypt(const Ciphertext &ct) {
+    // m = c0 + c1 s on the first one or two limbs; two limbs -> CRT lift mod q0 q1
     const size_t n = P.n;
-    std::vector<u64> m(n);
+    const size_t L2 = ct.limbs >= 2 ? 2 : 1;
+    std::vector<u64> m(L2 * n);
     const u64 *c0 = ct.poly(0, n), *c1 = ct.poly(1, n);
-    for (size_t k = 0; k < n; ++k)
-        m[k] = mod_add(c0[k], mod_mul(c1[k], s_ntt[k], tab[0].mod), P.primes[0]);
-    ntt_inverse(m.data(), tab[0], n);
-    return decode(m, ct.slots, ct.scale);
+    for (size_t l = 0; l < L2; ++l) {
+        for (size_t k = 0; k < n; ++k)
+            m[l * n + k] = mod_add(c0[l * n + k], mod_mul(c1[l * n + k], s_ntt[l * n + k], tab[l].mod), P.primes[l]);
+        ntt_inverse(m.data() + l * n, tab[l], n);
+    }
+    if (L2 == 1) return decode(m, ct.slots, ct.scale);
+    const u64 q0 = P.primes[0], q1 = P.primes[1];
+    const u64 q0inv = mod_inv(q0 % q1, tab[1].mod);
+    const u128 Q = (u128)q0 * q1;
+    std::vector<double> lifted(n);
+    for (size_t k = 0; k < n; ++k) {
+        const u64 a0 = m[k], a1 = m[n + k];
+        const u64 t = mod_mul(mod_sub(a1, a0 % q1, q1), q0inv, tab[1].mod);
+        const u128 x = (u128)a0 + (u128)q0 * t;
+        lifted[k] = x > Q / 2 ? -(double)(Q - x) : (double)x;
+    }
+    return decode_real(lifted, ct.slots, ct.scale);
+}
+
+std::vector<double> Context::decode_real(const std::vector<double> &m, int slots, double scale) const {
+    const size_t n = P.n;
+    const EncTables &T = enc_tables(n);
+    const size_t gap = n / (2 * (size_t)slots);
+    std::vector<cd> vals(slots);
+    for (size_t i = 0; i < (size_t)slots; ++i) vals[i] = cd(m[i * gap] / scale, m[i * gap + n / 2] / scale);
+    emb(vals, T);
+    std::vector<double> out(slots);
+    for (size_t i = 0; i < (size_t)slots; ++i) out[i] = vals[i].real();
+    return out;
 }
 
 // ================================================================== ops ====

@@ -1,0 +1,35 @@
+"""GPU precision diagnostic: rank error, index-check error with exact ranks,
+and end-to-end sort error for DirectSort at ring 2^16, per scale size."""
+import os, sys, time, json
+import numpy as np
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'fhe-sorting_amd'))
+import fhesort as F
+
+def cfg_of(N):
+    return (3, 2, 2) if N <= 16 else (3, 3, 2) if N <= 128 else (3, 4, 2) if N <= 512 else (3, 5, 2)
+
+def run(N, sb, logN=16, cfg=None):
+    depth, rots = F.size_parameters(N)
+    cfg = cfg or cfg_of(N)
+    c = F.Context(logN, depth, sb, 60, 3, seed=11)
+    c.gen_rotation_keys(rots)
+    x = np.random.default_rng(20250704).permutation(N) / N
+    ct = c.encrypt(x, N)
+    exp = np.array([np.sum(x < v) for v in x], dtype=float)
+    t = time.time()
+    rank = c.direct_sort(ct, N, rots, cfg, mode=1)
+    r = c.decrypt(rank)
+    rk = c.encrypt(exp, N, level=rank.level)
+    o1 = c.direct_sort(ct, N, rots, cfg, mode=2, rank=rk)
+    o2 = c.direct_sort(ct, N, rots, cfg, mode=2, rank=rank)
+    res = dict(N=N, scale_bits=sb, cfg=cfg, rank_err=float(np.max(np.abs(r - exp))),
+               check_exact_rank_err=float(np.max(np.abs(c.decrypt(o1) - np.sort(x)))),
+               sort_err=float(np.max(np.abs(c.decrypt(o2) - np.sort(x)))), level=o2.level, depth=depth,
+               secs=round(time.time() - t, 2))
+    print(json.dumps(res), flush=True)
+
+if __name__ == '__main__':
+    for spec in sys.argv[1:]:
+        N, sb = spec.split(':')
+        run(int(N), int(sb))

@@ -1,0 +1,68 @@
+"""CPU checks of the drop-in boundary: the HIP library loads, exports every
+symbol include/fhe_gpu.h declares, and its pure-host entry points
+(Decomposer, size parameters) agree with the oracle and the reference's
+tables.  No GPU compute is issued here.
+"""
+import ctypes
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import fhesort as F
+import pyoracle as O
+
+
+def declared_symbols():
+    src = open(F.HEADER).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(fhe_[a-z0-9_]+)\s*\(', src)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_symbols()
+    for must in ('fhe_ctx_create', 'fhe_ctx_load_keys', 'fhe_ct_upload', 'fhe_ct_download', 'fhe_mul_relin',
+                 'fhe_rotate', 'fhe_rotate_hoisted', 'fhe_cheb_ps', 'fhe_sign_composite', 'fhe_compare',
+                 'fhe_indicator', 'fhe_direct_sort', 'fhe_comm_init', 'fhe_ct_allreduce', 'fhe_ntt', 'fhe_modup',
+                 'fhe_moddown', 'fhe_automorph'):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(F.LIB_PATH)
+    missing = [n for n in declared_symbols() if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(['nm', '-D', '--defined-only', F.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r' T (fhe_[a-z0-9_]+)', out))
+    assert set(declared_symbols()) <= exported
+
+
+def test_library_has_gfx950_code_objects():
+    data = open(F.LIB_PATH, 'rb').read()
+    assert b'gfx950' in data
+    assert b'k_ntt_fwd_cols' in data and b'k_ks_inner' in data
+
+
+def test_binding_loads_without_gpu():
+    F.lib()  # binds every signature; no HIP call issued
+
+
+@pytest.mark.parametrize('N', [4, 8, 16, 32, 64, 128, 256, 512, 1024])
+def test_size_parameters_match_oracle(N):
+    assert F.size_parameters(N) == O.size_parameters(N)
+
+
+def test_decomposer_matches_oracle():
+    rng = np.random.default_rng(0)
+    for N in (128, 1024):
+        _, rots = O.size_parameters(N)
+        for r in rng.integers(1, 4 * N, size=40):
+            for algo in (F.NAF, F.BNAF, F.BINARY):
+                assert F.decompose(N, rots, int(r), N * N // 2, algo) == O.decompose(N, rots, int(r), N * N // 2, algo)
+
+
+def test_errors_cross_as_status_codes():
+    with pytest.raises(F.FheError) as e:
+        F.size_parameters(3)
+    assert e.value.code == F.FHE_EINVAL

@@ -1,0 +1,281 @@
+"""CPU tests of the oracle (test infrastructure) — pins it before it is
+trusted as the GPU engine's checker.
+
+Pins, in order of strength:
+  1. big-integer golden vectors (tests/golden/, generated from the math by
+     make_golden.py): NTT evaluation points/order, negacyclic products,
+     coefficient-domain automorphisms;
+  2. exact properties: fast basis conversion = x + u*Q with 0 <= u < |digit|,
+     ModDown = round-free division by P up to the conversion error;
+  3. the reference's own tests and tolerances, restated:
+       DecomposeTest.cpp:64-74, SignTest.cpp:41-122, CompareTest.cpp:43-63,
+       RotationTest.cpp:63-130, SincTest.cpp (indicator on k/(2N)),
+       DirectSortTest.cpp:90-170, DirectSortNTest.cpp:61-285.
+OpenFHE itself is not available, so ciphertext-level parity with the
+reference is "parity unpinned" (DESIGN.md §6).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+# ---------------------------------------------------------------- golden ---
+@pytest.mark.parametrize('case', load('ntt_golden.json'), ids=lambda c: f"logN{c['logN']}")
+def test_ntt_golden(case):
+    logN = case['logN']
+    ctx = O.Context(logN, 1, 40, 60, 3, seed=1, keygen=False)
+    q = int(case['q'])
+    assert int(ctx.primes[0]) == q
+    assert ctx.psi(0) == int(case['psi'])
+    a = np.array([int(v) for v in case['a']], dtype=np.uint64)
+    b = np.array([int(v) for v in case['b']], dtype=np.uint64)
+    A = ctx.ntt(0, a)
+    assert [int(v) for v in A] == [int(v) for v in case['ntt_a']]
+    assert np.array_equal(ctx.ntt(0, A, inverse=True), a)
+    B = ctx.ntt(0, b)
+    prod = np.array([(int(x) * int(y)) % q for x, y in zip(A, B)], dtype=np.uint64)
+    assert [int(v) for v in ctx.ntt(0, prod, inverse=True)] == [int(v) for v in case['negacyclic_ab']]
+
+
+@pytest.mark.parametrize('case', load('automorph_golden.json'), ids=lambda c: f"k{c['k']}")
+def test_automorphism_golden(case):
+    logN = case['logN']
+    ctx = O.Context(logN, 1, 40, 60, 3, seed=1, keygen=False)
+    assert int(ctx.primes[0]) == int(case['q'])
+    assert O.galois(logN, case['k']) == case['galois']
+    a = np.array([int(v) for v in case['a']], dtype=np.uint64)
+    perm = O.automorph_perm(logN, case['galois'])
+    got = ctx.ntt(0, ctx.ntt(0, a)[perm], inverse=True)
+    assert [int(v) for v in got] == [int(v) for v in case['sigma_a']]
+
+
+def test_sinc_coefficients_reproduce_indicator():
+    # SincTest.cpp:75-229 semantics: doubled sinc ~ [k == 0 or k == -N] on k/(2N)
+    for case in load('sinc_golden.json'):
+        N = case['N']
+        c = O.doubled_sinc(N)
+        x = np.array(case['x'])
+        f = np.array(case['f'])
+        approx = np.polynomial.chebyshev.chebval(x, np.concatenate([[c[0] / 2], c[1:]]))
+        assert np.max(np.abs(approx - f)) < 1e-3
+        ind = np.isclose(x * 2 * N, 0) | np.isclose(x * 2 * N, -N)
+        assert np.max(np.abs(approx - ind)) < 0.01
+
+
+def test_sinc_degrees():
+    # degree of the truncated degree-13011 fit (utils/generate_cheb_doubled_coeffs.cpp:14-36)
+    assert {N: len(O.doubled_sinc(N)) for N in (8, 128, 1024)} == {8: 71, 128: 849, 1024: 6511}
+
+
+# ----------------------------------------------------------------- params --
+def test_params_scale_stays_put():
+    ctx = O.Context(12, 39, 40, 60, 3, seed=1, keygen=False)
+    assert ctx.nq == 40 and ctx.alpha == 14 and ctx.K == 10
+    assert np.all(np.abs(np.log2(ctx.delta) - 40) < 1e-3)  # no scale drift down the chain
+    assert len(set(int(p) for p in ctx.primes)) == len(ctx.primes)
+    assert all(int(p) % (2 * 4096) == 1 for p in ctx.primes)
+
+
+def test_modup_is_exact_basis_extension():
+    ctx = O.Context(6, 5, 40, 60, 3, seed=1, keygen=False)
+    rng = np.random.default_rng(0)
+    ell = 5
+    primes = [int(p) for p in ctx.primes]
+    d = np.stack([rng.integers(0, primes[i], size=ctx.n, dtype=np.uint64) for i in range(ell)])
+    ext = ctx.modup(d)
+    coef = np.stack([ctx.ntt(i, d[i], inverse=True) for i in range(ell)])
+    tgt = list(range(ell)) + list(range(ctx.nq, ctx.nq + ctx.K))
+    for j in range((ell + ctx.alpha - 1) // ctx.alpha):
+        lo, hi = j * ctx.alpha, min(ell, (j + 1) * ctx.alpha)
+        Qj = 1
+        for i in range(lo, hi):
+            Qj *= primes[i]
+        for t_idx, pt in enumerate(tgt):
+            if lo <= t_idx < hi:
+                assert np.array_equal(ext[j, t_idx], d[t_idx])
+                continue
+            out = ctx.ntt(pt, ext[j, t_idx], inverse=True)
+            for k in range(0, ctx.n, 7):
+                X = 0  # CRT of the digit residues
+                for i in range(lo, hi):
+                    qh = Qj // primes[i]
+                    X += int(coef[i, k]) * qh * pow(qh, -1, primes[i])
+                X %= Qj
+                diff = (int(out[k]) - X) % primes[pt]
+                assert any(diff == (u * Qj) % primes[pt] for u in range(hi - lo)), (j, t_idx, k)
+
+
+# ---------------------------------------------------------- decomposer -----
+def test_decompose_compose_match():
+    # tests/DecomposeTest.cpp:64-74
+    rots = [1, 2, 4, 8, 16, 32, 64]
+    for num in [1, 2, 3, 4, 7, 8, 15, 16, 31, 32, 63, 64, 65, 127, 128]:
+        for algo in (O.NAF, O.BNAF, O.BINARY):
+            steps = O.decompose(128, rots, num, 128, algo)
+            assert sum(s for _, s in steps) == num, (num, algo, steps)
+
+
+def test_decompose_directsort_steps():
+    _, rots = O.size_parameters(1024)
+    assert O.decompose(1024, rots, 40, 32768, O.BINARY) == [(1, 32), (1, 8)]
+    assert O.decompose(1024, rots, 1016, 32768, O.BINARY) == [(1, 512), (1, 256), (1, 128), (1, 64),
+                                                               (1, 32), (1, 16), (1, 8)]
+
+
+def test_size_parameters_table():
+    # src/sort_algo.h:87-201
+    exp = {4: 23, 8: 24, 16: 25, 32: 28, 64: 29, 128: 30, 256: 34, 512: 35, 1024: 39}
+    for N, d in exp.items():
+        depth, rots = O.size_parameters(N)
+        assert depth == d
+    assert len(O.size_parameters(128)[1]) == 30
+    assert len(O.size_parameters(1024)[1]) == 161
+    with pytest.raises(ValueError):
+        O.size_parameters(3)
+
+
+# --------------------------------------------------------- ciphertexts -----
+@pytest.fixture(scope='module')
+def ctx30():
+    c = O.Context(12, 30, 50, 60, 3, seed=3)
+    c.gen_rotation_keys([-1, -2, -4, -8, -16, -32, 1, 2, 4, 8, 16, 32, 64, 512])
+    return c
+
+
+def test_encrypt_decrypt_roundtrip(ctx30):
+    x = np.random.default_rng(1).uniform(-5, 5, 64)
+    assert np.max(np.abs(ctx30.decrypt(ctx30.encrypt(x, 64)) - x)) < 1e-9
+
+
+def test_composite_sign3_signtest(ctx30):
+    # tests/SignTest.cpp:41-80: compositeSign<3>(dg=0, df=1)
+    x = np.array([0.5, -0.3, 0.1, -0.7, 0.0, 0.8, -0.9, 0.2])
+    y = ctx30.decrypt(ctx30.sign(ctx30.encrypt(x, 8), 3, 0, 1))
+    # plaintext model of g3 then f3 (the composition the reference evaluates)
+    g = lambda t: (4589 * t - 16577 * t**3 + 25614 * t**5 - 12860 * t**7) / 1024
+    f = lambda t: (35 * t - 35 * t**3 + 21 * t**5 - 5 * t**7) / 16
+    assert np.max(np.abs(y - f(g(x)))) < 1e-6
+    assert np.all(np.sign(y[x != 0]) == np.sign(x[x != 0])) and abs(y[4]) < 0.1
+    # the reference expects +-1 within 0.1 everywhere; f3(g3(0.1)) = 0.788 mathematically,
+    # so that one element cannot meet it on any engine (documented in DESIGN.md §6)
+    far = np.abs(x) >= 0.2
+    assert np.max(np.abs(y[far] - np.sign(x[far]))) < 0.1
+
+
+def test_composite_sign4_small_inputs(ctx30):
+    # tests/SignTest.cpp:82-122: compositeSign<4>(3, 3)
+    x = np.array([0.02, -0.02, 0.01, -0.01, 0.009, -0.009, 1, -1])
+    y = ctx30.decrypt(ctx30.sign(ctx30.encrypt(x, 8), 4, 3, 3))
+    assert np.max(np.abs(y - np.sign(x))) < 0.1
+
+
+def test_compare_vectors():
+    # tests/CompareTest.cpp:43-63 (depth 50; scaling mod 50 instead of 59: our limbs cap at 58 bits)
+    c = O.Context(12, 50, 50, 60, 3, seed=4)
+    a = c.encrypt([1.0, 5.0, 3.0, 4.0], 4)
+    b = c.encrypt([2.0, 4.0, 3.0, 3.0], 4)
+    y = c.decrypt(c.compare(a, b, 4, 3, 3))
+    assert np.max(np.abs(y - [0.0, 1.0, 0.5, 1.0])) < 0.1
+
+
+def test_indicator(ctx30):
+    # Comparison::indicator: 1 iff |x| < c   (src/comparison.cpp:24-40)
+    x = np.array([0.0, 0.3, -0.3, 0.05, -0.05, 0.6, -0.6, 0.0])
+    y = ctx30.decrypt(ctx30.indicator(ctx30.encrypt(x, 8), 0.15, 3, 2, 2))
+    assert np.max(np.abs(y - (np.abs(x) < 0.15))) < 0.1
+
+
+def test_rotation_composer(ctx30):
+    # tests/RotationTest.cpp:63-130 (NAF composer, keys {+-1..+-32, 64, 512})
+    rots = [-1, -2, -4, -8, -16, -32, 1, 2, 4, 8, 16, 32, 64, 512]
+    x = np.random.default_rng(2).permutation(128) / 100
+    ct = ctx30.encrypt(x, 128)
+    for r in (-4, 3, -7, 100, -128, 127):
+        out = ctx30.compose_rotate(ct, 128, rots, O.NAF, r)
+        assert np.max(np.abs(ctx30.decrypt(out) - np.roll(x, -r))) < 1e-6
+        back = ctx30.compose_rotate(out, 128, rots, O.NAF, -r)
+        assert np.max(np.abs(ctx30.decrypt(back) - x)) < 1e-5
+
+
+def test_hoisted_equals_single(ctx30):
+    ct = ctx30.encrypt(np.arange(16) / 16.0, 16)
+    hs = ctx30.rotate_hoisted(ct, [1, 2, 4])
+    for h, k in zip(hs, [1, 2, 4]):
+        assert np.array_equal(h.data(), ctx30.rotate(ct, k).data())
+
+
+def test_missing_key_raises(ctx30):
+    with pytest.raises(RuntimeError, match='no rotation key'):
+        ctx30.rotate(ctx30.encrypt([1.0, 2.0], 2), 3)
+
+
+@pytest.mark.parametrize('deg', [2, 3, 5, 15, 60])
+def test_chebyshev_ps_depth_and_value(deg):
+    c = O.Context(11, 12, 40, 60, 3, seed=5)
+    x = np.linspace(-1, 1, 32)
+    ct = c.encrypt(x, 32)
+    co = np.random.default_rng(deg).normal(size=deg + 1)
+    y = c.cheb(ct, co)
+    ref = np.polynomial.chebyshev.chebval(x, np.concatenate([[co[0] / 2], co[1:]]))
+    assert np.max(np.abs(c.decrypt(y) - ref)) < 2e-6 * np.sum(np.abs(co))
+    assert y.level == int(np.ceil(np.log2(deg + 1)))  # depth-optimal PS
+
+
+# ------------------------------------------------------------ DirectSort ---
+def sort_cfg(N):
+    return (3, 2, 2) if N <= 16 else (3, 3, 2) if N <= 128 else (3, 4, 2) if N <= 512 else (3, 5, 2)
+
+
+@pytest.mark.parametrize('N', [4, 8, 16, 32])
+def test_direct_sort(N):
+    # tests/DirectSortTest.cpp:90-170 at ring 2^12 (reference: 2^17)
+    depth, rots = O.size_parameters(N)
+    c = O.Context(12, depth, 40, 60, 3, seed=200 + N)
+    c.gen_rotation_keys(rots)
+    x = np.random.default_rng(N).permutation(N) / N
+    out = c.direct_sort(c.encrypt(x, N), N, rots, sort_cfg(N))
+    y = c.decrypt(out)
+    assert np.max(np.abs(y - np.sort(x))) < 0.01
+    if N in (4, 8, 32):
+        assert out.level == depth  # EXPECT_EQ(level, multDepth), DirectSortTest.cpp:128
+    else:
+        assert out.level <= depth
+
+
+def test_direct_sort_multi_batch():
+    # N=64 at ring 2^11: num_partition=16, 4 comparator batches
+    N = 64
+    depth, rots = O.size_parameters(N)
+    c = O.Context(11, depth, 40, 60, 3, seed=7)
+    c.gen_rotation_keys(rots)
+    x = np.random.default_rng(64).permutation(N) / N
+    y = c.decrypt(c.direct_sort(c.encrypt(x, N), N, rots, sort_cfg(N)))
+    assert np.max(np.abs(y - np.sort(x))) < 0.01
+
+
+def test_construct_rank_and_index_check():
+    # tests/DirectSortNTest.cpp:61-285 (ranks, exact-rank and noisy-rank index check)
+    N = 8
+    depth, rots = O.size_parameters(N)
+    c = O.Context(12, depth, 40, 60, 3, seed=9)
+    c.gen_rotation_keys(rots)
+    x = np.random.default_rng(3).permutation(N) / N
+    ct = c.encrypt(x, N)
+    ranks = np.array([np.sum(x < v) for v in x], dtype=float)
+    r = c.decrypt(c.direct_sort(ct, N, rots, (3, 2, 2), mode=1))
+    assert np.max(np.abs(r - ranks)) < 1e-4
+    for noise in (0.0, 1e-3):
+        noisy = ranks + np.random.default_rng(5).uniform(-noise, noise, N)
+        out = c.direct_sort(ct, N, rots, (3, 2, 2), mode=2, rank=c.encrypt(noisy, N))
+        assert np.max(np.abs(c.decrypt(out) - np.sort(x))) < 0.01
