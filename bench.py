@@ -46,6 +46,7 @@ def parse():
     ap.add_argument('--scale-bits', type=int, default=50,
                     help='scaling-prime size; 40 (the reference) leaves the N>=128 sort noise-limited, DESIGN.md §6')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-roofline', action='store_true', help='skip the instrumented roofline sort (PMC passes)')
     ap.add_argument('--cpu-sample-mults', type=int, default=0, help='override CPU sample size')
     return ap.parse_args()
 
@@ -110,13 +111,33 @@ def device_sync(ctx):
         pass
 
 
-def roofline(ctx, level_limbs):
-    """Time the dominant kernel with HIP events on the engine stream."""
-    r = F.time_kernel(ctx, 'ks_inner', level_limbs, iters=20)
-    achieved = r['bytes'] / (r['avg_ms'] * 1e-3) / 1e9
-    return {'kernel': r['name'], 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-            'avg_us': round(r['avg_ms'] * 1e3, 2), 'algorithmic_bytes': r['bytes'], 'limbs': level_limbs}
+def roofline(ctx, run_once):
+    """Roofline of the dominant kernel, measured live: one more (untimed) sort
+    runs with every NTT pass bracketed by HIP events on the engine stream (the
+    stream it is launched on); the kernel template with the largest total time
+    is reported.  achieved = algorithmic bytes (one read + one write of every
+    limb the pass touches) / average launch duration.  traffic =
+    HBM bytes per launch from the committed rocprofv3 PMC pass (FETCH_SIZE x2 on
+    gfx950 + WRITE_SIZE), when profiles/ holds one for this kernel."""
+    with F.KernelClock(ctx) as clk:
+        run_once()
+    stats = clk.stats
+    name, st = max(stats.items(), key=lambda kv: kv[1]['ms'])
+    avg_s = st['ms'] / st['launches'] * 1e-3
+    per_launch = st['bytes'] / st['launches']
+    achieved = per_launch / avg_s / 1e9
+    traffic, src = None, None
+    pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            t = json.load(f).get(name)
+        if t:
+            traffic, src = t['hbm_bytes_per_launch'], 'profiles/pmc_traffic.json'
+    ntt_ms = sum(v['ms'] for v in stats.values())
+    return {'kernel': name, 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_source': src,
+            'avg_us': round(avg_s * 1e6, 2), 'launches': st['launches'],
+            'algorithmic_bytes_per_launch': per_launch, 'ntt_ms_per_sort': round(ntt_ms, 1)}
 
 
 def cpu_baseline(logN, depth, N, sample_mults, scale_bits):
@@ -211,10 +232,12 @@ def main():
             'hmult_per_sort': int(hm_total / a.steps),
             'setup_s': round(setup_s, 1),
         }
-        try:
-            res['roofline'] = roofline(ctx, depth + 1)
-        except Exception as e:  # never hide the main number
-            res['roofline'] = {'error': str(e)}
+        res['roofline'] = None
+        if not a.no_roofline:
+            try:
+                res['roofline'] = roofline(ctx, lambda: ctx.direct_sort(ct, N, rots, cfg, shard=(0, 1)))
+            except Exception as e:  # never hide the main number
+                res['roofline'] = {'error': str(e)}
         if d.world == 1 and not a.no_cpu_baseline:
             try:
                 res['cpu_baseline'] = cpu_baseline(logN, depth, N, a.cpu_sample_mults, a.scale_bits)

@@ -371,4 +371,19 @@ int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double
     });
 }
 
+int fhe_kernel_clock_start(fhe_ctx *ctx) {
+    return guard([&] { ctx->eng->kernel_clock_start(); });
+}
+int fhe_kernel_clock_stop(fhe_ctx *ctx, char *json, size_t cap, size_t *needed) {
+    return guard([&] {
+        const std::string s = ctx->eng->kernel_clock_stop();
+        if (needed) *needed = s.size() + 1;
+        if (json && cap) {
+            const size_t m = std::min(cap - 1, s.size());
+            std::memcpy(json, s.data(), m);
+            json[m] = 0;
+        }
+    });
+}
+
 }  // extern "C"

@@ -228,10 +228,12 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef,
 }
 
 // grid: x = n / NT, y = W targets
+// fold (HMult tail, may be null): on limb t = ell-1 the accumulators start at
+// P * (d0, d1)[ell-1], so the fused ModDown+rescale sees x = d P + acc there.
 __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
                                                  int ell, int W, int nall, int alpha, int digits,
                                                  const uint32_t *perm, const int *pmap_ext, const Mod *mods,
-                                                 int logN) {
+                                                 int logN, KsFold fold) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
@@ -240,6 +242,10 @@ __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const
     const Mod m = mods[pt];
     const size_t kk = perm ? perm[k] : k;
     u64 a0 = 0, a1 = 0;
+    if (fold.d && t == ell - 1) {
+        a0 = mul_shoup(fold.d[k], fold.w, fold.ws, m.q);
+        a1 = mul_shoup(fold.d[fold.seg + k], fold.w, fold.ws, m.q);
+    }
     for (int j = 0; j < digits; ++j) {
         const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
         const u64 x = (t >= lo && t < hi) ? dntt[(size_t)t * n + kk] : ext[((size_t)j * W + t) * n + kk];
@@ -301,6 +307,76 @@ __global__ __launch_bounds__(NT) void k_moddown_finish(u64 *out, const u64 *acc,
         r.x = add_mod(r.x, d.x, q);
         r.y = add_mod(r.y, d.y, q);
     }
+    *reinterpret_cast<ulonglong2 *>(out + (size_t)s * seg_out + lo) = r;
+}
+
+// ------------------------------------------- fused ModDown + rescale ----
+// HMult tail.  acc [2][W][n]: limbs < ell-1 NTT form; limb ell-1 (= x_last =
+// d_last P + acc_last) and the K special limbs already inverse-transformed.
+// corr_i = Conv_{P->q_i}(acc_P) + P * [y_last]_centred  for i < ell-1, where
+// y_last = (x_last - Conv_{P->q_last}(acc_P)) * P^-1 mod q_last is the last
+// limb of the ModDown output.  grid: x = n / NT, y = ceil((ell-1) / TCH), z = seg
+__global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq,
+                                                                size_t seg_acc, size_t seg_corr, const u64 *phinv,
+                                                                const u64 *phinv_s, const u64 *phat,
+                                                                const u64 *phat_s, const u64 *pinv,
+                                                                const u64 *pinv_s, const u64 *pmod,
+                                                                const u64 *pmod_s, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const int last = ell - 1;
+    const u64 *src = acc + (size_t)blockIdx.z * seg_acc + (size_t)last * n;
+    u64 *dst = corr + (size_t)blockIdx.z * seg_corr;
+    u64 v[MAXSRC];
+#pragma unroll
+    for (int i = 0; i < MAXSRC; ++i)
+        if (i < K) v[i] = mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+    const u64 ql = mods[last].q;
+    u64 cl = 0;
+#pragma unroll
+    for (int kk = 0; kk < MAXSRC; ++kk)
+        if (kk < K) {
+            const size_t ix = (size_t)kk * nq + last;
+            cl = add_mod(cl, mul_shoup(v[kk], phat[ix], phat_s[ix], ql), ql);
+        }
+    const u64 y = mul_shoup(sub_mod(src[k], cl, ql), pinv[last], pinv_s[last], ql);
+    const bool neg = y > (ql >> 1);
+    const int i0 = blockIdx.y * TCH;
+    for (int i = i0; i < i0 + TCH && i < last; ++i) {
+        const Mod mi = mods[i];
+        u64 a = 0;
+#pragma unroll
+        for (int kk = 0; kk < MAXSRC; ++kk)
+            if (kk < K) {
+                const size_t ix = (size_t)kk * nq + i;
+                a = add_mod(a, mul_shoup(v[kk], phat[ix], phat_s[ix], mi.q), mi.q);
+            }
+        u64 lift = reduce64(y, mi);
+        if (neg) lift = sub_mod(lift, reduce64(ql, mi), mi.q);
+        a = add_mod(a, mul_shoup(lift, pmod[i], pmod_s[i], mi.q), mi.q);
+        dst[(size_t)i * n + k] = a;
+    }
+}
+// out_i = (acc_i + d_i P - corr_i) * (P q_last)^-1, i < ell-1, NTT form.
+// grid: x = n / (2 NT), y = i, z = seg
+__global__ __launch_bounds__(NT) void k_mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr,
+                                                        size_t seg_out, size_t seg_acc, size_t seg_d,
+                                                        const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
+                                                        const u64 *pmod_s, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y, s = blockIdx.z;
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const u64 q = mods[l].q;
+    const size_t lo = (size_t)l * n + k;
+    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(acc + (size_t)s * seg_acc + lo);
+    const ulonglong2 dd = *reinterpret_cast<const ulonglong2 *>(d + (size_t)s * seg_d + lo);
+    const ulonglong2 c = *reinterpret_cast<const ulonglong2 *>(corr + (size_t)s * seg_out + lo);
+    const u64 w = pmod[l], ws = pmod_s[l], z = pqlinv[l], zs = pqlinv_s[l];
+    ulonglong2 r;
+    r.x = mul_shoup(sub_mod(add_mod(x.x, mul_shoup(dd.x, w, ws, q), q), c.x, q), z, zs, q);
+    r.y = mul_shoup(sub_mod(add_mod(x.y, mul_shoup(dd.y, w, ws, q), q), c.y, q), z, zs, q);
     *reinterpret_cast<ulonglong2 *>(out + (size_t)s * seg_out + lo) = r;
 }
 
@@ -430,11 +506,27 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
 }
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
-              hipStream_t st) {
+              hipStream_t st, KsFold fold) {
     (void)nq;
     const int W = ell + K;
     hipLaunchKernelGGL(k_ks_inner, pt_grid(logN, W, 1), dim3(NT), 0, st, acc, ext, dntt, key, ell, W, nall, alpha,
-                       digits, perm, pmap_ext, mods, logN);
+                       digits, perm, pmap_ext, mods, logN, fold);
+}
+void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
+                             int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
+                             const u64 *pinv, const u64 *pinv_s, const u64 *pmod, const u64 *pmod_s,
+                             const Mod *mods, int logN, hipStream_t st) {
+    if (ell <= 1) return;
+    hipLaunchKernelGGL(k_moddown_rescale_convert, pt_grid(logN, (ell - 1 + TCH - 1) / TCH, segs), dim3(NT), 0, st,
+                       corr, acc, ell, K, nq, seg_acc, seg_corr, phinv, phinv_s, phat, phat_s, pinv, pinv_s, pmod,
+                       pmod_s, mods, logN);
+}
+void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, int ell, int segs, size_t seg_out,
+                     size_t seg_acc, size_t seg_d, const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
+                     const u64 *pmod_s, const Mod *mods, int logN, hipStream_t st) {
+    if (ell <= 1) return;
+    hipLaunchKernelGGL(k_mul_tail_finish, ew_grid(logN, ell - 1, segs), dim3(NT), 0, st, out, acc, d, corr, seg_out,
+                       seg_acc, seg_d, pqlinv, pqlinv_s, pmod, pmod_s, mods, logN);
 }
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
                      const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s, const Mod *mods,

@@ -24,11 +24,25 @@ struct NttTables {
     int logN;
 };
 
+// Optional per-launch clock used by the bench roofline: while one is installed,
+// the NTT passes are bracketed by HIP events on the stream they launch on and
+// reported with their algorithmic bytes.  Process-global; diagnostics only.
+struct LaunchClock {
+    virtual ~LaunchClock() = default;
+    // events handed to hipExtLaunchKernelGGL: recorded at the kernel's own start / end
+    virtual void events(hipEvent_t &start, hipEvent_t &stop) = 0;
+    virtual void record(const char *kernel, double bytes) = 0;
+};
+LaunchClock *&launch_clock();
+
 // forward / inverse negacyclic NTT of `limbs` limbs x `segs` segments
 void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
                  hipStream_t st);
 void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
                  hipStream_t st);
+// forward NTT of `count` limbs scattered in one buffer: limb y sits at
+// data + smap[y] * n and belongs to prime pmap[y] (ModUp: every digit at once)
+void ntt_forward_mapped(u64 *data, int count, const int *smap, const int *pmap, const NttTables &T, hipStream_t st);
 
 // element-wise, Q basis (limb l <-> prime l); out may alias inputs
 void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
@@ -66,9 +80,25 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
                    const u64 *tabs /* packed, see engine */, const size_t *tab_off, const Mod *mods, int logN,
                    hipStream_t st);
 // acc0/acc1 [W][n]: sum_j ext_j * key_j   (own-digit limbs read from dntt)
+// optional HMult fold: limb ell-1 of the accumulators starts at w * d[k], w * d[seg + k]
+struct KsFold {
+    const u64 *d = nullptr;  // d0[ell-1] (NTT); d1[ell-1] at d + seg
+    size_t seg = 0;
+    u64 w = 0, ws = 0;       // P mod q_{ell-1} and its Shoup companion
+};
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
-              hipStream_t st);
+              hipStream_t st, KsFold fold = KsFold());
+// fused ModDown + rescale of an HMult (see kernels.hip): corr [segs][ell-1][n]
+// from acc [segs][W][n] whose limbs ell-1 .. W-1 are in coefficient form
+void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
+                             int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
+                             const u64 *pinv, const u64 *pinv_s, const u64 *pmod, const u64 *pmod_s,
+                             const Mod *mods, int logN, hipStream_t st);
+// out [segs][ell-1][n] = (acc + d * P - corr) * (P q_{ell-1})^-1  (pqlinv: the row for this ell)
+void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, int ell, int segs, size_t seg_out,
+                     size_t seg_acc, size_t seg_d, const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
+                     const u64 *pmod_s, const Mod *mods, int logN, hipStream_t st);
 // conv[s][i][k] = sum_k' (pc[s][k'] * phinv_k') * phat[k'][i] mod q_i  for i < ell
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out,
                      int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,

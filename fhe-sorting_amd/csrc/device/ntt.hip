@@ -6,7 +6,7 @@
 // each hold E = 2^EB coefficients in VGPRs:
 //   round 1: the E coefficients of a lane differ in the top EB index bits, so
 //            EB radix-2 stages run in registers with no LDS traffic;
-//   one LDS exchange (padded tile) re-deals the coefficients so that each lane
+//   one LDS exchange (bank-conflict-free tile) re-deals the coefficients so that each lane
 //   owns 2^(PB-EB)-point groups differing in the low bits;
 //   round 2: the remaining PB-EB stages in registers.
 // A limb therefore crosses HBM twice per transform (one read + one write per
@@ -14,6 +14,10 @@
 // companions; round-1 twiddles of the column pass are wave-uniform.
 // The inverse runs the same machinery in Gentleman-Sande order (row pass first,
 // low bits first) and folds n^-1 into the final store.
+#include <hip/hip_ext.h>
+
+#include <string>
+
 #include "kernels.hpp"
 
 namespace fhe {
@@ -23,9 +27,19 @@ namespace {
 
 constexpr int NTB = 256;  // threads per block
 
-template <int PB>
-__device__ __forceinline__ int pad(int idx) {
-    return idx + (idx >> 4);  // one u64 of padding per 16 breaks power-of-two strides
+// LDS exchange tile.  ROWS: the lanes of one transform are adjacent, so each
+// transform owns a contiguous run padded by one u64 per 16.  COLS: adjacent
+// lanes are adjacent transforms, so the tile is element-major with a stride of
+// NB + 1 u64 -- a 16-lane ds_write_b64 group then hits 32 distinct banks and a
+// 32-lane ds_read_b64 group lands on the two bank halves (a per-transform run
+// here would put all 16 transforms of a group on one bank).
+template <int PB, int NB, bool COLS>
+constexpr int lds_words() {
+    return COLS ? (1 << PB) * (NB + 1) : NB * ((1 << PB) + (1 << PB) / 16);
+}
+template <int PB, int NB, bool COLS>
+__device__ __forceinline__ int lds_at(int tr, int idx) {
+    return COLS ? idx * (NB + 1) + tr : tr * ((1 << PB) + (1 << PB) / 16) + idx + (idx >> 4);
 }
 
 // Harvey lazy forward CT butterfly: x, y in [0, 4q) -> x, y in [0, 4q)
@@ -51,21 +65,21 @@ __device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0,
 // COLS: the transform index is a column `col`, element idx sits at idx * 2^k2 + col.
 // ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
 template <int PB, int EB, bool COLS>
-__global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const int *pmap, int logN, NttTables Tb) {
+__global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
+                                                  NttTables Tb) {
     constexpr int E = 1 << EB;          // coefficients per lane
     constexpr int RB = PB - EB;         // bits of round 2
     constexpr int T = 1 << RB;          // lanes per transform
     constexpr int NB = NTB / T;         // transforms per block
     constexpr int G = E >> RB;          // round-2 groups per lane
     constexpr int LEN = 1 << PB;
-    constexpr int STRIDE = LEN + (LEN >> 4);
-    __shared__ u64 tile[NB * STRIDE];
+    __shared__ u64 tile[lds_words<PB, NB, COLS>()];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
     const int limb = blockIdx.y;
     const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n;
+    u64 *a = data + (smap ? (size_t)smap[limb] * n : (size_t)blockIdx.z * seg + (size_t)limb * n);
     const u64 q = Tb.mods[p].q, q2 = 2 * q;
     const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
 
@@ -103,14 +117,13 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         }
     }
     // ---- exchange through LDS: L1 -> L2 (idx = (t*G + g) * 2^RB + r)
-    u64 *tl = tile + tr * STRIDE;
 #pragma unroll
-    for (int r = 0; r < E; ++r) tl[pad<PB>(t + T * r)] = x[r];
+    for (int r = 0; r < E; ++r) tile[lds_at<PB, NB, COLS>(tr, t + T * r)] = x[r];
     __syncthreads();
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int r = 0; r < T; ++r) x[g * T + r] = tl[pad<PB>((t * G + g) * T + r)];
+        for (int r = 0; r < T; ++r) x[g * T + r] = tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)];
     // ---- round 2: local stages EB..PB-1 (pair bit PB-1-s < RB)
 #pragma unroll
     for (int s = EB; s < PB; ++s) {
@@ -141,21 +154,21 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
 // m = n >> (sg + 1), i = j >> (sg + 1).  ROWS covers sg in [0, PB) (low bits),
 // COLS covers sg in [logN - PB, logN) and multiplies by n^-1 on the way out.
 template <int PB, int EB, bool COLS>
-__global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const int *pmap, int logN, NttTables Tb) {
+__global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
+                                                  NttTables Tb) {
     constexpr int E = 1 << EB;
     constexpr int RB = PB - EB;
     constexpr int T = 1 << RB;
     constexpr int NB = NTB / T;
     constexpr int G = E >> RB;
     constexpr int LEN = 1 << PB;
-    constexpr int STRIDE = LEN + (LEN >> 4);
-    __shared__ u64 tile[NB * STRIDE];
+    __shared__ u64 tile[lds_words<PB, NB, COLS>()];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
     const int limb = blockIdx.y;
     const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (size_t)blockIdx.z * seg + (size_t)limb * n;
+    u64 *a = data + (smap ? (size_t)smap[limb] * n : (size_t)blockIdx.z * seg + (size_t)limb * n);
     const u64 q = Tb.mods[p].q, q2 = 2 * q;
     const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
 
@@ -198,14 +211,13 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
             }
     }
     // ---- exchange L2 -> L1 (idx = t + T * r)
-    u64 *tl = tile + tr * STRIDE;
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int r = 0; r < T; ++r) tl[pad<PB>((t * G + g) * T + r)] = x[g * T + r];
+        for (int r = 0; r < T; ++r) tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] = x[g * T + r];
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < E; ++r) x[r] = tl[pad<PB>(t + T * r)];
+    for (int r = 0; r < E; ++r) x[r] = tile[lds_at<PB, NB, COLS>(tr, t + T * r)];
     // ---- round B: local stages RB..PB-1 (pair bit s >= RB, i.e. bit s-RB of r)
 #pragma unroll
     for (int s = RB; s < PB; ++s) {
@@ -232,47 +244,72 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
 }
 
 template <int PB, int EB, bool COLS, bool FWD>
-void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
+void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap, const NttTables &T,
+                 hipStream_t st) {
     constexpr int NB = NTB >> (PB - EB);
     const int count = 1 << (T.logN - PB);  // columns (COLS) or rows (ROWS)
     const dim3 grid((unsigned)((count + NB - 1) / NB), (unsigned)limbs, (unsigned)segs);
+    LaunchClock *clk = launch_clock();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (clk) clk->events(e0, e1);
     if (FWD)
-        hipLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS>), grid, dim3(NTB), 0, st, data, seg, pmap, T.logN, T);
+        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
+                              T);
     else
-        hipLaunchKernelGGL((k_ntt_inv<PB, EB, COLS>), grid, dim3(NTB), 0, st, data, seg, pmap, T.logN, T);
+        hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
+                              T);
+    if (clk) {
+        // same spelling as the demangled symbol rocprofv3 prints
+        static const std::string name = std::string(FWD ? "k_ntt_fwd<" : "k_ntt_inv<") + std::to_string(PB) + ", " +
+                                        std::to_string(EB) + (COLS ? ", true>" : ", false>");
+        // one read + one write of every limb touched
+        clk->record(name.c_str(), 2.0 * 8.0 * (double)limbs * segs * ((size_t)1 << T.logN));
+    }
 }
 
 // pass bits -> (PB, EB): EB = ceil(PB / 2)
 template <bool COLS, bool FWD>
-void dispatch(int PB, u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
-              hipStream_t st) {
+void dispatch(int PB, u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap,
+              const NttTables &T, hipStream_t st) {
     switch (PB) {
-    case 2: launch_pass<2, 1, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
-    case 3: launch_pass<3, 2, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
-    case 4: launch_pass<4, 2, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
-    case 5: launch_pass<5, 3, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
-    case 6: launch_pass<6, 3, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
-    case 7: launch_pass<7, 4, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
-    case 8: launch_pass<8, 4, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
-    case 9: launch_pass<9, 5, COLS, FWD>(data, limbs, segs, seg, pmap, T, st); break;
+    case 2: launch_pass<2, 1, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
+    case 3: launch_pass<3, 2, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
+    case 4: launch_pass<4, 2, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
+    case 5: launch_pass<5, 3, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
+    case 6: launch_pass<6, 3, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
+    case 7: launch_pass<7, 4, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
+    case 8: launch_pass<8, 4, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
+    case 9: launch_pass<9, 5, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
     default: break;
     }
 }
 
 }  // namespace
 
+LaunchClock *&launch_clock() {
+    static LaunchClock *clk = nullptr;
+    return clk;
+}
+
 void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
     if (limbs <= 0 || segs <= 0) return;
     const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
-    dispatch<true, true>(k1, data, limbs, segs, seg, pmap, T, st);
-    dispatch<false, true>(k2, data, limbs, segs, seg, pmap, T, st);
+    dispatch<true, true>(k1, data, limbs, segs, seg, pmap, nullptr, T, st);
+    dispatch<false, true>(k2, data, limbs, segs, seg, pmap, nullptr, T, st);
 }
 
 void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
     if (limbs <= 0 || segs <= 0) return;
     const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
-    dispatch<false, false>(k2, data, limbs, segs, seg, pmap, T, st);
-    dispatch<true, false>(k1, data, limbs, segs, seg, pmap, T, st);
+    dispatch<false, false>(k2, data, limbs, segs, seg, pmap, nullptr, T, st);
+    dispatch<true, false>(k1, data, limbs, segs, seg, pmap, nullptr, T, st);
+}
+
+void ntt_forward_mapped(u64 *data, int count, const int *smap, const int *pmap, const NttTables &T, hipStream_t st) {
+    if (count <= 0) return;
+    const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
+    dispatch<true, true>(k1, data, count, 1, 0, pmap, smap, T, st);
+    dispatch<false, true>(k2, data, count, 1, 0, pmap, smap, T, st);
 }
 
 }  // namespace dev

@@ -100,6 +100,8 @@ struct Engine::Impl {
     u64 *modup_tab = nullptr;  // packed ModUp tables
     u64 *phinv = nullptr, *phinv_s = nullptr, *phat = nullptr, *phat_s = nullptr, *pinv = nullptr, *pinv_s = nullptr;
     u64 *qlinv = nullptr, *qlinv_s = nullptr;
+    u64 *pmod = nullptr, *pmod_s = nullptr, *pqlinv = nullptr, *pqlinv_s = nullptr;
+    int *modup_smap = nullptr, *modup_pmap = nullptr;
 
     // keys
     std::shared_ptr<DevMem> s_ntt, pk, relin;
@@ -148,12 +150,8 @@ struct Engine::Impl {
         u64 *e = static_cast<u64 *>(extm->p);
         dev::modup_convert(e, c, (int)ell, P.K, P.alpha, digits, ext(ell), modup_tab, LT.modup_off[ell].data(), mods,
                            P.logN, st);
-        for (int j = 0; j < digits; ++j) {
-            const size_t lo = (size_t)j * P.alpha, hi = std::min(ell, (size_t)(j + 1) * P.alpha);
-            u64 *ej = e + (size_t)j * W * nn;
-            dev::ntt_forward(ej, (int)lo, 1, 0, ext(ell), T, st);
-            dev::ntt_forward(ej + hi * nn, (int)(W - hi), 1, 0, ext(ell) + hi, T, st);
-        }
+        const size_t mo = LT.modup_map_off[ell];
+        dev::ntt_forward_mapped(e, (int)LT.modup_map_cnt[ell], modup_smap + mo, modup_pmap + mo, T, st);
         return extm;
     }
     // out[2][ell][n] = ModDown(sum_j ext_j * key_j) (+ add for the first add_segs segments)
@@ -174,6 +172,32 @@ struct Engine::Impl {
         dev::ntt_forward(conv, (int)ell, 2, ell * nn, nullptr, T, st);
         dev::moddown_finish(out, acc, conv, add, add_segs, (int)ell, 2, ell * nn, W * nn, add_seg, pinv, pinv_s, mods,
                             P.logN, st);
+    }
+    // HMult tail, fused: out [2][ell-1][n] = Rescale(d01 + ModDown(Sum_j ext_j * key_j)).
+    // Bit-identical to ks_apply(add = d01) followed by rescale(): both compute
+    // ((acc - Conv(acc_P)) P^-1 + d - [y_last]) q_last^-1 mod q_i, but here only
+    // limb ell-1 and the P limbs leave the NTT domain and one forward NTT of
+    // ell-1 limbs per polynomial serves both divisions.
+    void mul_tail(const u64 *e, const u64 *d, size_t ell, u64 *out) {
+        const size_t nn = n(), K = (size_t)P.K, W = ell + K;
+        const int digits = P.digits_at(ell);
+        auto accm = alloc(2 * W * nn * 8);
+        u64 *acc = static_cast<u64 *>(accm->p);
+        dev::KsFold fold;
+        fold.d = d + (ell - 1) * nn;
+        fold.seg = ell * nn;
+        fold.w = LT.pmod[ell - 1];
+        fold.ws = LT.pmod_s[ell - 1];
+        dev::ks_inner(acc, e, d + 2 * ell * nn, static_cast<u64 *>(relin->p), (int)ell, P.K, (int)P.nq(),
+                      (int)P.nall(), P.alpha, digits, nullptr, ext(ell), mods, P.logN, st, fold);
+        dev::ntt_inverse(acc + (ell - 1) * nn, (int)K + 1, 2, W * nn, ext(ell) + (ell - 1), T, st);
+        auto corrm = alloc(2 * (ell - 1) * nn * 8);
+        u64 *corr = static_cast<u64 *>(corrm->p);
+        dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, 2, phinv, phinv_s,
+                                     phat, phat_s, pinv, pinv_s, pmod, pmod_s, mods, P.logN, st);
+        dev::ntt_forward(corr, (int)(ell - 1), 2, (ell - 1) * nn, nullptr, T, st);
+        dev::mul_tail_finish(out, acc, d, corr, (int)ell, 2, (ell - 1) * nn, W * nn, ell * nn, pqlinv + ell * P.nq(),
+                             pqlinv_s + ell * P.nq(), pmod, pmod_s, mods, P.logN, st);
     }
     // out [2][ell-1][n] from in [2][ell][n] with input segment stride seg_in
     void rescale(const u64 *in, size_t ell, size_t seg_in, u64 *out) {
@@ -246,6 +270,12 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.pinv_s = I.upload_static(I.LT.pinv_s);
     I.qlinv = I.upload_static(I.LT.qlinv);
     I.qlinv_s = I.upload_static(I.LT.qlinv_s);
+    I.pmod = I.upload_static(I.LT.pmod);
+    I.modup_smap = I.upload_static(I.LT.modup_smap);
+    I.modup_pmap = I.upload_static(I.LT.modup_pmap);
+    I.pmod_s = I.upload_static(I.LT.pmod_s);
+    I.pqlinv = I.upload_static(I.LT.pqlinv);
+    I.pqlinv_s = I.upload_static(I.LT.pqlinv_s);
     I.key_digits = I.P.digits_at(I.P.nq());
 }
 
@@ -691,12 +721,8 @@ CtPtr Engine::mul(const Ciphertext &a0, const Ciphertext &b0) {
     u64 *d = static_cast<u64 *>(dm->p);
     dev::ew_tensor(d, a->data, b->data, (int)ell, MODS, LOGN, ST);
     auto extm = I.modup(d + 2 * ell * nn, ell);
-    auto tm = I.alloc(2 * ell * nn * 8);
-    u64 *t = static_cast<u64 *>(tm->p);
-    I.ks_apply(static_cast<u64 *>(extm->p), d + 2 * ell * nn, ell, static_cast<u64 *>(I.relin->p), nullptr, t, d, 2,
-               ell * nn);
     auto r = new_ct(a->level + 1, a->slots, I.P.delta[a->level + 1], ell - 1);
-    I.rescale(t, ell, ell * nn, r->data);
+    I.mul_tail(static_cast<u64 *>(extm->p), d, ell, r->data);
     return r;
 }
 CtPtr Engine::square(const Ciphertext &a) { return mul(a, a); }
@@ -853,6 +879,77 @@ void Engine::automorph_host(const u64 *in, size_t limbs, u64 g, u64 *out) {
     HIP_OK(hipStreamSynchronize(ST));
 }
 
+namespace {
+struct EventClock final : dev::LaunchClock {
+    struct Rec {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        const char *name = nullptr;
+        double bytes = 0;
+    };
+    std::vector<Rec> recs;
+    size_t used = 0;
+    void events(hipEvent_t &start, hipEvent_t &stop) override {
+        if (used == recs.size()) {
+            Rec r;
+            HIP_OK(hipEventCreate(&r.e0));
+            HIP_OK(hipEventCreate(&r.e1));
+            recs.push_back(r);
+        }
+        start = recs[used].e0;
+        stop = recs[used].e1;
+    }
+    void record(const char *kernel, double bytes) override {
+        recs[used].name = kernel;
+        recs[used].bytes = bytes;
+        ++used;
+    }
+    ~EventClock() override {
+        for (auto &r : recs) {
+            (void)hipEventDestroy(r.e0);
+            (void)hipEventDestroy(r.e1);
+        }
+    }
+};
+std::unique_ptr<EventClock> g_clock;
+}  // namespace
+
+void Engine::kernel_clock_start() {
+    if (dev::launch_clock()) throw std::runtime_error("kernel clock already running");
+    g_clock = std::make_unique<EventClock>();
+    dev::launch_clock() = g_clock.get();
+}
+
+std::string Engine::kernel_clock_stop() {
+    if (!g_clock) throw std::runtime_error("kernel clock not running");
+    dev::launch_clock() = nullptr;
+    HIP_OK(hipStreamSynchronize(impl->st));
+    struct Agg {
+        long launches = 0;
+        double ms = 0, bytes = 0;
+    };
+    std::map<std::string, Agg> agg;
+    for (size_t i = 0; i < g_clock->used; ++i) {
+        auto &r = g_clock->recs[i];
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, r.e0, r.e1));
+        auto &a = agg[r.name];
+        a.launches += 1;
+        a.ms += ms;
+        a.bytes += r.bytes;
+    }
+    g_clock.reset();
+    std::string out = "{";
+    char buf[512];
+    bool first = true;
+    for (auto &kv : agg) {
+        snprintf(buf, sizeof buf, "%s\"%s\": {\"launches\": %ld, \"ms\": %.6f, \"bytes\": %.0f}", first ? "" : ", ",
+                 kv.first.c_str(), kv.second.launches, kv.second.ms, kv.second.bytes);
+        out += buf;
+        first = false;
+    }
+    return out + "}";
+}
+
 void Engine::time_kernel(const std::string &name, size_t ell, int iters, double &avg_ms, double &bytes) {
     auto &I = *impl;
     const size_t nn = n(), K = (size_t)I.P.K, W = ell + K, B = nn * 8;
@@ -883,9 +980,6 @@ void Engine::time_kernel(const std::string &name, size_t ell, int iters, double 
                                I.LT.modup_off[ell].data(), MODS, LOGN, ST);
         };
         bytes = (double)(ell + (size_t)digits * W - ell) * B;
-    } else if (name == "tensor") {
-        launch = [&] { dev::ew_tensor(d, acc, acc + ell * nn, (int)ell, MODS, LOGN, ST); };
-        bytes = 7.0 * (double)ell * B;
     } else {
         throw std::invalid_argument("time_kernel: unknown kernel " + name);
     }

@@ -120,6 +120,11 @@ class Engine {
     // (HIP events), shaped like a key switch at `limbs` Q limbs; returns the
     // average ms per launch and the algorithmic HBM bytes per launch.
     void time_kernel(const std::string &name, size_t limbs, int iters, double &avg_ms, double &bytes);
+    // live per-launch clock over real work: between start and stop every NTT
+    // pass is bracketed by HIP events on the engine stream; stop() returns JSON
+    // {"kernel": {"launches": c, "ms": total, "bytes": total_algorithmic}, ...}
+    void kernel_clock_start();
+    std::string kernel_clock_stop();
 
     // small device scratch (for collectives / headers); copies are synchronous
     struct DevBuf {

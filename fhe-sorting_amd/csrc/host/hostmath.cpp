@@ -356,6 +356,21 @@ LevelTables make_level_tables(const Params &P) {
         for (size_t k = 0; k < K; ++k) T.extmap[ell * Wmax + ell + k] = (int)(nq + k);
     }
     // ModUp
+    T.modup_map_off.assign(nq + 1, 0);
+    T.modup_map_cnt.assign(nq + 1, 0);
+    for (size_t ell = 1; ell <= nq; ++ell) {
+        const size_t W = ell + K, digits = (ell + alpha - 1) / alpha;
+        T.modup_map_off[ell] = T.modup_smap.size();
+        for (size_t j = 0; j < digits; ++j) {
+            const size_t lo = j * alpha, hi = std::min(ell, (j + 1) * alpha);
+            for (size_t t = 0; t < W; ++t) {
+                if (t >= lo && t < hi) continue;
+                T.modup_smap.push_back((int)(j * W + t));
+                T.modup_pmap.push_back(T.extmap[ell * Wmax + t]);
+            }
+        }
+        T.modup_map_cnt[ell] = T.modup_smap.size() - T.modup_map_off[ell];
+    }
     T.modup_off.assign(nq + 1, {});
     for (size_t ell = 1; ell <= nq; ++ell) {
         const size_t W = ell + K;
@@ -396,6 +411,8 @@ LevelTables make_level_tables(const Params &P) {
     T.phat_s.assign(K * nq, 0);
     T.pinv.resize(nq);
     T.pinv_s.resize(nq);
+    T.pmod.resize(nq);
+    T.pmod_s.resize(nq);
     for (size_t k = 0; k < K; ++k) {
         const Modulus &mk = mods[nq + k];
         u64 prod = 1;
@@ -417,6 +434,8 @@ LevelTables make_level_tables(const Params &P) {
         }
         T.pinv[i] = invmod(Pm, mi);
         T.pinv_s[i] = shoup(T.pinv[i], mi.q);
+        T.pmod[i] = Pm;
+        T.pmod_s[i] = shoup(Pm, mi.q);
     }
     // Rescale
     T.qlinv.assign((nq + 1) * nq, 0);
@@ -429,6 +448,14 @@ LevelTables make_level_tables(const Params &P) {
             T.qlinv_s[ell * nq + i] = shoup(v, P.primes[i]);
         }
     }
+    T.pqlinv.assign((nq + 1) * nq, 0);
+    T.pqlinv_s.assign((nq + 1) * nq, 0);
+    for (size_t ell = 2; ell <= nq; ++ell)
+        for (size_t i = 0; i + 1 < ell; ++i) {
+            const u64 v = mulmod(T.qlinv[ell * nq + i], T.pinv[i], mods[i]);
+            T.pqlinv[ell * nq + i] = v;
+            T.pqlinv_s[ell * nq + i] = shoup(v, P.primes[i]);
+        }
     return T;
 }
 

@@ -89,10 +89,17 @@ struct LevelTables {
     std::vector<u64> phinv, phinv_s;    // [K]
     std::vector<u64> phat, phat_s;      // [K][nq]
     std::vector<u64> pinv, pinv_s;      // [nq]
+    std::vector<u64> pmod, pmod_s;      // [nq]  P mod q_i
+    // fused ModDown + rescale (HMult tail): pqlinv[ell][i] = (P q_{ell-1})^{-1} mod q_i
+    std::vector<u64> pqlinv, pqlinv_s;  // [nq+1][nq]
     // Rescale, per ell: qlinv[ell][i] = q_{ell-1}^{-1} mod q_i
     std::vector<u64> qlinv, qlinv_s;    // [nq+1][nq]
     // prime maps: ext[ell] = {0..ell-1, nq..nq+K-1}
     std::vector<int> extmap;            // [nq+1][nq+K]
+    // ModUp forward-NTT map per ell: the non-own limbs of every digit,
+    // slot j*W + t (in units of n) and its prime; concatenated over ell
+    std::vector<int> modup_smap, modup_pmap;
+    std::vector<size_t> modup_map_off, modup_map_cnt;  // [nq+1]
 };
 LevelTables make_level_tables(const Params &P);
 

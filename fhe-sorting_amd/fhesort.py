@@ -100,6 +100,8 @@ _SIGS = {
     'fhe_sync': (C.c_int, [vp]),
     'fhe_stream': (vp, [vp]),
     'fhe_time_kernel': (C.c_int, [vp, C.c_char_p, C.c_int, C.c_int, dp, dp]),
+    'fhe_kernel_clock_start': (C.c_int, [vp]),
+    'fhe_kernel_clock_stop': (C.c_int, [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
 
 
@@ -392,6 +394,28 @@ def time_kernel(ctx, name, limbs, iters=20):
     ms, b = C.c_double(), C.c_double()
     _chk(lib().fhe_time_kernel(ctx.h, name.encode(), limbs, iters, C.byref(ms), C.byref(b)))
     return {'name': name, 'avg_ms': ms.value, 'bytes': b.value}
+
+
+class KernelClock:
+    """Live per-launch clock over real work (HIP events on the engine stream
+    around every NTT pass): `with KernelClock(ctx) as k: ...; k.stats`."""
+
+    def __init__(self, ctx):
+        self.ctx, self.stats = ctx, None
+
+    def __enter__(self):
+        _chk(lib().fhe_kernel_clock_start(self.ctx.h))
+        return self
+
+    def __exit__(self, *exc):
+        import json
+        need = C.c_size_t()
+        buf = C.create_string_buffer(1 << 16)
+        _chk(lib().fhe_kernel_clock_stop(self.ctx.h, buf, len(buf), C.byref(need)))
+        if need.value > len(buf):
+            raise FheError(FHE_EINTERNAL, 'kernel clock report truncated')
+        self.stats = json.loads(buf.value.decode())
+        return False
 
 
 def size_parameters(N):

@@ -170,9 +170,15 @@ int fhe_sync(fhe_ctx *ctx);
 /* opaque hipStream_t of the context (for event timing by the caller) */
 void *fhe_stream(fhe_ctx *ctx);
 /* time `iters` launches of one hot kernel ("ks_inner", "ntt_fwd",
- * "modup_convert", "tensor") with HIP events on the context stream, shaped as
- * a key switch at `limbs` Q limbs: average ms and algorithmic bytes/launch */
+ * "modup_convert") with HIP events on the context stream, shaped as a key
+ * switch at `limbs` Q limbs: average ms and algorithmic bytes/launch */
 int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double *avg_ms, double *bytes);
+/* live kernel clock over real work: after start, every NTT pass launched by
+ * this process is bracketed by HIP events on its stream; stop writes JSON
+ * {"<kernel>": {"launches": c, "ms": total, "bytes": algorithmic}, ...} into
+ * json (cap bytes, NUL-terminated, truncated if short; *needed = full size) */
+int fhe_kernel_clock_start(fhe_ctx *ctx);
+int fhe_kernel_clock_stop(fhe_ctx *ctx, char *json, size_t cap, size_t *needed);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round profile: bench line, rocprofv3 kernel trace + stats of one sort, and
+# two PMC passes (FETCH_SIZE, WRITE_SIZE) over the NTT kernels.
+# usage: gpu_job_profile.sh TAG [extra bench args]
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$R"
+TAG=${1:-run}; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+(while sleep 60; do echo "tick $(date +%T)"; done) & TICK=$!
+trap 'kill $TICK 2>/dev/null' EXIT
+timeout -k 10 600 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/trace" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline "$@" > $O/trace.log 2>&1 || { echo "trace failed"; tail -5 $O/trace.log; exit 1; }
+python scripts/trace_summary.py $O/trace/run_kernel_trace.csv > $O/trace_summary.txt && cat $O/trace_summary.txt || exit 1
+gzip -f $O/trace/run_kernel_trace.csv
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 900 rocprofv3 --pmc $C --kernel-include-regex 'k_ntt' --output-format csv -d "$R/$O/pmc_$C" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-roofline "$@" > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -5 $O/pmc_$C.log; exit 1; }
+done
+python scripts/pmc_summary.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv $O/pmc_traffic.json || exit 1
+gzip -f $O/pmc_*/run_counter_collection.csv
+echo ALLOK

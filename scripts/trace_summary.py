@@ -21,11 +21,11 @@ for k, v in sorted(stat.items(), key=lambda kv: -sum(x[0] for x in kv[1]))[:16]:
     tot = sum(x[0] for x in v)
     print(f'{k:34s} n={len(v):6d} {tot / 1e6:9.2f} ms {100 * tot / tot_all:5.1f}%  avg {tot / len(v) / 1e3:7.2f} us'
           f'  vgpr={v[0][4]} lds={v[0][5]}')
-for k in ('k_ntt_fwd_rows', 'k_ntt_fwd_cols', 'k_ntt_inv_rows', 'k_ntt_inv_cols'):
-    v = stat.get(k, [])
-    if not v:
+for k in sorted(stat):
+    if not k.startswith('k_ntt'):
         continue
+    v = stat[k]
     tb = sum(gy * gz * n * 16 for _, _, gy, gz, _, _ in v)
     tt = sum(x[0] for x in v)
     print(f'{k}: {tb / tt:.1f} GB/s algorithmic (2 x 8 B per coefficient), '
-          f'avg {sum(x[2] * x[3] for x in v) / len(v):.1f} limbs/launch')
+          f'avg {sum(x[2] * x[3] for x in v) / len(v):.1f} limbs/launch, avg {tt / len(v) / 1e3:.2f} us')

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_has_gfx950_code_objects():
     data = open(F.LIB_PATH, 'rb').read()
     assert b'gfx950' in data
-    assert b'k_ntt_fwd_cols' in data and b'k_ks_inner' in data
+    assert b'k_ntt_fwd' in data and b'k_ntt_inv' in data and b'k_ks_inner' in data
 
 
 def test_binding_loads_without_gpu():
