@@ -74,7 +74,8 @@ struct PSEval {
                 xs.push_back(T.at((int)i).get());
                 cs.push_back(a[i]);
             }
-        CtPtr r = xs.empty() ? cc.trivial_const(0.0, target, T[1]->slots) : cc.linear_sum_to(xs, cs, target);
+        CtPtr r = xs.empty() ? cc.trivial_const(0.0, target, T[1]->slots, T[1]->batch)
+                             : cc.linear_sum_to(xs, cs, target);
         if (a[0] != 0.0) r = cc.add_const(*r, a[0]);
         return r;
     }
@@ -116,7 +117,7 @@ CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<
     std::vector<double> s(c);
     s[0] = c[0] / 2.0;
     const int d = (int)s.size() - 1;
-    if (d == 0) return cc.add_const(*cc.trivial_const(0.0, x->level, x->slots), s[0]);
+    if (d == 0) return cc.add_const(*cc.trivial_const(0.0, x->level, x->slots, x->batch), s[0]);
     PSEval ev(cc, *x, d);
     ev.build_baby();
     return ev.eval(s, x->level + ev.D);
@@ -471,21 +472,38 @@ CtPtr DirectSortN::vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition,
     return result;
 }
 
+// The comparator batches of this rank run stacked: their inputs differ, but
+// the sign() op sequence is identical, so one compare over a ciphertext batch
+// replaces max_stack sequential ones.  compare(x, s_b) =
+// ((sign(x - s_b) + 1) / 2); the per-batch results are summed exactly mod q,
+// so the rank equals the reference's batch-by-batch accumulation
+// (src/sort_algo.h:474-491) word for word.
 CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg) {
     const SortShape s = rankShape(N, max_batch);
     std::vector<int> idx(s.np);
     for (int i = 0; i < s.np; ++i) idx[i] = i;
     std::vector<CtPtr> baby = rot.rotateMany(x, idx);
     for (auto &b : baby) b->slots = s.num_slots;
-    Comparison comp;
+    std::vector<int> mine;
+    for (int b = 0; b < s.num_batch; ++b)
+        if (b % shard_world == shard_rank) mine.push_back(b);
+    CtPtr dup = cc.clone(x);
+    dup->slots = s.num_slots;
     CtPtr rank;
-    for (int b = 0; b < s.num_batch; ++b) {
-        if (b % shard_world != shard_rank) continue;
-        CtPtr shifted = vecRotsOpt(baby, s.num_partition, s.num_slots, s.np, b);
-        CtPtr dup = cc.clone(x);
-        dup->slots = s.num_slots;
-        CtPtr c = comp.compare(cc, *dup, *shifted, f, cfg);
-        cc.add_inplace(rank, *c);
+    const size_t chunk = (size_t)std::max(1, max_stack);
+    for (size_t c0 = 0; c0 < mine.size(); c0 += chunk) {
+        std::vector<CtPtr> diffs;
+        std::vector<const Ciphertext *> ptrs;
+        for (size_t i = c0; i < std::min(mine.size(), c0 + chunk); ++i) {
+            CtPtr shifted = vecRotsOpt(baby, s.num_partition, s.num_slots, s.np, mine[i]);
+            diffs.push_back(cc.sub(*dup, *shifted));
+            ptrs.push_back(diffs.back().get());
+        }
+        CtPtr d = ptrs.size() == 1 ? diffs[0] : cc.stack(ptrs);
+        diffs.clear();
+        CtPtr sg = sign(*d, cc, f, cfg);
+        CtPtr c = cc.mul_const(*cc.add_const(*sg, 1.0), 0.5);
+        cc.add_inplace(rank, c->batch == 1 ? *c : *cc.sum_members(*c));
     }
     reducePartial(rank, s.num_slots);
     for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)
@@ -508,6 +526,27 @@ CtPtr DirectSortN::blindRotationOptN(const std::vector<CtPtr> &mi, int num_slots
     return result;
 }
 
+CtPtr DirectSortN::blindRotationStacked(const std::vector<CtPtr> &mi, int num_slots, int np, const std::vector<int> &ibs,
+                                        int num_partition) {
+    CtPtr result;
+    for (int i = 0; i < (num_slots / N) / np; ++i) {
+        CtPtr tmp;
+        for (int j = 0; j < np; ++j) {
+            const Plaintext &pm = mask(0, num_slots, np * i + j, j, mi[j]->level);
+            cc.add_inplace(tmp, *cc.mul_plain(*mi[j], pm));
+        }
+        for (size_t m = 0; m < ibs.size(); ++m) {
+            CtPtr one = tmp->batch == 1 ? tmp : cc.member(*tmp, (int)m);
+            cc.add_inplace(result, *rot.rotate(*one, ibs[m] * num_partition + i * np));
+        }
+    }
+    return result;
+}
+
+// Index check, stacked like constructRank: the doubled-sinc PS (the dominant
+// cost, ~200 HMult per batch at N=1024) and the masking product run once over
+// a batch of max_stack inputs; only the per-batch giant-step rotations run
+// member by member (src/sort_algo.h:713-742).
 CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext &x) {
     const SortShape s = checkShape(N, max_batch);
     std::vector<double> idx(N);
@@ -520,17 +559,31 @@ CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext 
     const std::vector<double> &coeffs = sincCoefficients();
     std::vector<int> ridx(s.np);
     for (int i = 0; i < s.np; ++i) ridx[i] = i;
+    std::vector<int> mine;
+    for (int b = 0; b < s.num_batch; ++b)
+        if (b % shard_world == shard_rank) mine.push_back(b);
     CtPtr out;
-    for (int b = 0; b < s.num_batch; ++b) {
-        if (b % shard_world != shard_rank) continue;
-        const Plaintext &chk = mask(1, s.num_slots, b * s.num_partition, 0, imr->level);
-        CtPtr ri = cc.sub_plain(*imr, chk);
-        ri = cc.mul_const(*ri, 1.0 / N / 2);
-        ri = evalChebyshevSeriesPS(cc, *ri, coeffs, -1.0, 1.0);
-        CtPtr masked = cc.mul(*ri, *xs);
+    const size_t chunk = (size_t)std::max(1, max_stack);
+    for (size_t c0 = 0; c0 < mine.size(); c0 += chunk) {
+        std::vector<CtPtr> ris;
+        std::vector<const Ciphertext *> ptrs;
+        std::vector<int> ibs;
+        for (size_t i = c0; i < std::min(mine.size(), c0 + chunk); ++i) {
+            const int b = mine[i];
+            const Plaintext &chk = mask(1, s.num_slots, b * s.num_partition, 0, imr->level);
+            CtPtr ri = cc.sub_plain(*imr, chk);
+            ris.push_back(cc.mul_const(*ri, 1.0 / N / 2));
+            ptrs.push_back(ris.back().get());
+            ibs.push_back(b);
+        }
+        CtPtr r = ptrs.size() == 1 ? ris[0] : cc.stack(ptrs);
+        ris.clear();
+        r = evalChebyshevSeriesPS(cc, *r, coeffs, -1.0, 1.0);
+        CtPtr masked = cc.mul(*r, *xs);  // xs broadcast over the members
+        r.reset();
         std::vector<CtPtr> mi = rot.rotateMany(*masked, ridx);
-        CtPtr r = blindRotationOptN(mi, s.num_slots, s.np, b, s.num_partition);
-        cc.add_inplace(out, *r);
+        masked.reset();
+        cc.add_inplace(out, *blindRotationStacked(mi, s.num_slots, s.np, ibs, s.num_partition));
     }
     reducePartial(out, s.num_slots);
     for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)

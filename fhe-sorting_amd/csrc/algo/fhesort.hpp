@@ -117,10 +117,16 @@ class DirectSortN {
     int N;
     RotationComposerN rot;
     int max_batch;
+    // how many of this rank's batches run stacked through one compare / one PS
+    // (every launch then carries that many ciphertexts; memory grows with it)
+    int max_stack = 32;
 
   private:
     CtPtr vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is);
     CtPtr blindRotationOptN(const std::vector<CtPtr> &masked, int num_slots, int np, int ib, int num_partition);
+    // blindRotationOptN over a stacked `masked` (member m belongs to batch ibs[m]), summed over members
+    CtPtr blindRotationStacked(const std::vector<CtPtr> &masked, int num_slots, int np, const std::vector<int> &ibs,
+                               int num_partition);
     void reducePartial(CtPtr &acc, int slots);
     const Plaintext &mask(int kind, int num_slots, int k, int rot, int level);
     std::map<std::tuple<int, int, int, int, int>, PtPtr> mask_cache;

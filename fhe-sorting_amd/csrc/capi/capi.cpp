@@ -3,6 +3,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <map>
 #include <memory>
 #include <new>
 #include <string>
@@ -17,6 +18,10 @@ struct fhe_ctx {
     std::unique_ptr<Engine> eng;
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
+    // one rank sorter per (N, rotation set): its encoded public masks persist
+    // across sorts like the keys do
+    std::map<std::pair<int, std::vector<int>>, std::unique_ptr<DirectSortN>> sorters;
+    int sort_stack = 32;
 };
 struct fhe_ct {
     CtPtr p;
@@ -152,6 +157,29 @@ int fhe_ct_free(fhe_ct *ct) {
     delete ct;
     return FHE_OK;
 }
+int fhe_ct_stack(fhe_ctx *ctx, const fhe_ct *const *xs, int m, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        std::vector<const Ciphertext *> v;
+        for (int i = 0; i < m; ++i) {
+            NEED(xs[i]);
+            v.push_back(xs[i]->p.get());
+        }
+        *out = wrap(ctx->eng->stack(v));
+    });
+}
+int fhe_ct_member(fhe_ctx *ctx, const fhe_ct *a, int m, fhe_ct **out) {
+    return guard([&] {
+        NEED(a);
+        *out = wrap(ctx->eng->member(*a->p, m));
+    });
+}
+int fhe_ct_sum_members(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out) {
+    return guard([&] {
+        NEED(a);
+        *out = wrap(ctx->eng->sum_members(*a->p));
+    });
+}
 int fhe_pt_encode(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_pt **out) {
     return guard([&] { *out = new fhe_pt{ctx->eng->encode(std::vector<double>(v, v + len), slots, level)}; });
 }
@@ -272,7 +300,12 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
     return guard([&] {
         NEED(ctx);
         NEED(x);
-        DirectSortN ds(*ctx->eng, N, std::vector<int>(rots, rots + nrot));
+        auto key = std::make_pair(N, std::vector<int>(rots, rots + nrot));
+        auto &slot = ctx->sorters[key];
+        if (!slot) slot = std::make_unique<DirectSortN>(*ctx->eng, N, key.second);
+        DirectSortN &ds = *slot;
+        ds.max_stack = ctx->sort_stack;
+        ds.allreduce = nullptr;
         ds.shard_rank = shard_rank;
         ds.shard_world = shard_world;
         if (fn) {
@@ -294,6 +327,14 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
             *out = wrap(ds.rotationIndexCheckN(*rank->p, *x->p));
         } else
             *out = wrap(ds.sort(*x->p, SignFunc::CompositeSign, cfg));
+    });
+}
+
+int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack) {
+    return guard([&] {
+        NEED(ctx);
+        if (max_stack < 1) throw std::invalid_argument("max_stack must be >= 1");
+        ctx->sort_stack = max_stack;
     });
 }
 

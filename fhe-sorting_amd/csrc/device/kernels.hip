@@ -23,105 +23,109 @@ constexpr int TCH = 8;      // target limbs per thread in basis conversions
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
 // --------------------------------------------------------- element-wise ----
-// grid: x = n / (2 NT), y = limb, z = segment; 2 coefficients per lane
+// grid: x = n / (2 NT), y = limb, z = segment; 2 coefficients per lane.
+// Segment z of out / a / b starts at z * S.o / S.a / S.b (u64 units), so one
+// launch covers both polynomials of every member of a ciphertext batch, reads
+// a wider (undropped) input in place, or broadcasts a plaintext (S.b = 0).
 #define EW_PROLOGUE                                                           \
     const size_t n = (size_t)1 << logN;                                       \
     const int l = blockIdx.y;                                                 \
-    const size_t off = (size_t)blockIdx.z * seg + (size_t)l * n;              \
+    const size_t ln = (size_t)l * n;                                          \
     const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;             \
     if (k >= n) return;                                                       \
+    const size_t oo = (size_t)blockIdx.z * S.o + ln + k;                      \
+    const size_t oa = (size_t)blockIdx.z * S.a + ln + k;                      \
+    const size_t ob = (size_t)blockIdx.z * S.b + ln + k;                      \
+    (void)ob;                                                                 \
     const u64 q = mods[l].q;
 
-__global__ __launch_bounds__(NT) void k_add(u64 *out, const u64 *a, const u64 *b, size_t seg, const Mod *mods,
-                                            int logN) {
+__device__ __forceinline__ ulonglong2 ld2(const u64 *p) { return *reinterpret_cast<const ulonglong2 *>(p); }
+__device__ __forceinline__ void st2(u64 *p, ulonglong2 v) { *reinterpret_cast<ulonglong2 *>(p) = v; }
+
+__global__ __launch_bounds__(NT) void k_add(u64 *out, const u64 *a, const u64 *b, Seg S, const Mod *mods, int logN) {
     EW_PROLOGUE
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
-    const ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(b + off + k);
-    ulonglong2 r;
-    r.x = add_mod(x.x, y.x, q);
-    r.y = add_mod(x.y, y.y, q);
-    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+    const ulonglong2 x = ld2(a + oa), y = ld2(b + ob);
+    st2(out + oo, make_ulonglong2(add_mod(x.x, y.x, q), add_mod(x.y, y.y, q)));
 }
-__global__ __launch_bounds__(NT) void k_sub(u64 *out, const u64 *a, const u64 *b, size_t seg, const Mod *mods,
-                                            int logN) {
+__global__ __launch_bounds__(NT) void k_sub(u64 *out, const u64 *a, const u64 *b, Seg S, const Mod *mods, int logN) {
     EW_PROLOGUE
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
-    const ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(b + off + k);
-    ulonglong2 r;
-    r.x = sub_mod(x.x, y.x, q);
-    r.y = sub_mod(x.y, y.y, q);
-    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+    const ulonglong2 x = ld2(a + oa), y = ld2(b + ob);
+    st2(out + oo, make_ulonglong2(sub_mod(x.x, y.x, q), sub_mod(x.y, y.y, q)));
 }
-__global__ __launch_bounds__(NT) void k_neg(u64 *out, const u64 *a, size_t seg, const Mod *mods, int logN) {
+__global__ __launch_bounds__(NT) void k_neg(u64 *out, const u64 *a, Seg S, const Mod *mods, int logN) {
     EW_PROLOGUE
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
-    ulonglong2 r;
-    r.x = sub_mod(0, x.x, q);
-    r.y = sub_mod(0, x.y, q);
-    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+    const ulonglong2 x = ld2(a + oa);
+    st2(out + oo, make_ulonglong2(sub_mod(0, x.x, q), sub_mod(0, x.y, q)));
 }
 __device__ __forceinline__ u64 smod(int64_t v, const Mod &m) {
     if (v >= 0) return reduce64((u64)v, m);
     const u64 r = reduce64((u64)0 - (u64)v, m);
     return r ? m.q - r : 0;
 }
-__global__ __launch_bounds__(NT) void k_mul_scalar(u64 *out, const u64 *a, int64_t K, size_t seg, const Mod *mods,
+__global__ __launch_bounds__(NT) void k_mul_scalar(u64 *out, const u64 *a, int64_t K, Seg S, const Mod *mods,
                                                    int logN) {
     EW_PROLOGUE
     const Mod m = mods[l];
     const u64 w = smod(K, m);
     (void)q;
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
-    ulonglong2 r;
-    r.x = mul_barrett(x.x, w, m);
-    r.y = mul_barrett(x.y, w, m);
-    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+    const ulonglong2 x = ld2(a + oa);
+    st2(out + oo, make_ulonglong2(mul_barrett(x.x, w, m), mul_barrett(x.y, w, m)));
 }
-__global__ __launch_bounds__(NT) void k_add_scalar(u64 *out, const u64 *a, int64_t K, size_t seg, const Mod *mods,
+__global__ __launch_bounds__(NT) void k_add_scalar(u64 *out, const u64 *a, int64_t K, Seg S, const Mod *mods,
                                                    int logN) {
     EW_PROLOGUE
     const u64 w = smod(K, mods[l]);
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
-    ulonglong2 r;
-    r.x = add_mod(x.x, w, q);
-    r.y = add_mod(x.y, w, q);
-    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+    const ulonglong2 x = ld2(a + oa);
+    st2(out + oo, make_ulonglong2(add_mod(x.x, w, q), add_mod(x.y, w, q)));
 }
-__global__ __launch_bounds__(NT) void k_mul_plain(u64 *out, const u64 *a, const u64 *p, size_t seg,
-                                                  const Mod *mods, int logN) {
+__global__ __launch_bounds__(NT) void k_mul_plain(u64 *out, const u64 *a, const u64 *p, Seg S, const Mod *mods,
+                                                  int logN) {
     EW_PROLOGUE
     const Mod m = mods[l];
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(a + off + k);
-    const ulonglong2 y = *reinterpret_cast<const ulonglong2 *>(p + (size_t)l * n + k);
-    ulonglong2 r;
-    r.x = mul_barrett(x.x, y.x, m);
-    r.y = mul_barrett(x.y, y.y, m);
     (void)q;
-    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+    const ulonglong2 x = ld2(a + oa), y = ld2(p + ob);
+    st2(out + oo, make_ulonglong2(mul_barrett(x.x, y.x, m), mul_barrett(x.y, y.y, m)));
 }
-// a, b: [2][limbs][n]; d: [3][limbs][n]  (seg = limbs * n)
-__global__ __launch_bounds__(NT) void k_tensor(u64 *d, const u64 *a, const u64 *b, size_t seg, const Mod *mods,
-                                               int logN) {
+// member z: a, b [2][limbs][n] at z * sa / z * sb (sb = 0 broadcasts b);
+// d01 [members][2][limbs][n], d2 [members][limbs][n]
+__global__ __launch_bounds__(NT) void k_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, size_t ln_all,
+                                               size_t sa, size_t sb, const Mod *mods, int logN) {
     const size_t n = (size_t)1 << logN;
     const int l = blockIdx.y;
     const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
     if (k >= n) return;
     const Mod m = mods[l];
-    const size_t o = (size_t)l * n + k;
-    const ulonglong2 a0 = *reinterpret_cast<const ulonglong2 *>(a + o);
-    const ulonglong2 a1 = *reinterpret_cast<const ulonglong2 *>(a + seg + o);
-    const ulonglong2 b0 = *reinterpret_cast<const ulonglong2 *>(b + o);
-    const ulonglong2 b1 = *reinterpret_cast<const ulonglong2 *>(b + seg + o);
-    ulonglong2 d0, d1, d2;
-    d0.x = mul_barrett(a0.x, b0.x, m);
-    d0.y = mul_barrett(a0.y, b0.y, m);
-    d1.x = add_mod(mul_barrett(a0.x, b1.x, m), mul_barrett(a1.x, b0.x, m), m.q);
-    d1.y = add_mod(mul_barrett(a0.y, b1.y, m), mul_barrett(a1.y, b0.y, m), m.q);
-    d2.x = mul_barrett(a1.x, b1.x, m);
-    d2.y = mul_barrett(a1.y, b1.y, m);
-    *reinterpret_cast<ulonglong2 *>(d + o) = d0;
-    *reinterpret_cast<ulonglong2 *>(d + seg + o) = d1;
-    *reinterpret_cast<ulonglong2 *>(d + 2 * seg + o) = d2;
+    const size_t z = blockIdx.z, o = (size_t)l * n + k;
+    const u64 *A = a + z * sa, *Bp = b + z * sb;
+    const ulonglong2 a0 = ld2(A + o), a1 = ld2(A + ln_all + o);
+    const ulonglong2 b0 = ld2(Bp + o), b1 = ld2(Bp + ln_all + o);
+    ulonglong2 e0, e1, e2;
+    e0.x = mul_barrett(a0.x, b0.x, m);
+    e0.y = mul_barrett(a0.y, b0.y, m);
+    e1.x = add_mod(mul_barrett(a0.x, b1.x, m), mul_barrett(a1.x, b0.x, m), m.q);
+    e1.y = add_mod(mul_barrett(a0.y, b1.y, m), mul_barrett(a1.y, b0.y, m), m.q);
+    e2.x = mul_barrett(a1.x, b1.x, m);
+    e2.y = mul_barrett(a1.y, b1.y, m);
+    st2(d01 + z * 2 * ln_all + o, e0);
+    st2(d01 + z * 2 * ln_all + ln_all + o, e1);
+    st2(d2 + z * ln_all + o, e2);
+}
+// out [2][limbs][n] = sum over members of in [members][2][limbs][n]
+__global__ __launch_bounds__(NT) void k_sum_members(u64 *out, const u64 *in, int members, size_t ln_all,
+                                                    const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const u64 q = mods[l].q;
+    const size_t o = (size_t)blockIdx.z * ln_all + (size_t)l * n + k;
+    u64 r0 = 0, r1 = 0;
+    for (int m = 0; m < members; ++m) {
+        const ulonglong2 x = ld2(in + (size_t)m * 2 * ln_all + o);
+        r0 = add_mod(r0, x.x, q);
+        r1 = add_mod(r1, x.y, q);
+    }
+    st2(out + o, make_ulonglong2(r0, r1));
 }
 constexpr int LIN_MAX = 32;
 struct LinArgs {
@@ -131,33 +135,35 @@ struct LinArgs {
     size_t xseg;
 };
 __global__ __launch_bounds__(NT) void k_linear_sum(u64 *out, LinArgs A, size_t seg, const Mod *mods, int logN) {
-    EW_PROLOGUE
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const size_t off = (size_t)blockIdx.z * seg + (size_t)l * n;
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const u64 q = mods[l].q;
     const Mod md = mods[l];
     u64 r0 = 0, r1 = 0;
     if (A.accumulate) {
-        const ulonglong2 o = *reinterpret_cast<const ulonglong2 *>(out + off + k);
+        const ulonglong2 o = ld2(out + off + k);
         r0 = o.x;
         r1 = o.y;
     }
     const size_t xo = (size_t)blockIdx.z * A.xseg + (size_t)l * n + k;
     for (int i = 0; i < A.m; ++i) {
         const u64 w = smod(A.K[i], md);
-        const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(A.x[i] + xo);
+        const ulonglong2 x = ld2(A.x[i] + xo);
         r0 = add_mod(r0, mul_barrett(x.x, w, md), q);
         r1 = add_mod(r1, mul_barrett(x.y, w, md), q);
     }
-    ulonglong2 r;
-    r.x = r0;
-    r.y = r1;
-    *reinterpret_cast<ulonglong2 *>(out + off + k) = r;
+    st2(out + off + k, make_ulonglong2(r0, r1));
 }
-__global__ __launch_bounds__(NT) void k_permute(u64 *out, const u64 *in, const uint32_t *perm, size_t seg,
-                                                int logN) {
+// grid: x = n / NT, y = limb, z = segment
+__global__ __launch_bounds__(NT) void k_permute(u64 *out, const u64 *in, const uint32_t *perm, Seg S, int logN) {
     const size_t n = (size_t)1 << logN;
-    const size_t off = (size_t)blockIdx.z * seg + (size_t)blockIdx.y * n;
+    const size_t ln = (size_t)blockIdx.y * n;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
-    out[off + k] = in[off + perm[k]];
+    out[(size_t)blockIdx.z * S.o + ln + k] = in[(size_t)blockIdx.z * S.a + ln + perm[k]];
 }
 __global__ __launch_bounds__(NT) void k_signed_to_rns(u64 *out, const int64_t *coef, const int *pmap,
                                                       const Mod *mods, int logN) {
@@ -176,29 +182,37 @@ __global__ __launch_bounds__(NT) void k_signed_to_rns(u64 *out, const int64_t *c
     }
     out[(size_t)l * n + k] = r;
 }
-__global__ __launch_bounds__(NT) void k_reduce(u64 *x, size_t seg, const Mod *mods, int logN) {
+__global__ __launch_bounds__(NT) void k_reduce(u64 *x, Seg S, const Mod *mods, int logN) {
     EW_PROLOGUE
     const Mod m = mods[l];
-    ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(x + off + k);
+    (void)q;
+    (void)oa;
+    ulonglong2 v = ld2(x + oo);
     v.x = reduce64(v.x, m);
     v.y = reduce64(v.y, m);
-    (void)q;
-    *reinterpret_cast<ulonglong2 *>(x + off + k) = v;
+    st2(x + oo, v);
 }
 
 // ------------------------------------------------------------ keyswitch ----
 struct ModUpArgs {
     const u64 *qhinv[8], *qhinv_s[8], *qhat[8], *qhat_s[8];
     int lo[8], hi[8];
+    int digits;
+    size_t coef_stride, ext_stride;
 };
 
-// grid: x = n / NT, y = target chunks of TCH, z = digit
+// grid: x = n / NT, y = target chunks of TCH, z = member * digits + digit.
+// coef: member m at m * A.coef_stride ([ell][n], coefficient form);
+// ext: member m at m * A.ext_stride ([digits][W][n]).
 __global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef, int W, ModUpArgs A,
                                                       const int *pmap_ext, const Mod *mods, int logN) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
-    const int j = blockIdx.z;
+    const int j = (int)(blockIdx.z % (unsigned)A.digits);
+    const size_t mb = blockIdx.z / (unsigned)A.digits;
+    coef += mb * A.coef_stride;
+    ext += mb * A.ext_stride;
     const int lo = A.lo[j], hi = A.hi[j], a = hi - lo;
     const int t0 = blockIdx.y * TCH;
     bool any = false;
@@ -227,24 +241,31 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef,
     }
 }
 
-// grid: x = n / NT, y = W targets
+// grid: x = n / NT, y = W targets, z = member.  Member m: acc at m * st.acc
+// ([2][W][n]), ext at m * st.ext, the switched polynomial (NTT) at m * st.d.
 // fold (HMult tail, may be null): on limb t = ell-1 the accumulators start at
-// P * (d0, d1)[ell-1], so the fused ModDown+rescale sees x = d P + acc there.
+// P * (d0, d1)[ell-1] of the member, so the fused ModDown+rescale sees
+// x = d P + acc there.
 __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
                                                  int ell, int W, int nall, int alpha, int digits,
                                                  const uint32_t *perm, const int *pmap_ext, const Mod *mods,
-                                                 int logN, KsFold fold) {
+                                                 int logN, KsStrides st, KsFold fold) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
     const int t = blockIdx.y;
+    const size_t mb = blockIdx.z;
+    acc += mb * st.acc;
+    ext += mb * st.ext;
+    dntt += mb * st.d;
     const int pt = pmap_ext[t];
     const Mod m = mods[pt];
     const size_t kk = perm ? perm[k] : k;
     u64 a0 = 0, a1 = 0;
     if (fold.d && t == ell - 1) {
-        a0 = mul_shoup(fold.d[k], fold.w, fold.ws, m.q);
-        a1 = mul_shoup(fold.d[fold.seg + k], fold.w, fold.ws, m.q);
+        const u64 *fd = fold.d + mb * fold.member;
+        a0 = mul_shoup(fd[k], fold.w, fold.ws, m.q);
+        a1 = mul_shoup(fd[fold.seg + k], fold.w, fold.ws, m.q);
     }
     for (int j = 0; j < digits; ++j) {
         const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
@@ -286,9 +307,11 @@ __global__ __launch_bounds__(NT) void k_moddown_convert(u64 *conv, const u64 *pc
     }
 }
 
-// grid: x = n / (2 NT), y = limb i < ell, z = segment
+// grid: x = n / (2 NT), y = limb i < ell, z = segment.  `add` (rotation: the
+// permuted c0) is added to the even segments (c0 of each member), member
+// s / 2 at (s / 2) * seg_add.
 __global__ __launch_bounds__(NT) void k_moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add,
-                                                       int add_segs, size_t seg_out, size_t seg_acc, size_t seg_add,
+                                                       size_t seg_out, size_t seg_acc, size_t seg_add,
                                                        const u64 *pinv, const u64 *pinv_s, const Mod *mods,
                                                        int logN) {
     const size_t n = (size_t)1 << logN;
@@ -297,17 +320,17 @@ __global__ __launch_bounds__(NT) void k_moddown_finish(u64 *out, const u64 *acc,
     if (k >= n) return;
     const u64 q = mods[l].q, w = pinv[l], wp = pinv_s[l];
     const size_t lo = (size_t)l * n + k;
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(acc + (size_t)s * seg_acc + lo);
-    const ulonglong2 c = *reinterpret_cast<const ulonglong2 *>(conv + (size_t)s * seg_out + lo);
+    const ulonglong2 x = ld2(acc + (size_t)s * seg_acc + lo);
+    const ulonglong2 c = ld2(conv + (size_t)s * seg_out + lo);
     ulonglong2 r;
     r.x = mul_shoup(sub_mod(x.x, c.x, q), w, wp, q);
     r.y = mul_shoup(sub_mod(x.y, c.y, q), w, wp, q);
-    if (add && s < add_segs) {
-        const ulonglong2 d = *reinterpret_cast<const ulonglong2 *>(add + (size_t)s * seg_add + lo);
+    if (add && !(s & 1)) {
+        const ulonglong2 d = ld2(add + (size_t)(s >> 1) * seg_add + lo);
         r.x = add_mod(r.x, d.x, q);
         r.y = add_mod(r.y, d.y, q);
     }
-    *reinterpret_cast<ulonglong2 *>(out + (size_t)s * seg_out + lo) = r;
+    st2(out + (size_t)s * seg_out + lo, r);
 }
 
 // ------------------------------------------- fused ModDown + rescale ----
@@ -423,38 +446,46 @@ inline dim3 pt_grid(int logN, int y, int z) {
 }  // namespace
 
 // ============================================================ wrappers =====
-void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, const Mod *mods, int logN,
             hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_add, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, b, seg, mods, logN);
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_add, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, b, S, mods, logN);
 }
-void ew_sub(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+void ew_sub(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, const Mod *mods, int logN,
             hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_sub, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, b, seg, mods, logN);
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_sub, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, b, S, mods, logN);
 }
-void ew_neg(u64 *out, const u64 *a, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_neg, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, seg, mods, logN);
+void ew_neg(u64 *out, const u64 *a, int limbs, int segs, Seg S, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_neg, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, S, mods, logN);
 }
-void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
                    hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_mul_scalar, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, K, seg, mods, logN);
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_mul_scalar, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, K, S, mods, logN);
 }
-void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, const Mod *mods, int logN, hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_add_scalar, ew_grid(logN, limbs, 1), dim3(NT), 0, st, out, a, K, (size_t)0, mods, logN);
+void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
+                   hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_add_scalar, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, K, S, mods, logN);
 }
-void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, size_t seg, const Mod *mods,
-                  int logN, hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_mul_plain, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, p, seg, mods, logN);
+void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, Seg S, const Mod *mods, int logN,
+                  hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_mul_plain, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, p, S, mods, logN);
 }
-void ew_tensor(u64 *d, const u64 *a, const u64 *b, int limbs, const Mod *mods, int logN, hipStream_t st) {
-    if (limbs <= 0) return;
-    const size_t seg = (size_t)limbs << logN;
-    hipLaunchKernelGGL(k_tensor, ew_grid(logN, limbs, 1), dim3(NT), 0, st, d, a, b, seg, mods, logN);
+void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int members, size_t sa, size_t sb,
+               const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0 || members <= 0) return;
+    const size_t ln_all = (size_t)limbs << logN;
+    hipLaunchKernelGGL(k_tensor, ew_grid(logN, limbs, members), dim3(NT), 0, st, d01, d2, a, b, ln_all, sa, sb, mods,
+                       logN);
+}
+void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0 || members <= 0) return;
+    const size_t ln_all = (size_t)limbs << logN;
+    hipLaunchKernelGGL(k_sum_members, ew_grid(logN, limbs, 2), dim3(NT), 0, st, out, in, members, ln_all, mods, logN);
 }
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
                    size_t xseg, const Mod *mods, int logN, hipStream_t st) {
@@ -472,10 +503,10 @@ void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int 
         if (m == 0) break;
     }
 }
-void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, size_t seg, int logN,
+void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,
                 hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_permute, pt_grid(logN, limbs, segs), dim3(NT), 0, st, out, in, perm, seg, logN);
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_permute, pt_grid(logN, limbs, segs), dim3(NT), 0, st, out, in, perm, S, logN);
 }
 void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap, const Mod *mods, int logN,
                       hipStream_t st) {
@@ -483,12 +514,13 @@ void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap,
     hipLaunchKernelGGL(k_signed_to_rns, pt_grid(logN, limbs, 1), dim3(NT), 0, st, out, coef, pmap, mods, logN);
 }
 void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_reduce, ew_grid(logN, limbs, segs), dim3(NT), 0, st, x, seg, mods, logN);
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_reduce, ew_grid(logN, limbs, segs), dim3(NT), 0, st, x, Seg{seg, seg, 0}, mods, logN);
 }
 
-void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, const int *pmap_ext,
-                   const u64 *tabs, const size_t *tab_off, const Mod *mods, int logN, hipStream_t st) {
+void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
+                   size_t coef_stride, size_t ext_stride, const int *pmap_ext, const u64 *tabs,
+                   const size_t *tab_off, const Mod *mods, int logN, hipStream_t st) {
     const int W = ell + K;
     ModUpArgs A{};
     for (int j = 0; j < digits; ++j) {
@@ -501,16 +533,19 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
         A.lo[j] = lo;
         A.hi[j] = hi;
     }
-    hipLaunchKernelGGL(k_modup_convert, pt_grid(logN, (W + TCH - 1) / TCH, digits), dim3(NT), 0, st, ext, coef, W, A,
-                       pmap_ext, mods, logN);
+    A.digits = digits;
+    A.coef_stride = coef_stride;
+    A.ext_stride = ext_stride;
+    hipLaunchKernelGGL(k_modup_convert, pt_grid(logN, (W + TCH - 1) / TCH, digits * members), dim3(NT), 0, st, ext,
+                       coef, W, A, pmap_ext, mods, logN);
 }
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
-              hipStream_t st, KsFold fold) {
+              hipStream_t st, int members, KsStrides str, KsFold fold) {
     (void)nq;
     const int W = ell + K;
-    hipLaunchKernelGGL(k_ks_inner, pt_grid(logN, W, 1), dim3(NT), 0, st, acc, ext, dntt, key, ell, W, nall, alpha,
-                       digits, perm, pmap_ext, mods, logN, fold);
+    hipLaunchKernelGGL(k_ks_inner, pt_grid(logN, W, members), dim3(NT), 0, st, acc, ext, dntt, key, ell, W, nall,
+                       alpha, digits, perm, pmap_ext, mods, logN, str, fold);
 }
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
@@ -534,11 +569,11 @@ void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t se
     hipLaunchKernelGGL(k_moddown_convert, pt_grid(logN, (ell + TCH - 1) / TCH, segs), dim3(NT), 0, st, conv, pc, ell,
                        K, nq, seg_in, seg_out, phinv, phinv_s, phat, phat_s, mods, logN);
 }
-void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int add_segs, int ell, int segs,
-                    size_t seg_out, size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s,
-                    const Mod *mods, int logN, hipStream_t st) {
-    hipLaunchKernelGGL(k_moddown_finish, ew_grid(logN, ell, segs), dim3(NT), 0, st, out, acc, conv, add, add_segs,
-                       seg_out, seg_acc, seg_add, pinv, pinv_s, mods, logN);
+void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,
+                    size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s, const Mod *mods, int logN,
+                    hipStream_t st) {
+    hipLaunchKernelGGL(k_moddown_finish, ew_grid(logN, ell, segs), dim3(NT), 0, st, out, acc, conv, add, seg_out,
+                       seg_acc, seg_add, pinv, pinv_s, mods, logN);
 }
 void rescale_prep(u64 *tmp, const u64 *last, int ell, int segs, size_t seg_last, size_t seg_tmp, const Mod *mods,
                   int logN, hipStream_t st) {

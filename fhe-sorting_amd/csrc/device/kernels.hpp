@@ -40,31 +40,46 @@ void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
                  hipStream_t st);
 void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
                  hipStream_t st);
-// forward NTT of `count` limbs scattered in one buffer: limb y sits at
-// data + smap[y] * n and belongs to prime pmap[y] (ModUp: every digit at once)
-void ntt_forward_mapped(u64 *data, int count, const int *smap, const int *pmap, const NttTables &T, hipStream_t st);
+// forward NTT of `count` limbs scattered in each of `segs` segments: limb y
+// of segment z sits at data + z * seg + smap[y] * n and belongs to prime
+// pmap[y] (ModUp: every digit of every member at once)
+void ntt_forward_mapped(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,
+                        const NttTables &T, hipStream_t st);
+
+// Segment strides (u64 units) of the output and the two inputs of an
+// element-wise launch: segment z of out/a/b starts at z*o / z*a / z*b.
+// A ciphertext batch of B members [B][2][limbs][n] is 2B segments of stride
+// limbs*n; a plaintext operand is broadcast with stride 0.
+struct Seg {
+    size_t o, a, b;
+};
 
 // element-wise, Q basis (limb l <-> prime l); out may alias inputs
-void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, const Mod *mods, int logN,
             hipStream_t st);
-void ew_sub(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+void ew_sub(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, const Mod *mods, int logN,
             hipStream_t st);
-void ew_neg(u64 *out, const u64 *a, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st);
+void ew_neg(u64 *out, const u64 *a, int limbs, int segs, Seg S, const Mod *mods, int logN, hipStream_t st);
 // out = a * (K mod q_l)   (K: signed integer constant, reduced in-kernel)
-void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, size_t seg, const Mod *mods, int logN,
+void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
                    hipStream_t st);
-// out = a + (K mod q_l)   (one segment)
-void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, const Mod *mods, int logN, hipStream_t st);
-// out[s] = a[s] * p  (p: one [limbs][n] plaintext, Barrett)
-void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, size_t seg, const Mod *mods,
-                  int logN, hipStream_t st);
-// d0 = a0 b0, d1 = a0 b1 + a1 b0, d2 = a1 b1   (a, b: [2][limbs][n]; d: [3][limbs][n])
-void ew_tensor(u64 *d, const u64 *a, const u64 *b, int limbs, const Mod *mods, int logN, hipStream_t st);
+// out = a + (K mod q_l)
+void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
+                   hipStream_t st);
+// out[s] = a[s] * p[s]  (Barrett; S.b = 0 broadcasts one plaintext)
+void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, Seg S, const Mod *mods, int logN,
+                  hipStream_t st);
+// per member m: d0 = a0 b0, d1 = a0 b1 + a1 b0 -> d01 [m][2][limbs][n]; d2 = a1 b1 -> d2 [m][limbs][n]
+// (a member m at m * sa, b member at m * sb; sb = 0 broadcasts one ciphertext)
+void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int members, size_t sa, size_t sb,
+               const Mod *mods, int logN, hipStream_t st);
+// out [2][limbs][n] = sum_m in [m][2][limbs][n]
+void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st);
 // out = sum_i (K_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride)
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
                    size_t xseg, const Mod *mods, int logN, hipStream_t st);
 // out[l][k] = in[l][perm[k]]
-void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, size_t seg, int logN,
+void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,
                 hipStream_t st);
 // out[l][k] = coef[k] mod q_{pmap[l]} (signed 64-bit coefficients)
 void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap, const Mod *mods, int logN,
@@ -75,20 +90,25 @@ struct ModUpTab {
     const u64 *qhinv, *qhinv_s;  // [alpha]        (digit source primes)
     const u64 *qhat, *qhat_s;    // [alpha][W]     (W = ell + K targets)
 };
-// ext[j][t][k] for every digit j and target t not in digit j (coefficient in, NTT NOT applied)
-void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, const int *pmap_ext,
+// ext[m][j][t][k] for every member m, digit j and target t not in digit j
+// (coefficient in, NTT NOT applied); coef member stride coef_stride, ext member stride ext_stride
+void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
+                   size_t coef_stride, size_t ext_stride, const int *pmap_ext,
                    const u64 *tabs /* packed, see engine */, const size_t *tab_off, const Mod *mods, int logN,
                    hipStream_t st);
-// acc0/acc1 [W][n]: sum_j ext_j * key_j   (own-digit limbs read from dntt)
+// acc0/acc1 [W][n] per member: sum_j ext_j * key_j   (own-digit limbs read from dntt)
+struct KsStrides {
+    size_t acc = 0, ext = 0, d = 0;  // member strides of acc [2][W][n], ext, dntt
+};
 // optional HMult fold: limb ell-1 of the accumulators starts at w * d[k], w * d[seg + k]
 struct KsFold {
-    const u64 *d = nullptr;  // d0[ell-1] (NTT); d1[ell-1] at d + seg
-    size_t seg = 0;
+    const u64 *d = nullptr;  // d0[ell-1] (NTT) of member 0; d1[ell-1] at d + seg
+    size_t seg = 0, member = 0;
     u64 w = 0, ws = 0;       // P mod q_{ell-1} and its Shoup companion
 };
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
-              hipStream_t st, KsFold fold = KsFold());
+              hipStream_t st, int members, KsStrides str, KsFold fold = KsFold());
 // fused ModDown + rescale of an HMult (see kernels.hip): corr [segs][ell-1][n]
 // from acc [segs][W][n] whose limbs ell-1 .. W-1 are in coefficient form
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
@@ -103,10 +123,10 @@ void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, in
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out,
                      int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
                      const Mod *mods, int logN, hipStream_t st);
-// out[s][i] = (acc[s][i] - conv[s][i]) * Pinv_i (+ add[s][i] for s < add_segs)
-void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int add_segs, int ell, int segs,
-                    size_t seg_out, size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s,
-                    const Mod *mods, int logN, hipStream_t st);
+// out[s][i] = (acc[s][i] - conv[s][i]) * Pinv_i (+ add[s/2][i] on even s, i.e. c0 of each member)
+void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,
+                    size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s, const Mod *mods, int logN,
+                    hipStream_t st);
 
 // ------------------------------------------------------------------ rescale
 // tmp[s][i][k] = centred(last[s][k]) mod q_i for i < ell-1

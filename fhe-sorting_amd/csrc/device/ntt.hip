@@ -79,7 +79,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
     const int k2 = COLS ? logN - PB : 0;
     const int limb = blockIdx.y;
     const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (smap ? (size_t)smap[limb] * n : (size_t)blockIdx.z * seg + (size_t)limb * n);
+    u64 *a = data + (size_t)blockIdx.z * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
     const u64 q = Tb.mods[p].q, q2 = 2 * q;
     const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
 
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
     const int k2 = COLS ? logN - PB : 0;
     const int limb = blockIdx.y;
     const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (smap ? (size_t)smap[limb] * n : (size_t)blockIdx.z * seg + (size_t)limb * n);
+    u64 *a = data + (size_t)blockIdx.z * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
     const u64 q = Tb.mods[p].q, q2 = 2 * q;
     const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
 
@@ -305,11 +305,12 @@ void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     dispatch<true, false>(k1, data, limbs, segs, seg, pmap, nullptr, T, st);
 }
 
-void ntt_forward_mapped(u64 *data, int count, const int *smap, const int *pmap, const NttTables &T, hipStream_t st) {
-    if (count <= 0) return;
+void ntt_forward_mapped(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,
+                        const NttTables &T, hipStream_t st) {
+    if (count <= 0 || segs <= 0) return;
     const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
-    dispatch<true, true>(k1, data, count, 1, 0, pmap, smap, T, st);
-    dispatch<false, true>(k2, data, count, 1, 0, pmap, smap, T, st);
+    dispatch<true, true>(k1, data, count, segs, seg, pmap, smap, T, st);
+    dispatch<false, true>(k2, data, count, segs, seg, pmap, smap, T, st);
 }
 
 }  // namespace dev

@@ -138,79 +138,101 @@ struct Engine::Impl {
     }
 
     // ------------------------------------------------------- key switch --
-    // ext[j][t] (NTT form) for all digits of d ([ell][n], NTT form)
-    std::shared_ptr<DevMem> modup(const u64 *d, size_t ell) {
+    // Every helper works on `members` independent polynomials at once (a
+    // ciphertext batch): member m of an input sits at m * stride.
+    //
+    // ext[m][j][t] (NTT form) for all digits of d[m] ([ell][n], NTT form)
+    std::shared_ptr<DevMem> modup(const u64 *d, size_t ell, int members, size_t d_stride) {
         const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         const int digits = P.digits_at(ell);
-        auto coef = alloc(ell * nn * 8);
+        auto coef = alloc((size_t)members * ell * nn * 8);
         u64 *c = static_cast<u64 *>(coef->p);
-        HIP_OK(hipMemcpyAsync(c, d, ell * nn * 8, hipMemcpyDeviceToDevice, st));
-        dev::ntt_inverse(c, (int)ell, 1, 0, nullptr, T, st);
-        auto extm = alloc((size_t)digits * W * nn * 8);
+        if (d_stride == ell * nn || members == 1)
+            HIP_OK(hipMemcpyAsync(c, d, (size_t)members * ell * nn * 8, hipMemcpyDeviceToDevice, st));
+        else
+            HIP_OK(hipMemcpy2DAsync(c, ell * nn * 8, d, d_stride * 8, ell * nn * 8, (size_t)members,
+                                    hipMemcpyDeviceToDevice, st));
+        dev::ntt_inverse(c, (int)ell, members, ell * nn, nullptr, T, st);
+        const size_t es = (size_t)digits * W * nn;
+        auto extm = alloc((size_t)members * es * 8);
         u64 *e = static_cast<u64 *>(extm->p);
-        dev::modup_convert(e, c, (int)ell, P.K, P.alpha, digits, ext(ell), modup_tab, LT.modup_off[ell].data(), mods,
-                           P.logN, st);
+        dev::modup_convert(e, c, (int)ell, P.K, P.alpha, digits, members, ell * nn, es, ext(ell), modup_tab,
+                           LT.modup_off[ell].data(), mods, P.logN, st);
         const size_t mo = LT.modup_map_off[ell];
-        dev::ntt_forward_mapped(e, (int)LT.modup_map_cnt[ell], modup_smap + mo, modup_pmap + mo, T, st);
+        dev::ntt_forward_mapped(e, (int)LT.modup_map_cnt[ell], members, es, modup_smap + mo, modup_pmap + mo, T, st);
         return extm;
     }
-    // out[2][ell][n] = ModDown(sum_j ext_j * key_j) (+ add for the first add_segs segments)
-    void ks_apply(const u64 *e, const u64 *d, size_t ell, const u64 *key, const uint32_t *pm, u64 *out,
-                  const u64 *add, int add_segs, size_t add_seg) {
+    // rotation key switch: out[m] (= [2][ell][n]) = ModDown(sum_j ext_j * key_j) + (add[m], 0);
+    // d: the switched polynomial of member m at m * d_stride (NTT form)
+    void ks_apply(const u64 *e, const u64 *d, size_t d_stride, size_t ell, int members, const u64 *key,
+                  const uint32_t *pm, u64 *out, const u64 *add, size_t add_stride) {
         const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         const int digits = P.digits_at(ell);
-        auto accm = alloc(2 * W * nn * 8);
+        const int segs = 2 * members;
+        auto accm = alloc((size_t)segs * W * nn * 8);
         u64 *acc = static_cast<u64 *>(accm->p);
+        dev::KsStrides str;
+        str.acc = 2 * W * nn;
+        str.ext = (size_t)digits * W * nn;
+        str.d = d_stride;
         dev::ks_inner(acc, e, d, key, (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha, digits, pm, ext(ell), mods,
-                      P.logN, st);
-        // ModDown of both accumulators
-        dev::ntt_inverse(acc + ell * nn, (int)K, 2, W * nn, ext(ell) + ell, T, st);
-        auto convm = alloc(2 * ell * nn * 8);
+                      P.logN, st, members, str);
+        // ModDown of both accumulators of every member
+        dev::ntt_inverse(acc + ell * nn, (int)K, segs, W * nn, ext(ell) + ell, T, st);
+        auto convm = alloc((size_t)segs * ell * nn * 8);
         u64 *conv = static_cast<u64 *>(convm->p);
-        dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, 2, phinv, phinv_s,
+        dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, segs, phinv, phinv_s,
                              phat, phat_s, mods, P.logN, st);
-        dev::ntt_forward(conv, (int)ell, 2, ell * nn, nullptr, T, st);
-        dev::moddown_finish(out, acc, conv, add, add_segs, (int)ell, 2, ell * nn, W * nn, add_seg, pinv, pinv_s, mods,
+        dev::ntt_forward(conv, (int)ell, segs, ell * nn, nullptr, T, st);
+        dev::moddown_finish(out, acc, conv, add, (int)ell, segs, ell * nn, W * nn, add_stride, pinv, pinv_s, mods,
                             P.logN, st);
     }
-    // HMult tail, fused: out [2][ell-1][n] = Rescale(d01 + ModDown(Sum_j ext_j * key_j)).
-    // Bit-identical to ks_apply(add = d01) followed by rescale(): both compute
-    // ((acc - Conv(acc_P)) P^-1 + d - [y_last]) q_last^-1 mod q_i, but here only
-    // limb ell-1 and the P limbs leave the NTT domain and one forward NTT of
-    // ell-1 limbs per polynomial serves both divisions.
-    void mul_tail(const u64 *e, const u64 *d, size_t ell, u64 *out) {
+    // HMult tail, fused: out[m] ([2][ell-1][n]) = Rescale(d01[m] + ModDown(Sum_j ext_j * key_j)).
+    // Bit-identical to a ModDown with d01 added followed by rescale(): both
+    // compute ((acc - Conv(acc_P)) P^-1 + d - [y_last]) q_last^-1 mod q_i, but
+    // here only limb ell-1 and the P limbs leave the NTT domain and one forward
+    // NTT of ell-1 limbs per polynomial serves both divisions.
+    // d01 [members][2][ell][n], d2 [members][ell][n] (NTT form).
+    void mul_tail(const u64 *e, const u64 *d01, const u64 *d2, size_t ell, int members, u64 *out) {
         const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         const int digits = P.digits_at(ell);
-        auto accm = alloc(2 * W * nn * 8);
+        const int segs = 2 * members;
+        auto accm = alloc((size_t)segs * W * nn * 8);
         u64 *acc = static_cast<u64 *>(accm->p);
+        dev::KsStrides str;
+        str.acc = 2 * W * nn;
+        str.ext = (size_t)digits * W * nn;
+        str.d = ell * nn;
         dev::KsFold fold;
-        fold.d = d + (ell - 1) * nn;
+        fold.d = d01 + (ell - 1) * nn;
         fold.seg = ell * nn;
+        fold.member = 2 * ell * nn;
         fold.w = LT.pmod[ell - 1];
         fold.ws = LT.pmod_s[ell - 1];
-        dev::ks_inner(acc, e, d + 2 * ell * nn, static_cast<u64 *>(relin->p), (int)ell, P.K, (int)P.nq(),
-                      (int)P.nall(), P.alpha, digits, nullptr, ext(ell), mods, P.logN, st, fold);
-        dev::ntt_inverse(acc + (ell - 1) * nn, (int)K + 1, 2, W * nn, ext(ell) + (ell - 1), T, st);
-        auto corrm = alloc(2 * (ell - 1) * nn * 8);
+        dev::ks_inner(acc, e, d2, static_cast<u64 *>(relin->p), (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha,
+                      digits, nullptr, ext(ell), mods, P.logN, st, members, str, fold);
+        dev::ntt_inverse(acc + (ell - 1) * nn, (int)K + 1, segs, W * nn, ext(ell) + (ell - 1), T, st);
+        auto corrm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *corr = static_cast<u64 *>(corrm->p);
-        dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, 2, phinv, phinv_s,
-                                     phat, phat_s, pinv, pinv_s, pmod, pmod_s, mods, P.logN, st);
-        dev::ntt_forward(corr, (int)(ell - 1), 2, (ell - 1) * nn, nullptr, T, st);
-        dev::mul_tail_finish(out, acc, d, corr, (int)ell, 2, (ell - 1) * nn, W * nn, ell * nn, pqlinv + ell * P.nq(),
-                             pqlinv_s + ell * P.nq(), pmod, pmod_s, mods, P.logN, st);
+        dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, segs, phinv,
+                                     phinv_s, phat, phat_s, pinv, pinv_s, pmod, pmod_s, mods, P.logN, st);
+        dev::ntt_forward(corr, (int)(ell - 1), segs, (ell - 1) * nn, nullptr, T, st);
+        dev::mul_tail_finish(out, acc, d01, corr, (int)ell, segs, (ell - 1) * nn, W * nn, ell * nn,
+                             pqlinv + ell * P.nq(), pqlinv_s + ell * P.nq(), pmod, pmod_s, mods, P.logN, st);
     }
-    // out [2][ell-1][n] from in [2][ell][n] with input segment stride seg_in
-    void rescale(const u64 *in, size_t ell, size_t seg_in, u64 *out) {
+    // out [segs][ell-1][n] from in [segs][ell][n] with input segment stride seg_in
+    void rescale(const u64 *in, size_t ell, size_t seg_in, int segs, u64 *out) {
         const size_t nn = n();
-        auto lastm = alloc(2 * nn * 8);
+        auto lastm = alloc((size_t)segs * nn * 8);
         u64 *last = static_cast<u64 *>(lastm->p);
-        HIP_OK(hipMemcpy2DAsync(last, nn * 8, in + (ell - 1) * nn, seg_in * 8, nn * 8, 2, hipMemcpyDeviceToDevice, st));
-        dev::ntt_inverse(last, 1, 2, nn, ext(ell) + (ell - 1), T, st);
-        auto tmpm = alloc(2 * (ell - 1) * nn * 8);
+        HIP_OK(hipMemcpy2DAsync(last, nn * 8, in + (ell - 1) * nn, seg_in * 8, nn * 8, (size_t)segs,
+                                hipMemcpyDeviceToDevice, st));
+        dev::ntt_inverse(last, 1, segs, nn, ext(ell) + (ell - 1), T, st);
+        auto tmpm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *tmp = static_cast<u64 *>(tmpm->p);
-        dev::rescale_prep(tmp, last, (int)ell, 2, nn, (ell - 1) * nn, mods, P.logN, st);
-        dev::ntt_forward(tmp, (int)(ell - 1), 2, (ell - 1) * nn, nullptr, T, st);
-        dev::rescale_finish(out, in, tmp, (int)ell, 2, (ell - 1) * nn, seg_in, (ell - 1) * nn,
+        dev::rescale_prep(tmp, last, (int)ell, segs, nn, (ell - 1) * nn, mods, P.logN, st);
+        dev::ntt_forward(tmp, (int)(ell - 1), segs, (ell - 1) * nn, nullptr, T, st);
+        dev::rescale_finish(out, in, tmp, (int)ell, segs, (ell - 1) * nn, seg_in, (ell - 1) * nn,
                             qlinv + ell * P.nq(), qlinv_s + ell * P.nq(), mods, P.logN, st);
     }
 };
@@ -313,9 +335,11 @@ void Engine::d2h(u64 *dst, const u64 *src, size_t count) {
 void *Engine::stream_handle() { return impl->st; }
 int Engine::device() const { return impl->device; }
 
-CtPtr Engine::new_ct(int level, int slots, double scale, size_t limbs) {
+CtPtr Engine::new_ct(int level, int slots, double scale, size_t limbs, int batch) {
+    if (batch < 1) throw std::invalid_argument("ciphertext batch must be >= 1");
     auto c = std::make_shared<Ciphertext>();
-    c->mem = impl->alloc(2 * limbs * n() * 8);
+    c->mem = impl->alloc(2 * (size_t)batch * limbs * n() * 8);
+    c->batch = batch;
     c->data = static_cast<u64 *>(c->mem->p);
     c->level = level;
     c->slots = slots;
@@ -362,12 +386,12 @@ void Engine::keygen() {
     u64 *t = static_cast<u64 *>(tmp->p);
     dev::ew_signed_to_rns(pk, static_cast<int64_t *>(ec->p), (int)nq, nullptr, I.mods, I.P.logN, I.st);
     dev::ntt_forward(pk, (int)nq, 1, 0, nullptr, I.T, I.st);
-    dev::ew_mul_plain(t, pk + nq * n, S, (int)nq, 1, 0, I.mods, I.P.logN, I.st);
-    dev::ew_sub(pk, pk, t, (int)nq, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_mul_plain(t, pk + nq * n, S, (int)nq, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
+    dev::ew_sub(pk, pk, t, (int)nq, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
     HIP_OK(hipStreamSynchronize(I.st));
     // relinearisation key: s' = s^2
     auto s2 = I.alloc(nq * n * 8);
-    dev::ew_mul_plain(static_cast<u64 *>(s2->p), S, S, (int)nq, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_mul_plain(static_cast<u64 *>(s2->p), S, S, (int)nq, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
     I.relin = I.alloc((size_t)I.key_digits * 2 * nall * n * 8);
     // (key material generated by the shared helper below)
     extern void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out);
@@ -414,12 +438,12 @@ void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out) {
         HIP_OK(hipMemcpyAsync(ec->p, E[j].data(), n * 8, hipMemcpyHostToDevice, I.st));
         dev::ew_signed_to_rns(bj, static_cast<int64_t *>(ec->p), (int)nall, nullptr, I.mods, I.P.logN, I.st);
         dev::ntt_forward(bj, (int)nall, 1, 0, nullptr, I.T, I.st);
-        dev::ew_mul_plain(tmp, aj, S, (int)nall, 1, 0, I.mods, I.P.logN, I.st);
-        dev::ew_sub(bj, bj, tmp, (int)nall, 1, 0, I.mods, I.P.logN, I.st);
+        dev::ew_mul_plain(tmp, aj, S, (int)nall, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
+        dev::ew_sub(bj, bj, tmp, (int)nall, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
         const size_t lo = (size_t)j * I.P.alpha, hi = std::min(nq, (size_t)(j + 1) * I.P.alpha);
         for (size_t i = lo; i < hi; ++i) {
-            dev::ew_mul_scalar(tmp, sp + i * n, Pmod[i], 1, 1, 0, I.mods + i, I.P.logN, I.st);
-            dev::ew_add(bj + i * n, bj + i * n, tmp, 1, 1, 0, I.mods + i, I.P.logN, I.st);
+            dev::ew_mul_scalar(tmp, sp + i * n, Pmod[i], 1, 1, dev::Seg{0, 0, 0}, I.mods + i, I.P.logN, I.st);
+            dev::ew_add(bj + i * n, bj + i * n, tmp, 1, 1, dev::Seg{0, 0, 0}, I.mods + i, I.P.logN, I.st);
         }
         HIP_OK(hipStreamSynchronize(I.st));  // host buffers A[j], E[j] go out of scope after the loop
     }
@@ -433,7 +457,7 @@ void Engine::gen_rotation_keys(const std::vector<int> &rot) {
     for (int k : rot) {
         const u64 g = host::galois_for_rotation(I.P.logN, k);
         if (g == 1 || I.rotkeys.count(g)) continue;
-        dev::ew_permute(static_cast<u64 *>(sp->p), static_cast<const u64 *>(I.s_ntt->p), I.perm(g), (int)nq, 1, 0,
+        dev::ew_permute(static_cast<u64 *>(sp->p), static_cast<const u64 *>(I.s_ntt->p), I.perm(g), (int)nq, 1, dev::Seg{0, 0, 0},
                         I.P.logN, I.st);
         auto key = I.alloc((size_t)I.key_digits * 2 * nall * n * 8);
         gen_switch_key_impl(I, static_cast<u64 *>(sp->p), g, static_cast<u64 *>(key->p));
@@ -522,11 +546,11 @@ CtPtr Engine::encrypt_pt(const Plaintext &pt) {
     auto ct = new_ct(pt.level, pt.slots, pt.scale, ell);
     const u64 *pk = static_cast<const u64 *>(I.pk->p);
     u64 *c0 = ct->data, *c1 = ct->data + ell * n;
-    dev::ew_mul_plain(c0, r, pk, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
-    dev::ew_add(c0, c0, r + ell * n, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
-    dev::ew_add(c0, c0, pt.data, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
-    dev::ew_mul_plain(c1, r, pk + nq * n, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
-    dev::ew_add(c1, c1, r + 2 * ell * n, (int)ell, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_mul_plain(c0, r, pk, (int)ell, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
+    dev::ew_add(c0, c0, r + ell * n, (int)ell, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
+    dev::ew_add(c0, c0, pt.data, (int)ell, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
+    dev::ew_mul_plain(c1, r, pk + nq * n, (int)ell, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
+    dev::ew_add(c1, c1, r + 2 * ell * n, (int)ell, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
     HIP_OK(hipStreamSynchronize(I.st));
     return ct;
 }
@@ -537,14 +561,15 @@ CtPtr Engine::encrypt(const std::vector<double> &v, int slots, int level) {
 
 std::vector<double> Engine::decrypt(const Ciphertext &ct) {
     auto &I = *impl;
+    if (ct.batch != 1) throw std::invalid_argument("decrypt: one ciphertext at a time (use member())");
     if (!I.s_ntt) throw std::runtime_error("decrypt: no secret key");
     const size_t n = I.n();
     const int L2 = ct.limbs >= 2 ? 2 : 1;  // m = c0 + c1 s on the first one or two limbs
     auto mm = I.alloc(L2 * n * 8);
     u64 *m = static_cast<u64 *>(mm->p);
-    dev::ew_mul_plain(m, ct.data + ct.limbs * n, static_cast<const u64 *>(I.s_ntt->p), L2, 1, 0, I.mods, I.P.logN,
+    dev::ew_mul_plain(m, ct.data + ct.limbs * n, static_cast<const u64 *>(I.s_ntt->p), L2, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN,
                       I.st);
-    dev::ew_add(m, m, ct.data, L2, 1, 0, I.mods, I.P.logN, I.st);
+    dev::ew_add(m, m, ct.data, L2, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
     dev::ntt_inverse(m, L2, 1, 0, nullptr, I.T, I.st);
     std::vector<u64> h(L2 * n);
     HIP_OK(hipMemcpyAsync(h.data(), m, L2 * n * 8, hipMemcpyDeviceToHost, I.st));
@@ -560,6 +585,7 @@ CtPtr Engine::upload(const u64 *h, size_t limbs, int level, int slots, double sc
     return ct;
 }
 void Engine::download(const Ciphertext &ct, u64 *h) {
+    if (ct.batch != 1) throw std::invalid_argument("download: one ciphertext at a time (use member())");
     HIP_OK(hipMemcpyAsync(h, ct.data, 2 * ct.limbs * n() * 8, hipMemcpyDeviceToHost, impl->st));
     HIP_OK(hipStreamSynchronize(impl->st));
 }
@@ -581,17 +607,27 @@ PtPtr Engine::upload_pt(const u64 *h, size_t limbs, int level, int slots, double
 #define MODS impl->mods
 #define ST impl->st
 
+// Every op below is batch-transparent: a ciphertext of `batch` members is
+// [batch][2][limbs][n], i.e. 2*batch segments of stride limbs*n, and each
+// kernel launch covers all of them.
+namespace {
+inline dev::Seg seg3(size_t o, size_t a, size_t b) { return dev::Seg{o, a, b}; }
+void same_batch(const Ciphertext &a, const Ciphertext &b, const char *op) {
+    if (a.batch != b.batch) throw std::invalid_argument(std::string(op) + ": batch size mismatch");
+}
+}  // namespace
+
 CtPtr Engine::clone(const Ciphertext &a) {
-    auto r = new_ct(a.level, a.slots, a.scale, a.limbs);
-    HIP_OK(hipMemcpyAsync(r->data, a.data, 2 * a.limbs * n() * 8, hipMemcpyDeviceToDevice, ST));
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
+    HIP_OK(hipMemcpyAsync(r->data, a.data, 2 * (size_t)a.batch * a.limbs * n() * 8, hipMemcpyDeviceToDevice, ST));
     return r;
 }
 
 CtPtr Engine::drop_to(const Ciphertext &a, int level) {
     if (level < a.level) throw std::invalid_argument("drop_to: cannot raise level");
     const size_t ell = impl->P.limbs_at(level), nn = n();
-    auto r = new_ct(level, a.slots, a.scale, ell);
-    HIP_OK(hipMemcpy2DAsync(r->data, ell * nn * 8, a.data, a.limbs * nn * 8, ell * nn * 8, 2,
+    auto r = new_ct(level, a.slots, a.scale, ell, a.batch);
+    HIP_OK(hipMemcpy2DAsync(r->data, ell * nn * 8, a.data, a.limbs * nn * 8, ell * nn * 8, 2 * (size_t)a.batch,
                             hipMemcpyDeviceToDevice, ST));
     return r;
 }
@@ -604,17 +640,21 @@ void Engine::match_levels(CtPtr &a, CtPtr &b) {
 }
 
 CtPtr Engine::add(const Ciphertext &a0, const Ciphertext &b0) {
+    same_batch(a0, b0, "add");
     auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
     match_levels(a, b);
-    auto r = new_ct(a->level, a->slots, a->scale, a->limbs);
-    dev::ew_add(r->data, a->data, b->data, (int)a->limbs, 2, a->limbs * n(), MODS, LOGN, ST);
+    const size_t ln = a->limbs * n();
+    auto r = new_ct(a->level, a->slots, a->scale, a->limbs, a->batch);
+    dev::ew_add(r->data, a->data, b->data, (int)a->limbs, 2 * a->batch, seg3(ln, ln, ln), MODS, LOGN, ST);
     return r;
 }
 CtPtr Engine::sub(const Ciphertext &a0, const Ciphertext &b0) {
+    same_batch(a0, b0, "sub");
     auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
     match_levels(a, b);
-    auto r = new_ct(a->level, a->slots, a->scale, a->limbs);
-    dev::ew_sub(r->data, a->data, b->data, (int)a->limbs, 2, a->limbs * n(), MODS, LOGN, ST);
+    const size_t ln = a->limbs * n();
+    auto r = new_ct(a->level, a->slots, a->scale, a->limbs, a->batch);
+    dev::ew_sub(r->data, a->data, b->data, (int)a->limbs, 2 * a->batch, seg3(ln, ln, ln), MODS, LOGN, ST);
     return r;
 }
 void Engine::add_inplace(CtPtr &acc, const Ciphertext &b) {
@@ -622,61 +662,70 @@ void Engine::add_inplace(CtPtr &acc, const Ciphertext &b) {
         acc = clone(b);
         return;
     }
+    same_batch(*acc, b, "add_inplace");
     if (acc->level == b.level && acc.use_count() == 1) {
-        dev::ew_add(acc->data, acc->data, b.data, (int)b.limbs, 2, b.limbs * n(), MODS, LOGN, ST);
+        const size_t ln = b.limbs * n();
+        dev::ew_add(acc->data, acc->data, b.data, (int)b.limbs, 2 * b.batch, seg3(ln, ln, ln), MODS, LOGN, ST);
         return;
     }
     acc = add(*acc, b);
 }
 CtPtr Engine::negate(const Ciphertext &a) {
-    auto r = new_ct(a.level, a.slots, a.scale, a.limbs);
-    dev::ew_neg(r->data, a.data, (int)a.limbs, 2, a.limbs * n(), MODS, LOGN, ST);
+    const size_t ln = a.limbs * n();
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
+    dev::ew_neg(r->data, a.data, (int)a.limbs, 2 * a.batch, seg3(ln, ln, 0), MODS, LOGN, ST);
     return r;
 }
+// plaintext ops touch c0 of every member: segments 0, 2, 4, ... (stride 2 limbs n)
 CtPtr Engine::add_plain(const Ciphertext &a, const Plaintext &p) {
     if (p.level != a.level) throw std::invalid_argument("add_plain: level mismatch");
     auto r = clone(a);
-    dev::ew_add(r->data, r->data, p.data, (int)a.limbs, 1, 0, MODS, LOGN, ST);
+    const size_t l2 = 2 * a.limbs * n();
+    dev::ew_add(r->data, r->data, p.data, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
     return r;
 }
 CtPtr Engine::sub_plain(const Ciphertext &a, const Plaintext &p) {
     if (p.level != a.level) throw std::invalid_argument("sub_plain: level mismatch");
     auto r = clone(a);
-    dev::ew_sub(r->data, r->data, p.data, (int)a.limbs, 1, 0, MODS, LOGN, ST);
+    const size_t l2 = 2 * a.limbs * n();
+    dev::ew_sub(r->data, r->data, p.data, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
     return r;
 }
 CtPtr Engine::plain_sub(const Plaintext &p, const Ciphertext &a) {
     if (p.level != a.level) throw std::invalid_argument("plain_sub: level mismatch");
     auto r = negate(a);
-    dev::ew_add(r->data, r->data, p.data, (int)a.limbs, 1, 0, MODS, LOGN, ST);
+    const size_t l2 = 2 * a.limbs * n();
+    dev::ew_add(r->data, r->data, p.data, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
     return r;
 }
 CtPtr Engine::add_const(const Ciphertext &a, double c) {
     auto r = clone(a);
     const i64 K = host::const_at_scale(c, a.scale);
-    dev::ew_add_scalar(r->data, r->data, K, (int)a.limbs, MODS, LOGN, ST);
+    const size_t l2 = 2 * a.limbs * n();
+    dev::ew_add_scalar(r->data, r->data, K, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
     return r;
 }
 CtPtr Engine::mul_int(const Ciphertext &a, i64 K) {
-    auto r = new_ct(a.level, a.slots, a.scale, a.limbs);
-    dev::ew_mul_scalar(r->data, a.data, K, (int)a.limbs, 2, a.limbs * n(), MODS, LOGN, ST);
+    const size_t ln = a.limbs * n();
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
+    dev::ew_mul_scalar(r->data, a.data, K, (int)a.limbs, 2 * a.batch, seg3(ln, ln, 0), MODS, LOGN, ST);
     return r;
 }
 CtPtr Engine::mul_const_to(const Ciphertext &a, double c, int target) {
     auto &I = *impl;
     if (target <= a.level) throw std::invalid_argument("mul_const_to: target must exceed level");
     if (target > I.P.L) throw std::runtime_error("mul_const_to: no levels left");
-    ctr.constmult++;
-    ctr.rescale++;
+    ctr.constmult += a.batch;
+    ctr.rescale += a.batch;
     const size_t nn = n(), ell = I.P.limbs_at(target - 1);
     const i64 K = host::const_to_target(c, I.P.delta[target], I.P.primes[I.P.L - target + 1], a.scale);
-    auto tm = I.alloc(2 * ell * nn * 8);
+    const int segs = 2 * a.batch;
+    auto tm = I.alloc((size_t)segs * ell * nn * 8);
     u64 *t = static_cast<u64 *>(tm->p);
     // multiply the (dropped) input: each segment is read with the input's own stride
-    dev::ew_mul_scalar(t, a.data, K, (int)ell, 1, 0, MODS, LOGN, ST);
-    dev::ew_mul_scalar(t + ell * nn, a.data + a.limbs * nn, K, (int)ell, 1, 0, MODS, LOGN, ST);
-    auto r = new_ct(target, a.slots, I.P.delta[target], ell - 1);
-    I.rescale(t, ell, ell * nn, r->data);
+    dev::ew_mul_scalar(t, a.data, K, (int)ell, segs, seg3(ell * nn, a.limbs * nn, 0), MODS, LOGN, ST);
+    auto r = new_ct(target, a.slots, I.P.delta[target], ell - 1, a.batch);
+    I.rescale(t, ell, ell * nn, segs, r->data);
     return r;
 }
 CtPtr Engine::mul_const(const Ciphertext &a, double c) { return mul_const_to(a, c, a.level + 1); }
@@ -687,49 +736,56 @@ CtPtr Engine::level_adjust(const Ciphertext &a, int target) {
 CtPtr Engine::rescale(const Ciphertext &a) {
     auto &I = *impl;
     if (a.level >= I.P.L) throw std::runtime_error("rescale: no levels left");
-    ctr.rescale++;
-    auto r = new_ct(a.level + 1, a.slots, a.scale / (double)I.P.primes[a.limbs - 1], a.limbs - 1);
-    I.rescale(a.data, a.limbs, a.limbs * n(), r->data);
+    ctr.rescale += a.batch;
+    auto r = new_ct(a.level + 1, a.slots, a.scale / (double)I.P.primes[a.limbs - 1], a.limbs - 1, a.batch);
+    I.rescale(a.data, a.limbs, a.limbs * n(), 2 * a.batch, r->data);
     return r;
 }
 CtPtr Engine::mul_plain(const Ciphertext &a, const Plaintext &p) {
     auto &I = *impl;
     if (p.level != a.level) throw std::invalid_argument("mul_plain: level mismatch");
     if (a.level >= I.P.L) throw std::runtime_error("mul_plain: no levels left");
-    ctr.ptmult++;
-    ctr.rescale++;
+    ctr.ptmult += a.batch;
+    ctr.rescale += a.batch;
     const size_t nn = n(), ell = a.limbs;
-    auto tm = I.alloc(2 * ell * nn * 8);
+    const int segs = 2 * a.batch;
+    auto tm = I.alloc((size_t)segs * ell * nn * 8);
     u64 *t = static_cast<u64 *>(tm->p);
-    dev::ew_mul_plain(t, a.data, p.data, (int)ell, 2, ell * nn, MODS, LOGN, ST);
-    auto r = new_ct(a.level + 1, a.slots, I.P.delta[a.level + 1], ell - 1);
-    I.rescale(t, ell, ell * nn, r->data);
+    dev::ew_mul_plain(t, a.data, p.data, (int)ell, segs, seg3(ell * nn, ell * nn, 0), MODS, LOGN, ST);
+    auto r = new_ct(a.level + 1, a.slots, I.P.delta[a.level + 1], ell - 1, a.batch);
+    I.rescale(t, ell, ell * nn, segs, r->data);
     return r;
 }
 
+// ct x ct with relinearisation and rescale.  b may be a single ciphertext
+// multiplied into every member of a (broadcast).
 CtPtr Engine::mul(const Ciphertext &a0, const Ciphertext &b0) {
     auto &I = *impl;
+    if (a0.batch != b0.batch && b0.batch != 1) throw std::invalid_argument("mul: batch size mismatch");
     auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
     match_levels(a, b);
     if (a->level >= I.P.L) throw std::runtime_error("mul: no levels left");
     if (!I.relin) throw std::runtime_error("mul: no relinearisation key");
-    ctr.hmult++;
-    ctr.keyswitch++;
-    ctr.rescale++;
+    const int B = a->batch;
+    ctr.hmult += B;
+    ctr.keyswitch += B;
+    ctr.rescale += B;
     const size_t nn = n(), ell = a->limbs;
-    auto dm = I.alloc(3 * ell * nn * 8);
-    u64 *d = static_cast<u64 *>(dm->p);
-    dev::ew_tensor(d, a->data, b->data, (int)ell, MODS, LOGN, ST);
-    auto extm = I.modup(d + 2 * ell * nn, ell);
-    auto r = new_ct(a->level + 1, a->slots, I.P.delta[a->level + 1], ell - 1);
-    I.mul_tail(static_cast<u64 *>(extm->p), d, ell, r->data);
+    auto d01m = I.alloc((size_t)B * 2 * ell * nn * 8), d2m = I.alloc((size_t)B * ell * nn * 8);
+    u64 *d01 = static_cast<u64 *>(d01m->p), *d2 = static_cast<u64 *>(d2m->p);
+    dev::ew_tensor(d01, d2, a->data, b->data, (int)ell, B, 2 * ell * nn, b->batch == 1 ? 0 : 2 * ell * nn, MODS,
+                   LOGN, ST);
+    auto extm = I.modup(d2, ell, B, ell * nn);
+    auto r = new_ct(a->level + 1, a->slots, I.P.delta[a->level + 1], ell - 1, B);
+    I.mul_tail(static_cast<u64 *>(extm->p), d01, d2, ell, B, r->data);
     return r;
 }
 CtPtr Engine::square(const Ciphertext &a) { return mul(a, a); }
 
 std::vector<CtPtr> Engine::rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks) {
     auto &I = *impl;
-    const size_t nn = n(), ell = a.limbs;
+    const size_t nn = n(), ell = a.limbs, ln = ell * nn;
+    const int B = a.batch;
     std::vector<CtPtr> outs;
     std::shared_ptr<DevMem> extm;
     for (long k : ks) {
@@ -740,16 +796,16 @@ std::vector<CtPtr> Engine::rotate_hoisted(const Ciphertext &a, const std::vector
         }
         auto it = I.rotkeys.find(g);
         if (it == I.rotkeys.end()) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
-        if (!extm) extm = I.modup(a.data + ell * nn, ell);
-        ctr.keyswitch++;
-        ctr.rotations++;
+        if (!extm) extm = I.modup(a.data + ln, ell, B, 2 * ln);  // c1 of every member
+        ctr.keyswitch += B;
+        ctr.rotations += B;
         const uint32_t *pm = I.perm(g);
-        auto c0m = I.alloc(ell * nn * 8);
+        auto c0m = I.alloc((size_t)B * ln * 8);
         u64 *c0p = static_cast<u64 *>(c0m->p);
-        dev::ew_permute(c0p, a.data, pm, (int)ell, 1, 0, LOGN, ST);
-        auto r = new_ct(a.level, a.slots, a.scale, ell);
-        I.ks_apply(static_cast<u64 *>(extm->p), a.data + ell * nn, ell, static_cast<u64 *>(it->second->p), pm,
-                   r->data, c0p, 1, ell * nn);
+        dev::ew_permute(c0p, a.data, pm, (int)ell, B, seg3(ln, 2 * ln, 0), LOGN, ST);
+        auto r = new_ct(a.level, a.slots, a.scale, ell, B);
+        I.ks_apply(static_cast<u64 *>(extm->p), a.data + ln, 2 * ln, ell, B, static_cast<u64 *>(it->second->p), pm,
+                   r->data, c0p, ln);
         outs.push_back(r);
     }
     return outs;
@@ -759,19 +815,21 @@ CtPtr Engine::rotate(const Ciphertext &a, long k) { return rotate_hoisted(a, {k}
 CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c, int target) {
     auto &I = *impl;
     if (target > I.P.L) throw std::runtime_error("linear_sum_to: no levels left");
+    if (xs.empty()) throw std::invalid_argument("linear_sum_to: no inputs");
+    const int B = xs[0]->batch;
+    const int segs = 2 * B;
     const size_t nn = n(), ell = I.P.limbs_at(target - 1);
     const double qd = (double)I.P.primes[I.P.L - target + 1];
-    auto tm = I.alloc(2 * ell * nn * 8);
+    auto tm = I.alloc((size_t)segs * ell * nn * 8);
     u64 *t = static_cast<u64 *>(tm->p);
-    std::vector<const u64 *> ptr0, ptr1;
-    std::vector<int64_t> K;
     // group inputs by their limb count (segment stride) so each launch has one xseg
     std::map<size_t, std::vector<size_t>> by_limbs;
     for (size_t i = 0; i < xs.size(); ++i) {
         if (xs[i]->level > target - 1) throw std::invalid_argument("linear_sum_to: input level too high");
+        if (xs[i]->batch != B) throw std::invalid_argument("linear_sum_to: batch size mismatch");
         by_limbs[xs[i]->limbs].push_back(i);
     }
-    ctr.constmult += xs.size();
+    ctr.constmult += xs.size() * B;
     bool first = true;
     for (auto &kv : by_limbs) {
         std::vector<const u64 *> p;
@@ -782,38 +840,68 @@ CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std
         }
         // accumulate: first group writes, later groups add
         if (first) {
-            dev::ew_linear_sum(t, p.data(), k.data(), (int)p.size(), (int)ell, 2, ell * nn, kv.first * nn, MODS, LOGN,
-                               ST);
+            dev::ew_linear_sum(t, p.data(), k.data(), (int)p.size(), (int)ell, segs, ell * nn, kv.first * nn, MODS,
+                               LOGN, ST);
             first = false;
         } else {
-            auto sm = I.alloc(2 * ell * nn * 8);
+            auto sm = I.alloc((size_t)segs * ell * nn * 8);
             u64 *s = static_cast<u64 *>(sm->p);
-            dev::ew_linear_sum(s, p.data(), k.data(), (int)p.size(), (int)ell, 2, ell * nn, kv.first * nn, MODS, LOGN,
-                               ST);
-            dev::ew_add(t, t, s, (int)ell, 2, ell * nn, MODS, LOGN, ST);
+            dev::ew_linear_sum(s, p.data(), k.data(), (int)p.size(), (int)ell, segs, ell * nn, kv.first * nn, MODS,
+                               LOGN, ST);
+            dev::ew_add(t, t, s, (int)ell, segs, seg3(ell * nn, ell * nn, ell * nn), MODS, LOGN, ST);
         }
     }
-    if (first) HIP_OK(hipMemsetAsync(t, 0, 2 * ell * nn * 8, ST));
-    ctr.rescale++;
-    auto r = new_ct(target, xs.empty() ? 0 : xs[0]->slots, I.P.delta[target], ell - 1);
-    I.rescale(t, ell, ell * nn, r->data);
+    ctr.rescale += B;
+    auto r = new_ct(target, xs[0]->slots, I.P.delta[target], ell - 1, B);
+    I.rescale(t, ell, ell * nn, segs, r->data);
     return r;
 }
 
-CtPtr Engine::trivial_const(double c, int level, int slots) {
-    auto r = zero_like(level, slots);
+CtPtr Engine::trivial_const(double c, int level, int slots, int batch) {
+    auto r = zero_like(level, slots, batch);
     const i64 K = host::const_at_scale(c, impl->P.delta[level]);
-    dev::ew_add_scalar(r->data, r->data, K, (int)r->limbs, MODS, LOGN, ST);
+    const size_t l2 = 2 * r->limbs * n();
+    dev::ew_add_scalar(r->data, r->data, K, (int)r->limbs, batch, seg3(l2, l2, 0), MODS, LOGN, ST);
     return r;
 }
-CtPtr Engine::zero_like(int level, int slots) {
+CtPtr Engine::zero_like(int level, int slots, int batch) {
     const size_t ell = impl->P.limbs_at(level);
-    auto r = new_ct(level, slots, impl->P.delta[level], ell);
-    HIP_OK(hipMemsetAsync(r->data, 0, 2 * ell * n() * 8, ST));
+    auto r = new_ct(level, slots, impl->P.delta[level], ell, batch);
+    HIP_OK(hipMemsetAsync(r->data, 0, 2 * (size_t)batch * ell * n() * 8, ST));
     return r;
 }
 void Engine::reduce_after_allreduce(Ciphertext &ct) {
-    dev::ew_reduce(ct.data, (int)ct.limbs, 2, ct.limbs * n(), MODS, LOGN, ST);
+    dev::ew_reduce(ct.data, (int)ct.limbs, 2 * ct.batch, ct.limbs * n(), MODS, LOGN, ST);
+}
+
+// ---------------------------------------------------------------- batches --
+CtPtr Engine::stack(const std::vector<const Ciphertext *> &xs) {
+    if (xs.empty()) throw std::invalid_argument("stack: no inputs");
+    int B = 0;
+    for (auto *x : xs) {
+        if (x->level != xs[0]->level) throw std::invalid_argument("stack: level mismatch");
+        B += x->batch;
+    }
+    auto r = new_ct(xs[0]->level, xs[0]->slots, xs[0]->scale, xs[0]->limbs, B);
+    const size_t ct_words = 2 * xs[0]->limbs * n();
+    size_t off = 0;
+    for (auto *x : xs) {
+        HIP_OK(hipMemcpyAsync(r->data + off, x->data, x->batch * ct_words * 8, hipMemcpyDeviceToDevice, ST));
+        off += x->batch * ct_words;
+    }
+    return r;
+}
+CtPtr Engine::member(const Ciphertext &a, int m) {
+    if (m < 0 || m >= a.batch) throw std::out_of_range("member: index out of range");
+    auto r = std::make_shared<Ciphertext>(a);
+    r->data = a.data + (size_t)m * 2 * a.limbs * n();
+    r->batch = 1;
+    return r;
+}
+CtPtr Engine::sum_members(const Ciphertext &a) {
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, 1);
+    dev::ew_sum_members(r->data, a.data, a.batch, (int)a.limbs, MODS, LOGN, ST);
+    return r;
 }
 
 // =================================================== kernel-level (tests) ==
@@ -840,7 +928,7 @@ void Engine::modup_host(const u64 *d, size_t ell, u64 *ext) {
     const int digits = I.P.digits_at(ell);
     auto dm = I.alloc(ell * nn * 8);
     HIP_OK(hipMemcpyAsync(dm->p, d, ell * nn * 8, hipMemcpyHostToDevice, ST));
-    auto e = I.modup(static_cast<u64 *>(dm->p), ell);
+    auto e = I.modup(static_cast<u64 *>(dm->p), ell, 1, ell * nn);
     // own-digit limbs are not materialised on the device: fill them from d
     u64 *ep = static_cast<u64 *>(e->p);
     for (int j = 0; j < digits; ++j) {
@@ -864,7 +952,7 @@ void Engine::moddown_host(const u64 *in, size_t ell, u64 *out) {
                          I.phinv_s, I.phat, I.phat_s, MODS, LOGN, ST);
     dev::ntt_forward(conv, (int)ell, 1, 0, nullptr, I.T, ST);
     auto om = I.alloc(ell * nn * 8);
-    dev::moddown_finish(static_cast<u64 *>(om->p), x, conv, nullptr, 0, (int)ell, 1, ell * nn, W * nn, 0, I.pinv,
+    dev::moddown_finish(static_cast<u64 *>(om->p), x, conv, nullptr, (int)ell, 1, ell * nn, W * nn, 0, I.pinv,
                         I.pinv_s, MODS, LOGN, ST);
     HIP_OK(hipMemcpyAsync(out, om->p, ell * nn * 8, hipMemcpyDeviceToHost, ST));
     HIP_OK(hipStreamSynchronize(ST));
@@ -874,7 +962,8 @@ void Engine::automorph_host(const u64 *in, size_t limbs, u64 g, u64 *out) {
     const size_t nn = n();
     auto im = I.alloc(limbs * nn * 8), om = I.alloc(limbs * nn * 8);
     HIP_OK(hipMemcpyAsync(im->p, in, limbs * nn * 8, hipMemcpyHostToDevice, ST));
-    dev::ew_permute(static_cast<u64 *>(om->p), static_cast<u64 *>(im->p), I.perm(g), (int)limbs, 1, 0, LOGN, ST);
+    dev::ew_permute(static_cast<u64 *>(om->p), static_cast<u64 *>(im->p), I.perm(g), (int)limbs, 1, dev::Seg{0, 0, 0},
+                    LOGN, ST);
     HIP_OK(hipMemcpyAsync(out, om->p, limbs * nn * 8, hipMemcpyDeviceToHost, ST));
     HIP_OK(hipStreamSynchronize(ST));
 }
@@ -966,9 +1055,13 @@ void Engine::time_kernel(const std::string &name, size_t ell, int iters, double 
     dev::ew_reduce(d, (int)ell, 3, ell * nn, MODS, LOGN, ST);
     std::function<void()> launch;
     if (name == "ks_inner") {
-        launch = [&] {
+        dev::KsStrides str;
+        str.acc = 2 * W * nn;
+        str.ext = (size_t)digits * W * nn;
+        str.d = ell * nn;
+        launch = [&, str] {
             dev::ks_inner(acc, e, d, static_cast<u64 *>(I.relin->p), (int)ell, (int)K, (int)I.P.nq(), (int)I.P.nall(),
-                          I.P.alpha, digits, nullptr, I.ext(ell), MODS, LOGN, ST);
+                          I.P.alpha, digits, nullptr, I.ext(ell), MODS, LOGN, ST, 1, str);
         };
         bytes = (double)((size_t)digits * W * 3 + 2 * W) * B;  // ext + key(b,a) read, 2 accumulators written
     } else if (name == "ntt_fwd") {
@@ -976,8 +1069,8 @@ void Engine::time_kernel(const std::string &name, size_t ell, int iters, double 
         bytes = 2.0 * 2.0 * (double)(W * digits) * B;  // two passes, each reads + writes every limb
     } else if (name == "modup_convert") {
         launch = [&] {
-            dev::modup_convert(e, d, (int)ell, (int)K, I.P.alpha, digits, I.ext(ell), I.modup_tab,
-                               I.LT.modup_off[ell].data(), MODS, LOGN, ST);
+            dev::modup_convert(e, d, (int)ell, (int)K, I.P.alpha, digits, 1, ell * nn, (size_t)digits * W * nn,
+                               I.ext(ell), I.modup_tab, I.LT.modup_off[ell].data(), MODS, LOGN, ST);
         };
         bytes = (double)(ell + (size_t)digits * W - ell) * B;
     } else {

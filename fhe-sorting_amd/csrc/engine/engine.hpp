@@ -28,13 +28,18 @@ using i64 = int64_t;
 
 struct DevMem;  // pooled device allocation (engine.hip)
 
+// A ciphertext batch: `batch` independent ciphertexts at one level, stored
+// [batch][2][limbs][n].  Every op applies member-wise in the same launches, so
+// the comparator / index-check pipelines of all rank-sort batches run as one
+// (DESIGN.md §6).  batch = 1 is an ordinary ciphertext.
 struct Ciphertext {
     std::shared_ptr<DevMem> mem;
-    u64 *data = nullptr;  // [2][limbs][n]
+    u64 *data = nullptr;  // [batch][2][limbs][n]
     int level = 0;
     int slots = 0;
     double scale = 0;
     size_t limbs = 0;
+    int batch = 1;
 };
 using CtPtr = std::shared_ptr<Ciphertext>;
 
@@ -105,8 +110,12 @@ class Engine {
     CtPtr rescale(const Ciphertext &a);
     CtPtr drop_to(const Ciphertext &a, int level);
     CtPtr linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c, int target);
-    CtPtr trivial_const(double c, int level, int slots);
-    CtPtr zero_like(int level, int slots);
+    CtPtr trivial_const(double c, int level, int slots, int batch = 1);
+    CtPtr zero_like(int level, int slots, int batch = 1);
+    // batches: stack (copies; equal levels), member view (no copy), member sum
+    CtPtr stack(const std::vector<const Ciphertext *> &xs);
+    CtPtr member(const Ciphertext &a, int m);
+    CtPtr sum_members(const Ciphertext &a);
     // sum over ranks already done into ct (u64 add, no reduction): reduce mod q
     void reduce_after_allreduce(Ciphertext &ct);
 
@@ -144,7 +153,7 @@ class Engine {
     std::unique_ptr<Impl> impl;
 
   private:
-    CtPtr new_ct(int level, int slots, double scale, size_t limbs);
+    CtPtr new_ct(int level, int slots, double scale, size_t limbs, int batch = 1);
 };
 
 // Raised on a rotation index with no key (the reference's OpenFHE raises on

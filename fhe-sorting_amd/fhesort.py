@@ -101,6 +101,10 @@ _SIGS = {
     'fhe_stream': (vp, [vp]),
     'fhe_time_kernel': (C.c_int, [vp, C.c_char_p, C.c_int, C.c_int, dp, dp]),
     'fhe_kernel_clock_start': (C.c_int, [vp]),
+    'fhe_set_sort_stack': (C.c_int, [vp, C.c_int]),
+    'fhe_ct_stack': (C.c_int, [vp, C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_void_p)]),
+    'fhe_ct_member': (C.c_int, [vp, vp, C.c_int, C.POINTER(C.c_void_p)]),
+    'fhe_ct_sum_members': (C.c_int, [vp, vp, C.POINTER(C.c_void_p)]),
     'fhe_kernel_clock_stop': (C.c_int, [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
 }
 
@@ -308,6 +312,15 @@ class Context:
         _chk(lib().fhe_rotate_hoisted(self.h, a.h, _int(ks), len(ks), outs))
         return [Ct(self, outs[i]) for i in range(len(ks))]
 
+    def stack(self, xs):
+        arr = (C.c_void_p * len(xs))(*[x.h for x in xs])
+        out = C.c_void_p()
+        _chk(lib().fhe_ct_stack(self.h, arr, len(xs), C.byref(out)))
+        return Ct(self, out.value)
+
+    def member(self, a, m): return self._new(lib().fhe_ct_member, a.h, m)
+    def sum_members(self, a): return self._new(lib().fhe_ct_sum_members, a.h)
+
     def linear_sum_to(self, xs, cs, target):
         arr = (C.c_void_p * len(xs))(*[x.h for x in xs])
         cs = np.ascontiguousarray(cs, dtype=np.float64)
@@ -343,6 +356,9 @@ class Context:
     def comm_init(self, uid, rank, world):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         _chk(lib().fhe_comm_init(self.h, buf, rank, world))
+
+    def set_sort_stack(self, m):
+        _chk(lib().fhe_set_sort_stack(self.h, m))
 
     def ct_allreduce(self, ct):
         _chk(lib().fhe_ct_allreduce(self.h, ct.h))

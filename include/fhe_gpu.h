@@ -87,6 +87,14 @@ int fhe_ct_info(const fhe_ct *ct, int *level, int *slots, double *scale, int *li
 /* Ciphertext::SetSlots (src/sort_algo.h:429,447,501) */
 int fhe_ct_set_slots(fhe_ct *ct, int slots);
 int fhe_ct_free(fhe_ct *ct);
+/* ciphertext batches: `m` ciphertexts at one level stacked into one handle of
+ * batch sum(batch_i) ([batch][2][limbs][n]); every op applies member-wise in
+ * the same kernel launches (the reference loops over batches instead:
+ * src/sort_algo.h:474-491, 713-742).  member() is a view (no copy);
+ * sum_members() adds all members into one ciphertext. */
+int fhe_ct_stack(fhe_ctx *ctx, const fhe_ct *const *xs, int m, fhe_ct **out);
+int fhe_ct_member(fhe_ctx *ctx, const fhe_ct *a, int m, fhe_ct **out);
+int fhe_ct_sum_members(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out);
 /* MakeCKKSPackedPlaintext(v, 1, level, nullptr, slots) (src/sort_algo.h:341,573) */
 int fhe_pt_encode(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_pt **out);
 int fhe_pt_upload(fhe_ctx *ctx, const uint64_t *host, int limbs, int level, int slots, double scale,
@@ -150,6 +158,11 @@ typedef void (*fhe_allreduce_fn)(uint64_t *dev_data, uint64_t count, void *user)
 int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, const int32_t *rots, int nrot,
                     int n, int dg, int df, int mode, int shard_rank, int shard_world, fhe_allreduce_fn allreduce,
                     void *user, fhe_ct **out);
+
+/* how many of a rank's sort batches run stacked through one compare / one
+ * sinc PS (default 32: every launch then carries up to 32 ciphertexts; HBM use
+ * grows with it).  Results do not depend on it. */
+int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack);
 
 /* ------------------------------------------------------ multi-GPU (RCCL) */
 int fhe_comm_get_unique_id(uint8_t id[128]);

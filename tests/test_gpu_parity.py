@@ -226,3 +226,65 @@ def test_direct_sort_bit_exact(N, cfg):
     y = gpu.decrypt(gout)
     assert np.max(np.abs(y - np.sort(x))) < 0.01
     assert gout.level <= depth
+
+
+def test_batched_ops_match_members(pair):
+    """A stacked ciphertext batch gives, member by member, exactly the oracle's
+    single-ciphertext result for every op the sort path uses."""
+    orc, gpu = pair
+    rng = np.random.default_rng(3)
+    oxs = [orc.encrypt(rng.uniform(-0.9, 0.9, 16), 16) for _ in range(3)]
+    S = gpu.stack([gpu.from_oracle(o) for o in oxs])
+    one = gpu.from_oracle(oxs[1])
+    pt_vals = rng.uniform(-1, 1, 16)
+    cases = [
+        ('square', lambda g: gpu.square(g), lambda o: orc.square(o)),
+        ('mul_self', lambda g: gpu.mul(g, g), lambda o: orc.mul(o, o)),
+        ('mul_bcast', lambda g: gpu.mul(g, one), lambda o: orc.mul(o, oxs[1])),
+        ('rotate', lambda g: gpu.rotate(g, 3), lambda o: orc.rotate(o, 3)),
+        ('hoisted', lambda g: gpu.rotate_hoisted(g, [1, -4])[1], lambda o: orc.rotate_hoisted(o, [1, -4])[1]),
+        ('add_const', lambda g: gpu.add_const(g, 0.375), lambda o: orc.add_const(o, 0.375)),
+        ('mul_const', lambda g: gpu.mul_const(g, -1.25), lambda o: orc.mul_const(o, -1.25)),
+        ('mul_const_to', lambda g: gpu.mul_const_to(g, 0.5, 3), lambda o: orc.mul_const_to(o, 0.5, 3)),
+        ('add', lambda g: gpu.add(g, g), lambda o: orc.add(o, o)),
+        ('negate', lambda g: gpu.negate(g), lambda o: orc.negate(o)),
+        ('lin', lambda g: gpu.linear_sum_to([g, gpu.square(g)], [0.5, -2.0], 2),
+         lambda o: orc.linear_sum_to([o, orc.square(o)], [0.5, -2.0], 2)),
+        ('mul_plain', lambda g: gpu.mul_plain(g, gpu.encode(pt_vals, 16, 0)),
+         lambda o: orc.mul_plain(o, orc.encode(pt_vals, 16, 0))),
+        ('cheb27', lambda g: gpu.cheb(g, np.linspace(1, 0.1, 28)), lambda o: orc.cheb(o, np.linspace(1, 0.1, 28))),
+        ('sign', lambda g: gpu.sign(g, 3, 1, 1), lambda o: orc.sign(o, 3, 1, 1)),
+    ]
+    for name, gop, oop in cases:
+        R = gop(S)
+        for m, o in enumerate(oxs):
+            try:
+                same(gpu.member(R, m), oop(o))
+            except AssertionError as e:
+                raise AssertionError(f'{name}, member {m}: {e}')
+    total = gpu.sum_members(S)
+    ref = orc.add(orc.add(oxs[0], oxs[1]), oxs[2])
+    same(total, ref)
+
+
+@pytest.mark.parametrize('stack', [32, 3])
+def test_direct_sort_multi_batch_stacked(stack):
+    """N=64 at ring 2^11: 4 comparator batches and 4 index-check batches run
+    stacked (all four at once, or 3 + 1) and match the oracle's serial loop."""
+    N, cfg = 64, (3, 3, 2)
+    depth, rots = O.size_parameters(N)
+    orc = O.Context(11, depth, 40, 60, 3, seed=7)
+    orc.gen_rotation_keys(rots)
+    gpu = F.Context(11, depth, 40, 60, 3, seed=7, keygen=False)
+    gpu.load_keys_from(orc, rots)
+    gpu.set_sort_stack(stack)
+    x = np.random.default_rng(64).permutation(N) / N
+    ox = orc.encrypt(x, N)
+    gx = gpu.from_oracle(ox)
+    grank = gpu.direct_sort(gx, N, rots, cfg, mode=1)
+    orank = orc.direct_sort(ox, N, rots, cfg, mode=1)
+    same(grank, orank)
+    gout = gpu.direct_sort(gx, N, rots, cfg)
+    oout = orc.direct_sort(ox, N, rots, cfg)
+    same(gout, oout)
+    assert np.max(np.abs(gpu.decrypt(gout) - np.sort(x))) < 0.01
