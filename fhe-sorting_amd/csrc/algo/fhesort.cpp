@@ -461,11 +461,13 @@ void DirectSortN::reducePartial(CtPtr &acc, int slots) {
 CtPtr DirectSortN::vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is) {
     CtPtr result;
     for (int j = 0; j < num_partition / np; ++j) {
-        CtPtr Tj;
+        std::vector<const Ciphertext *> cs;
+        std::vector<const Plaintext *> ps;
         for (int i = 0; i < np; ++i) {
-            const Plaintext &pm = mask(0, num_slots, np * j + i, -is * num_partition - j * np, baby[i]->level);
-            cc.add_inplace(Tj, *cc.mul_plain(*baby[i], pm));
+            cs.push_back(baby[i].get());
+            ps.push_back(&mask(0, num_slots, np * j + i, -is * num_partition - j * np, baby[i]->level));
         }
+        CtPtr Tj = cc.mul_plain_sum(cs, ps);  // one rescale per masked sum (src/sort_algo.h:341-346)
         CtPtr o = rot.rotate(*Tj, is * num_partition + j * np);
         cc.add_inplace(result, *o);
     }
@@ -515,11 +517,13 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
 CtPtr DirectSortN::blindRotationOptN(const std::vector<CtPtr> &mi, int num_slots, int np, int ib, int num_partition) {
     CtPtr result;
     for (int i = 0; i < (num_slots / N) / np; ++i) {
-        CtPtr tmp;
+        std::vector<const Ciphertext *> cs;
+        std::vector<const Plaintext *> ps;
         for (int j = 0; j < np; ++j) {
-            const Plaintext &pm = mask(0, num_slots, np * i + j, j, mi[j]->level);
-            cc.add_inplace(tmp, *cc.mul_plain(*mi[j], pm));
+            cs.push_back(mi[j].get());
+            ps.push_back(&mask(0, num_slots, np * i + j, j, mi[j]->level));
         }
+        CtPtr tmp = cc.mul_plain_sum(cs, ps);  // src/sort_algo.h:573-577
         tmp = rot.rotate(*tmp, ib * num_partition + i * np);
         cc.add_inplace(result, *tmp);
     }
@@ -530,11 +534,13 @@ CtPtr DirectSortN::blindRotationStacked(const std::vector<CtPtr> &mi, int num_sl
                                         int num_partition) {
     CtPtr result;
     for (int i = 0; i < (num_slots / N) / np; ++i) {
-        CtPtr tmp;
+        std::vector<const Ciphertext *> cs;
+        std::vector<const Plaintext *> ps;
         for (int j = 0; j < np; ++j) {
-            const Plaintext &pm = mask(0, num_slots, np * i + j, j, mi[j]->level);
-            cc.add_inplace(tmp, *cc.mul_plain(*mi[j], pm));
+            cs.push_back(mi[j].get());
+            ps.push_back(&mask(0, num_slots, np * i + j, j, mi[j]->level));
         }
+        CtPtr tmp = cc.mul_plain_sum(cs, ps);
         for (size_t m = 0; m < ibs.size(); ++m) {
             CtPtr one = tmp->batch == 1 ? tmp : cc.member(*tmp, (int)m);
             cc.add_inplace(result, *rot.rotate(*one, ibs[m] * num_partition + i * np));

@@ -157,6 +157,20 @@ int fhe_ct_free(fhe_ct *ct) {
     delete ct;
     return FHE_OK;
 }
+int fhe_mul_plain_sum(fhe_ctx *ctx, const fhe_ct *const *cts, const fhe_pt *const *pts, int m, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        std::vector<const Ciphertext *> a;
+        std::vector<const Plaintext *> p;
+        for (int i = 0; i < m; ++i) {
+            NEED(cts[i]);
+            NEED(pts[i]);
+            a.push_back(cts[i]->p.get());
+            p.push_back(pts[i]->p.get());
+        }
+        *out = wrap(ctx->eng->mul_plain_sum(a, p));
+    });
+}
 int fhe_ct_stack(fhe_ctx *ctx, const fhe_ct *const *xs, int m, fhe_ct **out) {
     return guard([&] {
         NEED(ctx);

@@ -134,29 +134,65 @@ struct LinArgs {
     int m, accumulate;
     size_t xseg;
 };
+// out = sum_i (K_i mod q_l) x_i: the block's limb constants are reduced once
+// into LDS, the sum is accumulated lazily in 128 bits and reduced once.
 __global__ __launch_bounds__(NT) void k_linear_sum(u64 *out, LinArgs A, size_t seg, const Mod *mods, int logN) {
+    __shared__ u64 w[LIN_MAX];
     const size_t n = (size_t)1 << logN;
     const int l = blockIdx.y;
+    const Mod md = mods[l];
+    if ((int)threadIdx.x < A.m) w[threadIdx.x] = smod(A.K[threadIdx.x], md);
+    __syncthreads();
     const size_t off = (size_t)blockIdx.z * seg + (size_t)l * n;
     const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
     if (k >= n) return;
-    const u64 q = mods[l].q;
-    const Mod md = mods[l];
-    u64 r0 = 0, r1 = 0;
+    Acc128 r0, r1;
     if (A.accumulate) {
         const ulonglong2 o = ld2(out + off + k);
-        r0 = o.x;
-        r1 = o.y;
+        r0.lo = o.x;
+        r1.lo = o.y;
     }
     const size_t xo = (size_t)blockIdx.z * A.xseg + (size_t)l * n + k;
     for (int i = 0; i < A.m; ++i) {
-        const u64 w = smod(A.K[i], md);
         const ulonglong2 x = ld2(A.x[i] + xo);
-        r0 = add_mod(r0, mul_barrett(x.x, w, md), q);
-        r1 = add_mod(r1, mul_barrett(x.y, w, md), q);
+        mac128(r0, x.x, w[i]);
+        mac128(r1, x.y, w[i]);
     }
-    st2(out + off + k, make_ulonglong2(r0, r1));
+    st2(out + off + k, make_ulonglong2(reduce128(r0, md), reduce128(r1, md)));
 }
+// out[m][c] = sum_i ct_i[m][c] * pt_i  (accumulate: + out), lazy 128-bit.
+// Segment z = 2m + c; ct_i member m at m * cmember (0 = broadcast), its c1 at
+// + cpoly; plaintexts are shared by all members.
+struct PlainSumArgs {
+    const u64 *ct[LIN_MAX];
+    const u64 *pt[LIN_MAX];
+    int m, accumulate;
+    size_t cmember, cpoly;
+};
+__global__ __launch_bounds__(NT) void k_mul_plain_sum(u64 *out, PlainSumArgs A, size_t seg, const Mod *mods,
+                                                      int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y, z = blockIdx.z;
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const Mod md = mods[l];
+    const size_t ln = (size_t)l * n + k;
+    const size_t co = (size_t)(z >> 1) * A.cmember + (size_t)(z & 1) * A.cpoly + ln;
+    u64 *o = out + (size_t)z * seg + ln;
+    Acc128 r0, r1;
+    if (A.accumulate) {
+        const ulonglong2 v = ld2(o);
+        r0.lo = v.x;
+        r1.lo = v.y;
+    }
+    for (int i = 0; i < A.m; ++i) {
+        const ulonglong2 x = ld2(A.ct[i] + co), p = ld2(A.pt[i] + ln);
+        mac128(r0, x.x, p.x);
+        mac128(r1, x.y, p.y);
+    }
+    st2(o, make_ulonglong2(reduce128(r0, md), reduce128(r1, md)));
+}
+
 // grid: x = n / NT, y = limb, z = segment
 __global__ __launch_bounds__(NT) void k_permute(u64 *out, const u64 *in, const uint32_t *perm, Seg S, int logN) {
     const size_t n = (size_t)1 << logN;
@@ -228,16 +264,12 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef,
     }
     for (int t = t0; t < t0 + TCH && t < W; ++t) {
         if (t >= lo && t < hi) continue;
-        const u64 qt = mods[pmap_ext[t]].q;
-        u64 acc = 0;
+        const Mod mt = mods[pmap_ext[t]];
+        Acc128 acc;  // lazy: one reduction per output
 #pragma unroll
-        for (int i = 0; i < MAXSRC; ++i) {
-            if (i < a) {
-                const size_t ti = (size_t)i * W + t;
-                acc = add_mod(acc, mul_shoup(y[i], A.qhat[j][ti], A.qhat_s[j][ti], qt), qt);
-            }
-        }
-        ext[((size_t)j * W + t) * n + k] = acc;
+        for (int i = 0; i < MAXSRC; ++i)
+            if (i < a) mac128(acc, y[i], A.qhat[j][(size_t)i * W + t]);
+        ext[((size_t)j * W + t) * n + k] = reduce128(acc, mt);
     }
 }
 
@@ -295,15 +327,11 @@ __global__ __launch_bounds__(NT) void k_moddown_convert(u64 *conv, const u64 *pc
         if (i < K) v[i] = mul_shoup(src[(size_t)i * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
     const int i0 = blockIdx.y * TCH;
     for (int i = i0; i < i0 + TCH && i < ell; ++i) {
-        const u64 qi = mods[i].q;
-        u64 acc = 0;
+        Acc128 acc;
 #pragma unroll
         for (int kk = 0; kk < MAXSRC; ++kk)
-            if (kk < K) {
-                const size_t ix = (size_t)kk * nq + i;
-                acc = add_mod(acc, mul_shoup(v[kk], phat[ix], phat_s[ix], qi), qi);
-            }
-        dst[(size_t)i * n + k] = acc;
+            if (kk < K) mac128(acc, v[kk], phat[(size_t)kk * nq + i]);
+        dst[(size_t)i * n + k] = reduce128(acc, mods[i]);
     }
 }
 
@@ -355,30 +383,26 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const
 #pragma unroll
     for (int i = 0; i < MAXSRC; ++i)
         if (i < K) v[i] = mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
-    const u64 ql = mods[last].q;
-    u64 cl = 0;
+    const Mod ml = mods[last];
+    const u64 ql = ml.q;
+    Acc128 cacc;
 #pragma unroll
     for (int kk = 0; kk < MAXSRC; ++kk)
-        if (kk < K) {
-            const size_t ix = (size_t)kk * nq + last;
-            cl = add_mod(cl, mul_shoup(v[kk], phat[ix], phat_s[ix], ql), ql);
-        }
+        if (kk < K) mac128(cacc, v[kk], phat[(size_t)kk * nq + last]);
+    const u64 cl = reduce128(cacc, ml);
     const u64 y = mul_shoup(sub_mod(src[k], cl, ql), pinv[last], pinv_s[last], ql);
     const bool neg = y > (ql >> 1);
     const int i0 = blockIdx.y * TCH;
     for (int i = i0; i < i0 + TCH && i < last; ++i) {
         const Mod mi = mods[i];
-        u64 a = 0;
-#pragma unroll
-        for (int kk = 0; kk < MAXSRC; ++kk)
-            if (kk < K) {
-                const size_t ix = (size_t)kk * nq + i;
-                a = add_mod(a, mul_shoup(v[kk], phat[ix], phat_s[ix], mi.q), mi.q);
-            }
         u64 lift = reduce64(y, mi);
         if (neg) lift = sub_mod(lift, reduce64(ql, mi), mi.q);
-        a = add_mod(a, mul_shoup(lift, pmod[i], pmod_s[i], mi.q), mi.q);
-        dst[(size_t)i * n + k] = a;
+        Acc128 acc;
+        mac128(acc, lift, pmod[i]);
+#pragma unroll
+        for (int kk = 0; kk < MAXSRC; ++kk)
+            if (kk < K) mac128(acc, v[kk], phat[(size_t)kk * nq + i]);
+        dst[(size_t)i * n + k] = reduce128(acc, mi);
     }
 }
 // out_i = (acc_i + d_i P - corr_i) * (P q_last)^-1, i < ell-1, NTT form.
@@ -501,6 +525,24 @@ void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int 
         }
         hipLaunchKernelGGL(k_linear_sum, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, A, seg, mods, logN);
         if (m == 0) break;
+    }
+}
+void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, int m, int limbs, int members,
+                      size_t cmember, size_t cpoly, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0 || members <= 0 || m <= 0) return;
+    const size_t seg = (size_t)limbs << logN;
+    for (int base = 0; base < m; base += LIN_MAX) {
+        PlainSumArgs A{};
+        A.m = std::min(LIN_MAX, m - base);
+        A.accumulate = base > 0;
+        A.cmember = cmember;
+        A.cpoly = cpoly;
+        for (int i = 0; i < A.m; ++i) {
+            A.ct[i] = cts[base + i];
+            A.pt[i] = pts[base + i];
+        }
+        hipLaunchKernelGGL(k_mul_plain_sum, ew_grid(logN, limbs, 2 * members), dim3(NT), 0, st, out, A, seg, mods,
+                           logN);
     }
 }
 void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,

@@ -78,6 +78,10 @@ void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *
 // out = sum_i (K_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride)
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
                    size_t xseg, const Mod *mods, int logN, hipStream_t st);
+// out [members][2][limbs][n] = sum_i ct_i * pt_i  (ct_i member stride cmember, 0 = broadcast;
+// c1 at + cpoly; pt_i [limbs][n] shared), lazy 128-bit accumulation
+void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, int m, int limbs, int members,
+                      size_t cmember, size_t cpoly, const Mod *mods, int logN, hipStream_t st);
 // out[l][k] = in[l][perm[k]]
 void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,
                 hipStream_t st);

@@ -21,6 +21,7 @@ struct Mod {
     u64 mu;     // floor(2^(2k) / q)
     int k;      // bit length of q
     int pad;
+    u64 r64, r64s;  // 2^64 mod q and its Shoup companion (128-bit reductions)
 };
 
 __device__ __forceinline__ u64 mulhi(u64 a, u64 b) { return __umul64hi(a, b); }
@@ -62,6 +63,28 @@ __device__ __forceinline__ u64 reduce64(u64 a, const Mod &m) {
     if (r >= m.q) r -= m.q;
     if (r >= m.q) r -= m.q;
     return r;
+}
+
+// Lazy 128-bit accumulation for sums of products (basis conversions, linear
+// sums, plaintext inner products): each term is a full 64x64 -> 128 product
+// built from four 32x32 -> 64 multiplies (v_mad_u64_u32), and the sum is
+// reduced once.  Residues are < 2^61, so a product is < 2^122 and up to 32
+// terms fit in 128 bits.
+struct Acc128 {
+    u64 lo = 0, hi = 0;
+};
+__device__ __forceinline__ void mac128(Acc128 &acc, u64 a, u64 b) {
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const u64 p00 = (u64)a0 * b0, p01 = (u64)a0 * b1, p10 = (u64)a1 * b0, p11 = (u64)a1 * b1;
+    const u64 mid = (p00 >> 32) + (uint32_t)p01 + (uint32_t)p10;
+    const u64 lo = (mid << 32) | (uint32_t)p00;
+    const u64 hi = p11 + (p01 >> 32) + (p10 >> 32) + (mid >> 32);
+    acc.lo += lo;
+    acc.hi += hi + (acc.lo < lo);
+}
+// (hi 2^64 + lo) mod q
+__device__ __forceinline__ u64 reduce128(const Acc128 &a, const Mod &m) {
+    return add_mod(reduce64(a.lo, m), mul_shoup(a.hi, m.r64, m.r64s, m.q), m.q);
 }
 
 }  // namespace dev

@@ -253,7 +253,8 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     std::vector<Mod> mods(nall);
     for (size_t i = 0; i < nall; ++i) {
         host::Modulus m(I.P.primes[i]);
-        mods[i] = Mod{m.q, m.mu, m.k, 0};
+        const u64 r64 = (u64)(((unsigned __int128)1 << 64) % m.q);
+        mods[i] = Mod{m.q, m.mu, m.k, 0, r64, host::shoup(r64, m.q)};
     }
     I.mods = I.upload_static(mods);
     std::vector<u64> fwd(2 * nall * n), inv(2 * nall * n), ninv(nall), ninv_s(nall);
@@ -754,6 +755,34 @@ CtPtr Engine::mul_plain(const Ciphertext &a, const Plaintext &p) {
     dev::ew_mul_plain(t, a.data, p.data, (int)ell, segs, seg3(ell * nn, ell * nn, 0), MODS, LOGN, ST);
     auto r = new_ct(a.level + 1, a.slots, I.P.delta[a.level + 1], ell - 1, a.batch);
     I.rescale(t, ell, ell * nn, segs, r->data);
+    return r;
+}
+
+// sum_i a_i * p_i with one rescale (the oracle's spec; OpenFHE's FLEXIBLEAUTO
+// also rescales a masked sum once).  All a_i share level and batch.
+CtPtr Engine::mul_plain_sum(const std::vector<const Ciphertext *> &a, const std::vector<const Plaintext *> &p) {
+    auto &I = *impl;
+    if (a.empty() || a.size() != p.size()) throw std::invalid_argument("mul_plain_sum: bad operand lists");
+    const int level = a[0]->level, B = a[0]->batch;
+    for (size_t i = 0; i < a.size(); ++i) {
+        if (a[i]->level != level || p[i]->level != level)
+            throw std::invalid_argument("mul_plain_sum: level mismatch");
+        if (a[i]->batch != B) throw std::invalid_argument("mul_plain_sum: batch size mismatch");
+    }
+    if (level >= I.P.L) throw std::runtime_error("mul_plain_sum: no levels left");
+    ctr.ptmult += a.size() * B;
+    ctr.rescale += B;
+    const size_t nn = n(), ell = a[0]->limbs;
+    std::vector<const u64 *> cp, pp;
+    for (size_t i = 0; i < a.size(); ++i) {
+        cp.push_back(a[i]->data);
+        pp.push_back(p[i]->data);
+    }
+    auto tm = I.alloc((size_t)2 * B * ell * nn * 8);
+    u64 *t = static_cast<u64 *>(tm->p);
+    dev::ew_mul_plain_sum(t, cp.data(), pp.data(), (int)a.size(), (int)ell, B, 2 * ell * nn, ell * nn, MODS, LOGN, ST);
+    auto r = new_ct(level + 1, a[0]->slots, I.P.delta[level + 1], ell - 1, B);
+    I.rescale(t, ell, ell * nn, 2 * B, r->data);
     return r;
 }
 

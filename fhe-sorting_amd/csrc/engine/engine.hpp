@@ -103,6 +103,8 @@ class Engine {
     CtPtr level_adjust(const Ciphertext &a, int target);
     void match_levels(CtPtr &a, CtPtr &b);
     CtPtr mul_plain(const Ciphertext &a, const Plaintext &p);
+    // sum_i a_i * p_i with one rescale (masked sums of src/sort_algo.h:341-346, 573-577)
+    CtPtr mul_plain_sum(const std::vector<const Ciphertext *> &a, const std::vector<const Plaintext *> &p);
     CtPtr mul(const Ciphertext &a, const Ciphertext &b);
     CtPtr square(const Ciphertext &a);
     CtPtr rotate(const Ciphertext &a, long k);

@@ -103,6 +103,8 @@ _SIGS = {
     'fhe_kernel_clock_start': (C.c_int, [vp]),
     'fhe_set_sort_stack': (C.c_int, [vp, C.c_int]),
     'fhe_ct_stack': (C.c_int, [vp, C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_void_p)]),
+    'fhe_mul_plain_sum': (C.c_int, [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int,
+                                    C.POINTER(C.c_void_p)]),
     'fhe_ct_member': (C.c_int, [vp, vp, C.c_int, C.POINTER(C.c_void_p)]),
     'fhe_ct_sum_members': (C.c_int, [vp, vp, C.POINTER(C.c_void_p)]),
     'fhe_kernel_clock_stop': (C.c_int, [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
@@ -316,6 +318,13 @@ class Context:
         arr = (C.c_void_p * len(xs))(*[x.h for x in xs])
         out = C.c_void_p()
         _chk(lib().fhe_ct_stack(self.h, arr, len(xs), C.byref(out)))
+        return Ct(self, out.value)
+
+    def mul_plain_sum(self, cts, pts):
+        ca = (C.c_void_p * len(cts))(*[c.h for c in cts])
+        pa = (C.c_void_p * len(pts))(*[p.h for p in pts])
+        out = C.c_void_p()
+        _chk(lib().fhe_mul_plain_sum(self.h, ca, pa, len(cts), C.byref(out)))
         return Ct(self, out.value)
 
     def member(self, a, m): return self._new(lib().fhe_ct_member, a.h, m)

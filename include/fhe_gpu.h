@@ -87,6 +87,10 @@ int fhe_ct_info(const fhe_ct *ct, int *level, int *slots, double *scale, int *li
 /* Ciphertext::SetSlots (src/sort_algo.h:429,447,501) */
 int fhe_ct_set_slots(fhe_ct *ct, int slots);
 int fhe_ct_free(fhe_ct *ct);
+/* sum_i ct_i * pt_i with ONE rescale: the masked sums of vecRotsOpt /
+ * blindRotationOptN (src/sort_algo.h:341-346, 573-577; OpenFHE FLEXIBLEAUTO
+ * rescales the sum lazily).  All operands at one level; cts share a batch. */
+int fhe_mul_plain_sum(fhe_ctx *ctx, const fhe_ct *const *cts, const fhe_pt *const *pts, int m, fhe_ct **out);
 /* ciphertext batches: `m` ciphertexts at one level stacked into one handle of
  * batch sum(batch_i) ([batch][2][limbs][n]); every op applies member-wise in
  * the same kernel launches (the reference loops over batches instead:

@@ -198,6 +198,9 @@ class Context {
     CtPtr mul_const(const Ciphertext &a, double c);                  // -> level+1
     CtPtr mul_const_to(const Ciphertext &a, double c, int target);   // -> target (> a.level)
     CtPtr mul_plain(const Ciphertext &a, const Plaintext &p);        // -> level+1
+    // sum_i a_i * p_i with ONE rescale (OpenFHE FLEXIBLEAUTO rescales lazily, so a
+    // masked sum of products is rescaled once: src/sort_algo.h:341-346, 573-577)
+    CtPtr mul_plain_sum(const std::vector<const Ciphertext *> &a, const std::vector<const Plaintext *> &p);
     CtPtr mul(const Ciphertext &a, const Ciphertext &b);             // relin + rescale
     CtPtr square(const Ciphertext &a);
     CtPtr rotate(const Ciphertext &a, long k);                       // keyed rotation

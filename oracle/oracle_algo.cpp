@@ -460,13 +460,18 @@ void DirectSort::reduce_partial(CtPtr &acc, int level_hint, int slots) {
 CtPtr DirectSort::vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is) {
     std::vector<CtPtr> outer(num_partition / np);
     for (int j = 0; j < num_partition / np; ++j) {
-        CtPtr T;
+        std::vector<Plaintext> pms;
+        pms.reserve(np);
+        std::vector<const Ciphertext *> cs;
+        std::vector<const Plaintext *> ps;
         for (int i = 0; i < np; ++i) {
             auto msk = mask_vector(num_slots, N, np * j + i);
             msk = vector_rotate(msk, -is * num_partition - j * np);
-            auto pm = cc.encode(msk, num_slots, baby[i]->level);
-            cc.add_inplace(T, *cc.mul_plain(*baby[i], pm));
+            pms.push_back(cc.encode(msk, num_slots, baby[i]->level));
+            cs.push_back(baby[i].get());
+            ps.push_back(&pms.back());
         }
+        CtPtr T = cc.mul_plain_sum(cs, ps);  // src/sort_algo.h:341-346
         outer[j] = rot.rotate(*T, is * num_partition + j * np);
     }
     CtPtr result;
@@ -500,13 +505,18 @@ CtPtr DirectSort::constructRank(const Ciphertext &x, SignFunc f, const SignConfi
 CtPtr DirectSort::blindRotationOptN(const std::vector<CtPtr> &mi, int num_slots, int np, int ib, int num_partition) {
     CtPtr result;
     for (int i = 0; i < (num_slots / N) / np; ++i) {
-        CtPtr tmp;
+        std::vector<Plaintext> pms;
+        pms.reserve(np);
+        std::vector<const Ciphertext *> cs;
+        std::vector<const Plaintext *> ps;
         for (int j = 0; j < np; ++j) {
             auto msk = mask_vector(num_slots, N, np * i + j);
             msk = vector_rotate(msk, j);
-            auto pm = cc.encode(msk, num_slots, mi[j]->level);
-            cc.add_inplace(tmp, *cc.mul_plain(*mi[j], pm));
+            pms.push_back(cc.encode(msk, num_slots, mi[j]->level));
+            cs.push_back(mi[j].get());
+            ps.push_back(&pms.back());
         }
+        CtPtr tmp = cc.mul_plain_sum(cs, ps);  // src/sort_algo.h:573-577
         tmp = rot.rotate(*tmp, ib * num_partition + i * np);
         cc.add_inplace(result, *tmp);
     }

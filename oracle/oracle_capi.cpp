@@ -177,6 +177,17 @@ void *orc_rotate(void *c, void *a, int k) { return guard([&]() -> void * { retur
 void *orc_mul_plain(void *c, void *a, void *p) {
     return guard([&]() -> void * { return wrap(CTX->mul_plain(CT(a), static_cast<PtH *>(p)->p)); }, (void *)nullptr);
 }
+void *orc_mul_plain_sum(void *c, void *const *as, void *const *ps, int m) {
+    return guard([&]() -> void * {
+        std::vector<const Ciphertext *> a;
+        std::vector<const Plaintext *> p;
+        for (int i = 0; i < m; ++i) {
+            a.push_back(&CT(as[i]));
+            p.push_back(&static_cast<PtH *>(ps[i])->p);
+        }
+        return wrap(CTX->mul_plain_sum(a, p));
+    }, (void *)nullptr);
+}
 void *orc_add_plain(void *c, void *a, void *p) {
     return guard([&]() -> void * { return wrap(CTX->add_plain(CT(a), static_cast<PtH *>(p)->p)); }, (void *)nullptr);
 }

@@ -769,6 +769,33 @@ CtPtr Context::mul_plain(const Ciphertext &a, const Plaintext &p) {
     return out;
 }
 
+CtPtr Context::mul_plain_sum(const std::vector<const Ciphertext *> &a, const std::vector<const Plaintext *> &p) {
+    if (a.empty() || a.size() != p.size()) throw std::invalid_argument("mul_plain_sum: bad operand lists");
+    const int level = a[0]->level;
+    for (size_t i = 0; i < a.size(); ++i)
+        if (a[i]->level != level || p[i]->level != level)
+            throw std::invalid_argument("mul_plain_sum: level mismatch");
+    ctr.ptmult += a.size();
+    auto r = make_ct(level, a[0]->slots, a[0]->scale, a[0]->limbs, P.n);
+    const size_t n = P.n;
+#pragma omp parallel for
+    for (size_t l = 0; l < a[0]->limbs; ++l) {
+        const Modulus &m = tab[l].mod;
+        for (int c = 0; c < 2; ++c) {
+            u64 *o = r->poly(c, n) + l * n;
+            for (size_t k = 0; k < n; ++k) {
+                u64 acc = 0;
+                for (size_t i = 0; i < a.size(); ++i)
+                    acc = mod_add(acc, mod_mul(a[i]->poly(c, n)[l * n + k], p[i]->m[l * n + k], m), m.q);
+                o[k] = acc;
+            }
+        }
+    }
+    auto out = rescale(*r);
+    out->scale = P.delta[level + 1];
+    return out;
+}
+
 // --------------------------------------------------------- key switching ---
 // ModUp (HYBRID): for each digit j of the level-ell basis, extend the digit's
 // residues to every other prime of Q_ell u P by fast basis conversion.

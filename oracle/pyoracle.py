@@ -63,6 +63,7 @@ def lib():
             'orc_rescale': (vp, [vp, vp]),
             'orc_rotate': (vp, [vp, vp, C.c_int]),
             'orc_mul_plain': (vp, [vp, vp, vp]),
+            'orc_mul_plain_sum': (vp, [vp, C.POINTER(vp), C.POINTER(vp), C.c_int]),
             'orc_add_plain': (vp, [vp, vp, vp]),
             'orc_rotate_hoisted': (C.c_int, [vp, vp, ip, C.c_int, C.POINTER(vp)]),
             'orc_linear_sum_to': (vp, [vp, C.POINTER(vp), dp, C.c_int, C.c_int]),
@@ -266,6 +267,11 @@ class Context:
     def rescale(self, a): return Ct(self, lib().orc_rescale(self.h, a.h))
     def rotate(self, a, k): return Ct(self, lib().orc_rotate(self.h, a.h, k))
     def mul_plain(self, a, p): return Ct(self, lib().orc_mul_plain(self.h, a.h, p.h))
+
+    def mul_plain_sum(self, cts, pts):
+        ca = (C.c_void_p * len(cts))(*[c.h for c in cts])
+        pa = (C.c_void_p * len(pts))(*[p.h for p in pts])
+        return Ct(self, lib().orc_mul_plain_sum(self.h, ca, pa, len(cts)))
     def add_plain(self, a, p): return Ct(self, lib().orc_add_plain(self.h, a.h, p.h))
 
     def rotate_hoisted(self, a, ks):

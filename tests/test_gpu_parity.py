@@ -253,6 +253,9 @@ def test_batched_ops_match_members(pair):
         ('mul_plain', lambda g: gpu.mul_plain(g, gpu.encode(pt_vals, 16, 0)),
          lambda o: orc.mul_plain(o, orc.encode(pt_vals, 16, 0))),
         ('cheb27', lambda g: gpu.cheb(g, np.linspace(1, 0.1, 28)), lambda o: orc.cheb(o, np.linspace(1, 0.1, 28))),
+        ('mul_plain_sum',
+         lambda g: gpu.mul_plain_sum([g, gpu.rotate(g, 1)], [gpu.encode(pt_vals, 16, 0), gpu.encode(-pt_vals, 16, 0)]),
+         lambda o: orc.mul_plain_sum([o, orc.rotate(o, 1)], [orc.encode(pt_vals, 16, 0), orc.encode(-pt_vals, 16, 0)])),
         ('sign', lambda g: gpu.sign(g, 3, 1, 1), lambda o: orc.sign(o, 3, 1, 1)),
     ]
     for name, gop, oop in cases:
