@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <fstream>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <tuple>
@@ -66,39 +67,107 @@ struct PSEval {
         T[G] = cc.add_const(*t, -1.0);
         return *T[G];
     }
-    CtPtr leaf(const std::vector<double> &a, int target) {
-        std::vector<const Ciphertext *> xs;
-        std::vector<double> cs;
-        for (size_t i = 1; i < a.size(); ++i)
-            if (a[i] != 0.0) {
-                xs.push_back(T.at((int)i).get());
-                cs.push_back(a[i]);
-            }
-        CtPtr r = xs.empty() ? cc.trivial_const(0.0, target, T[1]->slots, T[1]->batch)
-                             : cc.linear_sum_to(xs, cs, target);
-        if (a[0] != 0.0) r = cc.add_const(*r, a[0]);
-        return r;
-    }
-    CtPtr eval(std::vector<double> a, int target) {
-        trim_zeros(a);
-        const int d = (int)a.size() - 1;
-        if (d <= B) return leaf(a, target);
+    // ---- leaves.  The recursion below consumes leaves in a fixed order; they
+    // are collected first, and leaves sharing a target level are evaluated
+    // up to 8 at a time by one multi-output linear sum over the baby steps
+    // (each baby step is streamed once per 8 leaves).  Every leaf equals
+    // linear_sum_to(its nonzero terms) + a_0, word for word.
+    struct Leaf {
+        std::vector<double> a;
+        int target;
+    };
+    std::vector<Leaf> leaves;
+    std::map<size_t, CtPtr> ready;
+    size_t next_leaf = 0;
+
+    void split(const std::vector<double> &a, int d, std::vector<double> &q, std::vector<double> &r, int &G) const {
         int Dpp = beta + 1;
         while ((1L << Dpp) - B < d) ++Dpp;
-        int G = 1 << (Dpp - 1);
+        G = 1 << (Dpp - 1);
         while (G > d) G >>= 1;
-        std::vector<double> q(d - G + 1), r(a.begin(), a.begin() + G);
+        q.assign(d - G + 1, 0.0);
+        r.assign(a.begin(), a.begin() + G);
         q[0] = a[G];
         for (int j = 1; j <= d - G; ++j) {
             q[j] = 2.0 * a[G + j];
             r[G - j] -= a[G + j];
         }
+    }
+    void collect(std::vector<double> a, int target) {
+        trim_zeros(a);
+        const int d = (int)a.size() - 1;
+        if (d <= B) {
+            leaves.push_back({a, target});
+            return;
+        }
+        std::vector<double> q, r;
+        int G;
+        split(a, d, q, r, G);
+        collect(q, target - 1);
+        trim_zeros(r);
+        if (r.size() == 1 && r[0] == 0.0) return;
+        collect(r, target);
+    }
+    static bool has_terms(const std::vector<double> &a) {
+        for (size_t i = 1; i < a.size(); ++i)
+            if (a[i] != 0.0) return true;
+        return false;
+    }
+    void evaluate_chunk(size_t first) {
+        const int target = leaves[first].target;
+        std::vector<size_t> chunk;
+        for (size_t i = first; i < leaves.size() && chunk.size() < 8; ++i)
+            if (leaves[i].target == target && !ready.count(i) && has_terms(leaves[i].a)) chunk.push_back(i);
+        std::vector<int> idx;  // union of the baby steps the chunk uses
+        for (size_t c : chunk)
+            for (size_t i = 1; i < leaves[c].a.size(); ++i)
+                if (leaves[c].a[i] != 0.0) idx.push_back((int)i);
+        std::sort(idx.begin(), idx.end());
+        idx.erase(std::unique(idx.begin(), idx.end()), idx.end());
+        std::vector<const Ciphertext *> xs;
+        for (int i : idx) xs.push_back(T.at(i).get());
+        std::vector<std::vector<double>> rows;
+        for (size_t c : chunk) {
+            std::vector<double> row;
+            for (int i : idx) row.push_back((size_t)i < leaves[c].a.size() ? leaves[c].a[i] : 0.0);
+            rows.push_back(row);
+        }
+        auto outs = cc.linear_sums_to(xs, rows, target);
+        for (size_t g = 0; g < chunk.size(); ++g) {
+            CtPtr r = outs[g];
+            if (leaves[chunk[g]].a[0] != 0.0) r = cc.add_const(*r, leaves[chunk[g]].a[0]);
+            ready[chunk[g]] = r;
+        }
+    }
+    CtPtr leaf() {
+        const size_t i = next_leaf++;
+        const Leaf &L = leaves.at(i);
+        if (!has_terms(L.a)) {
+            CtPtr r = cc.trivial_const(0.0, L.target, T[1]->slots, T[1]->batch);
+            return L.a[0] != 0.0 ? cc.add_const(*r, L.a[0]) : r;
+        }
+        if (!ready.count(i)) evaluate_chunk(i);
+        CtPtr r = ready.at(i);
+        ready.erase(i);
+        return r;
+    }
+    CtPtr eval(std::vector<double> a, int target) {
+        trim_zeros(a);
+        const int d = (int)a.size() - 1;
+        if (d <= B) return leaf();
+        std::vector<double> q, r;
+        int G;
+        split(a, d, q, r, G);
         CtPtr qv = eval(q, target - 1);
         CtPtr prod = cc.mul(*qv, giant(G));
         trim_zeros(r);
         if (r.size() == 1 && r[0] == 0.0) return prod;
         CtPtr rv = eval(r, target);
         return cc.add(*prod, *rv);
+    }
+    CtPtr run(const std::vector<double> &a, int target) {
+        collect(a, target);
+        return eval(a, target);
     }
 };
 
@@ -120,7 +189,7 @@ CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<
     if (d == 0) return cc.add_const(*cc.trivial_const(0.0, x->level, x->slots, x->batch), s[0]);
     PSEval ev(cc, *x, d);
     ev.build_baby();
-    return ev.eval(s, x->level + ev.D);
+    return ev.run(s, x->level + ev.D);
 }
 
 // ====================================================== composite sign =====

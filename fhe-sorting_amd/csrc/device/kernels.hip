@@ -11,6 +11,8 @@
 //     companion.
 #include "kernels.hpp"
 
+#include <stdexcept>
+
 namespace fhe {
 namespace dev {
 
@@ -160,6 +162,52 @@ __global__ __launch_bounds__(NT) void k_linear_sum(u64 *out, LinArgs A, size_t s
     }
     st2(out + off + k, make_ulonglong2(reduce128(r0, md), reduce128(r1, md)));
 }
+// Several linear sums over one input set in one pass: out_g = sum_i (K[g][i]
+// mod q_l) x_i for g < G.  Each input coefficient is read once for all G
+// outputs (the Paterson-Stockmeyer leaves all combine the same baby steps).
+// Inputs may have different limb counts (segment stride xseg[i]); constants
+// are reduced once per block into LDS; lazy 128-bit accumulation.
+constexpr int MLS_G = 8, MLS_M = 32;
+struct MultiLinArgs {
+    u64 *out[MLS_G];
+    const u64 *x[MLS_M];
+    size_t xseg[MLS_M];
+    int64_t K[MLS_G * MLS_M];  // [g][i]
+    int m, G, accumulate;
+};
+__global__ __launch_bounds__(NT) void k_linear_sum_multi(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
+    __shared__ u64 w[MLS_G * MLS_M];
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const Mod md = mods[l];
+    for (int t = threadIdx.x; t < A.G * MLS_M; t += NT) w[t] = (t % MLS_M) < A.m ? smod(A.K[t], md) : 0;
+    __syncthreads();
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const size_t ln = (size_t)l * n + k, oo = (size_t)blockIdx.z * seg + ln;
+    Acc128 r[MLS_G][2];
+#pragma unroll
+    for (int g = 0; g < MLS_G; ++g)
+        if (g < A.G && A.accumulate) {
+            const ulonglong2 o = ld2(A.out[g] + oo);
+            r[g][0].lo = o.x;
+            r[g][1].lo = o.y;
+        }
+    for (int i = 0; i < A.m; ++i) {
+        const ulonglong2 x = ld2(A.x[i] + (size_t)blockIdx.z * A.xseg[i] + ln);
+#pragma unroll
+        for (int g = 0; g < MLS_G; ++g)
+            if (g < A.G) {
+                const u64 c = w[g * MLS_M + i];
+                mac128(r[g][0], x.x, c);
+                mac128(r[g][1], x.y, c);
+            }
+    }
+#pragma unroll
+    for (int g = 0; g < MLS_G; ++g)
+        if (g < A.G) st2(A.out[g] + oo, make_ulonglong2(reduce128(r[g][0], md), reduce128(r[g][1], md)));
+}
+
 // out[m][c] = sum_i ct_i[m][c] * pt_i  (accumulate: + out), lazy 128-bit.
 // Segment z = 2m + c; ct_i member m at m * cmember (0 = broadcast), its c1 at
 // + cpoly; plaintexts are shared by all members.
@@ -473,7 +521,8 @@ inline dim3 pt_grid(int logN, int y, int z) {
 void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, const Mod *mods, int logN,
             hipStream_t st) {
     if (limbs <= 0 || segs <= 0) return;
-    hipLaunchKernelGGL(k_add, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, b, S, mods, logN);
+    const double B = 8.0 * 3 * limbs * segs * ((size_t)1 << logN);
+    launch_clocked("k_add", B, k_add, ew_grid(logN, limbs, segs), dim3(NT), st, out, a, b, S, mods, logN);
 }
 void ew_sub(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, const Mod *mods, int logN,
             hipStream_t st) {
@@ -487,7 +536,8 @@ void ew_neg(u64 *out, const u64 *a, int limbs, int segs, Seg S, const Mod *mods,
 void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
                    hipStream_t st) {
     if (limbs <= 0 || segs <= 0) return;
-    hipLaunchKernelGGL(k_mul_scalar, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, K, S, mods, logN);
+    const double B = 8.0 * 2 * limbs * segs * ((size_t)1 << logN);
+    launch_clocked("k_mul_scalar", B, k_mul_scalar, ew_grid(logN, limbs, segs), dim3(NT), st, out, a, K, S, mods, logN);
 }
 void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
                    hipStream_t st) {
@@ -503,8 +553,9 @@ void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int mem
                const Mod *mods, int logN, hipStream_t st) {
     if (limbs <= 0 || members <= 0) return;
     const size_t ln_all = (size_t)limbs << logN;
-    hipLaunchKernelGGL(k_tensor, ew_grid(logN, limbs, members), dim3(NT), 0, st, d01, d2, a, b, ln_all, sa, sb, mods,
-                       logN);
+    const double B = 8.0 * (5.0 * members + 2.0 * (sb ? members : 1)) * ln_all;
+    launch_clocked("k_tensor", B, k_tensor, ew_grid(logN, limbs, members), dim3(NT), st, d01, d2, a, b, ln_all, sa, sb,
+                   mods, logN);
 }
 void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st) {
     if (limbs <= 0 || members <= 0) return;
@@ -523,8 +574,30 @@ void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int 
             A.x[i] = xs[base + i];
             A.K[i] = K[base + i];
         }
-        hipLaunchKernelGGL(k_linear_sum, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, A, seg, mods, logN);
+        const double B = 8.0 * (A.m + A.accumulate + 1) * limbs * segs * ((size_t)1 << logN);
+        launch_clocked("k_linear_sum", B, k_linear_sum, ew_grid(logN, limbs, segs), dim3(NT), st, out, A, seg, mods,
+                       logN);
         if (m == 0) break;
+    }
+}
+void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,
+                         int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0 || G <= 0 || m <= 0) return;
+    if (G > MLS_G) throw std::invalid_argument("ew_linear_sum_multi: at most 8 outputs per pass");
+    for (int base = 0; base < m; base += MLS_M) {
+        MultiLinArgs A{};
+        A.m = std::min(MLS_M, m - base);
+        A.G = G;
+        A.accumulate = base > 0;
+        for (int g = 0; g < G; ++g) A.out[g] = outs[g];
+        for (int i = 0; i < A.m; ++i) {
+            A.x[i] = xs[base + i];
+            A.xseg[i] = xseg[base + i];
+            for (int g = 0; g < G; ++g) A.K[g * MLS_M + i] = K[(size_t)g * m + base + i];
+        }
+        const double B = 8.0 * (A.m + (double)G * (1 + A.accumulate)) * limbs * segs * ((size_t)1 << logN);
+        launch_clocked("k_linear_sum_multi", B, k_linear_sum_multi, ew_grid(logN, limbs, segs), dim3(NT), st, A, seg,
+                       mods, logN);
     }
 }
 void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, int m, int limbs, int members,
@@ -541,8 +614,10 @@ void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, in
             A.ct[i] = cts[base + i];
             A.pt[i] = pts[base + i];
         }
-        hipLaunchKernelGGL(k_mul_plain_sum, ew_grid(logN, limbs, 2 * members), dim3(NT), 0, st, out, A, seg, mods,
-                           logN);
+        const double B = 8.0 * ((double)A.m * (cmember ? 2 * members : 2) + A.m + 2.0 * members * (1 + A.accumulate)) *
+                         limbs * ((size_t)1 << logN);
+        launch_clocked("k_mul_plain_sum", B, k_mul_plain_sum, ew_grid(logN, limbs, 2 * members), dim3(NT), st, out, A,
+                       seg, mods, logN);
     }
 }
 void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,
@@ -578,57 +653,66 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
     A.digits = digits;
     A.coef_stride = coef_stride;
     A.ext_stride = ext_stride;
-    hipLaunchKernelGGL(k_modup_convert, pt_grid(logN, (W + TCH - 1) / TCH, digits * members), dim3(NT), 0, st, ext,
-                       coef, W, A, pmap_ext, mods, logN);
+    const double B = 8.0 * members * (double)((size_t)digits * W) * ((size_t)1 << logN);  // ell in + (dW - ell) out
+    launch_clocked("k_modup_convert", B, k_modup_convert, pt_grid(logN, (W + TCH - 1) / TCH, digits * members), dim3(NT),
+                   st, ext, coef, W, A, pmap_ext, mods, logN);
 }
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
               hipStream_t st, int members, KsStrides str, KsFold fold) {
     (void)nq;
     const int W = ell + K;
-    hipLaunchKernelGGL(k_ks_inner, pt_grid(logN, W, members), dim3(NT), 0, st, acc, ext, dntt, key, ell, W, nall,
-                       alpha, digits, perm, pmap_ext, mods, logN, str, fold);
+    // ext (+ own digit) and 2 accumulators per member; the key once
+    const double B = 8.0 * ((double)members * (digits * W + 2.0 * W) + 2.0 * digits * W) * ((size_t)1 << logN);
+    launch_clocked("k_ks_inner", B, k_ks_inner, pt_grid(logN, W, members), dim3(NT), st, acc, ext, dntt, key, ell, W,
+                   nall, alpha, digits, perm, pmap_ext, mods, logN, str, fold);
 }
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
                              const u64 *pinv, const u64 *pinv_s, const u64 *pmod, const u64 *pmod_s,
                              const Mod *mods, int logN, hipStream_t st) {
     if (ell <= 1) return;
-    hipLaunchKernelGGL(k_moddown_rescale_convert, pt_grid(logN, (ell - 1 + TCH - 1) / TCH, segs), dim3(NT), 0, st,
-                       corr, acc, ell, K, nq, seg_acc, seg_corr, phinv, phinv_s, phat, phat_s, pinv, pinv_s, pmod,
-                       pmod_s, mods, logN);
+    const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
+    launch_clocked("k_moddown_rescale_convert", B, k_moddown_rescale_convert,
+                   pt_grid(logN, (ell - 1 + TCH - 1) / TCH, segs), dim3(NT), st, corr, acc, ell, K, nq, seg_acc, seg_corr,
+                   phinv, phinv_s, phat, phat_s, pinv, pinv_s, pmod, pmod_s, mods, logN);
 }
 void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, int ell, int segs, size_t seg_out,
                      size_t seg_acc, size_t seg_d, const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
                      const u64 *pmod_s, const Mod *mods, int logN, hipStream_t st) {
     if (ell <= 1) return;
-    hipLaunchKernelGGL(k_mul_tail_finish, ew_grid(logN, ell - 1, segs), dim3(NT), 0, st, out, acc, d, corr, seg_out,
-                       seg_acc, seg_d, pqlinv, pqlinv_s, pmod, pmod_s, mods, logN);
+    const double B = 8.0 * 4 * segs * (double)(ell - 1) * ((size_t)1 << logN);
+    launch_clocked("k_mul_tail_finish", B, k_mul_tail_finish, ew_grid(logN, ell - 1, segs), dim3(NT), st, out, acc, d,
+                   corr, seg_out, seg_acc, seg_d, pqlinv, pqlinv_s, pmod, pmod_s, mods, logN);
 }
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
                      const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s, const Mod *mods,
                      int logN, hipStream_t st) {
-    hipLaunchKernelGGL(k_moddown_convert, pt_grid(logN, (ell + TCH - 1) / TCH, segs), dim3(NT), 0, st, conv, pc, ell,
-                       K, nq, seg_in, seg_out, phinv, phinv_s, phat, phat_s, mods, logN);
+    const double B = 8.0 * segs * (double)(K + ell) * ((size_t)1 << logN);
+    launch_clocked("k_moddown_convert", B, k_moddown_convert, pt_grid(logN, (ell + TCH - 1) / TCH, segs), dim3(NT), st,
+                   conv, pc, ell, K, nq, seg_in, seg_out, phinv, phinv_s, phat, phat_s, mods, logN);
 }
 void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,
                     size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s, const Mod *mods, int logN,
                     hipStream_t st) {
-    hipLaunchKernelGGL(k_moddown_finish, ew_grid(logN, ell, segs), dim3(NT), 0, st, out, acc, conv, add, seg_out,
-                       seg_acc, seg_add, pinv, pinv_s, mods, logN);
+    const double B = 8.0 * (3.0 * segs + (add ? segs / 2 : 0)) * ell * ((size_t)1 << logN);
+    launch_clocked("k_moddown_finish", B, k_moddown_finish, ew_grid(logN, ell, segs), dim3(NT), st, out, acc, conv, add,
+                   seg_out, seg_acc, seg_add, pinv, pinv_s, mods, logN);
 }
 void rescale_prep(u64 *tmp, const u64 *last, int ell, int segs, size_t seg_last, size_t seg_tmp, const Mod *mods,
                   int logN, hipStream_t st) {
     if (ell <= 1) return;
-    hipLaunchKernelGGL(k_rescale_prep, pt_grid(logN, ell - 1, segs), dim3(NT), 0, st, tmp, last, ell, seg_last,
-                       seg_tmp, mods, logN);
+    const double B = 8.0 * segs * (double)ell * ((size_t)1 << logN);
+    launch_clocked("k_rescale_prep", B, k_rescale_prep, pt_grid(logN, ell - 1, segs), dim3(NT), st, tmp, last, ell,
+                   seg_last, seg_tmp, mods, logN);
 }
 void rescale_finish(u64 *out, const u64 *in, const u64 *tmp, int ell, int segs, size_t seg_out, size_t seg_in,
                     size_t seg_tmp, const u64 *qlinv, const u64 *qlinv_s, const Mod *mods, int logN,
                     hipStream_t st) {
     if (ell <= 1) return;
-    hipLaunchKernelGGL(k_rescale_finish, ew_grid(logN, ell - 1, segs), dim3(NT), 0, st, out, in, tmp, seg_out, seg_in,
-                       seg_tmp, qlinv, qlinv_s, mods, logN);
+    const double B = 8.0 * 3 * segs * (double)(ell - 1) * ((size_t)1 << logN);
+    launch_clocked("k_rescale_finish", B, k_rescale_finish, ew_grid(logN, ell - 1, segs), dim3(NT), st, out, in, tmp,
+                   seg_out, seg_in, seg_tmp, qlinv, qlinv_s, mods, logN);
 }
 
 }  // namespace dev

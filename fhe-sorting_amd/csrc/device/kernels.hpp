@@ -8,6 +8,7 @@
 //     the limbs are not Q primes 0..ell-1 (extended Q u P basis).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstddef>
 #include <cstdint>
 
@@ -34,6 +35,19 @@ struct LaunchClock {
     virtual void record(const char *kernel, double bytes) = 0;
 };
 LaunchClock *&launch_clock();
+
+// Launch through hipExtLaunchKernelGGL; when a clock is installed the launch is
+// timed by events recorded at the kernel's own start/end and booked under
+// `name` with its algorithmic HBM bytes.
+template <typename Kern, typename... Args>
+inline void launch_clocked(const char *name, double bytes, Kern kernel, dim3 grid, dim3 block, hipStream_t st,
+                           Args... args) {
+    LaunchClock *clk = launch_clock();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (clk) clk->events(e0, e1);
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, st, e0, e1, 0, args...);
+    if (clk) clk->record(name, bytes);
+}
 
 // forward / inverse negacyclic NTT of `limbs` limbs x `segs` segments
 void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
@@ -78,6 +92,10 @@ void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *
 // out = sum_i (K_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride)
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
                    size_t xseg, const Mod *mods, int logN, hipStream_t st);
+// outs[g] = sum_i (K[g*m + i] mod q_l) * x_i for g < G <= 8 in one pass over the
+// inputs (x_i: [segs][limbs][n] with segment stride xseg[i]; outs: stride seg)
+void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,
+                         int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st);
 // out [members][2][limbs][n] = sum_i ct_i * pt_i  (ct_i member stride cmember, 0 = broadcast;
 // c1 at + cpoly; pt_i [limbs][n] shared), lazy 128-bit accumulation
 void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, int m, int limbs, int members,

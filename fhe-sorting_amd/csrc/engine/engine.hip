@@ -886,6 +886,51 @@ CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std
     return r;
 }
 
+// Several linear sums of the same inputs to one target level: row g of `c`
+// gives the coefficients of output g.  Equal, word for word, to one
+// linear_sum_to per row, but each input is streamed once per 8 outputs.
+std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> &xs,
+                                          const std::vector<std::vector<double>> &c, int target) {
+    auto &I = *impl;
+    if (target > I.P.L) throw std::runtime_error("linear_sums_to: no levels left");
+    if (xs.empty()) throw std::invalid_argument("linear_sums_to: no inputs");
+    const int B = xs[0]->batch, segs = 2 * B;
+    const size_t nn = n(), ell = I.P.limbs_at(target - 1), m = xs.size();
+    const u64 qd = I.P.primes[I.P.L - target + 1];
+    std::vector<const u64 *> xp(m);
+    std::vector<size_t> xseg(m);
+    for (size_t i = 0; i < m; ++i) {
+        if (xs[i]->level > target - 1) throw std::invalid_argument("linear_sums_to: input level too high");
+        if (xs[i]->batch != B) throw std::invalid_argument("linear_sums_to: batch size mismatch");
+        xp[i] = xs[i]->data;
+        xseg[i] = xs[i]->limbs * nn;
+    }
+    std::vector<CtPtr> outs;
+    for (size_t g0 = 0; g0 < c.size(); g0 += 8) {
+        const int G = (int)std::min<size_t>(8, c.size() - g0);
+        std::vector<int64_t> K((size_t)G * m);
+        for (int g = 0; g < G; ++g) {
+            if (c[g0 + g].size() != m) throw std::invalid_argument("linear_sums_to: coefficient row size");
+            for (size_t i = 0; i < m; ++i)
+                K[(size_t)g * m + i] = host::const_to_target(c[g0 + g][i], I.P.delta[target], qd, xs[i]->scale);
+        }
+        auto tm = I.alloc((size_t)G * segs * ell * nn * 8);
+        u64 *t = static_cast<u64 *>(tm->p);
+        std::vector<u64 *> op(G);
+        for (int g = 0; g < G; ++g) op[g] = t + (size_t)g * segs * ell * nn;
+        dev::ew_linear_sum_multi(op.data(), G, xp.data(), xseg.data(), K.data(), (int)m, (int)ell, segs, ell * nn,
+                                 MODS, LOGN, ST);
+        for (int g = 0; g < G; ++g) {
+            auto r = new_ct(target, xs[0]->slots, I.P.delta[target], ell - 1, B);
+            I.rescale(op[g], ell, ell * nn, segs, r->data);
+            outs.push_back(r);
+        }
+        ctr.constmult += (u64)G * m * B;
+        ctr.rescale += (u64)G * B;
+    }
+    return outs;
+}
+
 CtPtr Engine::trivial_const(double c, int level, int slots, int batch) {
     auto r = zero_like(level, slots, batch);
     const i64 K = host::const_at_scale(c, impl->P.delta[level]);

@@ -112,6 +112,9 @@ class Engine {
     CtPtr rescale(const Ciphertext &a);
     CtPtr drop_to(const Ciphertext &a, int level);
     CtPtr linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c, int target);
+    // several linear sums of the same inputs (PS leaves): one output per row of c
+    std::vector<CtPtr> linear_sums_to(const std::vector<const Ciphertext *> &xs,
+                                      const std::vector<std::vector<double>> &c, int target);
     CtPtr trivial_const(double c, int level, int slots, int batch = 1);
     CtPtr zero_like(int level, int slots, int batch = 1);
     // batches: stack (copies; equal levels), member view (no copy), member sum
