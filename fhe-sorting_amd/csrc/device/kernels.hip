@@ -20,7 +20,7 @@ namespace {
 
 constexpr int NT = 256;     // threads per block
 constexpr int MAXSRC = 16;  // max limbs per digit / special primes held in registers
-constexpr int TCH = 8;      // target limbs per thread in basis conversions
+constexpr int TCH = 16;     // target limbs per thread in basis conversions
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 

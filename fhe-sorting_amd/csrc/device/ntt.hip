@@ -42,20 +42,32 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
     return COLS ? idx * (NB + 1) + tr : tr * ((1 << PB) + (1 << PB) / 16) + idx + (idx >> 4);
 }
 
+// Lazy Shoup product a * w mod q in [0, 2q): a*w - floor(a*w'/2^64)*q taken
+// mod 2^64, written as a*w + h*nq with nq = 2^64 - q so both low products
+// share one multiply-accumulate chain (2 v_mad_u64_u32 + 4 v_mul_lo_u32) and
+// no borrow chain is needed.
+__device__ __forceinline__ u64 shoup_fold(u64 a, u64 w, u64 wp, u64 nq) {
+    const u64 h = mulhi(a, wp);
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+    const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32), n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
+    const u64 t = (u64)a0 * w0 + (u64)h0 * n0;
+    const uint32_t cross = a0 * w1 + a1 * w0 + h0 * n1 + h1 * n0;
+    return t + ((u64)cross << 32);
+}
 // Harvey lazy forward CT butterfly: x, y in [0, 4q) -> x, y in [0, 4q)
-__device__ __forceinline__ void ct_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2) {
+__device__ __forceinline__ void ct_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2, u64 nq) {
     u64 u = x;
-    u = u >= q2 ? u - q2 : u;                        // [0, 2q)
-    const u64 v = mul_shoup_lazy(y, w.x, w.y, q2 >> 1);  // [0, 2q)
+    u = u >= q2 ? u - q2 : u;                   // [0, 2q)
+    const u64 v = shoup_fold(y, w.x, w.y, nq);  // [0, 2q)
     x = u + v;
     y = u + q2 - v;
 }
 // lazy inverse GS butterfly: x, y in [0, 2q) -> x, y in [0, 2q)
-__device__ __forceinline__ void gs_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2) {
+__device__ __forceinline__ void gs_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2, u64 nq) {
     const u64 u = x, v = y;
     u64 s = u + v;
     x = s >= q2 ? s - q2 : s;
-    y = mul_shoup_lazy(u + q2 - v, w.x, w.y, q2 >> 1);
+    y = shoup_fold(u + q2 - v, w.x, w.y, nq);
 }
 __device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0, q)
     x = x >= q2 ? x - q2 : x;
@@ -77,10 +89,13 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
-    const int limb = blockIdx.y;
+    // grid: x = segment (fastest, so the blocks of one prime's row/column
+    // block across all segments run back to back and share its twiddles in
+    // L2), y = block within the limb, z = limb
+    const int limb = blockIdx.z;
     const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (size_t)blockIdx.z * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
-    const u64 q = Tb.mods[p].q, q2 = 2 * q;
+    u64 *a = data + (size_t)blockIdx.x * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
+    const u64 q = Tb.mods[p].q, q2 = 2 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
 
     int t, tr;  // lane within its transform, transform within the block
@@ -91,7 +106,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         tr = threadIdx.x / T;
         t = threadIdx.x % T;
     }
-    const size_t tid_global = (size_t)blockIdx.x * NB + tr;  // column or row index
+    const size_t tid_global = (size_t)blockIdx.y * NB + tr;  // column or row index
     const bool valid = tid_global < ((size_t)1 << (logN - PB));  // small rings: partial block
     const int S0 = COLS ? 0 : logN - PB;                      // global stage of local stage 0
 
@@ -113,7 +128,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
             const int idx0 = t + T * r0;
             const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
             const size_t wi = ((size_t)1 << (S0 + s)) + i;
-            ct_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2);
+            ct_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2, nq);
         }
     }
     // ---- exchange through LDS: L1 -> L2 (idx = (t*G + g) * 2^RB + r)
@@ -136,18 +151,36 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
                 const int idx0 = (t * G + g) * T + r0;
                 const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
                 const size_t wi = ((size_t)1 << (S0 + s)) + i;
-                ct_bfly(x[g * T + r0], x[g * T + r0 + (1 << hb)], tw[wi], q2);
+                ct_bfly(x[g * T + r0], x[g * T + r0 + (1 << hb)], tw[wi], q2, nq);
             }
     }
-    // ---- store, layout L2
+    // ---- store.  COLS: layout L2 is already lane-contiguous in memory
+    // (adjacent lanes = adjacent columns).  ROWS: a lane now owns T
+    // consecutive coefficients, so the values go back through LDS to layout
+    // L1 and every store instruction writes contiguous 128-B runs.  Each lane
+    // rewrites only the tile words it read itself, so one barrier suffices.
+    if (COLS) {
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int r = 0; r < T; ++r) {
-            const int idx = (t * G + g) * T + r;
-            const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
-            if (valid) a[off] = COLS ? x[g * T + r] : canon4(x[g * T + r], q, q2);
+            for (int r = 0; r < T; ++r) {
+                const int idx = (t * G + g) * T + r;
+                if (valid) a[(size_t)idx * ((size_t)1 << k2) + tid_global] = x[g * T + r];
+            }
+    } else {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < T; ++r)
+                tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] = canon4(x[g * T + r], q, q2);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int idx = t + T * r;
+            const u64 v = tile[lds_at<PB, NB, COLS>(tr, idx)];
+            if (valid) a[tid_global * LEN + idx] = v;
         }
+    }
 }
 
 // Inverse: global GS stage sg has pair distance 2^sg, twiddle psi^-brev(m + i),
@@ -166,10 +199,13 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
-    const int limb = blockIdx.y;
+    // grid: x = segment (fastest, so the blocks of one prime's row/column
+    // block across all segments run back to back and share its twiddles in
+    // L2), y = block within the limb, z = limb
+    const int limb = blockIdx.z;
     const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (size_t)blockIdx.z * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
-    const u64 q = Tb.mods[p].q, q2 = 2 * q;
+    u64 *a = data + (size_t)blockIdx.x * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
+    const u64 q = Tb.mods[p].q, q2 = 2 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
 
     int t, tr;
@@ -180,12 +216,14 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
         tr = threadIdx.x / T;
         t = threadIdx.x % T;
     }
-    const size_t tid_global = (size_t)blockIdx.x * NB + tr;
+    const size_t tid_global = (size_t)blockIdx.y * NB + tr;
     const bool valid = tid_global < ((size_t)1 << (logN - PB));
     const int SG0 = COLS ? logN - PB : 0;  // global GS stage of local stage 0
 
     u64 x[E];
-    // ---- load, layout L2 (low bits within a lane group)
+    // ---- load, layout L2 (low bits within a lane group).  The ROWS pass's
+    // per-lane 128-B runs are served by L1 after the first touch; routing
+    // them through LDS instead measured slower.
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -207,7 +245,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
                 const size_t j = COLS ? 0 : tid_global * LEN;  // row offset (COLS: column bits vanish)
                 const size_t i = (j + (size_t)idx0 * (COLS ? ((size_t)1 << k2) : 1)) >> (sg + 1);
                 const size_t wi = (n >> (sg + 1)) + i;
-                gs_bfly(x[g * T + r0], x[g * T + r0 + (1 << s)], tw[wi], q2);
+                gs_bfly(x[g * T + r0], x[g * T + r0 + (1 << s)], tw[wi], q2, nq);
             }
     }
     // ---- exchange L2 -> L1 (idx = t + T * r)
@@ -230,7 +268,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
             const size_t j = COLS ? 0 : tid_global * LEN;
             const size_t i = (j + (size_t)idx0 * (COLS ? ((size_t)1 << k2) : 1)) >> (sg + 1);
             const size_t wi = (n >> (sg + 1)) + i;
-            gs_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2);
+            gs_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2, nq);
         }
     }
     // ---- store, layout L1 (COLS: times n^-1)
@@ -248,7 +286,7 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
                  hipStream_t st) {
     constexpr int NB = NTB >> (PB - EB);
     const int count = 1 << (T.logN - PB);  // columns (COLS) or rows (ROWS)
-    const dim3 grid((unsigned)((count + NB - 1) / NB), (unsigned)limbs, (unsigned)segs);
+    const dim3 grid((unsigned)segs, (unsigned)((count + NB - 1) / NB), (unsigned)limbs);
     LaunchClock *clk = launch_clock();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (clk) clk->events(e0, e1);
