@@ -12,6 +12,9 @@
 #include "kernels.hpp"
 
 #include <stdexcept>
+#include <utility>
+#include <type_traits>
+#include <string>
 
 namespace fhe {
 namespace dev {
@@ -20,7 +23,8 @@ namespace {
 
 constexpr int NT = 256;     // threads per block
 constexpr int MAXSRC = 16;  // max limbs per digit / special primes held in registers
-constexpr int TCH = 16;     // target limbs per thread in basis conversions
+constexpr int TCH = 64;     // target limbs per thread in basis conversions (all of them: the
+                            // per-coefficient prologue then runs once)
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
@@ -279,7 +283,7 @@ __global__ __launch_bounds__(NT) void k_reduce(u64 *x, Seg S, const Mod *mods, i
 
 // ------------------------------------------------------------ keyswitch ----
 struct ModUpArgs {
-    const u64 *qhinv[8], *qhinv_s[8], *qhat[8], *qhat_s[8];
+    const u64 *qhinv[8], *qhinv_s[8], *qhat[8];  // per digit; qhat [W][AT] (zero-padded rows)
     int lo[8], hi[8];
     int digits;
     size_t coef_stride, ext_stride;
@@ -287,8 +291,11 @@ struct ModUpArgs {
 
 // grid: x = n / NT, y = target chunks of TCH, z = member * digits + digit.
 // coef: member m at m * A.coef_stride ([ell][n], coefficient form);
-// ext: member m at m * A.ext_stride ([digits][W][n]).
-__global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef, int W, ModUpArgs A,
+// ext: member m at m * A.ext_stride ([digits][W][n]).  AT = alpha (digit
+// size): the source loop is straight-line; a shorter last digit reads a
+// clamped limb times a zero constant.
+template <int AT>
+__global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef, int W, int ell, ModUpArgs A,
                                                       const int *pmap_ext, const Mod *mods, int logN) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
@@ -297,27 +304,22 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef,
     const size_t mb = blockIdx.z / (unsigned)A.digits;
     coef += mb * A.coef_stride;
     ext += mb * A.ext_stride;
-    const int lo = A.lo[j], hi = A.hi[j], a = hi - lo;
+    const int lo = A.lo[j], hi = A.hi[j];
     const int t0 = blockIdx.y * TCH;
-    bool any = false;
-    for (int t = t0; t < t0 + TCH && t < W; ++t) any |= !(t >= lo && t < hi);
-    if (!any) return;
-    u64 y[MAXSRC];
+    Split30 y[AT];
 #pragma unroll
-    for (int i = 0; i < MAXSRC; ++i) {
-        if (i < a) {
-            const u64 qi = mods[lo + i].q;
-            y[i] = mul_shoup(coef[(size_t)(lo + i) * n + k], A.qhinv[j][i], A.qhinv_s[j][i], qi);
-        }
+    for (int i = 0; i < AT; ++i) {
+        const int src = min(lo + i, ell - 1);
+        y[i] = split30(mul_shoup(coef[(size_t)src * n + k], A.qhinv[j][i], A.qhinv_s[j][i], mods[src].q));
     }
+    const u64 *qh = A.qhat[j];
     for (int t = t0; t < t0 + TCH && t < W; ++t) {
         if (t >= lo && t < hi) continue;
         const Mod mt = mods[pmap_ext[t]];
-        Acc128 acc;  // lazy: one reduction per output
+        Acc4 acc;  // lazy: one reduction per output
 #pragma unroll
-        for (int i = 0; i < MAXSRC; ++i)
-            if (i < a) mac128(acc, y[i], A.qhat[j][(size_t)i * W + t]);
-        ext[((size_t)j * W + t) * n + k] = reduce128(acc, mt);
+        for (int i = 0; i < AT; ++i) mac4(acc, y[i], split30(qh[(size_t)t * AT + i]));
+        ext[((size_t)j * W + t) * n + k] = reduce4(acc, mt);
     }
 }
 
@@ -359,27 +361,26 @@ __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const
     acc[((size_t)W + t) * n + k] = a1;
 }
 
-// grid: x = n / NT, y = ceil(ell / TCH), z = segment
-__global__ __launch_bounds__(NT) void k_moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq,
-                                                        size_t seg_in, size_t seg_out, const u64 *phinv,
-                                                        const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
-                                                        const Mod *mods, int logN) {
+// grid: x = n / NT, y = ceil(ell / TCH), z = segment.  KT = K special primes;
+// phat [nq][KT] (the constants of one target contiguous: one scalar burst)
+template <int KT>
+__global__ __launch_bounds__(NT) void k_moddown_convert(u64 *conv, const u64 *pc, int ell, int nq, size_t seg_in,
+                                                        size_t seg_out, const u64 *phinv, const u64 *phinv_s,
+                                                        const u64 *phat, const Mod *mods, int logN) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
     const u64 *src = pc + (size_t)blockIdx.z * seg_in;
     u64 *dst = conv + (size_t)blockIdx.z * seg_out;
-    u64 v[MAXSRC];
+    Split30 v[KT];
 #pragma unroll
-    for (int i = 0; i < MAXSRC; ++i)
-        if (i < K) v[i] = mul_shoup(src[(size_t)i * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+    for (int i = 0; i < KT; ++i) v[i] = split30(mul_shoup(src[(size_t)i * n + k], phinv[i], phinv_s[i], mods[nq + i].q));
     const int i0 = blockIdx.y * TCH;
     for (int i = i0; i < i0 + TCH && i < ell; ++i) {
-        Acc128 acc;
+        Acc4 acc;
 #pragma unroll
-        for (int kk = 0; kk < MAXSRC; ++kk)
-            if (kk < K) mac128(acc, v[kk], phat[(size_t)kk * nq + i]);
-        dst[(size_t)i * n + k] = reduce128(acc, mods[i]);
+        for (int kk = 0; kk < KT; ++kk) mac4(acc, v[kk], split30(phat[(size_t)i * KT + kk]));
+        dst[(size_t)i * n + k] = reduce4(acc, mods[i]);
     }
 }
 
@@ -415,29 +416,28 @@ __global__ __launch_bounds__(NT) void k_moddown_finish(u64 *out, const u64 *acc,
 // corr_i = Conv_{P->q_i}(acc_P) + P * [y_last]_centred  for i < ell-1, where
 // y_last = (x_last - Conv_{P->q_last}(acc_P)) * P^-1 mod q_last is the last
 // limb of the ModDown output.  grid: x = n / NT, y = ceil((ell-1) / TCH), z = seg
-__global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq,
+template <int KT>
+__global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int nq,
                                                                 size_t seg_acc, size_t seg_corr, const u64 *phinv,
-                                                                const u64 *phinv_s, const u64 *phat,
-                                                                const u64 *phat_s, const u64 *pinv,
-                                                                const u64 *pinv_s, const u64 *pmod,
-                                                                const u64 *pmod_s, const Mod *mods, int logN) {
+                                                                const u64 *phinv_s, const u64 *phat, const u64 *pinv,
+                                                                const u64 *pinv_s, const u64 *pmod, const Mod *mods,
+                                                                int logN) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
     const int last = ell - 1;
     const u64 *src = acc + (size_t)blockIdx.z * seg_acc + (size_t)last * n;
     u64 *dst = corr + (size_t)blockIdx.z * seg_corr;
-    u64 v[MAXSRC];
+    Split30 v[KT];
 #pragma unroll
-    for (int i = 0; i < MAXSRC; ++i)
-        if (i < K) v[i] = mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+    for (int i = 0; i < KT; ++i)
+        v[i] = split30(mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q));
     const Mod ml = mods[last];
     const u64 ql = ml.q;
-    Acc128 cacc;
+    Acc4 cacc;
 #pragma unroll
-    for (int kk = 0; kk < MAXSRC; ++kk)
-        if (kk < K) mac128(cacc, v[kk], phat[(size_t)kk * nq + last]);
-    const u64 cl = reduce128(cacc, ml);
+    for (int kk = 0; kk < KT; ++kk) mac4(cacc, v[kk], split30(phat[(size_t)last * KT + kk]));
+    const u64 cl = reduce4(cacc, ml);
     const u64 y = mul_shoup(sub_mod(src[k], cl, ql), pinv[last], pinv_s[last], ql);
     const bool neg = y > (ql >> 1);
     const int i0 = blockIdx.y * TCH;
@@ -445,12 +445,11 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const
         const Mod mi = mods[i];
         u64 lift = reduce64(y, mi);
         if (neg) lift = sub_mod(lift, reduce64(ql, mi), mi.q);
-        Acc128 acc;
-        mac128(acc, lift, pmod[i]);
+        Acc4 a4;
+        mac4(a4, split30(lift), split30(pmod[i]));
 #pragma unroll
-        for (int kk = 0; kk < MAXSRC; ++kk)
-            if (kk < K) mac128(acc, v[kk], phat[(size_t)kk * nq + i]);
-        dst[(size_t)i * n + k] = reduce128(acc, mi);
+        for (int kk = 0; kk < KT; ++kk) mac4(a4, v[kk], split30(phat[(size_t)i * KT + kk]));
+        dst[(size_t)i * n + k] = reduce4(a4, mi);
     }
 }
 // out_i = (acc_i + d_i P - corr_i) * (P q_last)^-1, i < ell-1, NTT form.
@@ -635,27 +634,41 @@ void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int log
     hipLaunchKernelGGL(k_reduce, ew_grid(logN, limbs, segs), dim3(NT), 0, st, x, Seg{seg, seg, 0}, mods, logN);
 }
 
+// compile-time dispatch of a small runtime integer (digit size, special-prime count)
+template <int Lo, int Hi, typename F>
+void dispatch_int(int v, F &&f) {
+    if constexpr (Lo > Hi) {
+        throw std::invalid_argument("unsupported basis size " + std::to_string(v));
+    } else {
+        if (v == Lo)
+            f(std::integral_constant<int, Lo>{});
+        else
+            dispatch_int<Lo + 1, Hi>(v, std::forward<F>(f));
+    }
+}
+
 void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
                    size_t coef_stride, size_t ext_stride, const int *pmap_ext, const u64 *tabs,
                    const size_t *tab_off, const Mod *mods, int logN, hipStream_t st) {
     const int W = ell + K;
     ModUpArgs A{};
     for (int j = 0; j < digits; ++j) {
-        const int lo = j * alpha, hi = std::min((j + 1) * alpha, ell), a = hi - lo;
         const u64 *base = tabs + tab_off[j];
         A.qhinv[j] = base;
-        A.qhinv_s[j] = base + a;
-        A.qhat[j] = base + 2 * a;
-        A.qhat_s[j] = base + 2 * a + (size_t)a * W;
-        A.lo[j] = lo;
-        A.hi[j] = hi;
+        A.qhinv_s[j] = base + alpha;
+        A.qhat[j] = base + 2 * alpha;
+        A.lo[j] = j * alpha;
+        A.hi[j] = std::min((j + 1) * alpha, ell);
     }
     A.digits = digits;
     A.coef_stride = coef_stride;
     A.ext_stride = ext_stride;
     const double B = 8.0 * members * (double)((size_t)digits * W) * ((size_t)1 << logN);  // ell in + (dW - ell) out
-    launch_clocked("k_modup_convert", B, k_modup_convert, pt_grid(logN, (W + TCH - 1) / TCH, digits * members), dim3(NT),
-                   st, ext, coef, W, A, pmap_ext, mods, logN);
+    dispatch_int<1, 16>(alpha, [&](auto c) {
+        constexpr int AT = decltype(c)::value;
+        launch_clocked("k_modup_convert", B, k_modup_convert<AT>, pt_grid(logN, (W + TCH - 1) / TCH, digits * members),
+                       dim3(NT), st, ext, coef, W, ell, A, pmap_ext, mods, logN);
+    });
 }
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
@@ -668,14 +681,16 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
                    nall, alpha, digits, perm, pmap_ext, mods, logN, str, fold);
 }
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
-                             int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
-                             const u64 *pinv, const u64 *pinv_s, const u64 *pmod, const u64 *pmod_s,
-                             const Mod *mods, int logN, hipStream_t st) {
+                             int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
+                             const u64 *pinv_s, const u64 *pmod, const Mod *mods, int logN, hipStream_t st) {
     if (ell <= 1) return;
     const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
-    launch_clocked("k_moddown_rescale_convert", B, k_moddown_rescale_convert,
-                   pt_grid(logN, (ell - 1 + TCH - 1) / TCH, segs), dim3(NT), st, corr, acc, ell, K, nq, seg_acc, seg_corr,
-                   phinv, phinv_s, phat, phat_s, pinv, pinv_s, pmod, pmod_s, mods, logN);
+    dispatch_int<1, 15>(K, [&](auto c) {
+        constexpr int KT = decltype(c)::value;
+        launch_clocked("k_moddown_rescale_convert", B, k_moddown_rescale_convert<KT>,
+                       pt_grid(logN, (ell - 1 + TCH - 1) / TCH, segs), dim3(NT), st, corr, acc, ell, nq, seg_acc,
+                       seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, mods, logN);
+    });
 }
 void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, int ell, int segs, size_t seg_out,
                      size_t seg_acc, size_t seg_d, const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
@@ -686,11 +701,14 @@ void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, in
                    corr, seg_out, seg_acc, seg_d, pqlinv, pqlinv_s, pmod, pmod_s, mods, logN);
 }
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
-                     const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s, const Mod *mods,
-                     int logN, hipStream_t st) {
+                     const u64 *phinv, const u64 *phinv_s, const u64 *phat, const Mod *mods, int logN,
+                     hipStream_t st) {
     const double B = 8.0 * segs * (double)(K + ell) * ((size_t)1 << logN);
-    launch_clocked("k_moddown_convert", B, k_moddown_convert, pt_grid(logN, (ell + TCH - 1) / TCH, segs), dim3(NT), st,
-                   conv, pc, ell, K, nq, seg_in, seg_out, phinv, phinv_s, phat, phat_s, mods, logN);
+    dispatch_int<1, 15>(K, [&](auto c) {
+        constexpr int KT = decltype(c)::value;
+        launch_clocked("k_moddown_convert", B, k_moddown_convert<KT>, pt_grid(logN, (ell + TCH - 1) / TCH, segs),
+                       dim3(NT), st, conv, pc, ell, nq, seg_in, seg_out, phinv, phinv_s, phat, mods, logN);
+    });
 }
 void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,
                     size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s, const Mod *mods, int logN,

@@ -108,10 +108,6 @@ void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap,
                       hipStream_t st);
 
 // ---------------------------------------------------------------- keyswitch
-struct ModUpTab {
-    const u64 *qhinv, *qhinv_s;  // [alpha]        (digit source primes)
-    const u64 *qhat, *qhat_s;    // [alpha][W]     (W = ell + K targets)
-};
 // ext[m][j][t][k] for every member m, digit j and target t not in digit j
 // (coefficient in, NTT NOT applied); coef member stride coef_stride, ext member stride ext_stride
 void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
@@ -134,17 +130,16 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
 // fused ModDown + rescale of an HMult (see kernels.hip): corr [segs][ell-1][n]
 // from acc [segs][W][n] whose limbs ell-1 .. W-1 are in coefficient form
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
-                             int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
-                             const u64 *pinv, const u64 *pinv_s, const u64 *pmod, const u64 *pmod_s,
-                             const Mod *mods, int logN, hipStream_t st);
+                             int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
+                             const u64 *pinv_s, const u64 *pmod, const Mod *mods, int logN, hipStream_t st);
 // out [segs][ell-1][n] = (acc + d * P - corr) * (P q_{ell-1})^-1  (pqlinv: the row for this ell)
 void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, int ell, int segs, size_t seg_out,
                      size_t seg_acc, size_t seg_d, const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
                      const u64 *pmod_s, const Mod *mods, int logN, hipStream_t st);
-// conv[s][i][k] = sum_k' (pc[s][k'] * phinv_k') * phat[k'][i] mod q_i  for i < ell
-void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out,
-                     int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *phat_s,
-                     const Mod *mods, int logN, hipStream_t st);
+// conv[s][i][k] = sum_k' (pc[s][k'] * phinv_k') * phat[i][k'] mod q_i  for i < ell
+void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
+                     const u64 *phinv, const u64 *phinv_s, const u64 *phat, const Mod *mods, int logN,
+                     hipStream_t st);
 // out[s][i] = (acc[s][i] - conv[s][i]) * Pinv_i (+ add[s/2][i] on even s, i.e. c0 of each member)
 void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,
                     size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s, const Mod *mods, int logN,

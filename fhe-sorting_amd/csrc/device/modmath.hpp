@@ -87,5 +87,40 @@ __device__ __forceinline__ u64 reduce128(const Acc128 &a, const Mod &m) {
     return add_mod(reduce64(a.lo, m), mul_shoup(a.hi, m.r64, m.r64s, m.q), m.q);
 }
 
+// Basis-conversion accumulator: every prime is < 2^60 (checked at context
+// creation), so operands split into 30-bit halves and the four partial sums
+// a0*b0, a0*b1, a1*b0, a1*b1 (each < 2^60 per term) absorb up to 16 terms in
+// 64 bits -- one v_mad_u64_u32 with accumulate per partial product, no carry
+// handling until the single reduction per output.
+constexpr u64 MASK30 = (1ull << 30) - 1;
+struct Acc4 {
+    u64 s00 = 0, s01 = 0, s10 = 0, s11 = 0;
+};
+struct Split30 {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ Split30 split30(u64 b) { return Split30{(uint32_t)(b & MASK30), (uint32_t)(b >> 30)}; }
+__device__ __forceinline__ void mac4(Acc4 &s, Split30 a, Split30 b) {
+    s.s00 += (u64)a.lo * b.lo;
+    s.s01 += (u64)a.lo * b.hi;
+    s.s10 += (u64)a.hi * b.lo;
+    s.s11 += (u64)a.hi * b.hi;
+}
+// s00 + (s01 + s10) 2^30 + s11 2^60 mod q
+__device__ __forceinline__ u64 reduce4(const Acc4 &s, const Mod &m) {
+    const u64 mid = s.s01 + s.s10;
+    const u64 mc = mid < s.s01;  // carry of the middle sum (bit 64)
+    Acc128 r;
+    r.lo = s.s00;
+    r.hi = 0;
+    const u64 ml = mid << 30;
+    r.lo += ml;
+    r.hi += (mid >> 34) + (mc << 30) + (r.lo < ml);
+    const u64 tl = s.s11 << 60;
+    r.lo += tl;
+    r.hi += (s.s11 >> 4) + (r.lo < tl);
+    return reduce128(r, m);
+}
+
 }  // namespace dev
 }  // namespace fhe

@@ -98,7 +98,7 @@ struct Engine::Impl {
     dev::NttTables T{};
     int *extmap = nullptr;   // [nq+1][nq+K]
     u64 *modup_tab = nullptr;  // packed ModUp tables
-    u64 *phinv = nullptr, *phinv_s = nullptr, *phat = nullptr, *phat_s = nullptr, *pinv = nullptr, *pinv_s = nullptr;
+    u64 *phinv = nullptr, *phinv_s = nullptr, *phat = nullptr, *pinv = nullptr, *pinv_s = nullptr;
     u64 *qlinv = nullptr, *qlinv_s = nullptr;
     u64 *pmod = nullptr, *pmod_s = nullptr, *pqlinv = nullptr, *pqlinv_s = nullptr;
     int *modup_smap = nullptr, *modup_pmap = nullptr;
@@ -182,7 +182,7 @@ struct Engine::Impl {
         auto convm = alloc((size_t)segs * ell * nn * 8);
         u64 *conv = static_cast<u64 *>(convm->p);
         dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, segs, phinv, phinv_s,
-                             phat, phat_s, mods, P.logN, st);
+                             phat, mods, P.logN, st);
         dev::ntt_forward(conv, (int)ell, segs, ell * nn, nullptr, T, st);
         dev::moddown_finish(out, acc, conv, add, (int)ell, segs, ell * nn, W * nn, add_stride, pinv, pinv_s, mods,
                             P.logN, st);
@@ -215,7 +215,7 @@ struct Engine::Impl {
         auto corrm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *corr = static_cast<u64 *>(corrm->p);
         dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, segs, phinv,
-                                     phinv_s, phat, phat_s, pinv, pinv_s, pmod, pmod_s, mods, P.logN, st);
+                                     phinv_s, phat, pinv, pinv_s, pmod, mods, P.logN, st);
         dev::ntt_forward(corr, (int)(ell - 1), segs, (ell - 1) * nn, nullptr, T, st);
         dev::mul_tail_finish(out, acc, d01, corr, (int)ell, segs, (ell - 1) * nn, W * nn, ell * nn,
                              pqlinv + ell * P.nq(), pqlinv_s + ell * P.nq(), pmod, pmod_s, mods, P.logN, st);
@@ -249,6 +249,12 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.pool->device = device;
     I.P = host::make_params(logN, L, scale_bits, first_bits, dnum);
     I.LT = host::make_level_tables(I.P);
+    // kernel preconditions: basis conversions hold <= 16 source residues in
+    // registers and accumulate 30-bit-split products of residues < 2^60
+    for (u64 q : I.P.primes)
+        if (q >> 60) throw std::invalid_argument("engine: every prime must be < 2^60 (first_bits <= 60)");
+    if (I.P.alpha > 16 || I.P.K > 15)
+        throw std::invalid_argument("engine: digit size <= 16 and special primes <= 15 required (raise dnum)");
     const size_t nall = I.P.nall(), n = I.P.n;
     std::vector<Mod> mods(nall);
     for (size_t i = 0; i < nall; ++i) {
@@ -288,7 +294,6 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.phinv = I.upload_static(I.LT.phinv);
     I.phinv_s = I.upload_static(I.LT.phinv_s);
     I.phat = I.upload_static(I.LT.phat);
-    I.phat_s = I.upload_static(I.LT.phat_s);
     I.pinv = I.upload_static(I.LT.pinv);
     I.pinv_s = I.upload_static(I.LT.pinv_s);
     I.qlinv = I.upload_static(I.LT.qlinv);
@@ -1023,7 +1028,7 @@ void Engine::moddown_host(const u64 *in, size_t ell, u64 *out) {
     auto cm = I.alloc(ell * nn * 8);
     u64 *conv = static_cast<u64 *>(cm->p);
     dev::moddown_convert(conv, x + ell * nn, (int)ell, (int)K, (int)I.P.nq(), W * nn, ell * nn, 1, I.phinv,
-                         I.phinv_s, I.phat, I.phat_s, MODS, LOGN, ST);
+                         I.phinv_s, I.phat, MODS, LOGN, ST);
     dev::ntt_forward(conv, (int)ell, 1, 0, nullptr, I.T, ST);
     auto om = I.alloc(ell * nn * 8);
     dev::moddown_finish(static_cast<u64 *>(om->p), x, conv, nullptr, (int)ell, 1, ell * nn, W * nn, 0, I.pinv,

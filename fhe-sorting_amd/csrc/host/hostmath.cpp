@@ -378,7 +378,9 @@ LevelTables make_level_tables(const Params &P) {
         for (size_t j = 0; j < digits; ++j) {
             const size_t lo = j * alpha, hi = std::min(ell, (j + 1) * alpha), a = hi - lo;
             T.modup_off[ell].push_back(T.modup.size());
-            std::vector<u64> qhinv(a), qhinv_s(a), qhat(a * W, 0), qhat_s(a * W, 0);
+            // layout (device): qhinv[alpha], qhinv_s[alpha], qhat[W][alpha]; rows
+            // zero-padded to alpha so every digit runs the same unrolled code
+            std::vector<u64> qhinv(alpha, 0), qhinv_s(alpha, 0), qhat(W * alpha, 0);
             for (size_t i = lo; i < hi; ++i) {
                 u64 prod = 1;
                 for (size_t s = lo; s < hi; ++s)
@@ -394,21 +396,18 @@ LevelTables make_level_tables(const Params &P) {
                     u64 prod = 1;
                     for (size_t s = lo; s < hi; ++s)
                         if (s != i) prod = mulmod(prod, P.primes[s] % mt.q, mt);
-                    qhat[(i - lo) * W + t] = prod;
-                    qhat_s[(i - lo) * W + t] = shoup(prod, mt.q);
+                    qhat[t * alpha + (i - lo)] = prod;
                 }
             }
             T.modup.insert(T.modup.end(), qhinv.begin(), qhinv.end());
             T.modup.insert(T.modup.end(), qhinv_s.begin(), qhinv_s.end());
             T.modup.insert(T.modup.end(), qhat.begin(), qhat.end());
-            T.modup.insert(T.modup.end(), qhat_s.begin(), qhat_s.end());
         }
     }
     // ModDown
     T.phinv.resize(K);
     T.phinv_s.resize(K);
-    T.phat.assign(K * nq, 0);
-    T.phat_s.assign(K * nq, 0);
+    T.phat.assign(nq * K, 0);  // [nq][K]: the K constants of one target are contiguous
     T.pinv.resize(nq);
     T.pinv_s.resize(nq);
     T.pmod.resize(nq);
@@ -428,8 +427,7 @@ LevelTables make_level_tables(const Params &P) {
             u64 prod = 1;
             for (size_t s = 0; s < K; ++s)
                 if (s != k) prod = mulmod(prod, P.primes[nq + s] % mi.q, mi);
-            T.phat[k * nq + i] = prod;
-            T.phat_s[k * nq + i] = shoup(prod, mi.q);
+            T.phat[i * K + k] = prod;
             Pm = mulmod(Pm, P.primes[nq + k] % mi.q, mi);
         }
         T.pinv[i] = invmod(Pm, mi);

@@ -82,12 +82,12 @@ inline u64 enc_e1(u64 c) { return 0x80000000ULL + 3 * c + 2; }
 
 // Precomputed key-switching / rescale constants for every level.
 struct LevelTables {
-    // ModUp, per ell (1..nq) and digit: [qhinv(a), qhinv_s(a), qhat(a*W), qhat_s(a*W)]
+    // ModUp, per ell (1..nq) and digit: [qhinv(alpha), qhinv_s(alpha), qhat(W*alpha) as [t][i]]
     std::vector<u64> modup;             // packed
     std::vector<std::vector<size_t>> modup_off;  // [ell][digit] offset into modup
     // ModDown (level independent)
     std::vector<u64> phinv, phinv_s;    // [K]
-    std::vector<u64> phat, phat_s;      // [K][nq]
+    std::vector<u64> phat;              // [nq][K]
     std::vector<u64> pinv, pinv_s;      // [nq]
     std::vector<u64> pmod, pmod_s;      // [nq]  P mod q_i
     // fused ModDown + rescale (HMult tail): pqlinv[ell][i] = (P q_{ell-1})^{-1} mod q_i
