@@ -48,6 +48,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true', help='skip the instrumented roofline sort (PMC passes)')
     ap.add_argument('--cpu-sample-mults', type=int, default=0, help='override CPU sample size')
+    ap.add_argument('--clock-json', default=None, help='write the full per-kernel clock of the roofline sort here')
     return ap.parse_args()
 
 
@@ -111,7 +112,7 @@ def device_sync(ctx):
         pass
 
 
-def roofline(ctx, run_once):
+def roofline(ctx, run_once, dump=None):
     """Roofline of the dominant kernel, measured live: one more (untimed) sort
     runs with every hot kernel launched through hipExtLaunchKernelGGL with
     start/stop events on the engine stream (the stream it runs on); the kernel
@@ -123,6 +124,9 @@ def roofline(ctx, run_once):
     with F.KernelClock(ctx) as clk:
         run_once()
     stats = clk.stats
+    if dump:
+        with open(dump, 'w') as f:
+            json.dump(stats, f, indent=1)
     total_ms = sum(v['ms'] for v in stats.values())
     name, st = max(stats.items(), key=lambda kv: kv[1]['ms'])
     avg_s = st['ms'] / st['launches'] * 1e-3
@@ -239,7 +243,7 @@ def main():
         res['roofline'] = None
         if not a.no_roofline:
             try:
-                res['roofline'] = roofline(ctx, lambda: ctx.direct_sort(ct, N, rots, cfg, shard=(0, 1)))
+                res['roofline'] = roofline(ctx, lambda: ctx.direct_sort(ct, N, rots, cfg, shard=(0, 1)), a.clock_json)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
         if d.world == 1 and not a.no_cpu_baseline:

@@ -323,7 +323,7 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef,
     }
 }
 
-// grid: x = n / NT, y = W targets, z = member.  Member m: acc at m * st.acc
+// Member m: acc at m * st.acc
 // ([2][W][n]), ext at m * st.ext, the switched polynomial (NTT) at m * st.d.
 // fold (HMult tail, may be null): on limb t = ell-1 the accumulators start at
 // P * (d0, d1)[ell-1] of the member, so the fused ModDown+rescale sees
@@ -332,11 +332,13 @@ __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const
                                                  int ell, int W, int nall, int alpha, int digits,
                                                  const uint32_t *perm, const int *pmap_ext, const Mod *mods,
                                                  int logN, KsStrides st, KsFold fold) {
+    // grid: x = member (fastest: the blocks reading one key block for all
+    // members run back to back and share it in L2), y = coefficient block, z = target
     const size_t n = (size_t)1 << logN;
-    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    const size_t k = (size_t)blockIdx.y * NT + threadIdx.x;
     if (k >= n) return;
-    const int t = blockIdx.y;
-    const size_t mb = blockIdx.z;
+    const int t = blockIdx.z;
+    const size_t mb = blockIdx.x;
     acc += mb * st.acc;
     ext += mb * st.ext;
     dntt += mb * st.d;
@@ -677,8 +679,9 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
     const int W = ell + K;
     // ext (+ own digit) and 2 accumulators per member; the key once
     const double B = 8.0 * ((double)members * (digits * W + 2.0 * W) + 2.0 * digits * W) * ((size_t)1 << logN);
-    launch_clocked("k_ks_inner", B, k_ks_inner, pt_grid(logN, W, members), dim3(NT), st, acc, ext, dntt, key, ell, W,
-                   nall, alpha, digits, perm, pmap_ext, mods, logN, str, fold);
+    const dim3 grid((unsigned)members, (unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
+    launch_clocked("k_ks_inner", B, k_ks_inner, grid, dim3(NT), st, acc, ext, dntt, key, ell, W, nall, alpha, digits,
+                   perm, pmap_ext, mods, logN, str, fold);
 }
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,

@@ -35,6 +35,8 @@ struct LaunchClock {
     virtual void record(const char *kernel, double bytes) = 0;
 };
 LaunchClock *&launch_clock();
+// caller tag appended to clocked NTT names ("k_ntt_fwd<8, 4, true>@modup")
+const char *&launch_phase();
 
 // Launch through hipExtLaunchKernelGGL; when a clock is installed the launch is
 // timed by events recorded at the kernel's own start/end and booked under

@@ -83,6 +83,13 @@ struct DevMem {
 };
 
 // ================================================================ impl ====
+// tags the NTT launches of one engine helper in the live kernel clock
+struct Phase {
+    const char *prev;
+    explicit Phase(const char *p) : prev(dev::launch_phase()) { dev::launch_phase() = p; }
+    ~Phase() { dev::launch_phase() = prev; }
+};
+
 struct Engine::Impl {
     host::Params P;
     host::LevelTables LT;
@@ -143,6 +150,7 @@ struct Engine::Impl {
     //
     // ext[m][j][t] (NTT form) for all digits of d[m] ([ell][n], NTT form)
     std::shared_ptr<DevMem> modup(const u64 *d, size_t ell, int members, size_t d_stride) {
+        Phase phase_("modup");
         const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         const int digits = P.digits_at(ell);
         auto coef = alloc((size_t)members * ell * nn * 8);
@@ -166,6 +174,7 @@ struct Engine::Impl {
     // d: the switched polynomial of member m at m * d_stride (NTT form)
     void ks_apply(const u64 *e, const u64 *d, size_t d_stride, size_t ell, int members, const u64 *key,
                   const uint32_t *pm, u64 *out, const u64 *add, size_t add_stride) {
+        Phase phase_("ks_moddown");
         const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         const int digits = P.digits_at(ell);
         const int segs = 2 * members;
@@ -194,6 +203,7 @@ struct Engine::Impl {
     // NTT of ell-1 limbs per polynomial serves both divisions.
     // d01 [members][2][ell][n], d2 [members][ell][n] (NTT form).
     void mul_tail(const u64 *e, const u64 *d01, const u64 *d2, size_t ell, int members, u64 *out) {
+        Phase phase_("mul_tail");
         const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         const int digits = P.digits_at(ell);
         const int segs = 2 * members;
@@ -222,6 +232,7 @@ struct Engine::Impl {
     }
     // out [segs][ell-1][n] from in [segs][ell][n] with input segment stride seg_in
     void rescale(const u64 *in, size_t ell, size_t seg_in, int segs, u64 *out) {
+        Phase phase_("rescale");
         const size_t nn = n();
         auto lastm = alloc((size_t)segs * nn * 8);
         u64 *last = static_cast<u64 *>(lastm->p);
