@@ -75,6 +75,7 @@ struct PSEval {
     struct Leaf {
         std::vector<double> a;
         int target;
+        bool raw;  // folded remainder: the un-rescaled sum feeds mul_add_raw
     };
     std::vector<Leaf> leaves;
     std::map<size_t, CtPtr> ready;
@@ -97,7 +98,7 @@ struct PSEval {
         trim_zeros(a);
         const int d = (int)a.size() - 1;
         if (d <= B) {
-            leaves.push_back({a, target});
+            leaves.push_back({a, target, false});
             return;
         }
         std::vector<double> q, r;
@@ -106,7 +107,17 @@ struct PSEval {
         collect(q, target - 1);
         trim_zeros(r);
         if (r.size() == 1 && r[0] == 0.0) return;
+        if (folded(r)) {  // summed into the product before its rescale (eval)
+            leaves.push_back({r, target, true});
+            return;
+        }
         collect(r, target);
+    }
+    // a remainder that is a leaf with terms is added before the product's
+    // rescale (mul_add) instead of being evaluated on its own
+    bool folded(const std::vector<double> &r) const {
+        const int dr = (int)r.size() - 1;
+        return dr >= 1 && dr <= B;
     }
     static bool has_terms(const std::vector<double> &a) {
         for (size_t i = 1; i < a.size(); ++i)
@@ -115,9 +126,11 @@ struct PSEval {
     }
     void evaluate_chunk(size_t first) {
         const int target = leaves[first].target;
+        const bool raw = leaves[first].raw;
         std::vector<size_t> chunk;
         for (size_t i = first; i < leaves.size() && chunk.size() < 8; ++i)
-            if (leaves[i].target == target && !ready.count(i) && has_terms(leaves[i].a)) chunk.push_back(i);
+            if (leaves[i].target == target && leaves[i].raw == raw && !ready.count(i) && has_terms(leaves[i].a))
+                chunk.push_back(i);
         std::vector<int> idx;  // union of the baby steps the chunk uses
         for (size_t c : chunk)
             for (size_t i = 1; i < leaves[c].a.size(); ++i)
@@ -132,10 +145,10 @@ struct PSEval {
             for (int i : idx) row.push_back((size_t)i < leaves[c].a.size() ? leaves[c].a[i] : 0.0);
             rows.push_back(row);
         }
-        auto outs = cc.linear_sums_to(xs, rows, target);
+        auto outs = cc.linear_sums_to(xs, rows, target, !raw);
         for (size_t g = 0; g < chunk.size(); ++g) {
             CtPtr r = outs[g];
-            if (leaves[chunk[g]].a[0] != 0.0) r = cc.add_const(*r, leaves[chunk[g]].a[0]);
+            if (!raw && leaves[chunk[g]].a[0] != 0.0) r = cc.add_const(*r, leaves[chunk[g]].a[0]);
             ready[chunk[g]] = r;
         }
     }
@@ -159,9 +172,14 @@ struct PSEval {
         int G;
         split(a, d, q, r, G);
         CtPtr qv = eval(q, target - 1);
-        CtPtr prod = cc.mul(*qv, giant(G));
         trim_zeros(r);
-        if (r.size() == 1 && r[0] == 0.0) return prod;
+        if (r.size() == 1 && r[0] == 0.0) return cc.mul(*qv, giant(G));
+        if (folded(r)) {
+            CtPtr rawsum = leaf();  // the collected raw leaf (same order as collect)
+            CtPtr out = cc.mul_add_raw(*qv, giant(G), *rawsum);
+            return r[0] != 0.0 ? cc.add_const(*out, r[0]) : out;
+        }
+        CtPtr prod = cc.mul(*qv, giant(G));
         CtPtr rv = eval(r, target);
         return cc.add(*prod, *rv);
     }

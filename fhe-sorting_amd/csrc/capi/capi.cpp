@@ -323,7 +323,14 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
         ds.shard_rank = shard_rank;
         ds.shard_world = shard_world;
         if (fn) {
-            ds.allreduce = [fn, user](u64 *d, size_t c) { fn(d, (uint64_t)c, user); };
+            // the partial sums are produced asynchronously on the context stream:
+            // drain it so the callback sees finished data (it must complete the
+            // reduction before returning)
+            Engine *eng = ctx->eng.get();
+            ds.allreduce = [fn, user, eng](u64 *d, size_t c) {
+                eng->sync();
+                fn(d, (uint64_t)c, user);
+            };
         } else if (shard_world > 1) {
             if (!ctx->comm) throw std::runtime_error("sharded sort needs fhe_comm_init or an allreduce hook");
             ncclComm_t comm = ctx->comm;

@@ -564,12 +564,12 @@ void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *
     hipLaunchKernelGGL(k_sum_members, ew_grid(logN, limbs, 2), dim3(NT), 0, st, out, in, members, ln_all, mods, logN);
 }
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
-                   size_t xseg, const Mod *mods, int logN, hipStream_t st) {
+                   size_t xseg, const Mod *mods, int logN, hipStream_t st, bool accumulate) {
     if (limbs <= 0) return;
     for (int base = 0; base < m || (m == 0 && base == 0); base += LIN_MAX) {
         LinArgs A{};
         A.m = std::min(LIN_MAX, m - base);
-        A.accumulate = base > 0;
+        A.accumulate = base > 0 || accumulate;
         A.xseg = xseg;
         for (int i = 0; i < A.m; ++i) {
             A.x[i] = xs[base + i];

@@ -91,9 +91,9 @@ void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int mem
                const Mod *mods, int logN, hipStream_t st);
 // out [2][limbs][n] = sum_m in [m][2][limbs][n]
 void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st);
-// out = sum_i (K_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride)
+// out (+)= sum_i (K_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride)
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
-                   size_t xseg, const Mod *mods, int logN, hipStream_t st);
+                   size_t xseg, const Mod *mods, int logN, hipStream_t st, bool accumulate = false);
 // outs[g] = sum_i (K[g*m + i] mod q_l) * x_i for g < G <= 8 in one pass over the
 // inputs (x_i: [segs][limbs][n] with segment stride xseg[i]; outs: stride seg)
 void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,

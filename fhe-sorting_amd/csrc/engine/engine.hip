@@ -804,7 +804,13 @@ CtPtr Engine::mul_plain_sum(const std::vector<const Ciphertext *> &a, const std:
 
 // ct x ct with relinearisation and rescale.  b may be a single ciphertext
 // multiplied into every member of a (broadcast).
-CtPtr Engine::mul(const Ciphertext &a0, const Ciphertext &b0) {
+CtPtr Engine::mul(const Ciphertext &a0, const Ciphertext &b0) { return mul_add(a0, b0, {}, {}); }
+
+// a*b + sum_i c_i x_i with one rescale: the sum is formed at the product's
+// pre-rescale scale (the constants of linear_sum_to(xs, c, level+1)) and added
+// to the tensor's (d0, d1) before relinearisation (oracle: Context::mul_add).
+CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vector<const Ciphertext *> &xs,
+                      const std::vector<double> &cs, const Ciphertext *raw) {
     auto &I = *impl;
     if (a0.batch != b0.batch && b0.batch != 1) throw std::invalid_argument("mul: batch size mismatch");
     auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
@@ -820,10 +826,35 @@ CtPtr Engine::mul(const Ciphertext &a0, const Ciphertext &b0) {
     u64 *d01 = static_cast<u64 *>(d01m->p), *d2 = static_cast<u64 *>(d2m->p);
     dev::ew_tensor(d01, d2, a->data, b->data, (int)ell, B, 2 * ell * nn, b->batch == 1 ? 0 : 2 * ell * nn, MODS,
                    LOGN, ST);
+    if (!xs.empty()) {
+        const int target = a->level + 1;
+        const u64 qd = I.P.primes[I.P.L - target + 1];
+        std::map<size_t, std::pair<std::vector<const u64 *>, std::vector<int64_t>>> by_limbs;
+        for (size_t i = 0; i < xs.size(); ++i) {
+            if (xs[i]->level > a->level) throw std::invalid_argument("mul_add: summand level too high");
+            if (xs[i]->batch != B) throw std::invalid_argument("mul_add: batch size mismatch");
+            auto &g = by_limbs[xs[i]->limbs];
+            g.first.push_back(xs[i]->data);
+            g.second.push_back(host::const_to_target(cs[i], I.P.delta[target], qd, xs[i]->scale));
+        }
+        for (auto &kv : by_limbs)
+            dev::ew_linear_sum(d01, kv.second.first.data(), kv.second.second.data(), (int)kv.second.first.size(),
+                               (int)ell, 2 * B, ell * nn, kv.first * nn, MODS, LOGN, ST, true);
+        ctr.constmult += xs.size() * B;
+    }
+    if (raw) {
+        if (raw->level != a->level || raw->limbs != ell || raw->batch != B)
+            throw std::invalid_argument("mul_add: raw summand shape mismatch");
+        const size_t ln = ell * nn;
+        dev::ew_add(d01, d01, raw->data, (int)ell, 2 * B, dev::Seg{ln, ln, ln}, MODS, LOGN, ST);
+    }
     auto extm = I.modup(d2, ell, B, ell * nn);
     auto r = new_ct(a->level + 1, a->slots, I.P.delta[a->level + 1], ell - 1, B);
     I.mul_tail(static_cast<u64 *>(extm->p), d01, d2, ell, B, r->data);
     return r;
+}
+CtPtr Engine::mul_add_raw(const Ciphertext &a, const Ciphertext &b, const Ciphertext &raw) {
+    return mul_add(a, b, {}, {}, &raw);
 }
 CtPtr Engine::square(const Ciphertext &a) { return mul(a, a); }
 
@@ -906,7 +937,7 @@ CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std
 // gives the coefficients of output g.  Equal, word for word, to one
 // linear_sum_to per row, but each input is streamed once per 8 outputs.
 std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> &xs,
-                                          const std::vector<std::vector<double>> &c, int target) {
+                                          const std::vector<std::vector<double>> &c, int target, bool rescale) {
     auto &I = *impl;
     if (target > I.P.L) throw std::runtime_error("linear_sums_to: no levels left");
     if (xs.empty()) throw std::invalid_argument("linear_sums_to: no inputs");
@@ -936,9 +967,32 @@ std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> 
         for (int g = 0; g < G; ++g) op[g] = t + (size_t)g * segs * ell * nn;
         dev::ew_linear_sum_multi(op.data(), G, xp.data(), xseg.data(), K.data(), (int)m, (int)ell, segs, ell * nn,
                                  MODS, LOGN, ST);
+        if (!rescale) {  // raw sums at the pre-rescale scale, views into one allocation
+            for (int g = 0; g < G; ++g) {
+                auto r = std::make_shared<Ciphertext>();
+                r->mem = tm;
+                r->data = op[g];
+                r->level = target - 1;
+                r->slots = xs[0]->slots;
+                r->scale = I.P.delta[target] * (double)qd;
+                r->limbs = ell;
+                r->batch = B;
+                outs.push_back(r);
+            }
+            ctr.constmult += (u64)G * m * B;
+            continue;
+        }
+        auto rm = I.alloc((size_t)G * segs * (ell - 1) * nn * 8);  // all G outputs rescaled in one pass
+        I.rescale(t, ell, ell * nn, G * segs, static_cast<u64 *>(rm->p));
         for (int g = 0; g < G; ++g) {
-            auto r = new_ct(target, xs[0]->slots, I.P.delta[target], ell - 1, B);
-            I.rescale(op[g], ell, ell * nn, segs, r->data);
+            auto r = std::make_shared<Ciphertext>();
+            r->mem = rm;
+            r->data = static_cast<u64 *>(rm->p) + (size_t)g * segs * (ell - 1) * nn;
+            r->level = target;
+            r->slots = xs[0]->slots;
+            r->scale = I.P.delta[target];
+            r->limbs = ell - 1;
+            r->batch = B;
             outs.push_back(r);
         }
         ctr.constmult += (u64)G * m * B;

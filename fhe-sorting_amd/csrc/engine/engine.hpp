@@ -106,6 +106,11 @@ class Engine {
     // sum_i a_i * p_i with one rescale (masked sums of src/sort_algo.h:341-346, 573-577)
     CtPtr mul_plain_sum(const std::vector<const Ciphertext *> &a, const std::vector<const Plaintext *> &p);
     CtPtr mul(const Ciphertext &a, const Ciphertext &b);
+    // a*b + sum_i c_i x_i with one rescale (lazy rescaling of PS remainders)
+    CtPtr mul_add(const Ciphertext &a, const Ciphertext &b, const std::vector<const Ciphertext *> &xs,
+                  const std::vector<double> &cs, const Ciphertext *raw = nullptr);
+    // same with the sum already formed: raw = linear_sums_to(xs, {c}, level+1, false)[0]
+    CtPtr mul_add_raw(const Ciphertext &a, const Ciphertext &b, const Ciphertext &raw);
     CtPtr square(const Ciphertext &a);
     CtPtr rotate(const Ciphertext &a, long k);
     std::vector<CtPtr> rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks);
@@ -113,8 +118,9 @@ class Engine {
     CtPtr drop_to(const Ciphertext &a, int level);
     CtPtr linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c, int target);
     // several linear sums of the same inputs (PS leaves): one output per row of c
+    // (rescale = false: the raw sums at level target-1 and the pre-rescale scale, for mul_add_raw)
     std::vector<CtPtr> linear_sums_to(const std::vector<const Ciphertext *> &xs,
-                                      const std::vector<std::vector<double>> &c, int target);
+                                      const std::vector<std::vector<double>> &c, int target, bool rescale = true);
     CtPtr trivial_const(double c, int level, int slots, int batch = 1);
     CtPtr zero_like(int level, int slots, int batch = 1);
     // batches: stack (copies; equal levels), member view (no copy), member sum

@@ -152,7 +152,8 @@ int fhe_decompose(int N, const int32_t *rots, int nrot, int rotation, int wrap_n
 /* -------------------------------------------------------------- rank sort */
 /* DirectSort<N>::getSizeParameters (src/sort_algo.h:87-201); returns #rotations */
 int fhe_size_parameters(int N, int *mult_depth, int32_t *rots, int max_rots);
-/* u64 sum of `count` device words over all ranks, in place (RCCL, MPI, ...) */
+/* u64 sum of `count` device words over all ranks, in place (RCCL, MPI, ...).
+ * Called with the context stream drained; the sum must be complete on return. */
 typedef void (*fhe_allreduce_fn)(uint64_t *dev_data, uint64_t count, void *user);
 /* DirectSort<N>(cc, pk, rots, enc).{sort | constructRank | rotationIndexCheckN}
  * (src/sort_algo.h:752-774 / 368-506 / 658-750); mode 0 sort, 1 rank, 2 index

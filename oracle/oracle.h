@@ -202,6 +202,9 @@ class Context {
     // masked sum of products is rescaled once: src/sort_algo.h:341-346, 573-577)
     CtPtr mul_plain_sum(const std::vector<const Ciphertext *> &a, const std::vector<const Plaintext *> &p);
     CtPtr mul(const Ciphertext &a, const Ciphertext &b);             // relin + rescale
+    // a*b + sum_i c_i x_i with one rescale (lazy rescaling of PS remainders)
+    CtPtr mul_add(const Ciphertext &a, const Ciphertext &b, const std::vector<const Ciphertext *> &xs,
+                  const std::vector<double> &cs);
     CtPtr square(const Ciphertext &a);
     CtPtr rotate(const Ciphertext &a, long k);                       // keyed rotation
     std::vector<CtPtr> rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks);

@@ -113,10 +113,24 @@ struct PSEval {
             r[G - j] -= a[G + j];
         }
         CtPtr qv = eval(q, target - 1);
-        CtPtr prod = cc.mul(*qv, giant(G));
         trim(r);
         bool rzero = (r.size() == 1 && r[0] == 0.0);
-        if (rzero) return prod;
+        if (rzero) return cc.mul(*qv, giant(G));
+        const int dr = (int)r.size() - 1;
+        if (dr <= plan.B && dr >= 1) {
+            // the remainder is a leaf: fold its linear sum into the product
+            // before the product's rescale (one rescale instead of two)
+            std::vector<const Ciphertext *> xs;
+            std::vector<double> cs;
+            for (int i = 1; i <= dr; ++i)
+                if (r[i] != 0.0) {
+                    xs.push_back(T.at(i).get());
+                    cs.push_back(r[i]);
+                }
+            CtPtr out = cc.mul_add(*qv, giant(G), xs, cs);
+            return r[0] != 0.0 ? cc.add_const(*out, r[0]) : out;
+        }
+        CtPtr prod = cc.mul(*qv, giant(G));
         CtPtr rv = eval(r, target);
         return cc.add(*prod, *rv);
     }

@@ -952,7 +952,15 @@ CtPtr Context::rescale(const Ciphertext &a) {
     return r;
 }
 
-CtPtr Context::mul(const Ciphertext &a0, const Ciphertext &b0) {
+CtPtr Context::mul(const Ciphertext &a0, const Ciphertext &b0) { return mul_add(a0, b0, {}, {}); }
+
+// a*b + sum_i c_i x_i with ONE rescale: the linear sum is formed at the
+// product's pre-rescale scale Delta_{l}^2 = Delta_{l+1} q_removed (the same
+// integer constants linear_sum_to(xs, c, l+1) uses) and added to the tensor
+// before relinearisation; rescale(a*b + sum) then lands at Delta_{l+1}.
+// OpenFHE's Paterson-Stockmeyer also rescales such sums lazily.
+CtPtr Context::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vector<const Ciphertext *> &xs,
+                       const std::vector<double> &cs) {
     CtPtr a = clone(a0), b = std::make_shared<Ciphertext>(b0);
     match_levels(a, b);
     ctr.hmult++;
@@ -977,6 +985,28 @@ CtPtr Context::mul(const Ciphertext &a0, const Ciphertext &b0) {
                 o1[k] = mod_add(mod_mul(x0[k], y1[k], m), mod_mul(x1[k], y0[k], m), q);
             }
             o2[k] = mod_mul(x1[k], y1[k], m);
+        }
+    }
+    if (!xs.empty()) {
+        const int target = a->level + 1;
+        const double qd = (double)P.primes[P.L - target + 1];
+        std::vector<std::vector<u64>> Kmod(xs.size(), std::vector<u64>(ell));
+        for (size_t i = 0; i < xs.size(); ++i) {
+            if (xs[i]->level > a->level) throw std::invalid_argument("mul_add: summand level too high");
+            const i64 K = std::llround(cs[i] * P.delta[target] * qd / xs[i]->scale);
+            for (size_t l = 0; l < ell; ++l) Kmod[i][l] = signed_to_mod(K, P.primes[l]);
+        }
+        ctr.constmult += xs.size();
+#pragma omp parallel for
+        for (size_t l = 0; l < ell; ++l) {
+            const Modulus &m = tab[l].mod;
+            for (int p = 0; p < 2; ++p) {
+                u64 *o = t->poly(p, n) + l * n;
+                for (size_t i = 0; i < xs.size(); ++i) {
+                    const u64 *x = xs[i]->poly(p, n) + l * n;
+                    for (size_t k = 0; k < n; ++k) o[k] = mod_add(o[k], mod_mul(x[k], Kmod[i][l], m), m.q);
+                }
+            }
         }
     }
     std::vector<u64> ext, ks;
