@@ -67,12 +67,36 @@ class Dist:
         self.world = world
         self.rank = int(os.environ.get('RANK', '0'))
         self.local = int(os.environ.get('LOCAL_RANK', '0'))
+        try:  # one rank per GPU; ranks beyond the visible devices share them (rehearsals only)
+            import torch
+            ndev = torch.cuda.device_count()
+        except Exception:
+            ndev = 0
+        self.device = self.local % ndev if ndev > 0 else self.local
+        # RCCL needs distinct devices; a rehearsal with more ranks than GPUs
+        # exchanges the partial sums through host memory and gloo instead
+        self.rccl = world > 1 and (ndev == 0 or ndev >= int(os.environ.get('LOCAL_WORLD_SIZE', world)))
         self.pg = None
         if world > 1:
             import torch.distributed as dist
             os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
             dist.init_process_group('gloo', rank=self.rank, world_size=world)
             self.dist = dist
+
+    def host_allreduce(self):
+        import ctypes as C
+        import torch
+        hip = C.CDLL('libamdhip64.so')
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+
+        def fn(ptr, count, _user):
+            buf = np.empty(count, dtype=np.uint64)
+            if hip.hipMemcpy(buf.ctypes.data, C.cast(ptr, C.c_void_p), count * 8, 2) != 0:
+                raise RuntimeError('hipMemcpy D2H failed')
+            self.dist.all_reduce(torch.from_numpy(buf.view(np.int64)), op=self.dist.ReduceOp.SUM)
+            if hip.hipMemcpy(C.cast(ptr, C.c_void_p), buf.ctypes.data, count * 8, 1) != 0:
+                raise RuntimeError('hipMemcpy H2D failed')
+        return fn
 
     def barrier(self):
         if self.world > 1:
@@ -183,11 +207,14 @@ def main():
     depth, rots = F.size_parameters(N)
     cfg = sign_cfg(N)
     t0 = time.time()
-    ctx = F.Context(logN, depth, a.scale_bits, 60, 3, seed=a.seed, device=d.local)
+    ctx = F.Context(logN, depth, a.scale_bits, 60, 3, seed=a.seed, device=d.device)
     ctx.gen_rotation_keys(rots)
-    if d.world > 1:
+    allreduce = None
+    if d.world > 1 and d.rccl:
         uid = d.bcast_bytes(F.Context.comm_unique_id() if d.rank == 0 else None)
         ctx.comm_init(uid, d.rank, d.world)
+    elif d.world > 1:
+        allreduce = d.host_allreduce()
     x = np.random.default_rng(a.seed).permutation(N) / N  # getVectorWithMinDiff(N, 0, 1, 1/N)
     ct = ctx.encrypt(x, N)
     setup_s = time.time() - t0
@@ -195,7 +222,7 @@ def main():
 
     out = None
     for _ in range(a.warmup):
-        out = ctx.direct_sort(ct, N, rots, cfg, shard=shard)
+        out = ctx.direct_sort(ct, N, rots, cfg, shard=shard, allreduce=allreduce)
     device_sync(ctx)
     d.barrier()
     ctx.reset_counters()
@@ -203,12 +230,15 @@ def main():
     d.barrier()
     t = time.perf_counter()
     for _ in range(a.steps):
-        out = ctx.direct_sort(ct, N, rots, cfg, shard=shard)
+        out = ctx.direct_sort(ct, N, rots, cfg, shard=shard, allreduce=allreduce)
     device_sync(ctx)
     d.barrier()
     dt = time.perf_counter() - t
     dt = d.max(dt)
     cnt = ctx.counters()
+    peak_gb = ctx.pool_stats()['peak'] / 1e9
+    ctx.pool_trim()  # ranks idle at the final barrier hold no cache while rank 0 measures
+    d.barrier()
     hm_total = d.sum(cnt['hmult'])
     ks_total = d.sum(cnt['keyswitch'])
 
@@ -234,11 +264,13 @@ def main():
             'data': 'synthetic: seeded permutation of {k/N}, keys and encryption from a seeded PRNG',
             'config': {'workload': f'DirectSort N={N}, ringDim 2^{logN}, depth {depth}, scale 2^{a.scale_bits}, '
                                    f'{len(rots)} rotation keys, CompositeSign{cfg}, dnum 3',
-                       'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'parallelism': f'batch-shard x{d.world}'},
+                       'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'parallelism': f'batch-shard x{d.world}',
+                       'collective': 'none' if d.world == 1 else ('rccl' if d.rccl else 'host+gloo (more ranks than GPUs)')},
             'max_abs_err': max_err,
             'output_level': out.level,
             'hmult_per_sort': int(hm_total / a.steps),
             'setup_s': round(setup_s, 1),
+            'hbm_peak_gb_rank0': round(peak_gb, 1),
         }
         res['roofline'] = None
         if not a.no_roofline:

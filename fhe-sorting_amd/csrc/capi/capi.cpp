@@ -433,6 +433,18 @@ int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double
     });
 }
 
+int fhe_pool_trim(fhe_ctx *ctx) {
+    return guard([&] { ctx->eng->pool_trim(); });
+}
+int fhe_pool_stats(fhe_ctx *ctx, uint64_t *live, uint64_t *cached, uint64_t *peak) {
+    return guard([&] {
+        size_t l, c, p;
+        ctx->eng->pool_stats(l, c, p);
+        *live = l;
+        *cached = c;
+        *peak = p;
+    });
+}
 int fhe_kernel_clock_start(fhe_ctx *ctx) {
     return guard([&] { ctx->eng->kernel_clock_start(); });
 }

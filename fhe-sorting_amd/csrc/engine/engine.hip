@@ -29,7 +29,7 @@ using dev::Mod;
 struct Pool {
     std::mutex mu;
     std::multimap<size_t, void *> free_list;
-    size_t live = 0, cached = 0;
+    size_t live = 0, cached = 0, peak = 0;
     int device = 0;
     void *get(size_t bytes) {
         bytes = (bytes + 255) & ~(size_t)255;
@@ -41,6 +41,7 @@ struct Pool {
                 free_list.erase(it);
                 cached -= bytes;
                 live += bytes;
+                peak = std::max(peak, live);
                 return p;
             }
         }
@@ -52,6 +53,7 @@ struct Pool {
         }
         std::lock_guard<std::mutex> lk(mu);
         live += bytes;
+        peak = std::max(peak, live);
         return p;
     }
     void put(void *p, size_t bytes) {
@@ -1145,6 +1147,17 @@ struct EventClock final : dev::LaunchClock {
 };
 std::unique_ptr<EventClock> g_clock;
 }  // namespace
+
+void Engine::pool_trim() {
+    HIP_OK(hipStreamSynchronize(impl->st));
+    impl->pool->trim();
+}
+void Engine::pool_stats(size_t &live, size_t &cached, size_t &peak) const {
+    std::lock_guard<std::mutex> lk(impl->pool->mu);
+    live = impl->pool->live;
+    cached = impl->pool->cached;
+    peak = impl->pool->peak;
+}
 
 void Engine::kernel_clock_start() {
     if (dev::launch_clock()) throw std::runtime_error("kernel clock already running");

@@ -143,6 +143,9 @@ class Engine {
     // live per-launch clock over real work: between start and stop every NTT
     // pass is bracketed by HIP events on the engine stream; stop() returns JSON
     // {"kernel": {"launches": c, "ms": total, "bytes": total_algorithmic}, ...}
+    // device pool: release cached blocks; bytes live / cached / peak live
+    void pool_trim();
+    void pool_stats(size_t &live, size_t &cached, size_t &peak) const;
     void kernel_clock_start();
     std::string kernel_clock_stop();
 

@@ -102,6 +102,8 @@ _SIGS = {
     'fhe_time_kernel': (C.c_int, [vp, C.c_char_p, C.c_int, C.c_int, dp, dp]),
     'fhe_kernel_clock_start': (C.c_int, [vp]),
     'fhe_set_sort_stack': (C.c_int, [vp, C.c_int]),
+    'fhe_pool_trim': (C.c_int, [vp]),
+    'fhe_pool_stats': (C.c_int, [vp, u64p, u64p, u64p]),
     'fhe_ct_stack': (C.c_int, [vp, C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_void_p)]),
     'fhe_mul_plain_sum': (C.c_int, [vp, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int,
                                     C.POINTER(C.c_void_p)]),
@@ -365,6 +367,14 @@ class Context:
     def comm_init(self, uid, rank, world):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         _chk(lib().fhe_comm_init(self.h, buf, rank, world))
+
+    def pool_trim(self):
+        _chk(lib().fhe_pool_trim(self.h))
+
+    def pool_stats(self):
+        v = [C.c_uint64() for _ in range(3)]
+        _chk(lib().fhe_pool_stats(self.h, *[C.byref(x) for x in v]))
+        return {'live': v[0].value, 'cached': v[1].value, 'peak': v[2].value}
 
     def set_sort_stack(self, m):
         _chk(lib().fhe_set_sort_stack(self.h, m))

@@ -191,6 +191,10 @@ void *fhe_stream(fhe_ctx *ctx);
  * "modup_convert") with HIP events on the context stream, shaped as a key
  * switch at `limbs` Q limbs: average ms and algorithmic bytes/launch */
 int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double *avg_ms, double *bytes);
+/* device memory pool of the context: release cached blocks to HIP; bytes in
+ * use, cached, and the peak in use since creation */
+int fhe_pool_trim(fhe_ctx *ctx);
+int fhe_pool_stats(fhe_ctx *ctx, uint64_t *live, uint64_t *cached, uint64_t *peak);
 /* live kernel clock over real work: after start, every NTT pass launched by
  * this process is bracketed by HIP events on its stream; stop writes JSON
  * {"<kernel>": {"launches": c, "ms": total, "bytes": algorithmic}, ...} into
