@@ -454,60 +454,6 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const
         dst[(size_t)i * n + k] = reduce4(a4, mi);
     }
 }
-// out_i = (acc_i + d_i P - corr_i) * (P q_last)^-1, i < ell-1, NTT form.
-// grid: x = n / (2 NT), y = i, z = seg
-__global__ __launch_bounds__(NT) void k_mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr,
-                                                        size_t seg_out, size_t seg_acc, size_t seg_d,
-                                                        const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
-                                                        const u64 *pmod_s, const Mod *mods, int logN) {
-    const size_t n = (size_t)1 << logN;
-    const int l = blockIdx.y, s = blockIdx.z;
-    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
-    if (k >= n) return;
-    const u64 q = mods[l].q;
-    const size_t lo = (size_t)l * n + k;
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(acc + (size_t)s * seg_acc + lo);
-    const ulonglong2 dd = *reinterpret_cast<const ulonglong2 *>(d + (size_t)s * seg_d + lo);
-    const ulonglong2 c = *reinterpret_cast<const ulonglong2 *>(corr + (size_t)s * seg_out + lo);
-    const u64 w = pmod[l], ws = pmod_s[l], z = pqlinv[l], zs = pqlinv_s[l];
-    ulonglong2 r;
-    r.x = mul_shoup(sub_mod(add_mod(x.x, mul_shoup(dd.x, w, ws, q), q), c.x, q), z, zs, q);
-    r.y = mul_shoup(sub_mod(add_mod(x.y, mul_shoup(dd.y, w, ws, q), q), c.y, q), z, zs, q);
-    *reinterpret_cast<ulonglong2 *>(out + (size_t)s * seg_out + lo) = r;
-}
-
-// -------------------------------------------------------------- rescale ----
-// grid: x = n / NT, y = i < ell-1, z = segment
-__global__ __launch_bounds__(NT) void k_rescale_prep(u64 *tmp, const u64 *last, int ell, size_t seg_last,
-                                                     size_t seg_tmp, const Mod *mods, int logN) {
-    const size_t n = (size_t)1 << logN;
-    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
-    if (k >= n) return;
-    const int i = blockIdx.y, s = blockIdx.z;
-    const u64 ql = mods[ell - 1].q;
-    const Mod mi = mods[i];
-    const u64 c = last[(size_t)s * seg_last + k];
-    u64 v = reduce64(c, mi);
-    if (c > (ql >> 1)) v = sub_mod(v, reduce64(ql, mi), mi.q);
-    tmp[(size_t)s * seg_tmp + (size_t)i * n + k] = v;
-}
-__global__ __launch_bounds__(NT) void k_rescale_finish(u64 *out, const u64 *in, const u64 *tmp, size_t seg_out,
-                                                       size_t seg_in, size_t seg_tmp, const u64 *qlinv,
-                                                       const u64 *qlinv_s, const Mod *mods, int logN) {
-    const size_t n = (size_t)1 << logN;
-    const int l = blockIdx.y, s = blockIdx.z;
-    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
-    if (k >= n) return;
-    const u64 q = mods[l].q, w = qlinv[l], wp = qlinv_s[l];
-    const size_t lo = (size_t)l * n + k;
-    const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(in + (size_t)s * seg_in + lo);
-    const ulonglong2 t = *reinterpret_cast<const ulonglong2 *>(tmp + (size_t)s * seg_tmp + lo);
-    ulonglong2 r;
-    r.x = mul_shoup(sub_mod(x.x, t.x, q), w, wp, q);
-    r.y = mul_shoup(sub_mod(x.y, t.y, q), w, wp, q);
-    *reinterpret_cast<ulonglong2 *>(out + (size_t)s * seg_out + lo) = r;
-}
-
 inline dim3 ew_grid(int logN, int limbs, int segs) {
     const size_t n = (size_t)1 << logN;
     return dim3((unsigned)((n / 2 + NT - 1) / NT), (unsigned)limbs, (unsigned)segs);
@@ -695,14 +641,6 @@ void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, 
                        seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, mods, logN);
     });
 }
-void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, int ell, int segs, size_t seg_out,
-                     size_t seg_acc, size_t seg_d, const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
-                     const u64 *pmod_s, const Mod *mods, int logN, hipStream_t st) {
-    if (ell <= 1) return;
-    const double B = 8.0 * 4 * segs * (double)(ell - 1) * ((size_t)1 << logN);
-    launch_clocked("k_mul_tail_finish", B, k_mul_tail_finish, ew_grid(logN, ell - 1, segs), dim3(NT), st, out, acc, d,
-                   corr, seg_out, seg_acc, seg_d, pqlinv, pqlinv_s, pmod, pmod_s, mods, logN);
-}
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
                      const u64 *phinv, const u64 *phinv_s, const u64 *phat, const Mod *mods, int logN,
                      hipStream_t st) {
@@ -720,21 +658,5 @@ void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, i
     launch_clocked("k_moddown_finish", B, k_moddown_finish, ew_grid(logN, ell, segs), dim3(NT), st, out, acc, conv, add,
                    seg_out, seg_acc, seg_add, pinv, pinv_s, mods, logN);
 }
-void rescale_prep(u64 *tmp, const u64 *last, int ell, int segs, size_t seg_last, size_t seg_tmp, const Mod *mods,
-                  int logN, hipStream_t st) {
-    if (ell <= 1) return;
-    const double B = 8.0 * segs * (double)ell * ((size_t)1 << logN);
-    launch_clocked("k_rescale_prep", B, k_rescale_prep, pt_grid(logN, ell - 1, segs), dim3(NT), st, tmp, last, ell,
-                   seg_last, seg_tmp, mods, logN);
-}
-void rescale_finish(u64 *out, const u64 *in, const u64 *tmp, int ell, int segs, size_t seg_out, size_t seg_in,
-                    size_t seg_tmp, const u64 *qlinv, const u64 *qlinv_s, const Mod *mods, int logN,
-                    hipStream_t st) {
-    if (ell <= 1) return;
-    const double B = 8.0 * 3 * segs * (double)(ell - 1) * ((size_t)1 << logN);
-    launch_clocked("k_rescale_finish", B, k_rescale_finish, ew_grid(logN, ell - 1, segs), dim3(NT), st, out, in, tmp,
-                   seg_out, seg_in, seg_tmp, qlinv, qlinv_s, mods, logN);
-}
-
 }  // namespace dev
 }  // namespace fhe

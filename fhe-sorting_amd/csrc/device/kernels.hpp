@@ -56,6 +56,26 @@ void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
                  hipStream_t st);
 void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
                  hipStream_t st);
+// Operands of the fused forward NTTs (ntt.hip): the column pass can load the
+// centred lift of a coefficient-form limb; the row pass can finish a rescale
+// or an HMult tail in its store instead of writing the transform back.
+struct NttFuse {
+    const u64 *last = nullptr;  // [segs][n] coefficient-form limb to lift (prime lastp)
+    size_t seg_last = 0;
+    int lastp = 0;
+    u64 *out = nullptr;  // [segs][limbs][n] result
+    size_t seg_out = 0;
+    const u64 *x = nullptr;  // rescale: the input; HMult: the accumulators
+    size_t seg_x = 0;
+    const u64 *d = nullptr;  // HMult: d01
+    size_t seg_d = 0;
+    const u64 *c1 = nullptr, *c1s = nullptr;  // per limb: q_last^-1 (rescale) or (P q_last)^-1 (HMult)
+    const u64 *c2 = nullptr, *c2s = nullptr;  // per limb: P mod q_i (HMult)
+};
+// rescale of `segs` polys: out = (x - NTT(lift(last))) * c1 over `limbs` = ell-1 limbs (tmp: scratch)
+void ntt_forward_rescale(u64 *tmp, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
+// HMult tail: out = (x + d * c2 - NTT(corr)) * c1 (corr is overwritten by the first pass only)
+void ntt_forward_multail(u64 *corr, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
 // forward NTT of `count` limbs scattered in each of `segs` segments: limb y
 // of segment z sits at data + z * seg + smap[y] * n and belongs to prime
 // pmap[y] (ModUp: every digit of every member at once)
@@ -134,10 +154,6 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                              const u64 *pinv_s, const u64 *pmod, const Mod *mods, int logN, hipStream_t st);
-// out [segs][ell-1][n] = (acc + d * P - corr) * (P q_{ell-1})^-1  (pqlinv: the row for this ell)
-void mul_tail_finish(u64 *out, const u64 *acc, const u64 *d, const u64 *corr, int ell, int segs, size_t seg_out,
-                     size_t seg_acc, size_t seg_d, const u64 *pqlinv, const u64 *pqlinv_s, const u64 *pmod,
-                     const u64 *pmod_s, const Mod *mods, int logN, hipStream_t st);
 // conv[s][i][k] = sum_k' (pc[s][k'] * phinv_k') * phat[i][k'] mod q_i  for i < ell
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
                      const u64 *phinv, const u64 *phinv_s, const u64 *phat, const Mod *mods, int logN,
@@ -145,15 +161,6 @@ void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t se
 // out[s][i] = (acc[s][i] - conv[s][i]) * Pinv_i (+ add[s/2][i] on even s, i.e. c0 of each member)
 void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,
                     size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s, const Mod *mods, int logN,
-                    hipStream_t st);
-
-// ------------------------------------------------------------------ rescale
-// tmp[s][i][k] = centred(last[s][k]) mod q_i for i < ell-1
-void rescale_prep(u64 *tmp, const u64 *last, int ell, int segs, size_t seg_last, size_t seg_tmp, const Mod *mods,
-                  int logN, hipStream_t st);
-// out[s][i] = (in[s][i] - tmp[s][i]) * qlinv_i
-void rescale_finish(u64 *out, const u64 *in, const u64 *tmp, int ell, int segs, size_t seg_out, size_t seg_in,
-                    size_t seg_tmp, const u64 *qlinv, const u64 *qlinv_s, const Mod *mods, int logN,
                     hipStream_t st);
 
 // u64 all-reduce fix-up: x mod q_l per limb

@@ -75,11 +75,19 @@ __device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0,
     return x >= q ? x - q : x;
 }
 
+// Fused forward modes (MODE): 0 plain; 1 column pass loads the centred lift
+// of one coefficient-form limb (`last`, prime lastp) instead of `data`
+// (rescale: the lifted limb is never materialised per prime); 2 row pass
+// stores out = (x - NTT) * c1 (rescale finish); 3 row pass stores
+// out = (x + d * c2 - NTT) * c1 (fused ModDown+rescale finish of an HMult).
+// Modes 2/3 do not write `data` back.
+enum { NTT_PLAIN = 0, NTT_LIFT = 1, NTT_RESCALE = 2, NTT_MULTAIL = 3 };
+
 // COLS: the transform index is a column `col`, element idx sits at idx * 2^k2 + col.
 // ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
-template <int PB, int EB, bool COLS>
+template <int PB, int EB, bool COLS, int MODE>
 __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
-                                                  NttTables Tb) {
+                                                  NttTables Tb, NttFuse F) {
     constexpr int E = 1 << EB;          // coefficients per lane
     constexpr int RB = PB - EB;         // bits of round 2
     constexpr int T = 1 << RB;          // lanes per transform
@@ -113,11 +121,24 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
 
     u64 x[E];
     // ---- load, layout L1: idx = t + T * r
+    if (MODE == NTT_LIFT) {
+        const Mod mp = Tb.mods[p];
+        const u64 ql = Tb.mods[F.lastp].q, qlm = reduce64(ql, mp);
+        const u64 *src = F.last + (size_t)blockIdx.x * F.seg_last;
 #pragma unroll
-    for (int r = 0; r < E; ++r) {
-        const int idx = t + T * r;
-        const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
-        x[r] = valid ? a[off] : 0;
+        for (int r = 0; r < E; ++r) {
+            const int idx = t + T * r;
+            const u64 c = valid ? src[(size_t)idx * ((size_t)1 << k2) + tid_global] : 0;
+            const u64 v = reduce64(c, mp);
+            x[r] = c > (ql >> 1) ? sub_mod(v, qlm, q) : v;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int idx = t + T * r;
+            const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
+            x[r] = valid ? a[off] : 0;
+        }
     }
     // ---- round 1: local stages 0..EB-1
 #pragma unroll
@@ -175,11 +196,22 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
             for (int r = 0; r < T; ++r)
                 tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] = canon4(x[g * T + r], q, q2);
         __syncthreads();
+        const size_t z = blockIdx.x, lo = (size_t)limb * n + tid_global * LEN;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int idx = t + T * r;
             const u64 v = tile[lds_at<PB, NB, COLS>(tr, idx)];
-            if (valid) a[tid_global * LEN + idx] = v;
+            if (!valid) continue;
+            if (MODE == NTT_RESCALE) {
+                const u64 xin = F.x[z * F.seg_x + lo + idx];
+                F.out[z * F.seg_out + lo + idx] = mul_shoup(sub_mod(xin, v, q), F.c1[limb], F.c1s[limb], q);
+            } else if (MODE == NTT_MULTAIL) {
+                const u64 acc = F.x[z * F.seg_x + lo + idx], dd = F.d[z * F.seg_d + lo + idx];
+                const u64 tt = add_mod(acc, mul_shoup(dd, F.c2[limb], F.c2s[limb], q), q);
+                F.out[z * F.seg_out + lo + idx] = mul_shoup(sub_mod(tt, v, q), F.c1[limb], F.c1s[limb], q);
+            } else {
+                a[tid_global * LEN + idx] = v;
+            }
         }
     }
 }
@@ -295,9 +327,9 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
     }
 }
 
-template <int PB, int EB, bool COLS, bool FWD>
+template <int PB, int EB, bool COLS, bool FWD, int MODE>
 void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap, const NttTables &T,
-                 hipStream_t st) {
+                 const NttFuse &F, hipStream_t st) {
     constexpr int NB = NTB >> (PB - EB);
     const int count = 1 << (T.logN - PB);  // columns (COLS) or rows (ROWS)
     const dim3 grid((unsigned)segs, (unsigned)((count + NB - 1) / NB), (unsigned)limbs);
@@ -305,37 +337,39 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (clk) clk->events(e0, e1);
     if (FWD)
-        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
-                              T);
+        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
+                              T.logN, T, F);
     else
-        hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
-                              T);
+        hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
+                              T.logN, T);
     if (clk) {
         // same spelling as the demangled symbol rocprofv3 prints, plus the caller tag
         static const std::string base = std::string(FWD ? "k_ntt_fwd<" : "k_ntt_inv<") + std::to_string(PB) + ", " +
-                                        std::to_string(EB) + (COLS ? ", true>" : ", false>");
+                                        std::to_string(EB) + (COLS ? ", true" : ", false") +
+                                        (FWD ? ", " + std::to_string(MODE) : std::string()) + ">";
         static std::map<const char *, std::string> names;
         const char *ph = launch_phase();
         auto it = names.find(ph);
         if (it == names.end()) it = names.emplace(ph, ph ? base + "@" + ph : base).first;
-        // one read + one write of every limb touched
-        clk->record(it->second.c_str(), 2.0 * 8.0 * (double)limbs * segs * ((size_t)1 << T.logN));
+        // one read + one write of every limb touched (fused epilogues: + the extra operands)
+        const double extra = MODE == NTT_RESCALE ? 1.0 : MODE == NTT_MULTAIL ? 2.0 : 0.0;
+        clk->record(it->second.c_str(), (2.0 + extra) * 8.0 * (double)limbs * segs * ((size_t)1 << T.logN));
     }
 }
 
 // pass bits -> (PB, EB): EB = ceil(PB / 2)
-template <bool COLS, bool FWD>
+template <bool COLS, bool FWD, int MODE>
 void dispatch(int PB, u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap,
-              const NttTables &T, hipStream_t st) {
+              const NttTables &T, const NttFuse &F, hipStream_t st) {
     switch (PB) {
-    case 2: launch_pass<2, 1, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
-    case 3: launch_pass<3, 2, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
-    case 4: launch_pass<4, 2, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
-    case 5: launch_pass<5, 3, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
-    case 6: launch_pass<6, 3, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
-    case 7: launch_pass<7, 4, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
-    case 8: launch_pass<8, 4, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
-    case 9: launch_pass<9, 5, COLS, FWD>(data, limbs, segs, seg, pmap, smap, T, st); break;
+    case 2: launch_pass<2, 1, COLS, FWD, MODE>(data, limbs, segs, seg, pmap, smap, T, F, st); break;
+    case 3: launch_pass<3, 2, COLS, FWD, MODE>(data, limbs, segs, seg, pmap, smap, T, F, st); break;
+    case 4: launch_pass<4, 2, COLS, FWD, MODE>(data, limbs, segs, seg, pmap, smap, T, F, st); break;
+    case 5: launch_pass<5, 3, COLS, FWD, MODE>(data, limbs, segs, seg, pmap, smap, T, F, st); break;
+    case 6: launch_pass<6, 3, COLS, FWD, MODE>(data, limbs, segs, seg, pmap, smap, T, F, st); break;
+    case 7: launch_pass<7, 4, COLS, FWD, MODE>(data, limbs, segs, seg, pmap, smap, T, F, st); break;
+    case 8: launch_pass<8, 4, COLS, FWD, MODE>(data, limbs, segs, seg, pmap, smap, T, F, st); break;
+    case 9: launch_pass<9, 5, COLS, FWD, MODE>(data, limbs, segs, seg, pmap, smap, T, F, st); break;
     default: break;
     }
 }
@@ -354,23 +388,42 @@ const char *&launch_phase() {
 void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
     if (limbs <= 0 || segs <= 0) return;
     const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
-    dispatch<true, true>(k1, data, limbs, segs, seg, pmap, nullptr, T, st);
-    dispatch<false, true>(k2, data, limbs, segs, seg, pmap, nullptr, T, st);
+    const NttFuse F;
+    dispatch<true, true, NTT_PLAIN>(k1, data, limbs, segs, seg, pmap, nullptr, T, F, st);
+    dispatch<false, true, NTT_PLAIN>(k2, data, limbs, segs, seg, pmap, nullptr, T, F, st);
 }
 
 void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
     if (limbs <= 0 || segs <= 0) return;
     const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
-    dispatch<false, false>(k2, data, limbs, segs, seg, pmap, nullptr, T, st);
-    dispatch<true, false>(k1, data, limbs, segs, seg, pmap, nullptr, T, st);
+    const NttFuse F;
+    dispatch<false, false, NTT_PLAIN>(k2, data, limbs, segs, seg, pmap, nullptr, T, F, st);
+    dispatch<true, false, NTT_PLAIN>(k1, data, limbs, segs, seg, pmap, nullptr, T, F, st);
 }
 
 void ntt_forward_mapped(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,
                         const NttTables &T, hipStream_t st) {
     if (count <= 0 || segs <= 0) return;
     const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
-    dispatch<true, true>(k1, data, count, segs, seg, pmap, smap, T, st);
-    dispatch<false, true>(k2, data, count, segs, seg, pmap, smap, T, st);
+    const NttFuse F;
+    dispatch<true, true, NTT_PLAIN>(k1, data, count, segs, seg, pmap, smap, T, F, st);
+    dispatch<false, true, NTT_PLAIN>(k2, data, count, segs, seg, pmap, smap, T, F, st);
+}
+
+void ntt_forward_rescale(u64 *tmp, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
+    const size_t seg = (size_t)limbs << T.logN;
+    dispatch<true, true, NTT_LIFT>(k1, tmp, limbs, segs, seg, nullptr, nullptr, T, F, st);
+    dispatch<false, true, NTT_RESCALE>(k2, tmp, limbs, segs, seg, nullptr, nullptr, T, F, st);
+}
+
+void ntt_forward_multail(u64 *corr, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
+    const size_t seg = (size_t)limbs << T.logN;
+    dispatch<true, true, NTT_PLAIN>(k1, corr, limbs, segs, seg, nullptr, nullptr, T, F, st);
+    dispatch<false, true, NTT_MULTAIL>(k2, corr, limbs, segs, seg, nullptr, nullptr, T, F, st);
 }
 
 }  // namespace dev

@@ -228,9 +228,19 @@ struct Engine::Impl {
         u64 *corr = static_cast<u64 *>(corrm->p);
         dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, segs, phinv,
                                      phinv_s, phat, pinv, pinv_s, pmod, mods, P.logN, st);
-        dev::ntt_forward(corr, (int)(ell - 1), segs, (ell - 1) * nn, nullptr, T, st);
-        dev::mul_tail_finish(out, acc, d01, corr, (int)ell, segs, (ell - 1) * nn, W * nn, ell * nn,
-                             pqlinv + ell * P.nq(), pqlinv_s + ell * P.nq(), pmod, pmod_s, mods, P.logN, st);
+        // forward NTT of corr whose row pass finishes (acc + d P - corr) (P q_last)^-1 into `out`
+        dev::NttFuse F;
+        F.out = out;
+        F.seg_out = (ell - 1) * nn;
+        F.x = acc;
+        F.seg_x = W * nn;
+        F.d = d01;
+        F.seg_d = ell * nn;
+        F.c1 = pqlinv + ell * P.nq();
+        F.c1s = pqlinv_s + ell * P.nq();
+        F.c2 = pmod;
+        F.c2s = pmod_s;
+        dev::ntt_forward_multail(corr, (int)(ell - 1), segs, F, T, st);
     }
     // out [segs][ell-1][n] from in [segs][ell][n] with input segment stride seg_in
     void rescale(const u64 *in, size_t ell, size_t seg_in, int segs, u64 *out) {
@@ -241,12 +251,22 @@ struct Engine::Impl {
         HIP_OK(hipMemcpy2DAsync(last, nn * 8, in + (ell - 1) * nn, seg_in * 8, nn * 8, (size_t)segs,
                                 hipMemcpyDeviceToDevice, st));
         dev::ntt_inverse(last, 1, segs, nn, ext(ell) + (ell - 1), T, st);
+        if (ell <= 1) return;
         auto tmpm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *tmp = static_cast<u64 *>(tmpm->p);
-        dev::rescale_prep(tmp, last, (int)ell, segs, nn, (ell - 1) * nn, mods, P.logN, st);
-        dev::ntt_forward(tmp, (int)(ell - 1), segs, (ell - 1) * nn, nullptr, T, st);
-        dev::rescale_finish(out, in, tmp, (int)ell, segs, (ell - 1) * nn, seg_in, (ell - 1) * nn,
-                            qlinv + ell * P.nq(), qlinv_s + ell * P.nq(), mods, P.logN, st);
+        // column pass lifts `last` into every prime on load; row pass finishes
+        // (in - NTT(lift)) q_last^-1 straight into `out`
+        dev::NttFuse F;
+        F.last = last;
+        F.seg_last = nn;
+        F.lastp = (int)(ell - 1);
+        F.out = out;
+        F.seg_out = (ell - 1) * nn;
+        F.x = in;
+        F.seg_x = seg_in;
+        F.c1 = qlinv + ell * P.nq();
+        F.c1s = qlinv_s + ell * P.nq();
+        dev::ntt_forward_rescale(tmp, (int)(ell - 1), segs, F, T, st);
     }
 };
 
