@@ -106,19 +106,23 @@ __device__ __forceinline__ void mac4(Acc4 &s, Split30 a, Split30 b) {
     s.s10 += (u64)a.hi * b.lo;
     s.s11 += (u64)a.hi * b.hi;
 }
-// s00 + (s01 + s10) 2^30 + s11 2^60 mod q
-__device__ __forceinline__ u64 reduce4(const Acc4 &s, const Mod &m) {
+// r += s00 + (s01 + s10) 2^30 + s11 2^60  (exact, 128-bit)
+__device__ __forceinline__ void fold4(Acc128 &r, const Acc4 &s) {
     const u64 mid = s.s01 + s.s10;
     const u64 mc = mid < s.s01;  // carry of the middle sum (bit 64)
-    Acc128 r;
-    r.lo = s.s00;
-    r.hi = 0;
+    r.lo += s.s00;
+    r.hi += (r.lo < s.s00);
     const u64 ml = mid << 30;
     r.lo += ml;
     r.hi += (mid >> 34) + (mc << 30) + (r.lo < ml);
     const u64 tl = s.s11 << 60;
     r.lo += tl;
     r.hi += (s.s11 >> 4) + (r.lo < tl);
+}
+// s00 + (s01 + s10) 2^30 + s11 2^60 mod q
+__device__ __forceinline__ u64 reduce4(const Acc4 &s, const Mod &m) {
+    Acc128 r;
+    fold4(r, s);
     return reduce128(r, m);
 }
 
