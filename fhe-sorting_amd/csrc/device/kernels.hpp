@@ -71,7 +71,13 @@ struct NttFuse {
     size_t seg_d = 0;
     const u64 *c1 = nullptr, *c1s = nullptr;  // per limb: q_last^-1 (rescale) or (P q_last)^-1 (HMult)
     const u64 *c2 = nullptr, *c2s = nullptr;  // per limb: P mod q_i (HMult)
+    const u64 *src = nullptr;  // inverse: out-of-place input of the first pass
+    size_t seg_src = 0;
+    int64_t scalar = 0;  // rescale: multiply the input by this integer first (0 = none)
 };
+// inverse NTT reading the input from `src` (segment z, limb l at src + z*seg_src + l*n), writing dst
+void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int segs, size_t seg, const int *pmap,
+                      const NttTables &T, hipStream_t st);
 // rescale of `segs` polys: out = (x - NTT(lift(last))) * c1 over `limbs` = ell-1 limbs (tmp: scratch)
 void ntt_forward_rescale(u64 *tmp, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
 // HMult tail: out = (x + d * c2 - NTT(corr)) * c1 (corr is overwritten by the first pass only)

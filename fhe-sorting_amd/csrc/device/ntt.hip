@@ -70,6 +70,11 @@ __device__ __forceinline__ void gs_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2, u6
     x = s >= q2 ? s - q2 : s;
     y = shoup_fold(u + q2 - v, w.x, w.y, nq);
 }
+__device__ __forceinline__ u64 smod64(int64_t v, const Mod &m) {  // signed integer -> [0, q)
+    if (v >= 0) return reduce64((u64)v, m);
+    const u64 r = reduce64((u64)0 - (u64)v, m);
+    return r ? m.q - r : 0;
+}
 __device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0, q)
     x = x >= q2 ? x - q2 : x;
     return x >= q ? x - q : x;
@@ -122,13 +127,15 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
     u64 x[E];
     // ---- load, layout L1: idx = t + T * r
     if (MODE == NTT_LIFT) {
-        const Mod mp = Tb.mods[p];
-        const u64 ql = Tb.mods[F.lastp].q, qlm = reduce64(ql, mp);
+        const Mod mp = Tb.mods[p], ml = Tb.mods[F.lastp];
+        const u64 ql = ml.q, qlm = reduce64(ql, mp);
+        const u64 kl = F.scalar ? smod64(F.scalar, ml) : 0;  // K mod q_last (scaled rescale)
         const u64 *src = F.last + (size_t)blockIdx.x * F.seg_last;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int idx = t + T * r;
-            const u64 c = valid ? src[(size_t)idx * ((size_t)1 << k2) + tid_global] : 0;
+            u64 c = valid ? src[(size_t)idx * ((size_t)1 << k2) + tid_global] : 0;
+            if (F.scalar) c = mul_barrett(c, kl, ml);
             const u64 v = reduce64(c, mp);
             x[r] = c > (ql >> 1) ? sub_mod(v, qlm, q) : v;
         }
@@ -197,6 +204,9 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
                 tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] = canon4(x[g * T + r], q, q2);
         __syncthreads();
         const size_t z = blockIdx.x, lo = (size_t)limb * n + tid_global * LEN;
+        const Mod mp = Tb.mods[p];
+        // scaled rescale: out = (K x - v) q_last^-1 = x (K q_last^-1) - v q_last^-1
+        const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, mp), F.c1[limb], F.c1s[limb], q) : 0;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int idx = t + T * r;
@@ -204,7 +214,9 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
             if (!valid) continue;
             if (MODE == NTT_RESCALE) {
                 const u64 xin = F.x[z * F.seg_x + lo + idx];
-                F.out[z * F.seg_out + lo + idx] = mul_shoup(sub_mod(xin, v, q), F.c1[limb], F.c1s[limb], q);
+                F.out[z * F.seg_out + lo + idx] =
+                    F.scalar ? sub_mod(mul_barrett(xin, kq, mp), mul_shoup(v, F.c1[limb], F.c1s[limb], q), q)
+                             : mul_shoup(sub_mod(xin, v, q), F.c1[limb], F.c1s[limb], q);
             } else if (MODE == NTT_MULTAIL) {
                 const u64 acc = F.x[z * F.seg_x + lo + idx], dd = F.d[z * F.seg_d + lo + idx];
                 const u64 tt = add_mod(acc, mul_shoup(dd, F.c2[limb], F.c2s[limb], q), q);
@@ -219,9 +231,11 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
 // Inverse: global GS stage sg has pair distance 2^sg, twiddle psi^-brev(m + i),
 // m = n >> (sg + 1), i = j >> (sg + 1).  ROWS covers sg in [0, PB) (low bits),
 // COLS covers sg in [logN - PB, logN) and multiplies by n^-1 on the way out.
+// F.src (optional): read the input from there instead (out-of-place first
+// pass; segment z, limb l at F.src + z * F.seg_src + l * n)
 template <int PB, int EB, bool COLS>
 __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
-                                                  NttTables Tb) {
+                                                  NttTables Tb, NttFuse F) {
     constexpr int E = 1 << EB;
     constexpr int RB = PB - EB;
     constexpr int T = 1 << RB;
@@ -253,6 +267,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
     const bool valid = tid_global < ((size_t)1 << (logN - PB));
     const int SG0 = COLS ? logN - PB : 0;  // global GS stage of local stage 0
 
+    const u64 *ain = F.src ? F.src + (size_t)blockIdx.x * F.seg_src + (size_t)limb * n : a;
     u64 x[E];
     // ---- load, layout L2 (low bits within a lane group).  The ROWS pass's
     // per-lane runs of T consecutive words are read 16 B at a time (L1 serves
@@ -264,7 +279,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
             for (int r = 0; r < T; ++r) {
                 const int idx = (t * G + g) * T + r;
                 const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
-                x[g * T + r] = valid ? a[off] : 0;
+                x[g * T + r] = valid ? ain[off] : 0;
             }
     } else {
 #pragma unroll
@@ -272,7 +287,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
 #pragma unroll
             for (int r = 0; r < T; r += 2) {
                 const int idx = (t * G + g) * T + r;
-                const ulonglong2 v = valid ? *reinterpret_cast<const ulonglong2 *>(a + tid_global * LEN + idx)
+                const ulonglong2 v = valid ? *reinterpret_cast<const ulonglong2 *>(ain + tid_global * LEN + idx)
                                            : make_ulonglong2(0, 0);
                 x[g * T + r] = v.x;
                 x[g * T + r + 1] = v.y;
@@ -341,7 +356,7 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
                               T.logN, T, F);
     else
         hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
-                              T.logN, T);
+                              T.logN, T, F);
     if (clk) {
         // same spelling as the demangled symbol rocprofv3 prints, plus the caller tag
         static const std::string base = std::string(FWD ? "k_ntt_fwd<" : "k_ntt_inv<") + std::to_string(PB) + ", " +
@@ -399,6 +414,18 @@ void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     const NttFuse F;
     dispatch<false, false, NTT_PLAIN>(k2, data, limbs, segs, seg, pmap, nullptr, T, F, st);
     dispatch<true, false, NTT_PLAIN>(k1, data, limbs, segs, seg, pmap, nullptr, T, F, st);
+}
+
+void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int segs, size_t seg, const int *pmap,
+                      const NttTables &T, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
+    NttFuse F;
+    F.src = src;
+    F.seg_src = seg_src;
+    dispatch<false, false, NTT_PLAIN>(k2, dst, limbs, segs, seg, pmap, nullptr, T, F, st);
+    const NttFuse G;
+    dispatch<true, false, NTT_PLAIN>(k1, dst, limbs, segs, seg, pmap, nullptr, T, G, st);
 }
 
 void ntt_forward_mapped(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,

@@ -157,12 +157,7 @@ struct Engine::Impl {
         const int digits = P.digits_at(ell);
         auto coef = alloc((size_t)members * ell * nn * 8);
         u64 *c = static_cast<u64 *>(coef->p);
-        if (d_stride == ell * nn || members == 1)
-            HIP_OK(hipMemcpyAsync(c, d, (size_t)members * ell * nn * 8, hipMemcpyDeviceToDevice, st));
-        else
-            HIP_OK(hipMemcpy2DAsync(c, ell * nn * 8, d, d_stride * 8, ell * nn * 8, (size_t)members,
-                                    hipMemcpyDeviceToDevice, st));
-        dev::ntt_inverse(c, (int)ell, members, ell * nn, nullptr, T, st);
+        dev::ntt_inverse_from(c, d, d_stride, (int)ell, members, ell * nn, nullptr, T, st);
         const size_t es = (size_t)digits * W * nn;
         auto extm = alloc((size_t)members * es * 8);
         u64 *e = static_cast<u64 *>(extm->p);
@@ -242,15 +237,14 @@ struct Engine::Impl {
         F.c2s = pmod_s;
         dev::ntt_forward_multail(corr, (int)(ell - 1), segs, F, T, st);
     }
-    // out [segs][ell-1][n] from in [segs][ell][n] with input segment stride seg_in
-    void rescale(const u64 *in, size_t ell, size_t seg_in, int segs, u64 *out) {
+    // out [segs][ell-1][n] = Rescale(K * in) from the first ell limbs of
+    // in [segs][.][n] (segment stride seg_in); K = 0 means no scalar
+    void rescale(const u64 *in, size_t ell, size_t seg_in, int segs, u64 *out, int64_t K = 0) {
         Phase phase_("rescale");
         const size_t nn = n();
         auto lastm = alloc((size_t)segs * nn * 8);
         u64 *last = static_cast<u64 *>(lastm->p);
-        HIP_OK(hipMemcpy2DAsync(last, nn * 8, in + (ell - 1) * nn, seg_in * 8, nn * 8, (size_t)segs,
-                                hipMemcpyDeviceToDevice, st));
-        dev::ntt_inverse(last, 1, segs, nn, ext(ell) + (ell - 1), T, st);
+        dev::ntt_inverse_from(last, in + (ell - 1) * nn, seg_in, 1, segs, nn, ext(ell) + (ell - 1), T, st);
         if (ell <= 1) return;
         auto tmpm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *tmp = static_cast<u64 *>(tmpm->p);
@@ -266,6 +260,7 @@ struct Engine::Impl {
         F.seg_x = seg_in;
         F.c1 = qlinv + ell * P.nq();
         F.c1s = qlinv_s + ell * P.nq();
+        F.scalar = K;
         dev::ntt_forward_rescale(tmp, (int)(ell - 1), segs, F, T, st);
     }
 };
@@ -759,12 +754,13 @@ CtPtr Engine::mul_const_to(const Ciphertext &a, double c, int target) {
     const size_t nn = n(), ell = I.P.limbs_at(target - 1);
     const i64 K = host::const_to_target(c, I.P.delta[target], I.P.primes[I.P.L - target + 1], a.scale);
     const int segs = 2 * a.batch;
-    auto tm = I.alloc((size_t)segs * ell * nn * 8);
-    u64 *t = static_cast<u64 *>(tm->p);
-    // multiply the (dropped) input: each segment is read with the input's own stride
-    dev::ew_mul_scalar(t, a.data, K, (int)ell, segs, seg3(ell * nn, a.limbs * nn, 0), MODS, LOGN, ST);
     auto r = new_ct(target, a.slots, I.P.delta[target], ell - 1, a.batch);
-    I.rescale(t, ell, ell * nn, segs, r->data);
+    if (K == 0) {  // rescale(0 * a) = 0
+        HIP_OK(hipMemsetAsync(r->data, 0, (size_t)segs * (ell - 1) * nn * 8, ST));
+        return r;
+    }
+    // Rescale(K * a) of the first ell limbs, K folded into the fused NTT
+    I.rescale(a.data, ell, a.limbs * nn, segs, r->data, K);
     return r;
 }
 CtPtr Engine::mul_const(const Ciphertext &a, double c) { return mul_const_to(a, c, a.level + 1); }
