@@ -213,16 +213,15 @@ CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<
 // ====================================================== composite sign =====
 namespace {
 
+// c1 x + c3 x^3 + c5 x^5 + c7 x^7 in depth 3 (src/sign.cpp:15-59): the terms
+// that join a product are added before its rescale (mul_add), so only c3 x
+// and c7 x are rescaled on their own (oracle: oracle_algo.cpp odd7)
 CtPtr odd7(Engine &cc, const Ciphertext &x, double c1, double c3, double c5, double c7) {
-    const int l = x.level;
     CtPtr x2 = cc.square(x);
     CtPtr x4 = cc.square(*x2);
     CtPtr t3 = cc.mul(*cc.mul_const(x, c3), *x2);
-    CtPtr t7 = cc.mul(*cc.mul_const(x, c7), *x2);
-    CtPtr u = cc.add(*cc.mul_const_to(x, c5, l + 2), *t7);
-    CtPtr v = cc.mul(*u, *x4);
-    CtPtr y = cc.add(*cc.mul_const_to(x, c1, l + 3), *cc.level_adjust(*t3, l + 3));
-    return cc.add(*y, *v);
+    CtPtr u = cc.mul_add(*cc.mul_const(x, c7), *x2, {&x}, {c5});
+    return cc.mul_add(*u, *x4, {&x, t3.get()}, {c1, 1.0});
 }
 // g_3 = (4589x - 16577x^3 + 25614x^5 - 12860x^7)/2^10       (src/sign.cpp:15-36)
 CtPtr g3(Engine &cc, const Ciphertext &x) {

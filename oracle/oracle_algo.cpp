@@ -162,16 +162,18 @@ CtPtr cheb_series_ps(Context &cc, const Ciphertext &x0, const std::vector<double
 namespace {
 
 // c1 x + c3 x^3 + c5 x^5 + c7 x^7, depth 3, 5 relinearised products
+// c1 x + c3 x^3 + c5 x^5 + c7 x^7 in depth 3 (src/sign.cpp:15-59 evaluate the
+// same polynomials with EvalSquare / EvalMult / ct x const): the terms that
+// join a product are added before that product's rescale (mul_add), so only
+// c3 x and c7 x are rescaled on their own:
+//   u   = (c7 x) x^2 + c5 x                         (level l+2)
+//   out = u x^4 + c1 x + (c3 x) x^2                  (level l+3)
 CtPtr odd7(Context &cc, const Ciphertext &x, double c1, double c3, double c5, double c7) {
-    const int l = x.level;
     CtPtr x2 = cc.square(x);
     CtPtr x4 = cc.square(*x2);
     CtPtr t3 = cc.mul(*cc.mul_const(x, c3), *x2);
-    CtPtr t7 = cc.mul(*cc.mul_const(x, c7), *x2);
-    CtPtr u = cc.add(*cc.mul_const_to(x, c5, l + 2), *t7);
-    CtPtr v = cc.mul(*u, *x4);
-    CtPtr y = cc.add(*cc.mul_const_to(x, c1, l + 3), *cc.level_adjust(*t3, l + 3));
-    return cc.add(*y, *v);
+    CtPtr u = cc.mul_add(*cc.mul_const(x, c7), *x2, {&x}, {c5});
+    return cc.mul_add(*u, *x4, {&x, t3.get()}, {c1, 1.0});
 }
 
 CtPtr g3(Context &cc, const Ciphertext &x) {
