@@ -17,7 +17,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O
 python scripts/trace_summary.py $O/trace/run_kernel_trace.csv > $O/trace_summary.txt && cat $O/trace_summary.txt || exit 1
 gzip -f $O/trace/run_kernel_trace.csv
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 900 rocprofv3 --pmc $C --kernel-include-regex 'k_ntt' --output-format csv -d "$R/$O/pmc_$C" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-roofline "$@" > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -5 $O/pmc_$C.log; exit 1; }
+  timeout -k 10 900 rocprofv3 --pmc $C --kernel-include-regex 'k_[a-z]' --output-format csv -d "$R/$O/pmc_$C" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-roofline "$@" > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -5 $O/pmc_$C.log; exit 1; }
 done
 python scripts/pmc_summary.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv $O/pmc_traffic.json || exit 1
 gzip -f $O/pmc_*/run_counter_collection.csv

@@ -21,11 +21,13 @@ for k, v in sorted(stat.items(), key=lambda kv: -sum(x[0] for x in kv[1]))[:16]:
     tot = sum(x[0] for x in v)
     print(f'{k:34s} n={len(v):6d} {tot / 1e6:9.2f} ms {100 * tot / tot_all:5.1f}%  avg {tot / len(v) / 1e3:7.2f} us'
           f'  vgpr={v[0][4]} lds={v[0][5]}')
+# NTT passes launch grid (segments x 256 threads, blocks per limb, limbs)
 for k in sorted(stat):
     if not k.startswith('k_ntt'):
         continue
     v = stat[k]
-    tb = sum(gy * gz * n * 16 for _, _, gy, gz, _, _ in v)
+    limbs = [gx // 256 * gz for _, gx, _, gz, _, _ in v]
+    tb = sum(L * n * 16 for L in limbs)
     tt = sum(x[0] for x in v)
-    print(f'{k}: {tb / tt:.1f} GB/s algorithmic (2 x 8 B per coefficient), '
-          f'avg {sum(x[2] * x[3] for x in v) / len(v):.1f} limbs/launch, avg {tt / len(v) / 1e3:.2f} us')
+    print(f'{k}: {tb / tt:.1f} GB/s algorithmic (one read + one write per coefficient), '
+          f'avg {sum(limbs) / len(v):.1f} limbs/launch, avg {tt / len(v) / 1e3:.2f} us')
