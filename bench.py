@@ -49,6 +49,8 @@ def parse():
     ap.add_argument('--no-roofline', action='store_true', help='skip the instrumented roofline sort (PMC passes)')
     ap.add_argument('--cpu-sample-mults', type=int, default=0, help='override CPU sample size')
     ap.add_argument('--clock-json', default=None, help='write the full per-kernel clock of the roofline sort here')
+    ap.add_argument('--lanes', type=int, default=2, help='concurrent batch lanes (forked engines) per GPU')
+    ap.add_argument('--stack', type=int, default=32, help='max batches stacked into one ciphertext batch')
     return ap.parse_args()
 
 
@@ -209,6 +211,8 @@ def main():
     t0 = time.time()
     ctx = F.Context(logN, depth, a.scale_bits, 60, 3, seed=a.seed, device=d.device)
     ctx.gen_rotation_keys(rots)
+    ctx.set_sort_lanes(a.lanes)
+    ctx.set_sort_stack(a.stack)
     allreduce = None
     if d.world > 1 and d.rccl:
         uid = d.bcast_bytes(F.Context.comm_unique_id() if d.rank == 0 else None)
@@ -264,7 +268,8 @@ def main():
             'data': 'synthetic: seeded permutation of {k/N}, keys and encryption from a seeded PRNG',
             'config': {'workload': f'DirectSort N={N}, ringDim 2^{logN}, depth {depth}, scale 2^{a.scale_bits}, '
                                    f'{len(rots)} rotation keys, CompositeSign{cfg}, dnum 3',
-                       'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'parallelism': f'batch-shard x{d.world}',
+                       'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'lanes_per_gpu': a.lanes,
+                       'max_stack': a.stack, 'parallelism': f'batch-shard x{d.world}',
                        'collective': 'none' if d.world == 1 else ('rccl' if d.rccl else 'host+gloo (more ranks than GPUs)')},
             'max_abs_err': max_err,
             'output_level': out.level,

@@ -16,6 +16,8 @@
 #include <mutex>
 #include <stdexcept>
 #include <tuple>
+#include <exception>
+#include <thread>
 
 namespace fhe {
 
@@ -516,15 +518,65 @@ std::vector<double> checking_vector(int num_slots, int N, int k) {  // src/sort_
 }  // namespace
 
 DirectSortN::DirectSortN(Engine &c, int N_, const std::vector<int> &rotIndices)
-    : cc(c), N(N_), rot(c, N_, rotIndices), max_batch((int)(c.n() / 2)) {}
+    : cc(c), N(N_), rot(c, N_, rotIndices), max_batch((int)(c.n() / 2)), rot_indices(rotIndices) {}
+
+DirectSortN::Lane DirectSortN::lane(int l) {
+    if (l == 0) return Lane{&cc, &rot};
+    while ((int)lane_eng.size() < l) {
+        lane_eng.push_back(cc.fork());
+        lane_rot.push_back(std::make_unique<RotationComposerN>(*lane_eng.back(), N, rot_indices));
+    }
+    return Lane{lane_eng[l - 1].get(), lane_rot[l - 1].get()};
+}
+
+// Split `batches` into contiguous groups, one per lane; lane 0 runs on this
+// thread with the context's engine, the others on their own threads and
+// forked engines.  Everything the lanes read must be complete on the main
+// stream (callers sync before).  Returns each lane's partial (may be null),
+// with every lane stream drained.
+template <class F>
+std::vector<CtPtr> DirectSortN::run_lanes(const std::vector<int> &batches, F &&work) {
+    const int L = std::max(1, std::min(lanes, (int)batches.size()));
+    std::vector<std::vector<int>> groups(L);
+    for (size_t i = 0; i < batches.size(); ++i) groups[i * L / batches.size()].push_back(batches[i]);
+    std::vector<Lane> ls;
+    for (int l = 0; l < L; ++l) ls.push_back(lane(l));
+    std::vector<CtPtr> parts(L);
+    std::vector<std::exception_ptr> errs(L);
+    std::vector<std::thread> th;
+    for (int l = 1; l < L; ++l)
+        th.emplace_back([&, l] {
+            try {
+                parts[l] = work(ls[l], groups[l]);
+                ls[l].eng->sync();
+            } catch (...) {
+                errs[l] = std::current_exception();
+            }
+        });
+    try {
+        parts[0] = work(ls[0], groups[0]);
+    } catch (...) {
+        errs[0] = std::current_exception();
+    }
+    for (auto &t : th) t.join();
+    for (int l = 1; l < L; ++l) {  // the context's counters cover every lane
+        cc.ctr += ls[l].eng->ctr;
+        ls[l].eng->ctr = Counters();
+    }
+    for (auto &e : errs)
+        if (e) std::rethrow_exception(e);
+    return parts;
+}
 
 // kind 0: mask_vector(k) rotated by `r` (vector_rotate); kind 1: checking vector(k)
-const Plaintext &DirectSortN::mask(int kind, int num_slots, int k, int r, int level) {
+const Plaintext &DirectSortN::mask(Engine &E, int kind, int num_slots, int k, int r, int level) {
     auto key = std::make_tuple(kind, num_slots, k, r, level);
+    std::lock_guard<std::mutex> lk(mask_mu);
     auto it = mask_cache.find(key);
     if (it != mask_cache.end()) return *it->second;
     std::vector<double> v = kind == 0 ? vector_rotate(mask_vector(num_slots, N, k), r) : checking_vector(num_slots, N, k);
-    PtPtr p = cc.encode(v, num_slots, level);
+    PtPtr p = E.encode(v, num_slots, level);
+    E.sync();  // complete before another lane's stream reads it
     mask_cache[key] = p;
     return *p;
 }
@@ -544,28 +596,29 @@ void DirectSortN::reducePartial(CtPtr &acc, int slots) {
     cc.reduce_after_allreduce(*acc);
 }
 
-CtPtr DirectSortN::vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is) {
+CtPtr DirectSortN::vecRotsOpt(Lane L, const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np,
+                              int is) {
     CtPtr result;
     for (int j = 0; j < num_partition / np; ++j) {
         std::vector<const Ciphertext *> cs;
         std::vector<const Plaintext *> ps;
         for (int i = 0; i < np; ++i) {
             cs.push_back(baby[i].get());
-            ps.push_back(&mask(0, num_slots, np * j + i, -is * num_partition - j * np, baby[i]->level));
+            ps.push_back(&mask(*L.eng, 0, num_slots, np * j + i, -is * num_partition - j * np, baby[i]->level));
         }
-        CtPtr Tj = cc.mul_plain_sum(cs, ps);  // one rescale per masked sum (src/sort_algo.h:341-346)
-        CtPtr o = rot.rotate(*Tj, is * num_partition + j * np);
-        cc.add_inplace(result, *o);
+        CtPtr Tj = L.eng->mul_plain_sum(cs, ps);  // one rescale per masked sum (src/sort_algo.h:341-346)
+        CtPtr o = L.rot->rotate(*Tj, is * num_partition + j * np);
+        L.eng->add_inplace(result, *o);
     }
     return result;
 }
 
-// The comparator batches of this rank run stacked: their inputs differ, but
-// the sign() op sequence is identical, so one compare over a ciphertext batch
-// replaces max_stack sequential ones.  compare(x, s_b) =
-// ((sign(x - s_b) + 1) / 2); the per-batch results are summed exactly mod q,
-// so the rank equals the reference's batch-by-batch accumulation
-// (src/sort_algo.h:474-491) word for word.
+// The comparator batches run stacked: their inputs differ, but the sign() op
+// sequence is identical, so one compare over a ciphertext batch replaces
+// max_stack sequential ones, on `lanes` concurrent streams.
+// compare(x, s_b) = ((sign(x - s_b) + 1) / 2); the per-batch results are summed
+// exactly mod q, so the rank equals the reference's batch-by-batch
+// accumulation (src/sort_algo.h:474-491) word for word.
 CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg) {
     const SortShape s = rankShape(N, max_batch);
     std::vector<int> idx(s.np);
@@ -577,22 +630,32 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
         if (b % shard_world == shard_rank) mine.push_back(b);
     CtPtr dup = cc.clone(x);
     dup->slots = s.num_slots;
-    CtPtr rank;
+    cc.sync();  // baby steps and dup are read by every lane
     const size_t chunk = (size_t)std::max(1, max_stack);
-    for (size_t c0 = 0; c0 < mine.size(); c0 += chunk) {
-        std::vector<CtPtr> diffs;
-        std::vector<const Ciphertext *> ptrs;
-        for (size_t i = c0; i < std::min(mine.size(), c0 + chunk); ++i) {
-            CtPtr shifted = vecRotsOpt(baby, s.num_partition, s.num_slots, s.np, mine[i]);
-            diffs.push_back(cc.sub(*dup, *shifted));
-            ptrs.push_back(diffs.back().get());
+    auto parts = run_lanes(mine, [&](Lane L, const std::vector<int> &bs) -> CtPtr {
+        Engine &E = *L.eng;
+        CtPtr acc;
+        for (size_t c0 = 0; c0 < bs.size(); c0 += chunk) {
+            std::vector<CtPtr> diffs;
+            std::vector<const Ciphertext *> ptrs;
+            for (size_t i = c0; i < std::min(bs.size(), c0 + chunk); ++i) {
+                CtPtr shifted = vecRotsOpt(L, baby, s.num_partition, s.num_slots, s.np, bs[i]);
+                diffs.push_back(E.sub(*dup, *shifted));
+                ptrs.push_back(diffs.back().get());
+            }
+            CtPtr d = ptrs.size() == 1 ? diffs[0] : E.stack(ptrs);
+            diffs.clear();
+            CtPtr sg = sign(*d, E, f, cfg);
+            CtPtr c = E.mul_const(*E.add_const(*sg, 1.0), 0.5);
+            E.add_inplace(acc, c->batch == 1 ? *c : *E.sum_members(*c));
         }
-        CtPtr d = ptrs.size() == 1 ? diffs[0] : cc.stack(ptrs);
-        diffs.clear();
-        CtPtr sg = sign(*d, cc, f, cfg);
-        CtPtr c = cc.mul_const(*cc.add_const(*sg, 1.0), 0.5);
-        cc.add_inplace(rank, c->batch == 1 ? *c : *cc.sum_members(*c));
-    }
+        return acc;
+    });
+    CtPtr rank;
+    for (auto &p : parts)
+        if (p) cc.add_inplace(rank, *p);
+    cc.sync();  // lane buffers return to their pools only after the main stream read them
+    parts.clear();
     reducePartial(rank, s.num_slots);
     for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)
         rank = cc.add(*rank, *rot.rotate(*rank, s.num_slots / (1 << i)));
@@ -601,35 +664,24 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
 }
 
 CtPtr DirectSortN::blindRotationOptN(const std::vector<CtPtr> &mi, int num_slots, int np, int ib, int num_partition) {
-    CtPtr result;
-    for (int i = 0; i < (num_slots / N) / np; ++i) {
-        std::vector<const Ciphertext *> cs;
-        std::vector<const Plaintext *> ps;
-        for (int j = 0; j < np; ++j) {
-            cs.push_back(mi[j].get());
-            ps.push_back(&mask(0, num_slots, np * i + j, j, mi[j]->level));
-        }
-        CtPtr tmp = cc.mul_plain_sum(cs, ps);  // src/sort_algo.h:573-577
-        tmp = rot.rotate(*tmp, ib * num_partition + i * np);
-        cc.add_inplace(result, *tmp);
-    }
-    return result;
+    return blindRotationStacked(lane(0), mi, num_slots, np, {ib}, num_partition);
 }
 
-CtPtr DirectSortN::blindRotationStacked(const std::vector<CtPtr> &mi, int num_slots, int np, const std::vector<int> &ibs,
-                                        int num_partition) {
+CtPtr DirectSortN::blindRotationStacked(Lane L, const std::vector<CtPtr> &mi, int num_slots, int np,
+                                        const std::vector<int> &ibs, int num_partition) {
+    Engine &E = *L.eng;
     CtPtr result;
     for (int i = 0; i < (num_slots / N) / np; ++i) {
         std::vector<const Ciphertext *> cs;
         std::vector<const Plaintext *> ps;
         for (int j = 0; j < np; ++j) {
             cs.push_back(mi[j].get());
-            ps.push_back(&mask(0, num_slots, np * i + j, j, mi[j]->level));
+            ps.push_back(&mask(E, 0, num_slots, np * i + j, j, mi[j]->level));
         }
-        CtPtr tmp = cc.mul_plain_sum(cs, ps);
+        CtPtr tmp = E.mul_plain_sum(cs, ps);  // src/sort_algo.h:573-577
         for (size_t m = 0; m < ibs.size(); ++m) {
-            CtPtr one = tmp->batch == 1 ? tmp : cc.member(*tmp, (int)m);
-            cc.add_inplace(result, *rot.rotate(*one, ibs[m] * num_partition + i * np));
+            CtPtr one = tmp->batch == 1 ? tmp : E.member(*tmp, (int)m);
+            E.add_inplace(result, *L.rot->rotate(*one, ibs[m] * num_partition + i * np));
         }
     }
     return result;
@@ -637,8 +689,8 @@ CtPtr DirectSortN::blindRotationStacked(const std::vector<CtPtr> &mi, int num_sl
 
 // Index check, stacked like constructRank: the doubled-sinc PS (the dominant
 // cost, ~200 HMult per batch at N=1024) and the masking product run once over
-// a batch of max_stack inputs; only the per-batch giant-step rotations run
-// member by member (src/sort_algo.h:713-742).
+// a batch of max_stack inputs per lane; only the per-batch giant-step
+// rotations run member by member (src/sort_algo.h:713-742).
 CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext &x) {
     const SortShape s = checkShape(N, max_batch);
     std::vector<double> idx(N);
@@ -654,29 +706,39 @@ CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext 
     std::vector<int> mine;
     for (int b = 0; b < s.num_batch; ++b)
         if (b % shard_world == shard_rank) mine.push_back(b);
-    CtPtr out;
+    cc.sync();  // imr and xs are read by every lane
     const size_t chunk = (size_t)std::max(1, max_stack);
-    for (size_t c0 = 0; c0 < mine.size(); c0 += chunk) {
-        std::vector<CtPtr> ris;
-        std::vector<const Ciphertext *> ptrs;
-        std::vector<int> ibs;
-        for (size_t i = c0; i < std::min(mine.size(), c0 + chunk); ++i) {
-            const int b = mine[i];
-            const Plaintext &chk = mask(1, s.num_slots, b * s.num_partition, 0, imr->level);
-            CtPtr ri = cc.sub_plain(*imr, chk);
-            ris.push_back(cc.mul_const(*ri, 1.0 / N / 2));
-            ptrs.push_back(ris.back().get());
-            ibs.push_back(b);
+    auto parts = run_lanes(mine, [&](Lane L, const std::vector<int> &bs) -> CtPtr {
+        Engine &E = *L.eng;
+        CtPtr acc;
+        for (size_t c0 = 0; c0 < bs.size(); c0 += chunk) {
+            std::vector<CtPtr> ris;
+            std::vector<const Ciphertext *> ptrs;
+            std::vector<int> ibs;
+            for (size_t i = c0; i < std::min(bs.size(), c0 + chunk); ++i) {
+                const int b = bs[i];
+                const Plaintext &chk = mask(E, 1, s.num_slots, b * s.num_partition, 0, imr->level);
+                CtPtr ri = E.sub_plain(*imr, chk);
+                ris.push_back(E.mul_const(*ri, 1.0 / N / 2));
+                ptrs.push_back(ris.back().get());
+                ibs.push_back(b);
+            }
+            CtPtr r = ptrs.size() == 1 ? ris[0] : E.stack(ptrs);
+            ris.clear();
+            r = evalChebyshevSeriesPS(E, *r, coeffs, -1.0, 1.0);
+            CtPtr masked = E.mul(*r, *xs);  // xs broadcast over the members
+            r.reset();
+            std::vector<CtPtr> mi = L.rot->rotateMany(*masked, ridx);
+            masked.reset();
+            E.add_inplace(acc, *blindRotationStacked(L, mi, s.num_slots, s.np, ibs, s.num_partition));
         }
-        CtPtr r = ptrs.size() == 1 ? ris[0] : cc.stack(ptrs);
-        ris.clear();
-        r = evalChebyshevSeriesPS(cc, *r, coeffs, -1.0, 1.0);
-        CtPtr masked = cc.mul(*r, *xs);  // xs broadcast over the members
-        r.reset();
-        std::vector<CtPtr> mi = rot.rotateMany(*masked, ridx);
-        masked.reset();
-        cc.add_inplace(out, *blindRotationStacked(mi, s.num_slots, s.np, ibs, s.num_partition));
-    }
+        return acc;
+    });
+    CtPtr out;
+    for (auto &p : parts)
+        if (p) cc.add_inplace(out, *p);
+    cc.sync();
+    parts.clear();
     reducePartial(out, s.num_slots);
     for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)
         out = cc.add(*out, *rot.rotate(*out, s.num_slots / (1 << i)));

@@ -14,6 +14,7 @@
 #pragma once
 #include <functional>
 #include <map>
+#include <mutex>
 #include <set>
 #include <vector>
 
@@ -120,16 +121,31 @@ class DirectSortN {
     // how many of this rank's batches run stacked through one compare / one PS
     // (every launch then carries that many ciphertexts; memory grows with it)
     int max_stack = 32;
+    // concurrent lanes: the rank's batches are split over `lanes` host threads,
+    // each driving a forked engine (own HIP stream and pool, shared keys)
+    int lanes = 2;
 
   private:
-    CtPtr vecRotsOpt(const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is);
+    struct Lane {
+        Engine *eng;
+        RotationComposerN *rot;
+    };
+    Lane lane(int l);
+    template <class F>
+    std::vector<CtPtr> run_lanes(const std::vector<int> &batches, F &&work);
+    CtPtr vecRotsOpt(Lane L, const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is);
     CtPtr blindRotationOptN(const std::vector<CtPtr> &masked, int num_slots, int np, int ib, int num_partition);
     // blindRotationOptN over a stacked `masked` (member m belongs to batch ibs[m]), summed over members
-    CtPtr blindRotationStacked(const std::vector<CtPtr> &masked, int num_slots, int np, const std::vector<int> &ibs,
-                               int num_partition);
+    CtPtr blindRotationStacked(Lane L, const std::vector<CtPtr> &masked, int num_slots, int np,
+                               const std::vector<int> &ibs, int num_partition);
     void reducePartial(CtPtr &acc, int slots);
-    const Plaintext &mask(int kind, int num_slots, int k, int rot, int level);
+    // encoded on the calling lane's engine, published once complete (thread-safe)
+    const Plaintext &mask(Engine &E, int kind, int num_slots, int k, int rot, int level);
     std::map<std::tuple<int, int, int, int, int>, PtPtr> mask_cache;
+    std::mutex mask_mu;
+    std::vector<int> rot_indices;
+    std::vector<std::unique_ptr<Engine>> lane_eng;
+    std::vector<std::unique_ptr<RotationComposerN>> lane_rot;
 };
 template <int SIZE>
 class DirectSort : public DirectSortN {

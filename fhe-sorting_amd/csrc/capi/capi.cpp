@@ -22,6 +22,7 @@ struct fhe_ctx {
     // across sorts like the keys do
     std::map<std::pair<int, std::vector<int>>, std::unique_ptr<DirectSortN>> sorters;
     int sort_stack = 32;
+    int sort_lanes = 2;
 };
 struct fhe_ct {
     CtPtr p;
@@ -319,6 +320,7 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
         if (!slot) slot = std::make_unique<DirectSortN>(*ctx->eng, N, key.second);
         DirectSortN &ds = *slot;
         ds.max_stack = ctx->sort_stack;
+        ds.lanes = ctx->sort_lanes;
         ds.allreduce = nullptr;
         ds.shard_rank = shard_rank;
         ds.shard_world = shard_world;
@@ -356,6 +358,14 @@ int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack) {
         NEED(ctx);
         if (max_stack < 1) throw std::invalid_argument("max_stack must be >= 1");
         ctx->sort_stack = max_stack;
+    });
+}
+
+int fhe_set_sort_lanes(fhe_ctx *ctx, int lanes) {
+    return guard([&] {
+        NEED(ctx);
+        if (lanes < 1 || lanes > 8) throw std::invalid_argument("lanes must be in 1..8");
+        ctx->sort_lanes = lanes;
     });
 }
 

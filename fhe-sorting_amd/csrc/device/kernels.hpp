@@ -30,12 +30,13 @@ struct NttTables {
 // reported with their algorithmic bytes.  Process-global; diagnostics only.
 struct LaunchClock {
     virtual ~LaunchClock() = default;
-    // events handed to hipExtLaunchKernelGGL: recorded at the kernel's own start / end
-    virtual void events(hipEvent_t &start, hipEvent_t &stop) = 0;
-    virtual void record(const char *kernel, double bytes) = 0;
+    // events handed to hipExtLaunchKernelGGL (recorded at the kernel's own start /
+    // end); returns the slot to book the launch under.  Thread-safe.
+    virtual int events(hipEvent_t &start, hipEvent_t &stop) = 0;
+    virtual void record(int slot, const char *kernel, double bytes) = 0;
 };
 LaunchClock *&launch_clock();
-// caller tag appended to clocked NTT names ("k_ntt_fwd<8, 4, true>@modup")
+// caller tag appended to clocked NTT names ("k_ntt_fwd<8, 4, true>@modup"); per thread
 const char *&launch_phase();
 
 // Launch through hipExtLaunchKernelGGL; when a clock is installed the launch is
@@ -46,9 +47,9 @@ inline void launch_clocked(const char *name, double bytes, Kern kernel, dim3 gri
                            Args... args) {
     LaunchClock *clk = launch_clock();
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (clk) clk->events(e0, e1);
+    const int slot = clk ? clk->events(e0, e1) : -1;
     hipExtLaunchKernelGGL(kernel, grid, block, 0, st, e0, e1, 0, args...);
-    if (clk) clk->record(name, bytes);
+    if (clk) clk->record(slot, name, bytes);
 }
 
 // forward / inverse negacyclic NTT of `limbs` limbs x `segs` segments

@@ -17,6 +17,7 @@
 #include <hip/hip_ext.h>
 
 #include <map>
+#include <mutex>
 #include <string>
 
 #include "kernels.hpp"
@@ -350,7 +351,7 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     const dim3 grid((unsigned)segs, (unsigned)((count + NB - 1) / NB), (unsigned)limbs);
     LaunchClock *clk = launch_clock();
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (clk) clk->events(e0, e1);
+    const int slot = clk ? clk->events(e0, e1) : -1;
     if (FWD)
         hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
                               T.logN, T, F);
@@ -363,12 +364,14 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
                                         std::to_string(EB) + (COLS ? ", true" : ", false") +
                                         (FWD ? ", " + std::to_string(MODE) : std::string()) + ">";
         static std::map<const char *, std::string> names;
+        static std::mutex mu;
         const char *ph = launch_phase();
+        std::lock_guard<std::mutex> lk(mu);
         auto it = names.find(ph);
         if (it == names.end()) it = names.emplace(ph, ph ? base + "@" + ph : base).first;
         // one read + one write of every limb touched (fused epilogues: + the extra operands)
         const double extra = MODE == NTT_RESCALE ? 1.0 : MODE == NTT_MULTAIL ? 2.0 : 0.0;
-        clk->record(it->second.c_str(), (2.0 + extra) * 8.0 * (double)limbs * segs * ((size_t)1 << T.logN));
+        clk->record(slot, it->second.c_str(), (2.0 + extra) * 8.0 * (double)limbs * segs * ((size_t)1 << T.logN));
     }
 }
 
@@ -396,7 +399,7 @@ LaunchClock *&launch_clock() {
     return clk;
 }
 const char *&launch_phase() {
-    static const char *ph = nullptr;
+    static thread_local const char *ph = nullptr;
     return ph;
 }
 

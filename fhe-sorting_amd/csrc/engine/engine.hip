@@ -335,6 +335,28 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.key_digits = I.P.digits_at(I.P.nq());
 }
 
+Engine::Engine(ForkTag) {}
+
+std::unique_ptr<Engine> Engine::fork() const {
+    std::unique_ptr<Engine> e(new Engine(ForkTag{}));
+    e->impl.reset(new Impl(*impl));  // shares tables and keys (shared_ptr / raw device pointers)
+    auto &I = *e->impl;
+    HIP_OK(hipSetDevice(I.device));
+    I.st = nullptr;
+    HIP_OK(hipStreamCreateWithFlags(&I.st, hipStreamNonBlocking));
+    I.pool = std::make_shared<Pool>();
+    I.pool->device = I.device;
+    return e;
+}
+
+void Engine::wait_for(const Engine &other) {
+    hipEvent_t ev;
+    HIP_OK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(ev, other.impl->st));
+    HIP_OK(hipStreamWaitEvent(impl->st, ev, 0));
+    HIP_OK(hipEventDestroy(ev));
+}
+
 Engine::~Engine() {
     if (impl && impl->st) {
         (void)hipStreamSynchronize(impl->st);
@@ -1137,9 +1159,11 @@ struct EventClock final : dev::LaunchClock {
         const char *name = nullptr;
         double bytes = 0;
     };
+    std::mutex mu;
     std::vector<Rec> recs;
     size_t used = 0;
-    void events(hipEvent_t &start, hipEvent_t &stop) override {
+    int events(hipEvent_t &start, hipEvent_t &stop) override {
+        std::lock_guard<std::mutex> lk(mu);
         if (used == recs.size()) {
             Rec r;
             HIP_OK(hipEventCreate(&r.e0));
@@ -1148,11 +1172,12 @@ struct EventClock final : dev::LaunchClock {
         }
         start = recs[used].e0;
         stop = recs[used].e1;
+        return (int)used++;
     }
-    void record(const char *kernel, double bytes) override {
-        recs[used].name = kernel;
-        recs[used].bytes = bytes;
-        ++used;
+    void record(int slot, const char *kernel, double bytes) override {
+        std::lock_guard<std::mutex> lk(mu);
+        recs[(size_t)slot].name = kernel;
+        recs[(size_t)slot].bytes = bytes;
     }
     ~EventClock() override {
         for (auto &r : recs) {
@@ -1184,7 +1209,7 @@ void Engine::kernel_clock_start() {
 std::string Engine::kernel_clock_stop() {
     if (!g_clock) throw std::runtime_error("kernel clock not running");
     dev::launch_clock() = nullptr;
-    HIP_OK(hipStreamSynchronize(impl->st));
+    HIP_OK(hipDeviceSynchronize());  // lanes may have launched on their own streams
     struct Agg {
         long launches = 0;
         double ms = 0, bytes = 0;

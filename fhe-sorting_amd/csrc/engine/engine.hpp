@@ -55,12 +55,27 @@ using PtPtr = std::shared_ptr<Plaintext>;
 
 struct Counters {
     u64 hmult = 0, keyswitch = 0, rotations = 0, rescale = 0, ptmult = 0, constmult = 0;
+    Counters &operator+=(const Counters &o) {
+        hmult += o.hmult;
+        keyswitch += o.keyswitch;
+        rotations += o.rotations;
+        rescale += o.rescale;
+        ptmult += o.ptmult;
+        constmult += o.constmult;
+        return *this;
+    }
 };
 
 class Engine {
   public:
     Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int device, u64 seed);
     ~Engine();
+    // A second engine on its own HIP stream and memory pool sharing this one's
+    // keys and tables: independent work issued to both (from two host threads)
+    // runs concurrently on the GPU.  Keys must be complete before forking.
+    std::unique_ptr<Engine> fork() const;
+    // order this engine's stream after everything enqueued on `other` so far
+    void wait_for(const Engine &other);
     Engine(const Engine &) = delete;
     Engine &operator=(const Engine &) = delete;
 
@@ -165,6 +180,10 @@ class Engine {
 
     struct Impl;
     std::unique_ptr<Impl> impl;
+
+  private:
+    struct ForkTag {};
+    explicit Engine(ForkTag);
 
   private:
     CtPtr new_ct(int level, int slots, double scale, size_t limbs, int batch = 1);

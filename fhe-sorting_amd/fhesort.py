@@ -102,6 +102,7 @@ _SIGS = {
     'fhe_time_kernel': (C.c_int, [vp, C.c_char_p, C.c_int, C.c_int, dp, dp]),
     'fhe_kernel_clock_start': (C.c_int, [vp]),
     'fhe_set_sort_stack': (C.c_int, [vp, C.c_int]),
+    'fhe_set_sort_lanes': (C.c_int, [vp, C.c_int]),
     'fhe_pool_trim': (C.c_int, [vp]),
     'fhe_pool_stats': (C.c_int, [vp, u64p, u64p, u64p]),
     'fhe_ct_stack': (C.c_int, [vp, C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_void_p)]),
@@ -375,6 +376,9 @@ class Context:
         v = [C.c_uint64() for _ in range(3)]
         _chk(lib().fhe_pool_stats(self.h, *[C.byref(x) for x in v]))
         return {'live': v[0].value, 'cached': v[1].value, 'peak': v[2].value}
+
+    def set_sort_lanes(self, m):
+        _chk(lib().fhe_set_sort_lanes(self.h, m))
 
     def set_sort_stack(self, m):
         _chk(lib().fhe_set_sort_stack(self.h, m))

@@ -168,6 +168,10 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
  * sinc PS (default 32: every launch then carries up to 32 ciphertexts; HBM use
  * grows with it).  Results do not depend on it. */
 int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack);
+/* concurrent lanes per sort (default 2): the rank's batches are split over
+ * host threads driving forked engines (own HIP stream and pool, shared keys),
+ * so independent batch stacks overlap on the GPU.  Results do not depend on it. */
+int fhe_set_sort_lanes(fhe_ctx *ctx, int lanes);
 
 /* ------------------------------------------------------ multi-GPU (RCCL) */
 int fhe_comm_get_unique_id(uint8_t id[128]);

@@ -270,10 +270,11 @@ def test_batched_ops_match_members(pair):
     same(total, ref)
 
 
-@pytest.mark.parametrize('stack', [32, 3])
-def test_direct_sort_multi_batch_stacked(stack):
+@pytest.mark.parametrize('stack,lanes', [(32, 1), (3, 1), (32, 2), (1, 3)])
+def test_direct_sort_multi_batch_stacked(stack, lanes):
     """N=64 at ring 2^11: 4 comparator batches and 4 index-check batches run
-    stacked (all four at once, or 3 + 1) and match the oracle's serial loop."""
+    stacked (all four at once, or 3 + 1) on one or more concurrent lanes
+    (forked engines on their own streams) and match the oracle's serial loop."""
     N, cfg = 64, (3, 3, 2)
     depth, rots = O.size_parameters(N)
     orc = O.Context(11, depth, 40, 60, 3, seed=7)
@@ -281,6 +282,7 @@ def test_direct_sort_multi_batch_stacked(stack):
     gpu = F.Context(11, depth, 40, 60, 3, seed=7, keygen=False)
     gpu.load_keys_from(orc, rots)
     gpu.set_sort_stack(stack)
+    gpu.set_sort_lanes(lanes)
     x = np.random.default_rng(64).permutation(N) / N
     ox = orc.encrypt(x, N)
     gx = gpu.from_oracle(ox)
