@@ -445,8 +445,8 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const
     const int i0 = blockIdx.y * TCH;
     for (int i = i0; i < i0 + TCH && i < last; ++i) {
         const Mod mi = mods[i];
-        u64 lift = reduce64(y, mi);
-        if (neg) lift = sub_mod(lift, reduce64(ql, mi), mi.q);
+        // centred lift of y: q_last / 2 < q_i (checked at context creation)
+        const u64 lift = neg ? mi.q - (ql - y) : y;
         Acc4 a4;
         mac4(a4, split30(lift), split30(pmod[i]));
 #pragma unroll

@@ -128,8 +128,10 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
     u64 x[E];
     // ---- load, layout L1: idx = t + T * r
     if (MODE == NTT_LIFT) {
-        const Mod mp = Tb.mods[p], ml = Tb.mods[F.lastp];
-        const u64 ql = ml.q, qlm = reduce64(ql, mp);
+        // centred lift of c mod q_last into prime p: q_last / 2 < q_p (checked at
+        // context creation), so c or q_p - (q_last - c) is already reduced
+        const Mod ml = Tb.mods[F.lastp];
+        const u64 ql = ml.q, qh = ql >> 1;
         const u64 kl = F.scalar ? smod64(F.scalar, ml) : 0;  // K mod q_last (scaled rescale)
         const u64 *src = F.last + (size_t)blockIdx.x * F.seg_last;
 #pragma unroll
@@ -137,8 +139,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
             const int idx = t + T * r;
             u64 c = valid ? src[(size_t)idx * ((size_t)1 << k2) + tid_global] : 0;
             if (F.scalar) c = mul_barrett(c, kl, ml);
-            const u64 v = reduce64(c, mp);
-            x[r] = c > (ql >> 1) ? sub_mod(v, qlm, q) : v;
+            x[r] = c > qh ? q - (ql - c) : c;
         }
     } else {
 #pragma unroll

@@ -283,6 +283,14 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
         if (q >> 60) throw std::invalid_argument("engine: every prime must be < 2^60 (first_bits <= 60)");
     if (I.P.alpha > 16 || I.P.K > 15)
         throw std::invalid_argument("engine: digit size <= 16 and special primes <= 15 required (raise dnum)");
+    // rescales lift the last limb with a compare-select: every prime that can be
+    // rescaled away (q_1..q_L) must satisfy q_l / 2 < q_i for all Q primes
+    {
+        u64 qmin = ~0ull, qlmax = 0;
+        for (size_t i = 0; i < I.P.nq(); ++i) qmin = std::min(qmin, I.P.primes[i]);
+        for (size_t i = 1; i < I.P.nq(); ++i) qlmax = std::max(qlmax, I.P.primes[i]);
+        if (qlmax / 2 >= qmin) throw std::invalid_argument("engine: scaling primes must be < 2 x the smallest prime");
+    }
     const size_t nall = I.P.nall(), n = I.P.n;
     std::vector<Mod> mods(nall);
     for (size_t i = 0; i < nall; ++i) {
