@@ -138,17 +138,30 @@ def device_sync(ctx):
         pass
 
 
+def pmc_lookup(table, name):
+    """PMC entry for a clocked kernel name: the clock tags launches with their
+    caller phase ('k_ntt_fwd<8, 4, false, 2>@rescale') and omits template
+    arguments of the conversion kernels ('k_modup_convert'); rocprofv3 names
+    the instantiation."""
+    base = name.split('@')[0]
+    if base in table:
+        return table[base]
+    hits = [v for k, v in table.items() if k.split('<')[0] == base]
+    return hits[0] if len(hits) == 1 else None
+
+
 def roofline(ctx, run_once, dump=None):
     """Roofline of the dominant kernel, measured live: one more (untimed) sort
     runs with every hot kernel launched through hipExtLaunchKernelGGL with
-    start/stop events on the engine stream (the stream it runs on); the kernel
+    start/stop events on the engine stream (the stream it runs on), one lane so
+    no other kernel overlaps the measured span; the kernel
     with the largest total time is reported.  achieved = its algorithmic bytes
     per launch / its average launch duration.  traffic = HBM bytes
     per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950
     + WRITE_SIZE) when profiles/ holds them for this kernel.  `kernels` lists
     the top kernels by time with their achieved GB/s."""
     with F.KernelClock(ctx) as clk:
-        run_once()
+        run_once()  # single lane: concurrent lanes would inflate each kernel's event span
     stats = clk.stats
     if dump:
         with open(dump, 'w') as f:
@@ -162,7 +175,7 @@ def roofline(ctx, run_once, dump=None):
     pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     if os.path.exists(pmc):
         with open(pmc) as f:
-            t = json.load(f).get(name)
+            t = pmc_lookup(json.load(f), name)
         if t:
             traffic, src = t['hbm_bytes_per_launch'], 'profiles/pmc_traffic.json'
     top = sorted(stats.items(), key=lambda kv: -kv[1]['ms'])[:8]
@@ -280,7 +293,9 @@ def main():
         res['roofline'] = None
         if not a.no_roofline:
             try:
+                ctx.set_sort_lanes(1)
                 res['roofline'] = roofline(ctx, lambda: ctx.direct_sort(ct, N, rots, cfg, shard=(0, 1)), a.clock_json)
+                ctx.set_sort_lanes(a.lanes)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
         if d.world == 1 and not a.no_cpu_baseline:
