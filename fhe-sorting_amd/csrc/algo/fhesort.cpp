@@ -751,6 +751,314 @@ CtPtr DirectSortN::sort(const Ciphertext &x, SignFunc f, const SignConfig &cfg) 
     return rotationIndexCheckN(*rank, x);
 }
 
+// ============================================================== MEHP24 ======
+// Mazzone et al. ranking / sorting (src/mehp24/mehp24_sort.cpp,
+// mehp24_utils.cpp).  A vector of length m lives in an m x m slot matrix
+// (slot = m * row + col).  The reference runs its independent pair compares
+// and indicators on OpenMP threads; here they run stacked: one ciphertext
+// batch per level group through one sign pipeline (chunks of max_stack
+// members), each member bit-identical to the oracle's one-by-one evaluation.
+namespace mehp24 {
+
+namespace {
+size_t lg(size_t x) { return (size_t)ceil_log2((long)x); }  // LOG2 (mehp24_utils.h:25)
+}  // namespace
+
+namespace utils {
+
+std::vector<int> getRotationIndices(size_t m, size_t sub) {  // mehp24_utils.cpp:197-225
+    size_t sz = m;
+    std::vector<int> idx;
+    if (m > sub) {
+        for (size_t i = 0; i < m / sub; ++i) {
+            idx.push_back((int)(i * sub));
+            idx.push_back(-(int)(i * sub));
+        }
+        sz = sub;
+    }
+    for (size_t i = 0; i < lg(sz); ++i) {
+        const int t = (int)(sz * (sz - 1) / (1u << (i + 1)));
+        for (int k : {1 << i, -(1 << i), -(1 << (lg(sz) + i)), t, -t}) idx.push_back(k);
+    }
+    std::vector<int> out;
+    for (int k : idx)
+        if (k != 0 && std::find(out.begin(), out.end(), k) == out.end()) out.push_back(k);
+    return out;
+}
+
+const Plaintext &Masks::get(Engine &cc, int kind, size_t m, size_t idx, int level, int slots) {
+    auto key = std::make_tuple(kind, m, idx, level, slots);
+    auto it = cache.find(key);
+    if (it != cache.end()) return *it->second;
+    std::vector<double> v(m * m, 0.0);
+    for (size_t i = 0; i < m; ++i) v[kind == 0 ? m * idx + i : m * i + idx] = 1.0;  // 0: row idx, 1: column idx
+    return *(cache[key] = cc.encode(v, slots, level));
+}
+
+CtPtr maskRow(Engine &cc, Masks &mk, const Ciphertext &c, size_t m, size_t row) {  // :21-30
+    return cc.mul_plain(c, mk.get(cc, 0, m, row, c.level, c.slots));
+}
+CtPtr maskColumn(Engine &cc, Masks &mk, const Ciphertext &c, size_t m, size_t col) {  // :32-42
+    return cc.mul_plain(c, mk.get(cc, 1, m, col, c.level, c.slots));
+}
+CtPtr replicateRow(Engine &cc, CtPtr c, size_t m) {  // :44-50
+    for (size_t i = 0; i < lg(m); ++i) c = cc.add(*c, *cc.rotate(*c, -(1L << (lg(m) + i))));
+    return c;
+}
+CtPtr replicateColumn(Engine &cc, CtPtr c, size_t m) {  // :52-58
+    for (size_t i = 0; i < lg(m); ++i) c = cc.add(*c, *cc.rotate(*c, -(1L << i)));
+    return c;
+}
+CtPtr sumRows(Engine &cc, Masks &mk, CtPtr c, size_t m, bool mask, size_t row) {  // :60-69
+    c = replicateRow(cc, c, m);
+    return mask ? maskRow(cc, mk, *c, m, row) : c;
+}
+CtPtr sumColumns(Engine &cc, Masks &mk, CtPtr c, size_t m, bool mask) {  // :71-80
+    for (size_t i = 0; i < lg(m); ++i) c = cc.add(*c, *cc.rotate(*c, 1L << i));
+    return mask ? maskColumn(cc, mk, *c, m, 0) : c;
+}
+CtPtr transposeRow(Engine &cc, Masks &mk, CtPtr c, size_t m, bool mask) {  // :82-91
+    for (size_t i = 1; i <= lg(m); ++i) c = cc.add(*c, *cc.rotate(*c, -(long)(m * (m - 1) / (1u << i))));
+    return mask ? maskColumn(cc, mk, *c, m, 0) : c;
+}
+CtPtr transposeColumn(Engine &cc, Masks &mk, CtPtr c, size_t m, bool mask) {  // :93-103
+    for (size_t i = 1; i <= lg(m); ++i) c = cc.add(*c, *cc.rotate(*c, (long)(m * (m - 1) / (1u << i))));
+    return mask ? maskRow(cc, mk, *c, m, 0) : c;
+}
+
+// signAdv (mehp24_utils.cpp:244-260): g3 dg times, f3 df-1 times, then the
+// final 0.5 + f3/2 (output in [0, 1])
+CtPtr signAdv(Engine &cc, CtPtr c, size_t dg, size_t df) {
+    for (size_t d = 0; d < dg; ++d) c = g3(cc, *c);
+    for (size_t d = 0; d + 1 < df; ++d) c = f3(cc, *c);
+    c = odd7(cc, *c, 35.0 / 32.0, -35.0 / 32.0, 21.0 / 32.0, -5.0 / 32.0);
+    return cc.add_const(*c, 0.5);
+}
+
+}  // namespace utils
+
+namespace {
+
+// fn applied member-wise to xs: inputs grouped by level (stacking needs one
+// level; the oracle evaluates each at its own level), chunks of <= max_stack
+// stacked into one batch, results returned as member views in input order
+template <class Fn>
+std::vector<CtPtr> stacked(Engine &cc, const std::vector<CtPtr> &xs, int max_stack, Fn &&fn) {
+    std::vector<CtPtr> out(xs.size());
+    std::map<int, std::vector<size_t>> groups;
+    for (size_t i = 0; i < xs.size(); ++i) groups[xs[i]->level].push_back(i);
+    for (auto &g : groups) {
+        const auto &ids = g.second;
+        for (size_t b = 0; b < ids.size(); b += (size_t)max_stack) {
+            const size_t e = std::min(ids.size(), b + (size_t)max_stack);
+            if (e - b == 1) {
+                out[ids[b]] = fn(*xs[ids[b]]);
+                continue;
+            }
+            std::vector<const Ciphertext *> v;
+            for (size_t i = b; i < e; ++i) v.push_back(xs[ids[i]].get());
+            CtPtr r = fn(*cc.stack(v));
+            for (size_t i = b; i < e; ++i) out[ids[i]] = cc.member(*r, (int)(i - b));
+        }
+    }
+    return out;
+}
+// binary variant: pairs (xs[i], ys[i]); each side must share one level
+template <class Fn>
+std::vector<CtPtr> stacked2(Engine &cc, const std::vector<CtPtr> &xs, const std::vector<CtPtr> &ys, int max_stack,
+                            Fn &&fn) {
+    std::vector<CtPtr> out(xs.size());
+    std::map<std::pair<int, int>, std::vector<size_t>> groups;
+    for (size_t i = 0; i < xs.size(); ++i) groups[{xs[i]->level, ys[i]->level}].push_back(i);
+    for (auto &g : groups) {
+        const auto &ids = g.second;
+        for (size_t b = 0; b < ids.size(); b += (size_t)max_stack) {
+            const size_t e = std::min(ids.size(), b + (size_t)max_stack);
+            if (e - b == 1) {
+                out[ids[b]] = fn(*xs[ids[b]], *ys[ids[b]]);
+                continue;
+            }
+            std::vector<const Ciphertext *> u, v;
+            for (size_t i = b; i < e; ++i) {
+                u.push_back(xs[ids[i]].get());
+                v.push_back(ys[ids[i]].get());
+            }
+            CtPtr r = fn(*cc.stack(u), *cc.stack(v));
+            for (size_t i = b; i < e; ++i) out[ids[i]] = cc.member(*r, (int)(i - b));
+        }
+    }
+    return out;
+}
+// members of a stacked ciphertext
+std::vector<CtPtr> members(Engine &cc, const Ciphertext &s) {
+    std::vector<CtPtr> v;
+    for (int m = 0; m < s.batch; ++m) v.push_back(cc.member(s, m));
+    return v;
+}
+
+// indicatorAdv (mehp24_utils.cpp:166-174) of every x in xs: 1 on |x| < 1/2
+// for x in [-b, b].  The 2|xs| signAdv chains run stacked.
+std::vector<CtPtr> indicators(Engine &cc, const std::vector<CtPtr> &xs, double b, size_t dg, size_t df,
+                              int max_stack) {
+    const size_t n = xs.size();
+    std::vector<CtPtr> c12(2 * n);
+    auto t = stacked(cc, xs, max_stack, [&](const Ciphertext &x) { return cc.mul_const(x, 1.0 / b); });
+    for (size_t i = 0; i < n; ++i) {
+        c12[i] = cc.add_const(*t[i], 0.5 / b);
+        c12[n + i] = cc.add_const(*t[i], -0.5 / b);
+    }
+    t.clear();
+    auto sa = stacked(cc, c12, max_stack, [&](const Ciphertext &x) {
+        return utils::signAdv(cc, cc.clone(x), dg, df);
+    });
+    c12.clear();
+    std::vector<CtPtr> s1(sa.begin(), sa.begin() + n), s2(sa.begin() + n, sa.end());
+    return stacked2(cc, s1, s2, max_stack, [&](const Ciphertext &a, const Ciphertext &c) {
+        return cc.mul(a, *cc.add_const(*cc.negate(c), 1.0));
+    });
+}
+
+}  // namespace
+
+CtPtr indicatorAdv(Engine &cc, const Ciphertext &c, double b, size_t dg, size_t df) {
+    return indicators(cc, {cc.clone(c)}, b, dg, df, 1)[0];
+}
+
+// sortFG, one ciphertext of m values (mehp24_sort.cpp:248-283)
+CtPtr sortFG(const Ciphertext &c0, size_t m, SignFunc f, const SignConfig &cfg, uint32_t dg_i, uint32_t df_i,
+             Engine &cc, int max_stack) {
+    using namespace utils;
+    Masks mk;
+    CtPtr c = cc.clone(c0);
+    CtPtr VR = replicateRow(cc, c, m);
+    CtPtr VC = replicateColumn(cc, transposeRow(cc, mk, c, m, true), m);
+    CtPtr C = Comparison().compare(cc, *VR, *VC, f, cfg);
+    CtPtr R = sumRows(cc, mk, C, m, false, 0);
+    std::vector<double> sub(m * m);
+    for (size_t i = 0; i < m; ++i)
+        for (size_t j = 0; j < m; ++j) sub[i * m + j] = -1.0 * (double)i - 0.5;
+    CtPtr x = cc.add_plain(*R, *cc.encode(sub, R->slots, R->level));
+    CtPtr M = indicators(cc, {x}, (double)m, dg_i, df_i, max_stack)[0];
+    CtPtr S = sumColumns(cc, mk, cc.mul(*M, *VR), m, true);
+    return transposeColumn(cc, mk, S, m, true);
+}
+
+// sortFG over parts of `sub` values (mehp24_sort.cpp:445-604): the part-wise
+// rotation chains run on one stacked batch of all parts, the P(P+1)/2 pair
+// compares and the P^2 indicators stacked
+std::vector<CtPtr> sortFG(const std::vector<CtPtr> &c, size_t sub, SignFunc f, const SignConfig &cfg, uint32_t dg_i,
+                          uint32_t df_i, Engine &cc, int max_stack) {
+    using namespace utils;
+    const size_t P = c.size(), m = sub * P;
+    Masks mk;
+    std::vector<const Ciphertext *> cv;
+    for (auto &x : c) cv.push_back(x.get());
+    CtPtr parts = P > 1 ? cc.stack(cv) : cc.clone(*c[0]);
+    auto R = members(cc, *replicateRow(cc, parts, sub));
+    auto Cc = members(cc, *replicateColumn(cc, transposeRow(cc, mk, parts, sub, true), sub));
+    parts.reset();
+
+    std::vector<CtPtr> A, B;
+    std::vector<std::pair<size_t, size_t>> jk;
+    for (size_t j = 0; j < P; ++j)
+        for (size_t k = j; k < P; ++k) {
+            jk.push_back({j, k});
+            A.push_back(R[j]);
+            B.push_back(Cc[k]);
+        }
+    auto Cjk = stacked2(cc, A, B, max_stack, [&](const Ciphertext &a, const Ciphertext &b) {
+        return Comparison().compare(cc, a, b, f, cfg);
+    });
+    A.clear();
+    B.clear();
+    std::vector<CtPtr> Cv(P), Ch(P);
+    for (size_t i = 0; i < jk.size(); ++i) {
+        const size_t j = jk[i].first, k = jk[i].second;
+        cc.add_inplace(Cv[j], *Cjk[i]);
+        if (j != k) cc.add_inplace(Ch[k], *cc.add_const(*cc.negate(*Cjk[i]), 1.0));
+    }
+    Cjk.clear();
+    std::vector<CtPtr> s(P);
+    for (size_t j = 0; j < P; ++j) s[j] = sumRows(cc, mk, Cv[j], sub, false, 0);
+    if (P > 1) {  // the column sums of every Ch[j], j > 0, as one batch
+        std::vector<const Ciphertext *> hv;
+        for (size_t j = 1; j < P; ++j) hv.push_back(Ch[j].get());
+        CtPtr h = P > 2 ? cc.stack(hv) : cc.clone(*Ch[1]);
+        h = replicateRow(cc, transposeColumn(cc, mk, sumColumns(cc, mk, h, sub, true), sub, true), sub);
+        for (size_t j = 1; j < P; ++j) s[j] = cc.add(*s[j], *cc.member(*h, (int)j - 1));
+    }
+    Cv.clear();
+    Ch.clear();
+
+    std::vector<CtPtr> X, RR;
+    for (size_t j = 0; j < P; ++j) {
+        std::vector<double> sm(sub * sub);
+        for (size_t a = 0; a < sub; ++a)
+            for (size_t b = 0; b < sub; ++b) sm[a * sub + b] = -1.0 * (double)(j * sub + a) - 0.5;
+        std::map<int, PtPtr> by_level;
+        for (size_t k = 0; k < P; ++k) {
+            PtPtr &pt = by_level[s[k]->level];
+            if (!pt) pt = cc.encode(sm, s[k]->slots, s[k]->level);
+            X.push_back(cc.add_plain(*s[k], *pt));
+            RR.push_back(R[k]);
+        }
+    }
+    auto ind = indicators(cc, X, (double)m, dg_i, df_i, max_stack);
+    X.clear();
+    auto prod = stacked2(cc, ind, RR, max_stack, [&](const Ciphertext &a, const Ciphertext &b) { return cc.mul(a, b); });
+    ind.clear();
+    std::vector<CtPtr> acc(P);
+    for (size_t j = 0; j < P; ++j)
+        for (size_t k = 0; k < P; ++k) cc.add_inplace(acc[j], *prod[j * P + k]);
+    prod.clear();
+    std::vector<const Ciphertext *> av;
+    for (auto &x : acc) av.push_back(x.get());
+    CtPtr out = P > 1 ? cc.stack(av) : acc[0];
+    out = transposeColumn(cc, mk, sumColumns(cc, mk, out, sub, true), sub, true);
+    return members(cc, *out);
+}
+
+// sortLargeArrayFG (mehp24_sort.cpp:623-645, utils :265-303): split into
+// parts of `sub` values, sort them as one vector, recombine
+CtPtr sortLargeArrayFG(const Ciphertext &c, size_t total, size_t sub, SignFunc f, const SignConfig &cfg,
+                       uint32_t dg_i, uint32_t df_i, Engine &cc, int max_stack) {
+    const size_t P = total / sub;
+    if (P * sub != total || P == 0) throw std::invalid_argument("sortLargeArrayFG: totalLength % subLength != 0");
+    std::vector<CtPtr> parts(P);
+    for (size_t i = 0; i < P; ++i) {  // splitCiphertext
+        std::vector<double> mask(total, 0.0);
+        for (size_t j = 0; j < sub; ++j) mask[i * sub + j] = 1.0;
+        CtPtr part = cc.mul_plain(c, *cc.encode(mask, c.slots, c.level));
+        if (i > 0) part = cc.rotate(*part, (long)(i * sub));
+        parts[i] = part;
+    }
+    auto sorted = sortFG(parts, sub, f, cfg, dg_i, df_i, cc, max_stack);
+    CtPtr r = sorted[0];  // combineCiphertext
+    for (size_t i = 1; i < P; ++i) r = cc.add(*r, *cc.rotate(*sorted[i], -(long)(i * sub)));
+    return r;
+}
+
+// the reference test's parameters (tests/mehp24/Mehp24SortTest.cpp:26-128)
+Parameters parameters(size_t N) {
+    static const std::map<size_t, int> depth = {{4, 31},   {8, 35},   {16, 35},  {32, 42},   {64, 42},
+                                                {128, 46}, {256, 49}, {512, 57}, {1024, 60}, {2048, 64}};
+    auto it = depth.find(N);
+    if (it == depth.end()) throw std::invalid_argument("mehp24: N must be a power of two in [4, 2048]");
+    Parameters p;
+    p.multDepth = it->second;
+    p.dnum = std::max(3, (p.multDepth + 1 + 14) / 15);  // digits of <= 15 primes (engine limit: alpha <= 16)
+    p.logRingDim = 17;
+    p.scaleModSize = 40;
+    p.cfg = SignConfig(CompositeSignConfig(3, N <= 16 ? 2 : N <= 128 ? 3 : N <= 512 ? 4 : 5, 2));
+    p.dg_i = (uint32_t)((std::log2((double)N) + 1) / 2);
+    p.df_i = 2;
+    p.subLength = N <= 256 ? 0 : 256;
+    p.rotations = utils::getRotationIndices(N);
+    return p;
+}
+
+}  // namespace mehp24
+
 // ================================================== coefficient tables =====
 namespace {
 std::string g_dir = "fhe-sorting_amd/data";

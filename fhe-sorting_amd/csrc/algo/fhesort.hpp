@@ -16,6 +16,7 @@
 #include <map>
 #include <mutex>
 #include <set>
+#include <tuple>
 #include <vector>
 
 #include "../engine/engine.hpp"
@@ -155,6 +156,45 @@ class DirectSort : public DirectSortN {
         directSortSizeParameters(SIZE, multDepth, rotations);
     }
 };
+
+// MEHP24 (Mazzone et al.) ranking / sorting, src/mehp24/mehp24_sort.h and
+// mehp24_utils.h.  max_stack bounds how many independent compares /
+// indicators run stacked in one batch (memory grows with it).
+namespace mehp24 {
+namespace utils {
+// `sub` = sortLargeArrayFG's part length (256 in the reference)
+std::vector<int> getRotationIndices(size_t N, size_t sub = 256);
+// 0/1 row / column masks, encoded once per (kind, m, index, level, slots)
+struct Masks {
+    const Plaintext &get(Engine &cc, int kind, size_t m, size_t idx, int level, int slots);
+    std::map<std::tuple<int, size_t, size_t, int, int>, PtPtr> cache;
+};
+CtPtr maskRow(Engine &cc, Masks &mk, const Ciphertext &c, size_t m, size_t row);
+CtPtr maskColumn(Engine &cc, Masks &mk, const Ciphertext &c, size_t m, size_t col);
+CtPtr replicateRow(Engine &cc, CtPtr c, size_t m);
+CtPtr replicateColumn(Engine &cc, CtPtr c, size_t m);
+CtPtr sumRows(Engine &cc, Masks &mk, CtPtr c, size_t m, bool mask, size_t row);
+CtPtr sumColumns(Engine &cc, Masks &mk, CtPtr c, size_t m, bool mask);
+CtPtr transposeRow(Engine &cc, Masks &mk, CtPtr c, size_t m, bool mask);
+CtPtr transposeColumn(Engine &cc, Masks &mk, CtPtr c, size_t m, bool mask);
+CtPtr signAdv(Engine &cc, CtPtr c, size_t dg, size_t df);
+}  // namespace utils
+CtPtr indicatorAdv(Engine &cc, const Ciphertext &c, double b, size_t dg, size_t df);
+CtPtr sortFG(const Ciphertext &c, size_t vectorLength, SignFunc f, const SignConfig &cfg, uint32_t dg_i,
+             uint32_t df_i, Engine &cc, int max_stack = 32);
+std::vector<CtPtr> sortFG(const std::vector<CtPtr> &c, size_t subVectorLength, SignFunc f, const SignConfig &cfg,
+                          uint32_t dg_i, uint32_t df_i, Engine &cc, int max_stack = 32);
+CtPtr sortLargeArrayFG(const Ciphertext &c, size_t totalLength, size_t subLength, SignFunc f,
+                       const SignConfig &cfg, uint32_t dg_i, uint32_t df_i, Engine &cc, int max_stack = 32);
+struct Parameters {
+    int multDepth = 0, logRingDim = 17, scaleModSize = 40, dnum = 3;
+    SignConfig cfg;
+    uint32_t dg_i = 0, df_i = 2;
+    size_t subLength = 0;  // 0: sortFG on one ciphertext, else sortLargeArrayFG
+    std::vector<int> rotations;
+};
+Parameters parameters(size_t N);
+}  // namespace mehp24
 
 // coefficient tables (generated offline by data/gen_doubled_sinc.py)
 void setCoefficientDir(const std::string &dir);

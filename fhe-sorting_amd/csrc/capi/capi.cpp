@@ -353,6 +353,63 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
     });
 }
 
+int fhe_mehp24_parameters(int N, int *depth, int *log_ring, int *scale_bits, int *dnum, int cfg[3], int *dg_i,
+                          int *df_i, int *sub_length, int32_t *rots, int max_rots) {
+    int count = -1;
+    int rc = guard([&] {
+        auto p = mehp24::parameters((size_t)N);
+        *depth = p.multDepth;
+        *log_ring = p.logRingDim;
+        *scale_bits = p.scaleModSize;
+        *dnum = p.dnum;
+        cfg[0] = p.cfg.compos.n;
+        cfg[1] = p.cfg.compos.dg;
+        cfg[2] = p.cfg.compos.df;
+        *dg_i = (int)p.dg_i;
+        *df_i = (int)p.df_i;
+        *sub_length = (int)p.subLength;
+        count = (int)p.rotations.size();
+        for (int i = 0; i < count && i < max_rots; ++i) rots[i] = p.rotations[i];
+    });
+    return rc == FHE_OK ? count : -rc;
+}
+int fhe_mehp24_rotation_indices(int N, int sub, int32_t *rots, int max_rots) {
+    int count = -1;
+    int rc = guard([&] {
+        if (N < 1 || sub < 1) throw std::invalid_argument("mehp24: N and sub must be positive");
+        auto r = mehp24::utils::getRotationIndices((size_t)N, (size_t)sub);
+        count = (int)r.size();
+        for (int i = 0; i < count && i < max_rots; ++i) rots[i] = r[i];
+    });
+    return rc == FHE_OK ? count : -rc;
+}
+int fhe_mehp24_sort(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i,
+                    fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(x);
+        if (N < 2 || (N & (N - 1))) throw std::invalid_argument("mehp24: N must be a power of two >= 2");
+        const SignConfig cfg = cfgof(n, dg, df);
+        if (sub == 0) {
+            if ((long)N * N != (long)x->p->slots) throw std::invalid_argument("mehp24 sortFG: needs N*N slots");
+            *out = wrap(mehp24::sortFG(*x->p, N, SignFunc::CompositeSign, cfg, dg_i, df_i, *ctx->eng,
+                                       ctx->sort_stack));
+        } else {
+            if (sub < 2 || (sub & (sub - 1)) || N % sub) throw std::invalid_argument("mehp24: bad part length");
+            if ((long)sub * sub != (long)x->p->slots) throw std::invalid_argument("mehp24: needs sub*sub slots");
+            *out = wrap(mehp24::sortLargeArrayFG(*x->p, N, sub, SignFunc::CompositeSign, cfg, dg_i, df_i,
+                                                 *ctx->eng, ctx->sort_stack));
+        }
+    });
+}
+int fhe_mehp24_indicator(fhe_ctx *ctx, const fhe_ct *x, double b, int dg, int df, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(x);
+        *out = wrap(mehp24::indicatorAdv(*ctx->eng, *x->p, b, dg, df));
+    });
+}
+
 int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack) {
     return guard([&] {
         NEED(ctx);

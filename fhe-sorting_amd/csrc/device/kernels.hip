@@ -22,7 +22,6 @@ namespace dev {
 namespace {
 
 constexpr int NT = 256;     // threads per block
-constexpr int MAXSRC = 16;  // max limbs per digit / special primes held in registers
 constexpr int TCH = 64;     // target limbs per thread in basis conversions (all of them: the
                             // per-coefficient prologue then runs once)
 

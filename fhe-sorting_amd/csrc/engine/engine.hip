@@ -6,6 +6,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <stdexcept>
 #include <functional>
 #include <thread>
@@ -26,7 +27,26 @@ namespace fhe {
 using dev::Mod;
 
 // ================================================================ pool ====
+// Every engine (and every fork: concurrent sort lanes) owns a pool; an
+// allocation that fails first releases the cached blocks of all pools of the
+// process, so one lane's cache never starves another lane or a later phase.
+struct Pool;
+std::mutex &pool_registry_mu() {
+    static std::mutex m;
+    return m;
+}
+std::set<Pool *> &pool_registry() {
+    static std::set<Pool *> r;
+    return r;
+}
+void trim_all_pools();
+
 struct Pool {
+    Pool() {
+        std::lock_guard<std::mutex> lk(pool_registry_mu());
+        pool_registry().insert(this);
+    }
+    Pool(const Pool &) = delete;
     std::mutex mu;
     std::multimap<size_t, void *> free_list;
     size_t live = 0, cached = 0, peak = 0;
@@ -48,7 +68,7 @@ struct Pool {
         void *p = nullptr;
         hipError_t e = hipMalloc(&p, bytes);
         if (e != hipSuccess) {
-            trim();
+            trim_all_pools();
             HIP_OK(hipMalloc(&p, bytes));
         }
         std::lock_guard<std::mutex> lk(mu);
@@ -71,9 +91,17 @@ struct Pool {
         cached = 0;
     }
     ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(pool_registry_mu());
+            pool_registry().erase(this);
+        }
         for (auto &kv : free_list) (void)hipFree(kv.second);
     }
 };
+void trim_all_pools() {
+    std::lock_guard<std::mutex> lk(pool_registry_mu());
+    for (Pool *p : pool_registry()) p->trim();
+}
 
 struct DevMem {
     std::shared_ptr<Pool> pool;
@@ -1197,9 +1225,9 @@ struct EventClock final : dev::LaunchClock {
 std::unique_ptr<EventClock> g_clock;
 }  // namespace
 
-void Engine::pool_trim() {
+void Engine::pool_trim() {  // this engine's pool and those of its forks (all pools of the process)
     HIP_OK(hipStreamSynchronize(impl->st));
-    impl->pool->trim();
+    trim_all_pools();
 }
 void Engine::pool_stats(size_t &live, size_t &cached, size_t &peak) const {
     std::lock_guard<std::mutex> lk(impl->pool->mu);

@@ -376,7 +376,7 @@ LevelTables make_level_tables(const Params &P) {
         const size_t W = ell + K;
         const size_t digits = (ell + alpha - 1) / alpha;
         for (size_t j = 0; j < digits; ++j) {
-            const size_t lo = j * alpha, hi = std::min(ell, (j + 1) * alpha), a = hi - lo;
+            const size_t lo = j * alpha, hi = std::min(ell, (j + 1) * alpha);
             T.modup_off[ell].push_back(T.modup.size());
             // layout (device): qhinv[alpha], qhinv_s[alpha], qhat[W][alpha]; rows
             // zero-padded to alpha so every digit runs the same unrolled code

@@ -87,6 +87,10 @@ _SIGS = {
     'fhe_size_parameters': (C.c_int, [C.c_int, ip, ip, C.c_int]),
     'fhe_direct_sort': (C.c_int, [vp, vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_int, vp, vp, PP]),
+    'fhe_mehp24_parameters': (C.c_int, [C.c_int, ip, ip, ip, ip, ip, ip, ip, ip, ip, C.c_int]),
+    'fhe_mehp24_rotation_indices': (C.c_int, [C.c_int, C.c_int, ip, C.c_int]),
+    'fhe_mehp24_sort': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_mehp24_indicator': (C.c_int, [vp, vp, C.c_double, C.c_int, C.c_int, PP]),
     'fhe_comm_get_unique_id': (C.c_int, [C.POINTER(C.c_uint8)]),
     'fhe_comm_init': (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     'fhe_comm_destroy': (C.c_int, [vp]),
@@ -358,6 +362,14 @@ class Context:
                          cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1],
                          C.cast(cb, C.c_void_p) if cb else None, None)
 
+    def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0):
+        """mehp24::sortFG (sub 0; x holds N values in N*N slots) or
+        sortLargeArrayFG with parts of `sub` values (x in sub*sub slots)."""
+        return self._new(lib().fhe_mehp24_sort, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i)
+
+    def mehp24_indicator(self, x, b, dg, df):
+        return self._new(lib().fhe_mehp24_indicator, x.h, b, dg, df)
+
     # multi-GPU -----------------------------------------------------------
     @staticmethod
     def comm_unique_id():
@@ -464,6 +476,28 @@ def size_parameters(N):
     if m < 0:
         raise FheError(-m, lib().fhe_last_error().decode())
     return d.value, [int(x) for x in rots[:m]]
+
+
+def mehp24_parameters(N):
+    """The reference MEHP24 test's parameters for N (Mehp24SortTest.cpp:26-128)."""
+    v = [C.c_int() for _ in range(7)]
+    cfg = np.zeros(3, dtype=np.int32)
+    rots = np.zeros(1024, dtype=np.int32)
+    m = lib().fhe_mehp24_parameters(N, *(C.byref(x) for x in v[:4]), _int(cfg), *(C.byref(x) for x in v[4:]),
+                                    _int(rots), 1024)
+    if m < 0:
+        raise FheError(-m, lib().fhe_last_error().decode())
+    depth, log_ring, scale, dnum, dg_i, df_i, sub = (x.value for x in v)
+    return dict(depth=depth, log_ring=log_ring, scale_bits=scale, dnum=dnum, cfg=tuple(int(c) for c in cfg), dg_i=dg_i,
+                df_i=df_i, sub=sub, rots=[int(x) for x in rots[:m]])
+
+
+def mehp24_rotation_indices(N, sub=256):
+    rots = np.zeros(1024, dtype=np.int32)
+    m = lib().fhe_mehp24_rotation_indices(N, sub, _int(rots), 1024)
+    if m < 0:
+        raise FheError(-m, lib().fhe_last_error().decode())
+    return [int(x) for x in rots[:m]]
 
 
 def decompose(N, rots, rotation, wrapN, algo):

@@ -173,6 +173,26 @@ int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack);
  * so independent batch stacks overlap on the GPU.  Results do not depend on it. */
 int fhe_set_sort_lanes(fhe_ctx *ctx, int lanes);
 
+/* ------------------------------------------------------------ MEHP24 sort */
+/* the reference's MEHP24 test parameters for N (tests/mehp24/Mehp24SortTest.cpp:26-128)
+ * and mehp24::utils::getRotationIndices(N) (src/mehp24/mehp24_utils.cpp:197-225):
+ * depth, ring log, scale bits, key-switch digits (dnum: digits of <= 15 primes),
+ * CompositeSign (n, dg, df), indicator (dg_i, df_i), part length (0: one-ciphertext
+ * sortFG).  Returns #rotations. */
+int fhe_mehp24_parameters(int N, int *mult_depth, int *log_ring, int *scale_bits, int *dnum, int cfg[3],
+                          int *dg_i, int *df_i, int *sub_length, int32_t *rots, int max_rots);
+/* getRotationIndices with part length `sub` (the reference fixes 256) */
+int fhe_mehp24_rotation_indices(int N, int sub, int32_t *rots, int max_rots);
+/* sub == 0: mehp24::sortFG(c, N, CompositeSign, cfg, comp, dg_i, df_i, cc)
+ *           (src/mehp24/mehp24_sort.cpp:248-283), x holds N values in N*N slots;
+ * sub > 0:  mehp24::sortLargeArrayFG(c, N, sub, ...) (mehp24_sort.cpp:623-645),
+ *           x holds N values in sub*sub slots.
+ * Independent compares / indicators run stacked (fhe_set_sort_stack bounds it). */
+int fhe_mehp24_sort(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i,
+                    fhe_ct **out);
+/* mehp24::utils::indicatorAdv(c, b, dg, df) (src/mehp24/mehp24_utils.cpp:166-174) */
+int fhe_mehp24_indicator(fhe_ctx *ctx, const fhe_ct *x, double b, int dg, int df, fhe_ct **out);
+
 /* ------------------------------------------------------ multi-GPU (RCCL) */
 int fhe_comm_get_unique_id(uint8_t id[128]);
 int fhe_comm_init(fhe_ctx *ctx, const uint8_t id[128], int rank, int world);

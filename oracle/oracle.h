@@ -309,4 +309,17 @@ class DirectSort {
 const std::vector<double> &doubled_sinc_coefficients(int N);
 void set_coefficient_dir(const std::string &dir);
 
+// MEHP24 (Mazzone et al.) ranking / sorting, src/mehp24/*
+namespace mehp24 {
+std::vector<int> rotation_indices(size_t m, size_t sub = 256);
+CtPtr sign_adv(Context &cc, CtPtr c, size_t dg, size_t df);
+CtPtr indicator_adv(Context &cc, const CtPtr &c, double b, size_t dg, size_t df);
+CtPtr sort_fg(Context &cc, const Ciphertext &c, size_t m, SignFunc f, const SignConfig &cfg, size_t dg_i,
+              size_t df_i);
+std::vector<CtPtr> sort_fg_multi(Context &cc, const std::vector<CtPtr> &c, size_t sub, SignFunc f,
+                                 const SignConfig &cfg, size_t dg_i, size_t df_i);
+CtPtr sort_large_fg(Context &cc, const Ciphertext &c, size_t total, size_t sub, SignFunc f, const SignConfig &cfg,
+                    size_t dg_i, size_t df_i);
+}  // namespace mehp24
+
 }  // namespace oracle

@@ -575,6 +575,178 @@ CtPtr DirectSort::sort(const Ciphertext &x, SignFunc f, const SignConfig &cfg) {
 }
 
 // ============================================= coefficient data ============
+// ================================================================ MEHP24 ======
+// Mazzone et al. ranking / sorting (src/mehp24/mehp24_sort.cpp,
+// mehp24_utils.cpp).  A vector of length m lives in an m x m slot matrix
+// (row-major, slot = m * row + col); rotations and masks move it between row
+// and column layouts.  Masks are plaintext products (one level each), as the
+// reference's EvalMult(ct, pt).
+namespace mehp24 {
+
+namespace {
+size_t lg(size_t x) { return (size_t)ceil_log2((long)x); }  // LOG2 (mehp24_utils.h:25)
+CtPtr rot(Context &cc, const CtPtr &c, long k) { return cc.rotate(*c, k); }
+CtPtr times_mask(Context &cc, const CtPtr &c, const std::vector<double> &m) {
+    return cc.mul_plain(*c, cc.encode(m, c->slots, c->level));
+}
+}  // namespace
+
+// `sub` is the part length of sortLargeArrayFG (256 in the reference; smaller
+// values exercise the split path at test sizes)
+std::vector<int> rotation_indices(size_t m, size_t sub) {  // mehp24_utils.cpp:197-225
+    size_t sz = m;
+    std::vector<int> idx;
+    if (m > sub) {
+        for (size_t i = 0; i < m / sub; ++i) {
+            idx.push_back((int)(i * sub));
+            idx.push_back(-(int)(i * sub));
+        }
+        sz = sub;
+    }
+    for (size_t i = 0; i < lg(sz); ++i) {
+        idx.push_back(1 << i);
+        idx.push_back(-(1 << i));
+        idx.push_back(-(1 << (lg(sz) + i)));
+        const int t = (int)(sz * (sz - 1) / (1u << (i + 1)));
+        idx.push_back(t);
+        idx.push_back(-t);
+    }
+    std::vector<int> out;
+    for (int k : idx)
+        if (k != 0 && std::find(out.begin(), out.end(), k) == out.end()) out.push_back(k);
+    return out;
+}
+
+CtPtr mask_row(Context &cc, const CtPtr &c, size_t m, size_t row) {  // :21-30
+    std::vector<double> mk(m * m, 0.0);
+    for (size_t i = 0; i < m; ++i) mk[m * row + i] = 1.0;
+    return times_mask(cc, c, mk);
+}
+CtPtr mask_column(Context &cc, const CtPtr &c, size_t m, size_t col) {  // :32-42
+    std::vector<double> mk(m * m, 0.0);
+    for (size_t i = 0; i < m; ++i) mk[m * i + col] = 1.0;
+    return times_mask(cc, c, mk);
+}
+CtPtr replicate_row(Context &cc, CtPtr c, size_t m) {  // :44-50
+    for (size_t i = 0; i < lg(m); ++i) c = cc.add(*c, *rot(cc, c, -(1L << (lg(m) + i))));
+    return c;
+}
+CtPtr replicate_column(Context &cc, CtPtr c, size_t m) {  // :52-58
+    for (size_t i = 0; i < lg(m); ++i) c = cc.add(*c, *rot(cc, c, -(1L << i)));
+    return c;
+}
+CtPtr sum_rows(Context &cc, CtPtr c, size_t m, bool mask, size_t row) {  // :60-69
+    c = replicate_row(cc, c, m);
+    return mask ? mask_row(cc, c, m, row) : c;
+}
+CtPtr sum_columns(Context &cc, CtPtr c, size_t m, bool mask) {  // :71-80
+    for (size_t i = 0; i < lg(m); ++i) c = cc.add(*c, *rot(cc, c, 1L << i));
+    return mask ? mask_column(cc, c, m, 0) : c;
+}
+CtPtr transpose_row(Context &cc, CtPtr c, size_t m, bool mask) {  // :82-91
+    for (size_t i = 1; i <= lg(m); ++i) c = cc.add(*c, *rot(cc, c, -(long)(m * (m - 1) / (1u << i))));
+    return mask ? mask_column(cc, c, m, 0) : c;
+}
+CtPtr transpose_column(Context &cc, CtPtr c, size_t m, bool mask) {  // :93-103
+    for (size_t i = 1; i <= lg(m); ++i) c = cc.add(*c, *rot(cc, c, (long)(m * (m - 1) / (1u << i))));
+    return mask ? mask_row(cc, c, m, 0) : c;
+}
+
+// signAdv (mehp24_utils.cpp:244-260): g3 dg times, f3 df-1 times, then
+// 0.5 + f3 / 2 -- output in [0, 1]
+CtPtr sign_adv(Context &cc, CtPtr c, size_t dg, size_t df) {
+    for (size_t d = 0; d < dg; ++d) c = g3(cc, *c);
+    for (size_t d = 0; d + 1 < df; ++d) c = f3(cc, *c);
+    c = odd7(cc, *c, 35.0 / 32.0, -35.0 / 32.0, 21.0 / 32.0, -5.0 / 32.0);
+    return cc.add_const(*c, 0.5);
+}
+// indicatorAdv (mehp24_utils.cpp:166-174): 1 on |x| < 1/2 for x in [-b, b]
+CtPtr indicator_adv(Context &cc, const CtPtr &c, double b, size_t dg, size_t df) {
+    CtPtr t = cc.mul_const(*c, 1.0 / b);
+    CtPtr c1 = sign_adv(cc, cc.add_const(*t, 0.5 / b), dg, df);
+    CtPtr c2 = sign_adv(cc, cc.add_const(*t, -0.5 / b), dg, df);
+    return cc.mul(*c1, *cc.add_const(*cc.negate(*c2), 1.0));
+}
+
+// sortFG, one ciphertext of m values in an m x m matrix (mehp24_sort.cpp:248-283)
+CtPtr sort_fg(Context &cc, const Ciphertext &c0, size_t m, SignFunc f, const SignConfig &cfg, size_t dg_i,
+              size_t df_i) {
+    CtPtr c = cc.clone(c0);
+    CtPtr VR = replicate_row(cc, c, m);
+    CtPtr VC = replicate_column(cc, transpose_row(cc, c, m, true), m);
+    CtPtr C = compare(cc, *VR, *VC, f, cfg);
+    CtPtr R = sum_rows(cc, C, m, false, 0);
+    std::vector<double> sub(m * m);
+    for (size_t i = 0; i < m; ++i)
+        for (size_t j = 0; j < m; ++j) sub[i * m + j] = -1.0 * (double)i - 0.5;
+    CtPtr M = indicator_adv(cc, cc.add_plain(*R, cc.encode(sub, R->slots, R->level)), (double)m, dg_i, df_i);
+    CtPtr S = sum_columns(cc, cc.mul(*M, *VR), m, true);
+    return transpose_column(cc, S, m, true);
+}
+
+// sortFG over parts of `sub` values each (mehp24_sort.cpp:445-645)
+std::vector<CtPtr> sort_fg_multi(Context &cc, const std::vector<CtPtr> &c, size_t sub, SignFunc f,
+                                 const SignConfig &cfg, size_t dg_i, size_t df_i) {
+    const size_t P = c.size(), m = sub * P;
+    std::vector<CtPtr> R(P), Cc(P);
+    for (size_t j = 0; j < P; ++j) {
+        R[j] = replicate_row(cc, c[j], sub);
+        Cc[j] = replicate_column(cc, transpose_row(cc, c[j], sub, true), sub);
+    }
+    std::vector<CtPtr> Cv(P), Ch(P);
+    for (size_t j = 0; j < P; ++j)
+        for (size_t k = j; k < P; ++k) {  // pair order of :480-495
+            CtPtr Cjk = compare(cc, *R[j], *Cc[k], f, cfg);
+            cc.add_inplace(Cv[j], *Cjk);
+            if (j != k) cc.add_inplace(Ch[k], *cc.add_const(*cc.negate(*Cjk), 1.0));
+        }
+    std::vector<CtPtr> s(P);
+    for (size_t j = 0; j < P; ++j) {
+        s[j] = sum_rows(cc, Cv[j], sub, false, 0);
+        if (j > 0) {
+            CtPtr h = sum_columns(cc, Ch[j], sub, true);
+            h = transpose_column(cc, h, sub, true);
+            h = replicate_row(cc, h, sub);
+            s[j] = cc.add(*s[j], *h);
+        }
+    }
+    std::vector<CtPtr> out(P);
+    for (size_t j = 0; j < P; ++j) {
+        std::vector<double> sm(sub * sub);
+        for (size_t a = 0; a < sub; ++a)
+            for (size_t b = 0; b < sub; ++b) sm[a * sub + b] = -1.0 * (double)(j * sub + a) - 0.5;
+        CtPtr acc;
+        for (size_t k = 0; k < P; ++k) {
+            CtPtr x = cc.add_plain(*s[k], cc.encode(sm, s[k]->slots, s[k]->level));
+            CtPtr ind = cc.mul(*indicator_adv(cc, x, (double)m, dg_i, df_i), *R[k]);
+            cc.add_inplace(acc, *ind);
+        }
+        out[j] = transpose_column(cc, sum_columns(cc, acc, sub, true), sub, true);
+    }
+    return out;
+}
+
+// sortLargeArrayFG (mehp24_sort.cpp:623-645 with utils :265-303): split into
+// parts of `sub` values, sort them as one vector, recombine
+CtPtr sort_large_fg(Context &cc, const Ciphertext &c, size_t total, size_t sub, SignFunc f, const SignConfig &cfg,
+                    size_t dg_i, size_t df_i) {
+    const size_t P = total / sub;
+    std::vector<CtPtr> parts(P);
+    for (size_t i = 0; i < P; ++i) {
+        std::vector<double> mk(total, 0.0);
+        for (size_t j = 0; j < sub; ++j) mk[i * sub + j] = 1.0;
+        CtPtr part = cc.mul_plain(c, cc.encode(mk, c.slots, c.level));
+        if (i > 0) part = cc.rotate(*part, (long)(i * sub));
+        parts[i] = part;
+    }
+    auto sorted = sort_fg_multi(cc, parts, sub, f, cfg, dg_i, df_i);
+    CtPtr r = sorted[0];
+    for (size_t i = 1; i < P; ++i) r = cc.add(*r, *cc.rotate(*sorted[i], -(long)(i * sub)));
+    return r;
+}
+
+}  // namespace mehp24
+
 static std::string g_coeff_dir = "fhe-sorting_amd/data";
 static std::map<int, std::vector<double>> g_coeff_cache;
 static std::mutex g_coeff_mu;

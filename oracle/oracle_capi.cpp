@@ -249,6 +249,28 @@ void *orc_direct_sort(void *c, void *x, void *rank, int N, const int *rots, int 
     }, (void *)nullptr);
 }
 
+// MEHP24: sub == 0 -> sortFG on one ciphertext; otherwise sortLargeArrayFG
+// with parts of `sub` values (mehp24_sort.h sortFG / sortLargeArrayFG)
+void *orc_mehp24_sort(void *c, void *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i) {
+    return guard([&]() -> void * {
+        auto cfg = cfg3(n, dg, df);
+        if (sub == 0) return wrap(mehp24::sort_fg(*CTX, CT(x), N, SignFunc::CompositeSign, cfg, dg_i, df_i));
+        return wrap(mehp24::sort_large_fg(*CTX, CT(x), N, sub, SignFunc::CompositeSign, cfg, dg_i, df_i));
+    }, (void *)nullptr);
+}
+void *orc_mehp24_indicator(void *c, void *a, double b, int dg, int df) {
+    return guard([&]() -> void * { return wrap(mehp24::indicator_adv(*CTX, CTX->clone(CT(a)), b, dg, df)); },
+                 (void *)nullptr);
+}
+int orc_mehp24_rotation_indices(int N, int sub, int *rots, int maxr) {
+    return guard([&]() {
+        auto r = mehp24::rotation_indices(N, sub);
+        int m = std::min((int)r.size(), maxr);
+        for (int i = 0; i < m; ++i) rots[i] = r[i];
+        return (int)r.size();
+    }, -1);
+}
+
 int orc_size_parameters(int N, int *multDepth, int *rots, int maxr) {
     return guard([&]() {
         std::vector<int> r;

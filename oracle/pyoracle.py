@@ -75,6 +75,9 @@ def lib():
             'orc_direct_sort': (vp, [vp, vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.c_int, C.c_int, C.c_int, vp, vp]),
             'orc_size_parameters': (C.c_int, [C.c_int, ip, ip, C.c_int]),
+            'orc_mehp24_sort': (vp, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+            'orc_mehp24_indicator': (vp, [vp, vp, C.c_double, C.c_int, C.c_int]),
+            'orc_mehp24_rotation_indices': (C.c_int, [C.c_int, C.c_int, ip, C.c_int]),
             'orc_decompose': (C.c_int, [C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip, C.c_int]),
             'orc_set_coeff_dir': (None, [C.c_char_p]),
             'orc_doubled_sinc': (C.c_int, [C.c_int, dp, C.c_int]),
@@ -306,6 +309,12 @@ class Context:
                                   C.cast(cb, C.c_void_p) if cb else None, None)
         return Ct(self, h)
 
+    def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0):
+        return Ct(self, lib().orc_mehp24_sort(self.h, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i))
+
+    def mehp24_indicator(self, a, b, dg, df):
+        return Ct(self, lib().orc_mehp24_indicator(self.h, a.h, b, dg, df))
+
     # kernel level -----------------------------------------------------
     def ntt(self, prime_index, data, inverse=False):
         d = np.ascontiguousarray(data, dtype=np.uint64).copy()
@@ -356,6 +365,14 @@ def size_parameters(N):
     if m < 0:
         raise ValueError(lib().orc_last_error().decode())
     return d.value, [int(x) for x in rots[:m]]
+
+
+def mehp24_rotation_indices(N, sub=256):
+    rots = np.zeros(1024, dtype=np.int32)
+    m = lib().orc_mehp24_rotation_indices(N, sub, _int(rots), 1024)
+    if m < 0:
+        raise ValueError(lib().orc_last_error().decode())
+    return [int(x) for x in rots[:m]]
 
 
 def decompose(N, rots, rotation, wrapN, algo):

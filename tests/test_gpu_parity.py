@@ -40,7 +40,7 @@ def test_params_identical(pair):
     assert np.array_equal(orc.delta, gpu.delta)
 
 
-@pytest.mark.parametrize('logN', [12, 13, 16])
+@pytest.mark.parametrize('logN', [12, 13, 16, 17])
 def test_ntt_matches_oracle(logN):
     orc = O.Context(logN, 3, 40, 60, 3, seed=1, keygen=False)
     gpu = F.Context(logN, 3, 40, 60, 3, seed=1, keygen=False)
