@@ -1046,7 +1046,8 @@ Parameters parameters(size_t N) {
     if (it == depth.end()) throw std::invalid_argument("mehp24: N must be a power of two in [4, 2048]");
     Parameters p;
     p.multDepth = it->second;
-    p.dnum = std::max(3, (p.multDepth + 1 + 14) / 15);  // digits of <= 15 primes (engine limit: alpha <= 16)
+    p.levels = p.multDepth + 1;  // + the FLEXIBLEAUTOEXT encryption level (Engine::encrypt_ext)
+    p.dnum = std::max(3, (p.levels + 1 + 14) / 15);  // digits of <= 15 primes (engine limit: alpha <= 16)
     p.logRingDim = 17;
     p.scaleModSize = 40;
     p.cfg = SignConfig(CompositeSignConfig(3, N <= 16 ? 2 : N <= 128 ? 3 : N <= 512 ? 4 : 5, 2));

@@ -188,6 +188,7 @@ CtPtr sortLargeArrayFG(const Ciphertext &c, size_t totalLength, size_t subLength
                        const SignConfig &cfg, uint32_t dg_i, uint32_t df_i, Engine &cc, int max_stack = 32);
 struct Parameters {
     int multDepth = 0, logRingDim = 17, scaleModSize = 40, dnum = 3;
+    int levels = 0;  // context depth: multDepth + 1 (input encrypted with encrypt_ext)
     SignConfig cfg;
     uint32_t dg_i = 0, df_i = 2;
     size_t subLength = 0;  // 0: sortFG on one ciphertext, else sortLargeArrayFG

@@ -127,6 +127,9 @@ uint64_t fhe_key_bytes(fhe_ctx *ctx) { return ctx ? ctx->eng->key_bytes() : 0; }
 int fhe_encrypt(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_ct **out) {
     return guard([&] { *out = wrap(ctx->eng->encrypt(std::vector<double>(v, v + len), slots, level)); });
 }
+int fhe_encrypt_ext(fhe_ctx *ctx, const double *v, int len, int slots, fhe_ct **out) {
+    return guard([&] { *out = wrap(ctx->eng->encrypt_ext(std::vector<double>(v, v + len), slots)); });
+}
 int fhe_decrypt(fhe_ctx *ctx, const fhe_ct *ct, double *out) {
     return guard([&] {
         auto v = ctx->eng->decrypt(*ct->p);

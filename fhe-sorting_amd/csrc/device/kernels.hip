@@ -364,23 +364,42 @@ __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const
 
 // grid: x = n / NT, y = ceil(ell / TCH), z = segment.  KT = K special primes;
 // phat [nq][KT] (the constants of one target contiguous: one scalar burst)
+// Exact centred conversion: y_k = [x P_k^-1]_{p_k}, x mod P = sum_k y_k P_k -
+// v P with v = round(sum_k y_k / p_k) (fp64, fixed order; oracle: moddown), so
+// ModDown rounds x / P to nearest instead of flooring with a 0..K overshoot --
+// that overshoot is a biased error which, multiplied by s, concentrates in a
+// few slots.
+template <int KT>
+__device__ __forceinline__ u64 centre_count(const u64 (&y)[KT], const double *pinvd) {
+    double t = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) t = t + (double)y[kk] * pinvd[kk];
+    return (u64)(t + 0.5);
+}
 template <int KT>
 __global__ __launch_bounds__(NT) void k_moddown_convert(u64 *conv, const u64 *pc, int ell, int nq, size_t seg_in,
                                                         size_t seg_out, const u64 *phinv, const u64 *phinv_s,
-                                                        const u64 *phat, const Mod *mods, int logN) {
+                                                        const u64 *phat, const u64 *pmod, const double *pinvd,
+                                                        const Mod *mods, int logN) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
     const u64 *src = pc + (size_t)blockIdx.z * seg_in;
     u64 *dst = conv + (size_t)blockIdx.z * seg_out;
+    u64 y[KT];
     Split30 v[KT];
 #pragma unroll
-    for (int i = 0; i < KT; ++i) v[i] = split30(mul_shoup(src[(size_t)i * n + k], phinv[i], phinv_s[i], mods[nq + i].q));
+    for (int i = 0; i < KT; ++i) {
+        y[i] = mul_shoup(src[(size_t)i * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+        v[i] = split30(y[i]);
+    }
+    const Split30 cnt = split30(centre_count<KT>(y, pinvd));
     const int i0 = blockIdx.y * TCH;
     for (int i = i0; i < i0 + TCH && i < ell; ++i) {
         Acc4 acc;
 #pragma unroll
         for (int kk = 0; kk < KT; ++kk) mac4(acc, v[kk], split30(phat[(size_t)i * KT + kk]));
+        mac4(acc, cnt, split30(mods[i].q - pmod[i]));  // - v P
         dst[(size_t)i * n + k] = reduce4(acc, mods[i]);
     }
 }
@@ -421,23 +440,29 @@ template <int KT>
 __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int nq,
                                                                 size_t seg_acc, size_t seg_corr, const u64 *phinv,
                                                                 const u64 *phinv_s, const u64 *phat, const u64 *pinv,
-                                                                const u64 *pinv_s, const u64 *pmod, const Mod *mods,
-                                                                int logN) {
+                                                                const u64 *pinv_s, const u64 *pmod, const double *pinvd,
+                                                                const Mod *mods, int logN) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
     const int last = ell - 1;
     const u64 *src = acc + (size_t)blockIdx.z * seg_acc + (size_t)last * n;
     u64 *dst = corr + (size_t)blockIdx.z * seg_corr;
+    u64 yk[KT];
     Split30 v[KT];
 #pragma unroll
-    for (int i = 0; i < KT; ++i)
-        v[i] = split30(mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q));
+    for (int i = 0; i < KT; ++i) {
+        yk[i] = mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+        v[i] = split30(yk[i]);
+    }
+    const u64 cntv = centre_count<KT>(yk, pinvd);  // exact centred Conv (k_moddown_convert)
+    const Split30 cnt = split30(cntv);
     const Mod ml = mods[last];
     const u64 ql = ml.q;
     Acc4 cacc;
 #pragma unroll
     for (int kk = 0; kk < KT; ++kk) mac4(cacc, v[kk], split30(phat[(size_t)last * KT + kk]));
+    mac4(cacc, cnt, split30(ql - pmod[last]));
     const u64 cl = reduce4(cacc, ml);
     const u64 y = mul_shoup(sub_mod(src[k], cl, ql), pinv[last], pinv_s[last], ql);
     const bool neg = y > (ql >> 1);
@@ -446,8 +471,10 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const
         const Mod mi = mods[i];
         // centred lift of y: q_last / 2 < q_i (checked at context creation)
         const u64 lift = neg ? mi.q - (ql - y) : y;
+        // P (lift - v): one term, so K + 1 terms stay within Acc4's 16
+        const u64 lv = lift >= cntv ? lift - cntv : lift + mi.q - cntv;
         Acc4 a4;
-        mac4(a4, split30(lift), split30(pmod[i]));
+        mac4(a4, split30(lv), split30(pmod[i]));
 #pragma unroll
         for (int kk = 0; kk < KT; ++kk) mac4(a4, v[kk], split30(phat[(size_t)i * KT + kk]));
         dst[(size_t)i * n + k] = reduce4(a4, mi);
@@ -630,24 +657,26 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
 }
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
-                             const u64 *pinv_s, const u64 *pmod, const Mod *mods, int logN, hipStream_t st) {
+                             const u64 *pinv_s, const u64 *pmod, const double *pinvd, const Mod *mods, int logN,
+                             hipStream_t st) {
     if (ell <= 1) return;
     const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
     dispatch_int<1, 15>(K, [&](auto c) {
         constexpr int KT = decltype(c)::value;
         launch_clocked("k_moddown_rescale_convert", B, k_moddown_rescale_convert<KT>,
                        pt_grid(logN, (ell - 1 + TCH - 1) / TCH, segs), dim3(NT), st, corr, acc, ell, nq, seg_acc,
-                       seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, mods, logN);
+                       seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, pinvd, mods, logN);
     });
 }
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
-                     const u64 *phinv, const u64 *phinv_s, const u64 *phat, const Mod *mods, int logN,
-                     hipStream_t st) {
+                     const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pmod, const double *pinvd,
+                     const Mod *mods, int logN, hipStream_t st) {
     const double B = 8.0 * segs * (double)(K + ell) * ((size_t)1 << logN);
     dispatch_int<1, 15>(K, [&](auto c) {
         constexpr int KT = decltype(c)::value;
         launch_clocked("k_moddown_convert", B, k_moddown_convert<KT>, pt_grid(logN, (ell + TCH - 1) / TCH, segs),
-                       dim3(NT), st, conv, pc, ell, nq, seg_in, seg_out, phinv, phinv_s, phat, mods, logN);
+                       dim3(NT), st, conv, pc, ell, nq, seg_in, seg_out, phinv, phinv_s, phat, pmod, pinvd, mods,
+                       logN);
     });
 }
 void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,

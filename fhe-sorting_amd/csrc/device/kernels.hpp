@@ -160,11 +160,13 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
 // from acc [segs][W][n] whose limbs ell-1 .. W-1 are in coefficient form
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
-                             const u64 *pinv_s, const u64 *pmod, const Mod *mods, int logN, hipStream_t st);
-// conv[s][i][k] = sum_k' (pc[s][k'] * phinv_k') * phat[i][k'] mod q_i  for i < ell
+                             const u64 *pinv_s, const u64 *pmod, const double *pinvd, const Mod *mods, int logN,
+                             hipStream_t st);
+// conv[s][i][k] = (sum_k' y_k' phat[i][k'] - v P) mod q_i for i < ell, y_k' =
+// pc[s][k'] * phinv_k', v = round(sum_k' y_k' pinvd_k'): the centred Conv_{P->q_i}
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
-                     const u64 *phinv, const u64 *phinv_s, const u64 *phat, const Mod *mods, int logN,
-                     hipStream_t st);
+                     const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pmod, const double *pinvd,
+                     const Mod *mods, int logN, hipStream_t st);
 // out[s][i] = (acc[s][i] - conv[s][i]) * Pinv_i (+ add[s/2][i] on even s, i.e. c0 of each member)
 void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,
                     size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s, const Mod *mods, int logN,

@@ -154,8 +154,8 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
     for (int s = 0; s < EB; ++s) {
         const int hb = EB - 1 - s;  // pair bit in r
 #pragma unroll
-        for (int r0 = 0; r0 < E; ++r0) {
-            if (r0 & (1 << hb)) continue;
+        for (int b = 0; b < E / 2; ++b) {  // butterfly b: r0 = b with a 0 inserted at bit hb
+            const int r0 = ((b >> hb) << (hb + 1)) | (b & ((1 << hb) - 1));
             const int idx0 = t + T * r0;
             const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
             const size_t wi = ((size_t)1 << (S0 + s)) + i;
@@ -324,8 +324,8 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
     for (int s = RB; s < PB; ++s) {
         const int hb = s - RB;
 #pragma unroll
-        for (int r0 = 0; r0 < E; ++r0) {
-            if (r0 & (1 << hb)) continue;
+        for (int b = 0; b < E / 2; ++b) {
+            const int r0 = ((b >> hb) << (hb + 1)) | (b & ((1 << hb) - 1));
             const int idx0 = t + T * r0;
             const int sg = SG0 + s;
             const size_t j = COLS ? 0 : tid_global * LEN;

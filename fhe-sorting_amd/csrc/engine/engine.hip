@@ -138,6 +138,7 @@ struct Engine::Impl {
     u64 *phinv = nullptr, *phinv_s = nullptr, *phat = nullptr, *pinv = nullptr, *pinv_s = nullptr;
     u64 *qlinv = nullptr, *qlinv_s = nullptr;
     u64 *pmod = nullptr, *pmod_s = nullptr, *pqlinv = nullptr, *pqlinv_s = nullptr;
+    double *pinvd = nullptr;
     int *modup_smap = nullptr, *modup_pmap = nullptr;
 
     // keys
@@ -216,7 +217,7 @@ struct Engine::Impl {
         auto convm = alloc((size_t)segs * ell * nn * 8);
         u64 *conv = static_cast<u64 *>(convm->p);
         dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, segs, phinv, phinv_s,
-                             phat, mods, P.logN, st);
+                             phat, pmod, pinvd, mods, P.logN, st);
         dev::ntt_forward(conv, (int)ell, segs, ell * nn, nullptr, T, st);
         dev::moddown_finish(out, acc, conv, add, (int)ell, segs, ell * nn, W * nn, add_stride, pinv, pinv_s, mods,
                             P.logN, st);
@@ -250,7 +251,7 @@ struct Engine::Impl {
         auto corrm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *corr = static_cast<u64 *>(corrm->p);
         dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, segs, phinv,
-                                     phinv_s, phat, pinv, pinv_s, pmod, mods, P.logN, st);
+                                     phinv_s, phat, pinv, pinv_s, pmod, pinvd, mods, P.logN, st);
         // forward NTT of corr whose row pass finishes (acc + d P - corr) (P q_last)^-1 into `out`
         dev::NttFuse F;
         F.out = out;
@@ -363,6 +364,7 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.qlinv = I.upload_static(I.LT.qlinv);
     I.qlinv_s = I.upload_static(I.LT.qlinv_s);
     I.pmod = I.upload_static(I.LT.pmod);
+    I.pinvd = I.upload_static(I.LT.pinvd);
     I.modup_smap = I.upload_static(I.LT.modup_smap);
     I.modup_pmap = I.upload_static(I.LT.modup_pmap);
     I.pmod_s = I.upload_static(I.LT.pmod_s);
@@ -595,9 +597,12 @@ size_t Engine::key_bytes() const {
 
 // ==================================================== encode / encrypt ====
 PtPtr Engine::encode(const std::vector<double> &v, int slots, int level) {
+    return encode_scaled(v, slots, level, impl->P.delta[level]);
+}
+PtPtr Engine::encode_scaled(const std::vector<double> &v, int slots, int level, double scale) {
     auto &I = *impl;
     const size_t n = I.n(), ell = I.P.limbs_at(level);
-    auto coef = host::encode_coeffs(v, n, slots, I.P.delta[level]);
+    auto coef = host::encode_coeffs(v, n, slots, scale);
     auto cm = I.alloc(n * 8);
     HIP_OK(hipMemcpyAsync(cm->p, coef.data(), n * 8, hipMemcpyHostToDevice, I.st));
     auto pt = std::make_shared<Plaintext>();
@@ -605,7 +610,7 @@ PtPtr Engine::encode(const std::vector<double> &v, int slots, int level) {
     pt->data = static_cast<u64 *>(pt->mem->p);
     pt->level = level;
     pt->slots = slots;
-    pt->scale = I.P.delta[level];
+    pt->scale = scale;
     pt->limbs = ell;
     dev::ew_signed_to_rns(pt->data, static_cast<int64_t *>(cm->p), (int)ell, nullptr, I.mods, I.P.logN, I.st);
     dev::ntt_forward(pt->data, (int)ell, 1, 0, nullptr, I.T, I.st);
@@ -649,6 +654,22 @@ CtPtr Engine::encrypt_pt(const Plaintext &pt) {
 
 CtPtr Engine::encrypt(const std::vector<double> &v, int slots, int level) {
     return encrypt_pt(*encode(v, slots, level));
+}
+
+// FLEXIBLEAUTOEXT-style fresh encryption (oracle: Context::encrypt_ext): encode
+// at Delta_1 on the level-0 basis, times q_L, encrypt, rescale by q_L -- the
+// encryption noise shrinks by q_L; result at level 1, scale Delta_1
+CtPtr Engine::encrypt_ext(const std::vector<double> &v, int slots) {
+    auto &I = *impl;
+    if (I.P.L < 1) throw std::runtime_error("encrypt_ext: needs one extra level");
+    PtPtr pt = encode_scaled(v, slots, 0, I.P.delta[1]);
+    const u64 qL = I.P.primes[I.P.nq() - 1];
+    dev::ew_mul_scalar(pt->data, pt->data, (int64_t)qL, (int)pt->limbs, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN,
+                       I.st);
+    pt->scale = I.P.delta[1] * (double)qL;
+    CtPtr r = rescale(*encrypt_pt(*pt));
+    r->scale = I.P.delta[1];
+    return r;
 }
 
 std::vector<double> Engine::decrypt(const Ciphertext &ct) {
@@ -1169,7 +1190,7 @@ void Engine::moddown_host(const u64 *in, size_t ell, u64 *out) {
     auto cm = I.alloc(ell * nn * 8);
     u64 *conv = static_cast<u64 *>(cm->p);
     dev::moddown_convert(conv, x + ell * nn, (int)ell, (int)K, (int)I.P.nq(), W * nn, ell * nn, 1, I.phinv,
-                         I.phinv_s, I.phat, MODS, LOGN, ST);
+                         I.phinv_s, I.phat, I.pmod, I.pinvd, MODS, LOGN, ST);
     dev::ntt_forward(conv, (int)ell, 1, 0, nullptr, I.T, ST);
     auto om = I.alloc(ell * nn * 8);
     dev::moddown_finish(static_cast<u64 *>(om->p), x, conv, nullptr, (int)ell, 1, ell * nn, W * nn, 0, I.pinv,

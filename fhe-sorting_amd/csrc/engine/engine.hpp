@@ -95,8 +95,12 @@ class Engine {
 
     // ------------------------------------------------- encode / encrypt ---
     PtPtr encode(const std::vector<double> &v, int slots, int level);
+    PtPtr encode_scaled(const std::vector<double> &v, int slots, int level, double scale);
     CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
     CtPtr encrypt_pt(const Plaintext &pt);
+    // OpenFHE FLEXIBLEAUTOEXT-style encryption: one extra level absorbs the
+    // encryption noise (divided by q_L); the result sits at level 1
+    CtPtr encrypt_ext(const std::vector<double> &v, int slots);
     std::vector<double> decrypt(const Ciphertext &ct);
     CtPtr upload(const u64 *host, size_t limbs, int level, int slots, double scale);
     void download(const Ciphertext &ct, u64 *host);

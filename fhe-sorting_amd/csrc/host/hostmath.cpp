@@ -125,7 +125,10 @@ Params make_params(int logN, int L, int scale_bits, int first_bits, int dnum) {
         for (int i = j * P.alpha; i < std::min((j + 1) * P.alpha, L + 1); ++i) b += std::log2((double)q[i]);
         maxbits = std::max(maxbits, b);
     }
-    P.K = (int)std::ceil(maxbits / 60.0);
+    // P must exceed every digit product by the ModUp overshoot (the extended
+    // digit is exact only up to a multiple < alpha of Q_j): with P ~ Q_j the
+    // key-switch noise grows alpha-fold (measured: 10x at alpha 13, 40-bit scale)
+    P.K = (int)std::ceil((maxbits + std::log2((double)P.alpha)) / 60.0);
     u64 p = q[0];
     for (int k = 0; k < P.K; ++k) {
         do {
@@ -410,6 +413,8 @@ LevelTables make_level_tables(const Params &P) {
     T.phat.assign(nq * K, 0);  // [nq][K]: the K constants of one target are contiguous
     T.pinv.resize(nq);
     T.pinv_s.resize(nq);
+    T.pinvd.resize(K);
+    for (size_t k = 0; k < K; ++k) T.pinvd[k] = 1.0 / (double)P.primes[nq + k];
     T.pmod.resize(nq);
     T.pmod_s.resize(nq);
     for (size_t k = 0; k < K; ++k) {

@@ -90,6 +90,7 @@ struct LevelTables {
     std::vector<u64> phat;              // [nq][K]
     std::vector<u64> pinv, pinv_s;      // [nq]
     std::vector<u64> pmod, pmod_s;      // [nq]  P mod q_i
+    std::vector<double> pinvd;          // [K]   1 / p_k (ModDown's centring count)
     // fused ModDown + rescale (HMult tail): pqlinv[ell][i] = (P q_{ell-1})^{-1} mod q_i
     std::vector<u64> pqlinv, pqlinv_s;  // [nq+1][nq]
     // Rescale, per ell: qlinv[ell][i] = q_{ell-1}^{-1} mod q_i

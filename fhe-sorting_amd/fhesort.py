@@ -53,6 +53,7 @@ _SIGS = {
     'fhe_ctx_load_keys': (C.c_int, [vp, u64p, ip, C.POINTER(u64p), C.c_int]),
     'fhe_key_bytes': (C.c_uint64, [vp]),
     'fhe_encrypt': (C.c_int, [vp, dp, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_encrypt_ext': (C.c_int, [vp, dp, C.c_int, C.c_int, PP]),
     'fhe_decrypt': (C.c_int, [vp, vp, dp]),
     'fhe_ct_upload': (C.c_int, [vp, u64p, C.c_int, C.c_int, C.c_int, C.c_double, PP]),
     'fhe_ct_download': (C.c_int, [vp, vp, u64p]),
@@ -284,6 +285,11 @@ class Context:
     def encrypt(self, v, slots=None, level=0):
         v = np.ascontiguousarray(v, dtype=np.float64)
         return self._new(lib().fhe_encrypt, _dbl(v), len(v), slots or len(v), level)
+
+    def encrypt_ext(self, v, slots=None):
+        """FLEXIBLEAUTOEXT-style encryption (lands at level 1, noise / q_L)."""
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        return self._new(lib().fhe_encrypt_ext, _dbl(v), len(v), slots or len(v))
 
     def decrypt(self, ct):
         out = np.empty(ct.slots)

@@ -78,6 +78,11 @@ uint64_t fhe_key_bytes(fhe_ctx *ctx);
 /* ------------------------------------------------------ ciphertext / pt */
 /* Encryption::encryptInput = MakeCKKSPackedPlaintext + Encrypt (src/encryption.cpp:5-12) */
 int fhe_encrypt(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_ct **out);
+/* the same under OpenFHE's default FLEXIBLEAUTOEXT scaling (the reference's MEHP24
+ * tests, tests/mehp24/Mehp24SortTest.cpp:25-70, leave it at that default): one extra
+ * level, consumed at encryption, divides the encryption noise by the top prime; the
+ * ciphertext starts at level 1.  Build the context with multDepth + 1 levels. */
+int fhe_encrypt_ext(fhe_ctx *ctx, const double *v, int len, int slots, fhe_ct **out);
 /* DebugEncryption::getPlaintext / Decrypt (src/encryption.cpp:14-27); out: slots values */
 int fhe_decrypt(fhe_ctx *ctx, const fhe_ct *ct, double *out);
 int fhe_ct_upload(fhe_ctx *ctx, const uint64_t *host, int limbs, int level, int slots, double scale,
@@ -178,7 +183,8 @@ int fhe_set_sort_lanes(fhe_ctx *ctx, int lanes);
  * and mehp24::utils::getRotationIndices(N) (src/mehp24/mehp24_utils.cpp:197-225):
  * depth, ring log, scale bits, key-switch digits (dnum: digits of <= 15 primes),
  * CompositeSign (n, dg, df), indicator (dg_i, df_i), part length (0: one-ciphertext
- * sortFG).  Returns #rotations. */
+ * sortFG).  The context gets mult_depth + 1 levels and the input is encrypted with
+ * fhe_encrypt_ext (OpenFHE's default FLEXIBLEAUTOEXT).  Returns #rotations. */
 int fhe_mehp24_parameters(int N, int *mult_depth, int *log_ring, int *scale_bits, int *dnum, int cfg[3],
                           int *dg_i, int *df_i, int *sub_length, int32_t *rots, int max_rots);
 /* getRotationIndices with part length `sub` (the reference fixes 256) */

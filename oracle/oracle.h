@@ -178,10 +178,12 @@ class Context {
 
     // encode / decode
     Plaintext encode(const std::vector<double> &v, int slots, int level) const;
+    Plaintext encode_scaled(const std::vector<double> &v, int slots, int level, double scale) const;
     std::vector<double> decode(const std::vector<u64> &m0_coeff_limb0, int slots, double scale) const;
     std::vector<double> decode_real(const std::vector<double> &m_coeff, int slots, double scale) const;
     CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
     CtPtr encrypt_pt(const Plaintext &pt);
+    CtPtr encrypt_ext(const std::vector<double> &v, int slots);  // FLEXIBLEAUTOEXT-style, lands at level 1
     std::vector<double> decrypt(const Ciphertext &ct);
 
     // ------------------------------------------------------------ ops -----

@@ -122,6 +122,11 @@ void *orc_encrypt(void *c, const double *v, int len, int slots, int level) {
         return wrap(cc->encrypt(std::vector<double>(v, v + len), slots, level));
     }, (void *)nullptr);
 }
+void *orc_encrypt_ext(void *c, const double *v, int len, int slots) {
+    return guard([&]() -> void * {
+        return wrap(static_cast<Context *>(c)->encrypt_ext(std::vector<double>(v, v + len), slots));
+    }, (void *)nullptr);
+}
 int orc_decrypt(void *c, void *ct, double *out) {
     return guard([&]() {
         auto *cc = static_cast<Context *>(c);

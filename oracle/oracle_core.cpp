@@ -154,7 +154,10 @@ Params make_params(int logN, int L, int scale_bits, int first_bits, int dnum) {
         for (int i = j * P.alpha; i < std::min((j + 1) * P.alpha, L + 1); ++i) b += std::log2((double)q[i]);
         maxbits = std::max(maxbits, b);
     }
-    P.K = (int)std::ceil(maxbits / 60.0);
+    // P must exceed every digit product by the ModUp overshoot (the extended
+    // digit is exact only up to a multiple < alpha of Q_j): with P ~ Q_j the
+    // key-switch noise grows alpha-fold (measured: 10x at alpha 13, 40-bit scale)
+    P.K = (int)std::ceil((maxbits + std::log2((double)P.alpha)) / 60.0);
     u64 p = q0;
     for (int k = 0; k < P.K; ++k) {
         do { p -= m2; } while (!is_prime(p) || used.count(p));
@@ -382,6 +385,9 @@ Context::Context(const Params &p, u64 seed_) : P(p), seed(seed_) {
 }
 
 Plaintext Context::encode(const std::vector<double> &v, int slots, int level) const {
+    return encode_scaled(v, slots, level, P.delta[level]);
+}
+Plaintext Context::encode_scaled(const std::vector<double> &v, int slots, int level, double scale) const {
     const size_t n = P.n;
     if (slots <= 0 || (slots & (slots - 1)) || (size_t)slots > n / 2)
         throw std::invalid_argument("encode: slots must be a power of two <= n/2");
@@ -389,7 +395,6 @@ Plaintext Context::encode(const std::vector<double> &v, int slots, int level) co
     std::vector<cd> vals(slots, cd(0, 0));
     for (size_t i = 0; i < v.size() && i < (size_t)slots; ++i) vals[i] = cd(v[i], 0);
     emb_inv(vals, T);
-    const double scale = P.delta[level];
     const size_t gap = n / (2 * (size_t)slots);
     std::vector<i64> coef(n, 0);
     for (size_t i = 0; i < (size_t)slots; ++i) {
@@ -561,6 +566,29 @@ CtPtr Context::encrypt_pt(const Plaintext &pt) {
 
 CtPtr Context::encrypt(const std::vector<double> &v, int slots, int level) {
     return encrypt_pt(encode(v, slots, level));
+}
+
+// Fresh encryption one level up, as OpenFHE's FLEXIBLEAUTOEXT (its default
+// CKKS scaling technique, which the reference's tests run under): the message
+// is encoded at scale Delta_1 on the level-0 basis and multiplied by the top
+// prime q_L (scale Delta_1 q_L), encrypted, and rescaled by q_L -- the
+// encryption noise is divided by q_L and the result sits at level 1 with the
+// canonical scale Delta_1.
+CtPtr Context::encrypt_ext(const std::vector<double> &v, int slots) {
+    if (P.L < 1) throw std::runtime_error("encrypt_ext: needs one extra level");
+    Plaintext pt = encode_scaled(v, slots, 0, P.delta[1]);
+    const size_t n = P.n;
+    const u64 qL = P.primes[P.nq() - 1];
+#pragma omp parallel for
+    for (size_t l = 0; l < pt.limbs; ++l) {
+        const u64 kv = qL % P.primes[l];
+        u64 *d = pt.m.data() + l * n;
+        for (size_t k = 0; k < n; ++k) d[k] = mod_mul(d[k], kv, tab[l].mod);
+    }
+    pt.scale = P.delta[1] * (double)qL;
+    CtPtr r = rescale(*encrypt_pt(pt));
+    r->scale = P.delta[1];
+    return r;
 }
 
 std::vector<double> Context::decrypt(const Ciphertext &ct) {
@@ -877,11 +905,21 @@ void Context::moddown(const u64 *in, size_t ell, u64 *out) const {
             Pm = mod_mul(Pm, P.primes[nq + k] % mi.q, mi);
         }
         u64 Pinv = mod_inv(Pm, mi);
+        // centred exact conversion: x mod P = sum_k y_k Phat_k - v P, v =
+        // round(sum_k y_k / p_k) in fp64 (k ascending), so the result is
+        // round(x / P); a plain fast conversion floors with a 0..K overshoot,
+        // a biased error that s turns into a few large slot errors
+        const u64 Pq = Pm;
         std::vector<u64> conv(n);
         for (size_t c = 0; c < n; ++c) {
             u64 acc = 0;
-            for (size_t k = 0; k < K; ++k) acc = mod_add(acc, mod_mul(pc[k * n + c] % mi.q, phat[k], mi), mi.q);
-            conv[c] = acc;
+            double t = 0.0;
+            for (size_t k = 0; k < K; ++k) {
+                acc = mod_add(acc, mod_mul(pc[k * n + c] % mi.q, phat[k], mi), mi.q);
+                t = t + (double)pc[k * n + c] * (1.0 / (double)P.primes[nq + k]);
+            }
+            const u64 v = (u64)(t + 0.5);
+            conv[c] = mod_sub(acc, mod_mul(v, Pq, mi), mi.q);
         }
         ntt_forward(conv.data(), tab[i], n);
         const u64 *x = in + i * n;

@@ -44,6 +44,7 @@ def lib():
             'orc_pt_data': (C.c_int, [vp, u64p]),
             'orc_pt_free': (None, [vp]),
             'orc_encrypt': (vp, [vp, dp, C.c_int, C.c_int, C.c_int]),
+            'orc_encrypt_ext': (vp, [vp, dp, C.c_int, C.c_int]),
             'orc_decrypt': (C.c_int, [vp, vp, dp]),
             'orc_ct_free': (None, [vp]),
             'orc_ct_info': (C.c_int, [vp, ip, ip, dp, ip]),
@@ -243,6 +244,10 @@ class Context:
         v = np.ascontiguousarray(v, dtype=np.float64)
         slots = slots or len(v)
         return Ct(self, lib().orc_encrypt(self.h, _dbl(v), len(v), slots, level))
+
+    def encrypt_ext(self, v, slots=None):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        return Ct(self, lib().orc_encrypt_ext(self.h, _dbl(v), len(v), slots or len(v)))
 
     def decrypt(self, ct):
         out = np.empty(ct.slots)

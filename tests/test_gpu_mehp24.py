@@ -36,6 +36,18 @@ def same(gct, oct_):
         raise AssertionError(f'{len(bad)} limb words differ, first at {bad[0].tolist()}')
 
 
+def test_encrypt_ext_matches_oracle():
+    """Same seed, same encryption counter: identical ciphertexts."""
+    orc = O.Context(LOGN, 4, 40, 60, 3, seed=8)
+    gpu = F.Context(LOGN, 4, 40, 60, 3, seed=8)
+    x = np.random.default_rng(8).uniform(-1, 1, 64)
+    o = orc.encrypt_ext(x, 64)
+    g = gpu.encrypt_ext(x, 64)
+    assert o.level == g.level == 1
+    same(g, o)
+    assert np.max(np.abs(gpu.decrypt(g) - x)) < 1e-8
+
+
 def test_indicator_adv_matches_oracle(pair):
     orc, gpu = pair
     v = np.array([-3.0, -1.0, 0.0, 0.2, 1.0, 2.0, -0.1, 3.0])
@@ -67,20 +79,57 @@ def test_sort_matches_oracle(pair, N, sub, stack):
 
 def _full(N):
     p = F.mehp24_parameters(N)
-    ctx = F.Context(p['log_ring'], p['depth'], p['scale_bits'], 60, p['dnum'], seed=N)
+    ctx = F.Context(p['log_ring'], p['depth'] + 1, p['scale_bits'], 60, p['dnum'], seed=N)
     ctx.gen_rotation_keys(p['rots'])
     x = np.random.default_rng(N).permutation(N) / N  # getVectorWithMinDiff(N, 0, 1, 1/N)
     slots = min(N * N, 1 << (p['log_ring'] - 1))
-    out = ctx.mehp24_sort(ctx.encrypt(x, slots), N, p['cfg'], p['dg_i'], p['df_i'], p['sub'])
+    out = ctx.mehp24_sort(ctx.encrypt_ext(x, slots), N, p['cfg'], p['dg_i'], p['df_i'], p['sub'])
     y = ctx.decrypt(out)[:N]
     return x, y, out
 
 
-@pytest.mark.parametrize('N', [16, 512])
+@pytest.mark.parametrize('N', [16, 256, 512])
 def test_reference_parameters_sort(N):
-    """The reference test at its own parameters: N=16 (sortFG) and N=512
-    (sortLargeArrayFG, two parts of 256) at ring 2^17."""
+    """The reference test at its own parameters: N=16 and N=256 (sortFG) and
+    N=512 (sortLargeArrayFG, two parts of 256) at ring 2^17, input encrypted
+    FLEXIBLEAUTOEXT-style (OpenFHE's default, which the reference runs under)."""
     x, y, out = _full(N)
     err = np.max(np.abs(y - np.sort(x)))
     assert err < 0.01, err
-    assert out.level <= F.mehp24_parameters(N)['depth']
+    assert out.level <= F.mehp24_parameters(N)['depth'] + 1
+
+
+def test_full_slot_ops_match_oracle():
+    """slots = n/2 (the reference packs N*N = 65536 values at ring 2^17):
+    encryption, every MEHP24 rotation for N=32, masks and a product, bit-exact."""
+    N = 32
+    rots = O.mehp24_rotation_indices(N)
+    orc = O.Context(LOGN, 12, 40, 60, 3, seed=4)
+    orc.gen_rotation_keys(rots)
+    gpu = F.Context(LOGN, 12, 40, 60, 3, seed=4, keygen=False)
+    gpu.load_keys_from(orc, rots)
+    x = np.random.default_rng(2).uniform(-1, 1, N * N)
+    o = orc.encrypt(x, N * N)
+    g = gpu.from_oracle(o)
+    assert np.max(np.abs(gpu.decrypt(g) - x)) < 1e-6
+    for k in rots:
+        try:
+            same(gpu.rotate(g, k), orc.rotate(o, k))
+        except AssertionError as e:
+            raise AssertionError(f'rotation {k}: {e}')
+    mask = (np.arange(N * N) % N == 0).astype(float)
+    same(gpu.mul_plain(g, gpu.encode(mask, N * N, 0)), orc.mul_plain(o, orc.encode(mask, N * N, 0)))
+    same(gpu.mul(g, g), orc.mul(o, o))
+
+
+def test_full_slot_sort_matches_oracle():
+    N = 32
+    rots = O.mehp24_rotation_indices(N)
+    orc = O.Context(LOGN, 42, 40, 60, 3, seed=6)
+    orc.gen_rotation_keys(rots)
+    gpu = F.Context(LOGN, 42, 40, 60, 3, seed=6, keygen=False)
+    gpu.load_keys_from(orc, rots)
+    x = np.random.default_rng(N).permutation(N) / N
+    o = orc.encrypt(x, N * N)
+    rg = gpu.mehp24_sort(gpu.from_oracle(o), N, (3, 3, 2), 3, 2)
+    same(rg, orc.mehp24_sort(o, N, (3, 3, 2), 3, 2))

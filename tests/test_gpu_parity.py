@@ -293,3 +293,32 @@ def test_direct_sort_multi_batch_stacked(stack, lanes):
     oout = orc.direct_sort(ox, N, rots, cfg)
     same(gout, oout)
     assert np.max(np.abs(gpu.decrypt(gout) - np.sort(x))) < 0.01
+
+
+def test_ring_2_17_ops_match_oracle():
+    """Ring 2^17 (the reference's MEHP24 ring; 2^8 x 2^9 NTT passes): encryption,
+    products, rescales, rotations and plaintext products bit-exact."""
+    orc = O.Context(17, 5, 40, 60, 3, seed=17)
+    orc.gen_rotation_keys([1, -256, 32640, -32768])
+    gpu = F.Context(17, 5, 40, 60, 3, seed=17, keygen=False)
+    gpu.load_keys_from(orc, [1, -256, 32640, -32768])
+    rng = np.random.default_rng(17)
+    x = rng.uniform(-1, 1, 1 << 16)
+    o = orc.encrypt_ext(x, 1 << 16)
+    g = gpu.from_oracle(o)
+    for name, gop, oop in [
+        ('square', lambda c: gpu.square(c), lambda c: orc.square(c)),
+        ('mul_const', lambda c: gpu.mul_const(c, 0.75), lambda c: orc.mul_const(c, 0.75)),
+        ('rot1', lambda c: gpu.rotate(c, 1), lambda c: orc.rotate(c, 1)),
+        ('rot-256', lambda c: gpu.rotate(c, -256), lambda c: orc.rotate(c, -256)),
+        ('rot32640', lambda c: gpu.rotate(c, 32640), lambda c: orc.rotate(c, 32640)),
+        ('rot-32768', lambda c: gpu.rotate(c, -32768), lambda c: orc.rotate(c, -32768)),
+        ('mul_plain', lambda c: gpu.mul_plain(c, gpu.encode(x, 1 << 16, 1)),
+         lambda c: orc.mul_plain(c, orc.encode(x, 1 << 16, 1))),
+    ]:
+        try:
+            same(gop(g), oop(o))
+        except AssertionError as e:
+            raise AssertionError(f'{name}: {e}')
+    r = gpu.rotate(g, -32768)
+    assert np.max(np.abs(gpu.decrypt(r) - np.roll(x, 32768))) < 1e-5
