@@ -178,37 +178,45 @@ struct MultiLinArgs {
     int64_t K[MLS_G * MLS_M];  // [g][i]
     int m, G, accumulate;
 };
+// One coefficient per lane, G outputs.  Every residue and constant is < 2^60,
+// so both split into 30-bit halves and a term costs four v_mad_u64_u32 with
+// accumulate (mac4, no carries); 16 terms fit the four 64-bit partial sums, so
+// each chunk of 16 baby steps is folded and reduced once into a running
+// residue.  The constants are split once per block into LDS (wave-uniform
+// broadcast reads).
+template <int G>
 __global__ __launch_bounds__(NT) void k_linear_sum_multi(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
-    __shared__ u64 w[MLS_G * MLS_M];
+    __shared__ Split30 w[G * MLS_M];
     const size_t n = (size_t)1 << logN;
     const int l = blockIdx.y;
     const Mod md = mods[l];
-    for (int t = threadIdx.x; t < A.G * MLS_M; t += NT) w[t] = (t % MLS_M) < A.m ? smod(A.K[t], md) : 0;
+    for (int t = threadIdx.x; t < G * MLS_M; t += NT) w[t] = split30((t % MLS_M) < A.m ? smod(A.K[t], md) : 0);
     __syncthreads();
-    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
     const size_t ln = (size_t)l * n + k, oo = (size_t)blockIdx.z * seg + ln;
-    Acc128 r[MLS_G][2];
+    u64 run[G];
 #pragma unroll
-    for (int g = 0; g < MLS_G; ++g)
-        if (g < A.G && A.accumulate) {
-            const ulonglong2 o = ld2(A.out[g] + oo);
-            r[g][0].lo = o.x;
-            r[g][1].lo = o.y;
+    for (int g = 0; g < G; ++g) run[g] = A.accumulate ? A.out[g][oo] : 0;
+    for (int base = 0; base < A.m; base += 16) {
+        const int end = min(A.m, base + 16);
+        Acc4 s[G];
+        // issue the chunk's loads up front (memory-level parallelism), then MAC
+        u64 xv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xv[u] = base + u < end ? A.x[base + u][(size_t)blockIdx.z * A.xseg[base + u] + ln] : 0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            if (base + u >= end) break;
+            const Split30 x = split30(xv[u]);
+#pragma unroll
+            for (int g = 0; g < G; ++g) mac4(s[g], x, w[g * MLS_M + base + u]);
         }
-    for (int i = 0; i < A.m; ++i) {
-        const ulonglong2 x = ld2(A.x[i] + (size_t)blockIdx.z * A.xseg[i] + ln);
 #pragma unroll
-        for (int g = 0; g < MLS_G; ++g)
-            if (g < A.G) {
-                const u64 c = w[g * MLS_M + i];
-                mac128(r[g][0], x.x, c);
-                mac128(r[g][1], x.y, c);
-            }
+        for (int g = 0; g < G; ++g) run[g] = add_mod(run[g], reduce4(s[g], md), md.q);
     }
 #pragma unroll
-    for (int g = 0; g < MLS_G; ++g)
-        if (g < A.G) st2(A.out[g] + oo, make_ulonglong2(reduce128(r[g][0], md), reduce128(r[g][1], md)));
+    for (int g = 0; g < G; ++g) A.out[g][oo] = run[g];
 }
 
 // out[m][c] = sum_i ct_i[m][c] * pt_i  (accumulate: + out), lazy 128-bit.
@@ -294,7 +302,7 @@ struct ModUpArgs {
 // size): the source loop is straight-line; a shorter last digit reads a
 // clamped limb times a zero constant.
 template <int AT>
-__global__ __launch_bounds__(NT) void k_modup_convert(u64 *ext, const u64 *coef, int W, int ell, ModUpArgs A,
+__global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, const u64 *__restrict__ coef, int W, int ell, ModUpArgs A,
                                                       const int *pmap_ext, const Mod *mods, int logN) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
@@ -377,7 +385,7 @@ __device__ __forceinline__ u64 centre_count(const u64 (&y)[KT], const double *pi
     return (u64)(t + 0.5);
 }
 template <int KT>
-__global__ __launch_bounds__(NT) void k_moddown_convert(u64 *conv, const u64 *pc, int ell, int nq, size_t seg_in,
+__global__ __launch_bounds__(NT) void k_moddown_convert(u64 *__restrict__ conv, const u64 *__restrict__ pc, int ell, int nq, size_t seg_in,
                                                         size_t seg_out, const u64 *phinv, const u64 *phinv_s,
                                                         const u64 *phat, const u64 *pmod, const double *pinvd,
                                                         const Mod *mods, int logN) {
@@ -437,7 +445,7 @@ __global__ __launch_bounds__(NT) void k_moddown_finish(u64 *out, const u64 *acc,
 // y_last = (x_last - Conv_{P->q_last}(acc_P)) * P^-1 mod q_last is the last
 // limb of the ModDown output.  grid: x = n / NT, y = ceil((ell-1) / TCH), z = seg
 template <int KT>
-__global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int nq,
+__global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict__ corr, const u64 *__restrict__ acc, int ell, int nq,
                                                                 size_t seg_acc, size_t seg_corr, const u64 *phinv,
                                                                 const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                                                                 const u64 *pinv_s, const u64 *pmod, const double *pinvd,
@@ -569,8 +577,15 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
             for (int g = 0; g < G; ++g) A.K[g * MLS_M + i] = K[(size_t)g * m + base + i];
         }
         const double B = 8.0 * (A.m + (double)G * (1 + A.accumulate)) * limbs * segs * ((size_t)1 << logN);
-        launch_clocked("k_linear_sum_multi", B, k_linear_sum_multi, ew_grid(logN, limbs, segs), dim3(NT), st, A, seg,
-                       mods, logN);
+        const dim3 grid = pt_grid(logN, limbs, segs);
+        switch (G) {
+#define MLS_CASE(g)                                                                                          \
+    case g:                                                                                                  \
+        launch_clocked("k_linear_sum_multi", B, k_linear_sum_multi<g>, grid, dim3(NT), st, A, seg, mods, logN); \
+        break;
+            MLS_CASE(1) MLS_CASE(2) MLS_CASE(3) MLS_CASE(4) MLS_CASE(5) MLS_CASE(6) MLS_CASE(7) MLS_CASE(8)
+#undef MLS_CASE
+        }
     }
 }
 void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, int m, int limbs, int members,
