@@ -14,6 +14,9 @@ constructRank and the 32 index-check batches of rotationIndexCheckN are
 sharded over ranks (batch b -> rank b % world); the partial ranks/outputs are
 summed by one RCCL all-reduce each (u64 sum + mod q) -- strong scaling.
 
+--workload mehp24: MEHP24 sortLargeArrayFG of N=4096 at ring 2^17 (BASELINE
+config 5), pair compares and indicators sharded over ranks.
+
 Output: one JSON line.  value = ciphertext-mults/s (relinearised ct x ct
 products, incl. those in the Chebyshev PS, summed over ranks / wall time);
 ms_per_step = sort wall time.  Also: roofline of the dominant kernel (HIP
@@ -40,7 +43,10 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--n-sort', type=int, default=1024)
+    ap.add_argument('--workload', choices=('direct', 'mehp24'), default='direct',
+                    help='direct: DirectSort rank sort (the BASELINE metric); mehp24: MEHP24 sortLargeArrayFG '
+                         '(BASELINE config 5, ring 2^17)')
+    ap.add_argument('--n-sort', type=int, default=None, help='values to sort (default 1024; mehp24: 4096)')
     ap.add_argument('--log-n', type=int, default=16)
     ap.add_argument('--seed', type=int, default=20250704)
     ap.add_argument('--scale-bits', type=int, default=50,
@@ -150,7 +156,7 @@ def pmc_lookup(table, name):
     return hits[0] if len(hits) == 1 else None
 
 
-def roofline(ctx, run_once, dump=None):
+def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json'):
     """Roofline of the dominant kernel, measured live: one more (untimed) sort
     runs with every hot kernel launched through hipExtLaunchKernelGGL with
     start/stop events on the engine stream (the stream it runs on), one lane so
@@ -172,12 +178,12 @@ def roofline(ctx, run_once, dump=None):
     per_launch = st['bytes'] / st['launches']
     achieved = per_launch / avg_s / 1e9
     traffic, src = None, None
-    pmc = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
+    pmc = os.path.join(REPO, 'profiles', pmc_file)  # PMC passes of this same workload only
     if os.path.exists(pmc):
         with open(pmc) as f:
             t = pmc_lookup(json.load(f), name)
         if t:
-            traffic, src = t['hbm_bytes_per_launch'], 'profiles/pmc_traffic.json'
+            traffic, src = t['hbm_bytes_per_launch'], 'profiles/' + pmc_file
     top = sorted(stats.items(), key=lambda kv: -kv[1]['ms'])[:8]
     table = {k: {'share': round(v['ms'] / total_ms, 3), 'avg_us': round(v['ms'] / v['launches'] * 1e3, 1),
                  'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1)} for k, v in top}
@@ -187,13 +193,14 @@ def roofline(ctx, run_once, dump=None):
             'algorithmic_bytes_per_launch': per_launch, 'clocked_ms_per_sort': round(total_ms, 1), 'kernels': table}
 
 
-def cpu_baseline(logN, depth, N, sample_mults, scale_bits):
+def cpu_baseline(logN, depth, N, sample_mults, scale_bits, dnum=3):
     """CPU oracle (this repo's C++ restatement, OpenMP) on a bounded sample of
     the same workload: the comparator of one constructRank batch
-    (CompositeSign(3,5,2): 35 relinearised products at ring 2^logN, depth 39)."""
+    (CompositeSign(3,5,2): 35 relinearised products at ring 2^logN, depth 39),
+    or `sample_mults` chained relinearised squarings."""
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import pyoracle as O
-    orc = O.Context(logN, depth, scale_bits, 60, 3, seed=7)
+    orc = O.Context(logN, depth, scale_bits, 60, dnum, seed=7)
     rng = np.random.default_rng(1)
     a = orc.encrypt(rng.uniform(0, 1, N), N)
     b = orc.encrypt(rng.uniform(0, 1, N), N)
@@ -215,10 +222,113 @@ def cpu_baseline(logN, depth, N, sample_mults, scale_bits):
             'kind': 'port', 'sample': sample, 'seconds': round(dt, 2), 'hmults': c['hmult']}
 
 
+def make_allreduce(ctx, d):
+    """RCCL when every rank has its own GPU, else a host + gloo exchange."""
+    if d.world > 1 and d.rccl:
+        uid = d.bcast_bytes(F.Context.comm_unique_id() if d.rank == 0 else None)
+        ctx.comm_init(uid, d.rank, d.world)
+        return None
+    if d.world > 1:
+        return d.host_allreduce()
+    return None
+
+
+def run_mehp24(a, d):
+    """MEHP24 sortLargeArrayFG (src/mehp24/mehp24_sort.cpp:623-645) at the
+    reference test's parameters (tests/mehp24/Mehp24SortTest.cpp:26-143: ring
+    2^17, scale 2^40, Cfg (3,5,2), dg_i, df_i = 2, parts of 256), N = 4096 by
+    default (BASELINE config 5; depth 64 as for 2048).  The P(P+1)/2 pair
+    compares and P^2 indicators are sharded over ranks (strong scaling)."""
+    N = a.n_sort or 4096
+    p = F.mehp24_parameters(N)
+    t0 = time.time()
+    ctx = F.Context(p['log_ring'], p['depth'] + 1, p['scale_bits'], 60, p['dnum'], seed=a.seed, device=d.device)
+    ctx.gen_rotation_keys(p['rots'])
+    ctx.set_sort_stack(a.stack)
+    allreduce = make_allreduce(ctx, d)
+    x = np.random.default_rng(a.seed).permutation(N) / N  # getVectorWithMinDiff(N, 0, 1, 1/N)
+    slots = min(N * N, 1 << (p['log_ring'] - 1)) if p['sub'] == 0 else p['sub'] * p['sub']
+    ct = ctx.encrypt_ext(x, slots)
+    setup_s = time.time() - t0
+    shard = (d.rank, d.world)
+
+    def run():
+        return ctx.mehp24_sort(ct, N, p['cfg'], p['dg_i'], p['df_i'], p['sub'], shard=shard, allreduce=allreduce)
+
+    out = None
+    for _ in range(a.warmup):
+        out = run()
+    device_sync(ctx)
+    d.barrier()
+    ctx.reset_counters()
+    device_sync(ctx)
+    d.barrier()
+    t = time.perf_counter()
+    for _ in range(a.steps):
+        out = run()
+    device_sync(ctx)
+    d.barrier()
+    dt = d.max(time.perf_counter() - t)
+    cnt = ctx.counters()
+    peak_gb = ctx.pool_stats()['peak'] / 1e9
+    hm_total = d.sum(cnt['hmult'])
+    ks_total = d.sum(cnt['keyswitch'])
+    if d.rank == 0:
+        y = ctx.decrypt(out)[:N]
+        ms = dt / a.steps * 1e3
+        P = N // p['sub'] if p['sub'] else 1
+        res = {
+            'metric': f'MEHP24 encrypted sort seconds + ciphertext-mults/sec, N={N} @ ringDim 2^{p["log_ring"]}',
+            'value': round(hm_total / dt, 2),
+            'unit': 'ciphertext-mults/s',
+            'n_gpus': d.world,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': round(ms, 2),
+            'sort_seconds': round(ms / 1e3, 4),
+            'keyswitches_per_s': round(ks_total / dt, 2),
+            'higher_is_better': True,
+            'scaling': 'strong',
+            'vs_baseline': None,
+            'dtype': 'u64',
+            'data': 'synthetic: seeded permutation of {k/N}, keys and encryption from a seeded PRNG',
+            'config': {'workload': f'MEHP24 sortLargeArrayFG N={N}, parts of {p["sub"]}, ringDim 2^{p["log_ring"]}, '
+                                   f'depth {p["depth"]} (+1 FLEXIBLEAUTOEXT), scale 2^{p["scale_bits"]}, dnum '
+                                   f'{p["dnum"]}, CompositeSign{p["cfg"]}, indicator ({p["dg_i"]}, {p["df_i"]}), '
+                                   f'{len(p["rots"])} rotation keys',
+                       'N': N, 'ring_dim': 1 << p['log_ring'], 'mult_depth': p['depth'],
+                       'pair_compares': P * (P + 1) // 2, 'indicators': P * P, 'max_stack': a.stack,
+                       'parallelism': f'pair/indicator-shard x{d.world}',
+                       'collective': 'none' if d.world == 1 else ('rccl' if d.rccl else 'host+gloo (more ranks than GPUs)')},
+            'max_abs_err': float(np.max(np.abs(y - np.sort(x)))),
+            'output_level': out.level,
+            'hmult_per_sort': int(hm_total / a.steps),
+            'setup_s': round(setup_s, 1),
+            'hbm_peak_gb_rank0': round(peak_gb, 1),
+            'roofline': None,
+        }
+        if not a.no_roofline and d.world == 1:
+            try:
+                ctx.pool_trim()
+                res['roofline'] = roofline(ctx, run, a.clock_json, 'pmc_traffic_mehp24.json')
+            except Exception as e:  # never hide the main number
+                res['roofline'] = {'error': str(e)}
+        if d.world == 1 and not a.no_cpu_baseline:
+            try:
+                res['cpu_baseline'] = cpu_baseline(p['log_ring'], p['depth'] + 1, N, a.cpu_sample_mults or 6,
+                                                   p['scale_bits'], dnum=p['dnum'])
+            except Exception as e:
+                res['cpu_baseline'] = {'error': str(e)}
+        print(json.dumps(res), flush=True)
+    d.barrier()
+
+
 def main():
     a = parse()
     d = Dist(a.gpus)
-    N, logN = a.n_sort, a.log_n
+    if a.workload == 'mehp24':
+        return run_mehp24(a, d)
+    N, logN = a.n_sort or 1024, a.log_n
     depth, rots = F.size_parameters(N)
     cfg = sign_cfg(N)
     t0 = time.time()
@@ -226,12 +336,7 @@ def main():
     ctx.gen_rotation_keys(rots)
     ctx.set_sort_lanes(a.lanes)
     ctx.set_sort_stack(a.stack)
-    allreduce = None
-    if d.world > 1 and d.rccl:
-        uid = d.bcast_bytes(F.Context.comm_unique_id() if d.rank == 0 else None)
-        ctx.comm_init(uid, d.rank, d.world)
-    elif d.world > 1:
-        allreduce = d.host_allreduce()
+    allreduce = make_allreduce(ctx, d)
     x = np.random.default_rng(a.seed).permutation(N) / N  # getVectorWithMinDiff(N, 0, 1, 1/N)
     ct = ctx.encrypt(x, N)
     setup_s = time.time() - t0

@@ -105,6 +105,19 @@ SortShape checkShape(int N, int max_batch);
 // u64); the engine reduces mod q afterwards.  nullptr = single rank.
 using CtAllReduce = std::function<void(u64 *dev_data, size_t count)>;
 
+// Independent work items i handled by this rank iff i % world == rank; partial
+// sums combined by `allreduce`.
+struct Shard {
+    int rank = 0, world = 1;
+    CtAllReduce allreduce;
+    bool mine(size_t i) const { return world <= 1 || (int)(i % (size_t)world) == rank; }
+};
+// Combines per-rank partial sums of one ciphertext: a 2-word header (level + 1,
+// presence) is summed first so ranks that hold no partial agree on the level
+// and contribute a zero ciphertext, then the limbs are summed as u64 and
+// reduced mod q.  No-op for one rank.
+void reducePartial(Engine &cc, const Shard &sh, CtPtr &acc, int slots);
+
 class DirectSortN {
   public:
     DirectSortN(Engine &cc, int N, const std::vector<int> &rotIndices);
@@ -182,10 +195,14 @@ CtPtr signAdv(Engine &cc, CtPtr c, size_t dg, size_t df);
 CtPtr indicatorAdv(Engine &cc, const Ciphertext &c, double b, size_t dg, size_t df);
 CtPtr sortFG(const Ciphertext &c, size_t vectorLength, SignFunc f, const SignConfig &cfg, uint32_t dg_i,
              uint32_t df_i, Engine &cc, int max_stack = 32);
+// Multi-ciphertext sortFG shards its P(P+1)/2 pair compares and its P^2
+// indicators over `sh` (one all-reduce per partial Cv / Ch / result sum);
+// everything else is replicated.  The output does not depend on the sharding.
 std::vector<CtPtr> sortFG(const std::vector<CtPtr> &c, size_t subVectorLength, SignFunc f, const SignConfig &cfg,
-                          uint32_t dg_i, uint32_t df_i, Engine &cc, int max_stack = 32);
+                          uint32_t dg_i, uint32_t df_i, Engine &cc, int max_stack = 32, const Shard &sh = Shard());
 CtPtr sortLargeArrayFG(const Ciphertext &c, size_t totalLength, size_t subLength, SignFunc f,
-                       const SignConfig &cfg, uint32_t dg_i, uint32_t df_i, Engine &cc, int max_stack = 32);
+                       const SignConfig &cfg, uint32_t dg_i, uint32_t df_i, Engine &cc, int max_stack = 32,
+                       const Shard &sh = Shard());
 struct Parameters {
     int multDepth = 0, logRingDim = 17, scaleModSize = 40, dnum = 3;
     int levels = 0;  // context depth: multDepth + 1 (input encrypted with encrypt_ext)

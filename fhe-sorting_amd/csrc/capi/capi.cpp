@@ -312,6 +312,28 @@ int fhe_size_parameters(int N, int *depth, int32_t *rots, int max_rots) {
     return rc == FHE_OK ? count : -rc;
 }
 
+// The reduction a sharded sort uses: the caller's hook if given, else RCCL on
+// the context's communicator (fhe_comm_init), on the engine stream.
+static CtAllReduce make_allreduce(fhe_ctx *ctx, int shard_world, fhe_allreduce_fn fn, void *user) {
+    if (fn) {
+        // the partial sums are produced asynchronously on the context stream:
+        // drain it so the callback sees finished data (it must complete the
+        // reduction before returning)
+        Engine *eng = ctx->eng.get();
+        return [fn, user, eng](u64 *d, size_t c) {
+            eng->sync();
+            fn(d, (uint64_t)c, user);
+        };
+    }
+    if (shard_world <= 1) return nullptr;
+    if (!ctx->comm) throw std::runtime_error("sharded sort needs fhe_comm_init or an allreduce hook");
+    ncclComm_t comm = ctx->comm;
+    hipStream_t st = static_cast<hipStream_t>(ctx->eng->stream_handle());
+    return [comm, st](u64 *d, size_t c) {
+        if (ncclAllReduce(d, d, c, ncclUint64, ncclSum, comm, st) != ncclSuccess)
+            throw std::runtime_error("HIP error: ncclAllReduce failed");
+    };
+}
 int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, const int32_t *rots, int nrot, int n,
                     int dg, int df, int mode, int shard_rank, int shard_world, fhe_allreduce_fn fn, void *user,
                     fhe_ct **out) {
@@ -324,27 +346,9 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
         DirectSortN &ds = *slot;
         ds.max_stack = ctx->sort_stack;
         ds.lanes = ctx->sort_lanes;
-        ds.allreduce = nullptr;
         ds.shard_rank = shard_rank;
         ds.shard_world = shard_world;
-        if (fn) {
-            // the partial sums are produced asynchronously on the context stream:
-            // drain it so the callback sees finished data (it must complete the
-            // reduction before returning)
-            Engine *eng = ctx->eng.get();
-            ds.allreduce = [fn, user, eng](u64 *d, size_t c) {
-                eng->sync();
-                fn(d, (uint64_t)c, user);
-            };
-        } else if (shard_world > 1) {
-            if (!ctx->comm) throw std::runtime_error("sharded sort needs fhe_comm_init or an allreduce hook");
-            ncclComm_t comm = ctx->comm;
-            hipStream_t st = static_cast<hipStream_t>(ctx->eng->stream_handle());
-            ds.allreduce = [comm, st](u64 *d, size_t c) {
-                if (ncclAllReduce(d, d, c, ncclUint64, ncclSum, comm, st) != ncclSuccess)
-                    throw std::runtime_error("HIP error: ncclAllReduce failed");
-            };
-        }
+        ds.allreduce = make_allreduce(ctx, shard_world, fn, user);
         const SignConfig cfg = cfgof(n, dg, df);
         if (mode == 1)
             *out = wrap(ds.constructRank(*x->p, SignFunc::CompositeSign, cfg));
@@ -388,10 +392,21 @@ int fhe_mehp24_rotation_indices(int N, int sub, int32_t *rots, int max_rots) {
 }
 int fhe_mehp24_sort(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i,
                     fhe_ct **out) {
+    return fhe_mehp24_sort_sharded(ctx, x, N, sub, n, dg, df, dg_i, df_i, 0, 1, nullptr, nullptr, out);
+}
+int fhe_mehp24_sort_sharded(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n, int dg, int df, int dg_i,
+                            int df_i, int shard_rank, int shard_world, fhe_allreduce_fn fn, void *user,
+                            fhe_ct **out) {
     return guard([&] {
         NEED(ctx);
         NEED(x);
         if (N < 2 || (N & (N - 1))) throw std::invalid_argument("mehp24: N must be a power of two >= 2");
+        if (shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world)
+            throw std::invalid_argument("mehp24: bad shard");
+        Shard sh;
+        sh.rank = shard_rank;
+        sh.world = shard_world;
+        sh.allreduce = make_allreduce(ctx, shard_world, fn, user);
         const SignConfig cfg = cfgof(n, dg, df);
         if (sub == 0) {
             if ((long)N * N != (long)x->p->slots) throw std::invalid_argument("mehp24 sortFG: needs N*N slots");
@@ -401,7 +416,7 @@ int fhe_mehp24_sort(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n, int dg
             if (sub < 2 || (sub & (sub - 1)) || N % sub) throw std::invalid_argument("mehp24: bad part length");
             if ((long)sub * sub != (long)x->p->slots) throw std::invalid_argument("mehp24: needs sub*sub slots");
             *out = wrap(mehp24::sortLargeArrayFG(*x->p, N, sub, SignFunc::CompositeSign, cfg, dg_i, df_i,
-                                                 *ctx->eng, ctx->sort_stack));
+                                                 *ctx->eng, ctx->sort_stack, sh));
         }
     });
 }

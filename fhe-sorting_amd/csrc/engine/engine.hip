@@ -41,6 +41,17 @@ std::set<Pool *> &pool_registry() {
 }
 void trim_all_pools();
 
+// Allocation size classes: 256-B granules up to 1 MiB, above that 8 classes
+// per power of two (<= 12.5% slack).  Ciphertext batches come in many limb
+// counts x member counts; with exact sizes every new shape missed the cache
+// and cost a hipMalloc (MEHP24 at ring 2^17 cached 135 GB of odd sizes).
+inline size_t size_class(size_t bytes) {
+    if (bytes <= ((size_t)1 << 20)) return (bytes + 255) & ~(size_t)255;
+    int top = 63 - __builtin_clzll((unsigned long long)bytes);
+    const size_t step = (size_t)1 << (top - 3);
+    return (bytes + step - 1) & ~(step - 1);
+}
+
 struct Pool {
     Pool() {
         std::lock_guard<std::mutex> lk(pool_registry_mu());
@@ -51,13 +62,17 @@ struct Pool {
     std::multimap<size_t, void *> free_list;
     size_t live = 0, cached = 0, peak = 0;
     int device = 0;
-    void *get(size_t bytes) {
-        bytes = (bytes + 255) & ~(size_t)255;
+    // Best fit: the smallest cached block of at least `bytes` is reused if it is
+    // no more than 1.5x the request (its real size is returned in `bytes`, to be
+    // handed back to put), else a new class-sized block is allocated.
+    void *get(size_t &bytes) {
+        bytes = size_class(bytes);
         {
             std::lock_guard<std::mutex> lk(mu);
-            auto it = free_list.find(bytes);
-            if (it != free_list.end()) {
+            auto it = free_list.lower_bound(bytes);
+            if (it != free_list.end() && it->first <= bytes + bytes / 2) {
                 void *p = it->second;
+                bytes = it->first;
                 free_list.erase(it);
                 cached -= bytes;
                 live += bytes;
@@ -76,8 +91,7 @@ struct Pool {
         peak = std::max(peak, live);
         return p;
     }
-    void put(void *p, size_t bytes) {
-        bytes = (bytes + 255) & ~(size_t)255;
+    void put(void *p, size_t bytes) {  // bytes: the block size get() returned
         std::lock_guard<std::mutex> lk(mu);
         free_list.emplace(bytes, p);
         live -= bytes;
@@ -150,7 +164,7 @@ struct Engine::Impl {
     std::shared_ptr<DevMem> alloc(size_t bytes) {
         auto m = std::make_shared<DevMem>();
         m->pool = pool;
-        m->p = pool->get(bytes);
+        m->p = pool->get(bytes);  // bytes becomes the block size
         m->bytes = bytes;
         return m;
     }

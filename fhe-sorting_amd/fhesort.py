@@ -91,6 +91,8 @@ _SIGS = {
     'fhe_mehp24_parameters': (C.c_int, [C.c_int, ip, ip, ip, ip, ip, ip, ip, ip, ip, C.c_int]),
     'fhe_mehp24_rotation_indices': (C.c_int, [C.c_int, C.c_int, ip, C.c_int]),
     'fhe_mehp24_sort': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_mehp24_sort_sharded': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.c_int, C.c_int, vp, vp, PP]),
     'fhe_mehp24_indicator': (C.c_int, [vp, vp, C.c_double, C.c_int, C.c_int, PP]),
     'fhe_comm_get_unique_id': (C.c_int, [C.POINTER(C.c_uint8)]),
     'fhe_comm_init': (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
@@ -368,10 +370,17 @@ class Context:
                          cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1],
                          C.cast(cb, C.c_void_p) if cb else None, None)
 
-    def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0):
+    def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0, shard=(0, 1), allreduce=None):
         """mehp24::sortFG (sub 0; x holds N values in N*N slots) or
-        sortLargeArrayFG with parts of `sub` values (x in sub*sub slots)."""
-        return self._new(lib().fhe_mehp24_sort, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i)
+        sortLargeArrayFG with parts of `sub` values (x in sub*sub slots).
+        shard=(rank, world): the pair compares and indicators are split over
+        ranks and combined by `allreduce` (or RCCL after comm_init)."""
+        if shard == (0, 1) and allreduce is None:
+            return self._new(lib().fhe_mehp24_sort, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i)
+        cb = ALLREDUCE_FN(allreduce) if allreduce else None
+        self._cb = cb  # keep alive for the duration of the call
+        return self._new(lib().fhe_mehp24_sort_sharded, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i,
+                         shard[0], shard[1], C.cast(cb, C.c_void_p) if cb else None, None)
 
     def mehp24_indicator(self, x, b, dg, df):
         return self._new(lib().fhe_mehp24_indicator, x.h, b, dg, df)

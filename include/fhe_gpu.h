@@ -196,6 +196,15 @@ int fhe_mehp24_rotation_indices(int N, int sub, int32_t *rots, int max_rots);
  * Independent compares / indicators run stacked (fhe_set_sort_stack bounds it). */
 int fhe_mehp24_sort(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i,
                     fhe_ct **out);
+/* fhe_mehp24_sort with sortLargeArrayFG's P(P+1)/2 pair compares
+ * (mehp24_sort.cpp:477-514, an OpenMP loop in the reference) and P^2 indicators
+ * (:574-594) sharded over ranks (item i on rank i % shard_world); the partial
+ * Cv / Ch / subSorted sums are combined by `allreduce` (or RCCL after
+ * fhe_comm_init when it is NULL), so every rank returns the same, unsharded
+ * result.  sub == 0 (one ciphertext) has nothing to shard and runs replicated. */
+int fhe_mehp24_sort_sharded(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n, int dg, int df, int dg_i,
+                            int df_i, int shard_rank, int shard_world, fhe_allreduce_fn allreduce, void *user,
+                            fhe_ct **out);
 /* mehp24::utils::indicatorAdv(c, b, dg, df) (src/mehp24/mehp24_utils.cpp:166-174) */
 int fhe_mehp24_indicator(fhe_ctx *ctx, const fhe_ct *x, double b, int dg, int df, fhe_ct **out);
 

@@ -282,6 +282,15 @@ SortShape check_shape(int N, int max_batch);
 // Reduction hook for sharded runs: sums the ciphertext limbs over ranks in place
 // (u64 add), the callee leaves values < world*q; caller reduces mod q.
 using CtAllReduce = std::function<void(u64 *data, size_t count)>;
+// Independent items i handled by this rank iff i % world == rank.
+struct Shard {
+    int rank = 0, world = 1;
+    CtAllReduce allreduce;
+    bool mine(size_t i) const { return world <= 1 || (int)(i % (size_t)world) == rank; }
+};
+// Sum of per-rank partials (level agreed through a 2-word header; a rank with
+// no partial contributes zeros), reduced mod q.  No-op for one rank.
+void reduce_partial(Context &cc, const Shard &sh, CtPtr &acc, int slots);
 
 class DirectSort {
   public:
@@ -318,10 +327,12 @@ CtPtr sign_adv(Context &cc, CtPtr c, size_t dg, size_t df);
 CtPtr indicator_adv(Context &cc, const CtPtr &c, double b, size_t dg, size_t df);
 CtPtr sort_fg(Context &cc, const Ciphertext &c, size_t m, SignFunc f, const SignConfig &cfg, size_t dg_i,
               size_t df_i);
+// the pair compares (index in mehp24_sort.cpp:480-495 order) and the
+// indicators (index j * P + k) are sharded over `sh`
 std::vector<CtPtr> sort_fg_multi(Context &cc, const std::vector<CtPtr> &c, size_t sub, SignFunc f,
-                                 const SignConfig &cfg, size_t dg_i, size_t df_i);
+                                 const SignConfig &cfg, size_t dg_i, size_t df_i, const Shard &sh = Shard());
 CtPtr sort_large_fg(Context &cc, const Ciphertext &c, size_t total, size_t sub, SignFunc f, const SignConfig &cfg,
-                    size_t dg_i, size_t df_i);
+                    size_t dg_i, size_t df_i, const Shard &sh = Shard());
 }  // namespace mehp24
 
 }  // namespace oracle

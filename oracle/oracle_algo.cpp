@@ -456,14 +456,22 @@ DirectSort::DirectSort(Context &c, int N_, const std::vector<int> &rotIndices)
 
 void DirectSort::reduce_partial(CtPtr &acc, int level_hint, int slots) {
     (void)level_hint;
-    if (shard_world <= 1) return;
-    if (!allreduce) throw std::runtime_error("DirectSort: sharded run without an allreduce hook");
+    Shard sh;
+    sh.rank = shard_rank;
+    sh.world = shard_world;
+    sh.allreduce = allreduce;
+    oracle::reduce_partial(cc, sh, acc, slots);
+}
+
+void reduce_partial(Context &cc, const Shard &sh, CtPtr &acc, int slots) {
+    if (sh.world <= 1) return;
+    if (!sh.allreduce) throw std::runtime_error("sharded run without an allreduce hook");
     u64 hdr[2] = {acc ? (u64)(acc->level + 1) : 0, acc ? 1ULL : 0ULL};
-    allreduce(hdr, 2);
-    if (hdr[1] == 0) throw std::runtime_error("DirectSort: no shard produced a partial");
+    sh.allreduce(hdr, 2);
+    if (hdr[1] == 0) throw std::runtime_error("sharded run: no shard produced a partial");
     int level = (int)(hdr[0] / hdr[1]) - 1;
     if (!acc) acc = cc.zero_like(level, slots);
-    allreduce(acc->c.data(), acc->c.size());
+    sh.allreduce(acc->c.data(), acc->c.size());
     const size_t n = cc.P.n;
     for (int p = 0; p < 2; ++p)
         for (size_t l = 0; l < acc->limbs; ++l) {
@@ -686,7 +694,7 @@ CtPtr sort_fg(Context &cc, const Ciphertext &c0, size_t m, SignFunc f, const Sig
 
 // sortFG over parts of `sub` values each (mehp24_sort.cpp:445-645)
 std::vector<CtPtr> sort_fg_multi(Context &cc, const std::vector<CtPtr> &c, size_t sub, SignFunc f,
-                                 const SignConfig &cfg, size_t dg_i, size_t df_i) {
+                                 const SignConfig &cfg, size_t dg_i, size_t df_i, const Shard &sh) {
     const size_t P = c.size(), m = sub * P;
     std::vector<CtPtr> R(P), Cc(P);
     for (size_t j = 0; j < P; ++j) {
@@ -694,12 +702,17 @@ std::vector<CtPtr> sort_fg_multi(Context &cc, const std::vector<CtPtr> &c, size_
         Cc[j] = replicate_column(cc, transpose_row(cc, c[j], sub, true), sub);
     }
     std::vector<CtPtr> Cv(P), Ch(P);
+    size_t pair = 0;
     for (size_t j = 0; j < P; ++j)
-        for (size_t k = j; k < P; ++k) {  // pair order of :480-495
+        for (size_t k = j; k < P; ++k, ++pair) {  // pair order of :480-495
+            if (!sh.mine(pair)) continue;
             CtPtr Cjk = compare(cc, *R[j], *Cc[k], f, cfg);
             cc.add_inplace(Cv[j], *Cjk);
             if (j != k) cc.add_inplace(Ch[k], *cc.add_const(*cc.negate(*Cjk), 1.0));
         }
+    const int slots = R[0]->slots;
+    for (size_t j = 0; j < P; ++j) reduce_partial(cc, sh, Cv[j], slots);
+    for (size_t k = 1; k < P; ++k) reduce_partial(cc, sh, Ch[k], slots);
     std::vector<CtPtr> s(P);
     for (size_t j = 0; j < P; ++j) {
         s[j] = sum_rows(cc, Cv[j], sub, false, 0);
@@ -717,10 +730,12 @@ std::vector<CtPtr> sort_fg_multi(Context &cc, const std::vector<CtPtr> &c, size_
             for (size_t b = 0; b < sub; ++b) sm[a * sub + b] = -1.0 * (double)(j * sub + a) - 0.5;
         CtPtr acc;
         for (size_t k = 0; k < P; ++k) {
+            if (!sh.mine(j * P + k)) continue;
             CtPtr x = cc.add_plain(*s[k], cc.encode(sm, s[k]->slots, s[k]->level));
             CtPtr ind = cc.mul(*indicator_adv(cc, x, (double)m, dg_i, df_i), *R[k]);
             cc.add_inplace(acc, *ind);
         }
+        reduce_partial(cc, sh, acc, slots);
         out[j] = transpose_column(cc, sum_columns(cc, acc, sub, true), sub, true);
     }
     return out;
@@ -729,7 +744,7 @@ std::vector<CtPtr> sort_fg_multi(Context &cc, const std::vector<CtPtr> &c, size_
 // sortLargeArrayFG (mehp24_sort.cpp:623-645 with utils :265-303): split into
 // parts of `sub` values, sort them as one vector, recombine
 CtPtr sort_large_fg(Context &cc, const Ciphertext &c, size_t total, size_t sub, SignFunc f, const SignConfig &cfg,
-                    size_t dg_i, size_t df_i) {
+                    size_t dg_i, size_t df_i, const Shard &sh) {
     const size_t P = total / sub;
     std::vector<CtPtr> parts(P);
     for (size_t i = 0; i < P; ++i) {
@@ -739,7 +754,7 @@ CtPtr sort_large_fg(Context &cc, const Ciphertext &c, size_t total, size_t sub, 
         if (i > 0) part = cc.rotate(*part, (long)(i * sub));
         parts[i] = part;
     }
-    auto sorted = sort_fg_multi(cc, parts, sub, f, cfg, dg_i, df_i);
+    auto sorted = sort_fg_multi(cc, parts, sub, f, cfg, dg_i, df_i, sh);
     CtPtr r = sorted[0];
     for (size_t i = 1; i < P; ++i) r = cc.add(*r, *cc.rotate(*sorted[i], -(long)(i * sub)));
     return r;

@@ -256,12 +256,20 @@ void *orc_direct_sort(void *c, void *x, void *rank, int N, const int *rots, int 
 
 // MEHP24: sub == 0 -> sortFG on one ciphertext; otherwise sortLargeArrayFG
 // with parts of `sub` values (mehp24_sort.h sortFG / sortLargeArrayFG)
-void *orc_mehp24_sort(void *c, void *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i) {
+void *orc_mehp24_sort_sharded(void *c, void *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i,
+                              int shard_rank, int shard_world, orc_allreduce_fn fn, void *user) {
     return guard([&]() -> void * {
         auto cfg = cfg3(n, dg, df);
         if (sub == 0) return wrap(mehp24::sort_fg(*CTX, CT(x), N, SignFunc::CompositeSign, cfg, dg_i, df_i));
-        return wrap(mehp24::sort_large_fg(*CTX, CT(x), N, sub, SignFunc::CompositeSign, cfg, dg_i, df_i));
+        Shard sh;
+        sh.rank = shard_rank;
+        sh.world = shard_world;
+        if (fn) sh.allreduce = [fn, user](uint64_t *d, size_t cnt) { fn(d, (uint64_t)cnt, user); };
+        return wrap(mehp24::sort_large_fg(*CTX, CT(x), N, sub, SignFunc::CompositeSign, cfg, dg_i, df_i, sh));
     }, (void *)nullptr);
+}
+void *orc_mehp24_sort(void *c, void *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i) {
+    return orc_mehp24_sort_sharded(c, x, N, sub, n, dg, df, dg_i, df_i, 0, 1, nullptr, nullptr);
 }
 void *orc_mehp24_indicator(void *c, void *a, double b, int dg, int df) {
     return guard([&]() -> void * { return wrap(mehp24::indicator_adv(*CTX, CTX->clone(CT(a)), b, dg, df)); },

@@ -77,6 +77,8 @@ def lib():
                                      C.c_int, C.c_int, C.c_int, vp, vp]),
             'orc_size_parameters': (C.c_int, [C.c_int, ip, ip, C.c_int]),
             'orc_mehp24_sort': (vp, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+            'orc_mehp24_sort_sharded': (vp, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             C.c_int, C.c_int, vp, vp]),
             'orc_mehp24_indicator': (vp, [vp, vp, C.c_double, C.c_int, C.c_int]),
             'orc_mehp24_rotation_indices': (C.c_int, [C.c_int, C.c_int, ip, C.c_int]),
             'orc_decompose': (C.c_int, [C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip, C.c_int]),
@@ -314,8 +316,14 @@ class Context:
                                   C.cast(cb, C.c_void_p) if cb else None, None)
         return Ct(self, h)
 
-    def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0):
-        return Ct(self, lib().orc_mehp24_sort(self.h, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i))
+    def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0, shard=(0, 1), allreduce=None):
+        if shard == (0, 1) and allreduce is None:
+            return Ct(self, lib().orc_mehp24_sort(self.h, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i))
+        cb = ALLREDUCE_FN(allreduce) if allreduce else None
+        self._cb = cb
+        return Ct(self, lib().orc_mehp24_sort_sharded(self.h, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i,
+                                                      shard[0], shard[1], C.cast(cb, C.c_void_p) if cb else None,
+                                                      None))
 
     def mehp24_indicator(self, a, b, dg, df):
         return Ct(self, lib().orc_mehp24_indicator(self.h, a.h, b, dg, df))

@@ -1,4 +1,4 @@
-"""Multi-rank DirectSort on CPU: world_size 2 over gloo.
+"""Multi-rank DirectSort and MEHP24 sortLargeArrayFG on CPU: world_size 2 over gloo.
 
 The bench shards the comparator batches of constructRank and the index-check
 batches of rotationIndexCheckN over ranks (batch b -> rank b % world) and sums
@@ -7,6 +7,8 @@ DESIGN.md §7.  Here the same protocol runs through the oracle's allreduce hook
 with torch.distributed (gloo) as the transport, and the sharded result must be
 bit-identical to the unsharded one (reference behaviour: src/sort_algo.h:
 182-214 runs the batches serially; sharding must not change the answer).
+MEHP24 shards its pair compares and indicators the same way (item i on rank
+i % world, partial Cv / Ch / subSorted sums all-reduced).
 The GPU engine implements the identical hook (fhe_direct_sort allreduce
 callback / RCCL); tests/test_gpu_parity.py checks it against this oracle.
 """
@@ -39,20 +41,42 @@ def _gloo_allreduce(buf_ptr, count, _user):
     arr[:] = t.numpy().view(np.uint64)
 
 
-def _worker(rank, world, port, outdir):
+def _input(c, kind):
+    """DirectSort N=64, or MEHP24 sortLargeArrayFG of 16 values in parts of 4
+    (10 pair compares, 16 indicators -- mehp24_sort.cpp:477-514, 574-594)."""
+    n = N if kind == 'direct' else 16
+    x = np.random.default_rng(n).permutation(n) / n
+    return x, c.encrypt(x, n)
+
+
+def _run(c, kind, ct, shard=(0, 1), allreduce=None):
+    if kind == 'direct':
+        depth, rots = O.size_parameters(N)
+        return c.direct_sort(ct, N, rots, (3, 3, 2), shard=shard, allreduce=allreduce)
+    return c.mehp24_sort(ct, 16, (3, 2, 2), 2, 2, 4, shard=shard, allreduce=allreduce)
+
+
+def _context(kind):
+    if kind == 'direct':
+        depth, rots = O.size_parameters(N)
+    else:
+        depth, rots = 35, O.mehp24_rotation_indices(16, 4)
+    c = O.Context(LOGN, depth, 40, 60, 3, seed=7)
+    c.gen_rotation_keys(rots)
+    return c
+
+
+def _worker(rank, world, port, outdir, kind):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     os.environ['OMP_NUM_THREADS'] = '2'
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    depth, rots = O.size_parameters(N)
-    c = O.Context(LOGN, depth, 40, 60, 3, seed=7)
-    c.gen_rotation_keys(rots)
-    x = np.random.default_rng(64).permutation(N) / N
-    ct = c.encrypt(x, N)
-    out = c.direct_sort(ct, N, rots, (3, 3, 2), shard=(rank, world), allreduce=_gloo_allreduce)
+    c = _context(kind)
+    x, ct = _input(c, kind)
+    out = _run(c, kind, ct, shard=(rank, world), allreduce=_gloo_allreduce)
     np.save(os.path.join(outdir, f'rank{rank}.npy'), out.data())
     if rank == 0:
-        ref = c.direct_sort(ct, N, rots, (3, 3, 2))
+        ref = _run(c, kind, ct)
         np.save(os.path.join(outdir, 'unsharded.npy'), ref.data())
         np.save(os.path.join(outdir, 'decrypted.npy'), c.decrypt(out))
         np.save(os.path.join(outdir, 'x.npy'), x)
@@ -61,9 +85,10 @@ def _worker(rank, world, port, outdir):
 
 
 @pytest.mark.slow
-def test_sharded_direct_sort_world2_matches_unsharded(tmp_path):
+@pytest.mark.parametrize('kind', ['direct', 'mehp24'])
+def test_sharded_sort_world2_matches_unsharded(tmp_path, kind):
     world = 2
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), kind), nprocs=world, join=True,
                        start_method='spawn')
     r0 = np.load(tmp_path / 'rank0.npy')
     r1 = np.load(tmp_path / 'rank1.npy')
@@ -71,5 +96,5 @@ def test_sharded_direct_sort_world2_matches_unsharded(tmp_path):
     assert np.array_equal(r0, r1), 'ranks disagree after the all-reduce'
     assert np.array_equal(r0, ref), 'sharded result differs from the unsharded sort'
     x = np.load(tmp_path / 'x.npy')
-    y = np.load(tmp_path / 'decrypted.npy')
+    y = np.load(tmp_path / 'decrypted.npy')[:len(x)]
     assert np.max(np.abs(y - np.sort(x))) < 0.01

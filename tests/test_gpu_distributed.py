@@ -1,4 +1,4 @@
-"""Sharded DirectSort on the GPU engine, two ranks on one MI355X.
+"""Sharded DirectSort and MEHP24 sortLargeArrayFG on the GPU engine, two ranks on one MI355X.
 
 Each rank owns a context on device 0 (deterministic key generation: identical
 keys and encryptions), runs batches b with b % 2 == rank, and sums the partial
@@ -25,7 +25,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, kind):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     import torch
@@ -43,26 +43,37 @@ def _worker(rank, world, port, outdir):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)  # two's-complement wrap == u64 add
         assert hip.hipMemcpy(C.cast(ptr, C.c_void_p), buf.ctypes.data, count * 8, H2D) == 0
 
-    depth, rots = F.size_parameters(N)
+    if kind == 'direct':
+        depth, rots = F.size_parameters(N)
+        n = N
+    else:  # MEHP24 sortLargeArrayFG, 16 values in parts of 4: 10 pair compares, 16 indicators
+        depth, rots, n = 35, F.mehp24_rotation_indices(16, 4), 16
     ctx = F.Context(LOGN, depth, 40, 60, 3, seed=31)
     ctx.gen_rotation_keys(rots)
     ctx.set_sort_stack(2)
-    x = np.random.default_rng(5).permutation(N) / N
-    ct = ctx.encrypt(x, N)
-    out = ctx.direct_sort(ct, N, rots, (3, 3, 2), shard=(rank, world), allreduce=allreduce)
+    x = np.random.default_rng(5).permutation(n) / n
+    ct = ctx.encrypt(x, n)
+
+    def run(**kw):
+        if kind == 'direct':
+            return ctx.direct_sort(ct, N, rots, (3, 3, 2), **kw)
+        return ctx.mehp24_sort(ct, 16, (3, 2, 2), 2, 2, 4, **kw)
+    out = run(shard=(rank, world), allreduce=allreduce)
     np.save(os.path.join(outdir, f'rank{rank}.npy'), out.data())
     if rank == 0:
-        ref = ctx.direct_sort(ct, N, rots, (3, 3, 2))
+        ref = run()
         np.save(os.path.join(outdir, 'ref.npy'), ref.data())
-        np.save(os.path.join(outdir, 'dec.npy'), ctx.decrypt(out))
+        np.save(os.path.join(outdir, 'dec.npy'), ctx.decrypt(out)[:n])
         np.save(os.path.join(outdir, 'x.npy'), x)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_ranks_one_gpu_match_unsharded(tmp_path):
+@pytest.mark.parametrize('kind', ['direct', 'mehp24'])
+def test_two_ranks_one_gpu_match_unsharded(tmp_path, kind):
     import torch.multiprocessing as mp
-    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method='spawn')
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), kind), nprocs=2, join=True,
+                       start_method='spawn')
     r0, r1, ref = (np.load(tmp_path / f) for f in ('rank0.npy', 'rank1.npy', 'ref.npy'))
     assert np.array_equal(r0, r1), 'ranks disagree after the all-reduce'
     assert np.array_equal(r0, ref), 'sharded GPU sort differs from the unsharded one'

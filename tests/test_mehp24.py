@@ -57,6 +57,14 @@ def test_parameters_match_reference_test(N):
     assert alpha <= 15
 
 
+def test_parameters_4096_extension():
+    """N=4096 (BASELINE config 5) is beyond the reference table (which ends at
+    2048); it keeps 2048's Cfg (3,5,2), dg_i = 6 and depth, parts of 256."""
+    p, q = F.mehp24_parameters(4096), F.mehp24_parameters(2048)
+    assert (p['depth'], p['cfg'], p['dg_i'], p['df_i'], p['sub']) == (q['depth'], q['cfg'], 6, 2, 256)
+    assert p['rots'] == ref_rotation_indices(4096)
+
+
 def test_parameters_reject_bad_n():
     with pytest.raises(F.FheError):
         F.mehp24_parameters(12)
