@@ -153,7 +153,12 @@ def pmc_lookup(table, name):
     if base in table:
         return table[base]
     hits = [v for k, v in table.items() if k.split('<')[0] == base]
-    return hits[0] if len(hits) == 1 else None
+    if not hits:
+        return None
+    # several instantiations booked under one clock name (k_linear_sum_multi<G>):
+    # launch-weighted mean, like the clock's own per-launch average
+    n = sum(v['launches'] for v in hits)
+    return {'launches': n, 'hbm_bytes_per_launch': sum(v['hbm_bytes_per_launch'] * v['launches'] for v in hits) / n}
 
 
 def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json'):
