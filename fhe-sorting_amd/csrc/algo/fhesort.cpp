@@ -10,6 +10,7 @@
 #include "fhesort.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cmath>
 #include <fstream>
 #include <map>
@@ -403,6 +404,59 @@ std::vector<CtPtr> RotationComposerN::rotateMany(const Ciphertext &in, const std
 }
 
 // ============================================================ DirectSort ===
+// ---------------------------------------------------------- RotationTree ----
+RotationTreeN::RotationTreeN(Engine &c, int N, const std::vector<int> &rotIndices, DecomposeAlgo a)
+    : cc(c), dec(N, rotIndices), algo(a), root(std::make_unique<Node>(0, nullptr)) {}
+
+void RotationTreeN::buildTree(int start, int end) {  // src/rotation.h:272-279
+    for (int i = start; i <= end; ++i) addToTree(root.get(), dec.decompose(i, end, algo), 0, i);
+}
+
+void RotationTreeN::addToTree(Node *node, const std::vector<Step> &steps, size_t i, int value) {  // :293-312
+    for (; i < steps.size(); ++i) {
+        if (steps[i].value == 0) continue;
+        auto &child = node->children[steps[i].stepSize];
+        if (!child) child = std::make_unique<Node>(steps[i].stepSize, node);
+        node = child.get();
+    }
+    node->finalValues.push_back(value);
+}
+
+CtPtr RotationTreeN::treeRotate(const Ciphertext &input, int rotation) {  // :281-291
+    auto steps = dec.decompose(rotation, input.slots, algo);
+    return traverse(cc.clone(input), root.get(), steps, 0);
+}
+
+CtPtr RotationTreeN::traverse(const CtPtr &input, Node *node, const std::vector<Step> &steps, size_t i) {
+    for (; i < steps.size() && steps[i].value == 0; ++i) {
+    }
+    if (i >= steps.size()) return input;
+    auto it = node->children.find(steps[i].stepSize);
+    if (it == node->children.end()) {  // the reference reports and returns the partial rotation (:323-327)
+        std::fprintf(stderr, "Error: Child node not found for step size %d\n", steps[i].stepSize);
+        return input;
+    }
+    Node *child = it->second.get();
+    if (child->rotated) {
+        ++stats.cacheHits;
+    } else {
+        // all not-yet-rotated children of this node share the node's ModUp
+        std::vector<Node *> todo;
+        std::vector<long> ks;
+        for (auto &kv : node->children)
+            if (!kv.second->rotated) {
+                todo.push_back(kv.second.get());
+                ks.push_back(kv.first);
+            }
+        auto outs = cc.rotate_hoisted(*input, ks);
+        for (size_t j = 0; j < todo.size(); ++j) todo[j]->rotated = outs[j];
+        stats.cacheMisses += 1;
+        stats.fastRotationCount += todo.size();
+        stats.totalRotationCount += todo.size();
+    }
+    return traverse(child->rotated, child, steps, i + 1);
+}
+
 void directSortSizeParameters(int N, int &multDepth, std::vector<int> &r) {
     // restated from src/sort_algo.h:87-201 (depth, rotation-key set per N)
     switch (N) {

@@ -94,6 +94,53 @@ class RotationComposer : public RotationComposerN {
         : RotationComposerN(cc, SIZE, rot, a) {}
 };
 
+// src/rotation.h:168-191
+struct RotationStats {
+    size_t fastRotationCount = 0, normalRotationCount = 0, totalRotationCount = 0, cacheHits = 0, cacheMisses = 0;
+    void reset() { *this = RotationStats(); }
+};
+
+// RotationTree<N> (src/rotation.h:240-358): rotations by any k as paths of
+// keyed steps in a prefix tree; every node's rotated ciphertext is cached, and
+// the children of a node are rotations of one ciphertext, so they share one
+// ModUp.  The reference computes a child on first use with
+// EvalFastRotation(node precompute); here the first use of any child of a
+// node computes all of that node's built children in one hoisted launch
+// sequence (fhe_rotate_hoisted) -- hoisted and single rotations are
+// bit-identical in this engine, so results do not depend on the order of
+// requests.  As in the reference, the cache belongs to the first input
+// rotated: one tree per input ciphertext.
+class RotationTreeN {
+  public:
+    RotationTreeN(Engine &cc, int N, const std::vector<int> &rotIndices, DecomposeAlgo algo = DecomposeAlgo::NAF);
+    void buildTree(int start, int end);
+    CtPtr treeRotate(const Ciphertext &input, int rotation);
+    const RotationStats &getStats() const { return stats; }
+
+  private:
+    struct Node {
+        int stepSize;
+        Node *parent;
+        std::map<int, std::unique_ptr<Node>> children;
+        std::vector<int> finalValues;
+        CtPtr rotated;
+        Node(int s, Node *p) : stepSize(s), parent(p) {}
+    };
+    void addToTree(Node *node, const std::vector<Step> &steps, size_t i, int value);
+    CtPtr traverse(const CtPtr &input, Node *node, const std::vector<Step> &steps, size_t i);
+    Engine &cc;
+    DecomposerN dec;
+    DecomposeAlgo algo;
+    std::unique_ptr<Node> root;
+    RotationStats stats;
+};
+template <int SIZE>
+class RotationTree : public RotationTreeN {
+  public:
+    RotationTree(Engine &cc, const std::vector<int> &rot, DecomposeAlgo a = DecomposeAlgo::NAF)
+        : RotationTreeN(cc, SIZE, rot, a) {}
+};
+
 struct SortShape {
     int N, num_partition, num_batch, num_slots, np;
 };

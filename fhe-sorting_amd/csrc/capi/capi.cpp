@@ -30,6 +30,9 @@ struct fhe_ct {
 struct fhe_pt {
     PtPtr p;
 };
+struct fhe_rot_tree {
+    std::unique_ptr<RotationTreeN> t;
+};
 
 namespace {
 thread_local std::string g_err;
@@ -287,6 +290,38 @@ int fhe_compose_rotate(fhe_ctx *ctx, const fhe_ct *a, int N, const int32_t *rots
         *out = wrap(rc.rotate(*a->p, rotation));
     });
 }
+int fhe_rotation_tree_create(fhe_ctx *ctx, int N, const int32_t *rots, int nrot, int algo, fhe_rot_tree **out) {
+    return guard([&] {
+        NEED(ctx);
+        if (algo < 0 || algo > 2) throw std::invalid_argument("rotation tree: algo must be 0 (NAF), 1 (BNAF), 2 (BINARY)");
+        auto t = std::make_unique<fhe_rot_tree>();
+        t->t = std::make_unique<RotationTreeN>(*ctx->eng, N, std::vector<int>(rots, rots + nrot), (DecomposeAlgo)algo);
+        *out = t.release();
+    });
+}
+int fhe_rotation_tree_build(fhe_rot_tree *t, int start, int end) {
+    return guard([&] {
+        NEED(t);
+        t->t->buildTree(start, end);
+    });
+}
+int fhe_rotation_tree_rotate(fhe_rot_tree *t, const fhe_ct *a, int rotation, fhe_ct **out) {
+    return guard([&] {
+        NEED(t);
+        NEED(a);
+        *out = wrap(t->t->treeRotate(*a->p, rotation));
+    });
+}
+int fhe_rotation_tree_stats(const fhe_rot_tree *t, uint64_t stats[5]) {
+    return guard([&] {
+        NEED(t);
+        const RotationStats &s = t->t->getStats();
+        const uint64_t v[5] = {s.fastRotationCount, s.normalRotationCount, s.totalRotationCount, s.cacheHits,
+                               s.cacheMisses};
+        for (int i = 0; i < 5; ++i) stats[i] = v[i];
+    });
+}
+void fhe_rotation_tree_destroy(fhe_rot_tree *t) { delete t; }
 int fhe_decompose(int N, const int32_t *rots, int nrot, int rotation, int wrap_n, int algo, int32_t *values,
                   int32_t *sizes, int max_steps) {
     int count = -1;

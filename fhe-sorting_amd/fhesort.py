@@ -85,6 +85,11 @@ _SIGS = {
     'fhe_indicator': (C.c_int, [vp, vp, C.c_double, C.c_int, C.c_int, C.c_int, PP]),
     'fhe_compose_rotate': (C.c_int, [vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, PP]),
     'fhe_decompose': (C.c_int, [C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip, C.c_int]),
+    'fhe_rotation_tree_create': (C.c_int, [vp, C.c_int, ip, C.c_int, C.c_int, PP]),
+    'fhe_rotation_tree_build': (C.c_int, [vp, C.c_int, C.c_int]),
+    'fhe_rotation_tree_rotate': (C.c_int, [vp, vp, C.c_int, PP]),
+    'fhe_rotation_tree_stats': (C.c_int, [vp, C.POINTER(C.c_uint64)]),
+    'fhe_rotation_tree_destroy': (None, [vp]),
     'fhe_size_parameters': (C.c_int, [C.c_int, ip, ip, C.c_int]),
     'fhe_direct_sort': (C.c_int, [vp, vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_int, vp, vp, PP]),
@@ -153,6 +158,36 @@ def _dbl(a):
 
 def _int(a):
     return a.ctypes.data_as(ip)
+
+
+class RotationTree:
+    """Handle over fhe_rotation_tree_*: build(start, end), rotate(ct, k), stats()."""
+
+    def __init__(self, ctx, N, rots, algo=0):
+        r = np.asarray(rots, dtype=np.int32)
+        out = C.c_void_p()
+        _chk(lib().fhe_rotation_tree_create(ctx.h, N, _int(r), len(r), algo, C.byref(out)))
+        self.ctx, self.h = ctx, out.value
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().fhe_rotation_tree_destroy(self.h)
+        except Exception:
+            pass
+
+    def build(self, start, end):
+        _chk(lib().fhe_rotation_tree_build(self.h, start, end))
+
+    def rotate(self, a, rotation):
+        out = C.c_void_p()
+        _chk(lib().fhe_rotation_tree_rotate(self.h, a.h, rotation, C.byref(out)))
+        return Ct(self.ctx, out.value)
+
+    def stats(self):
+        v = (C.c_uint64 * 5)()
+        _chk(lib().fhe_rotation_tree_stats(self.h, v))
+        return dict(zip(('fast', 'normal', 'total', 'cache_hits', 'cache_misses'), (int(x) for x in v)))
 
 
 class Ct:
@@ -357,6 +392,10 @@ class Context:
     def sign(self, a, n, dg, df): return self._new(lib().fhe_sign_composite, a.h, n, dg, df)
     def compare(self, a, b, n, dg, df): return self._new(lib().fhe_compare, a.h, b.h, n, dg, df)
     def indicator(self, a, c, n, dg, df): return self._new(lib().fhe_indicator, a.h, c, n, dg, df)
+
+    def rotation_tree(self, N, rots, algo=0):
+        """RotationTree<N>(cc, rots, algo) (src/rotation.h:240-358); algo 0 = NAF."""
+        return RotationTree(self, N, rots, algo)
 
     def compose_rotate(self, a, N, rots, algo, rotation):
         r = np.asarray(rots, dtype=np.int32)

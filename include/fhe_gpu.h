@@ -150,6 +150,18 @@ int fhe_indicator(fhe_ctx *ctx, const fhe_ct *x, double c, int n, int dg, int df
  * algo: 0 NAF, 1 BNAF, 2 BINARY */
 int fhe_compose_rotate(fhe_ctx *ctx, const fhe_ct *a, int N, const int32_t *rots, int nrot, int algo,
                        int rotation, fhe_ct **out);
+/* RotationTree<N>(cc, rots, algo) (src/rotation.h:240-358): buildTree(start, end)
+ * (:272-279), treeRotate(ct, rotation) (:281-291) with every node's rotation cached
+ * (one tree per input ciphertext, as in the reference) and the children of a node
+ * sharing one ModUp; getStats() (:168-191) as {fast, normal, total, cache hits,
+ * cache misses}.  A rotation whose path was not built returns the partial rotation
+ * after a message on stderr, like the reference (:323-327). */
+typedef struct fhe_rot_tree fhe_rot_tree;
+int fhe_rotation_tree_create(fhe_ctx *ctx, int N, const int32_t *rots, int nrot, int algo, fhe_rot_tree **out);
+int fhe_rotation_tree_build(fhe_rot_tree *t, int start, int end);
+int fhe_rotation_tree_rotate(fhe_rot_tree *t, const fhe_ct *a, int rotation, fhe_ct **out);
+int fhe_rotation_tree_stats(const fhe_rot_tree *t, uint64_t stats[5]);
+void fhe_rotation_tree_destroy(fhe_rot_tree *t);
 /* Decomposer<N>(rots).decompose(rotation, wrapN, algo) (src/rotation.h:54-102); returns #steps */
 int fhe_decompose(int N, const int32_t *rots, int nrot, int rotation, int wrap_n, int algo, int32_t *values,
                   int32_t *sizes, int max_steps);

@@ -130,6 +130,38 @@ def test_rotations(pair):
         gpu.rotate(gx, 7)
 
 
+TREE_ROTS = [-1, -2, -4, -8, -16, -32, 1, 2, 4, 8, 16, 32, 64, 512]  # tests/RotationTest.cpp:43
+
+
+def test_rotation_tree():
+    """RotationTest.RotateTreeVector (tests/RotationTest.cpp:77-108): RotationTree<8>
+    with NAF, treeRotate(ct, r) for r in [-4, 4] equals the rotated input (the
+    reference's 1e-6), and word for word the oracle's chain of single rotations
+    along the same NAF path (hoisted == single rotation).  The tree is built over
+    [-8, 8]: buildTree(start, end) decomposes with wrapN = end while treeRotate uses
+    the ciphertext's slots (src/rotation.h:275,284), so the reference's
+    buildTree(-4, 4) leaves e.g. the path of -3 at 8 slots ([4, 1]) unbuilt."""
+    orc = O.Context(12, 3, 40, 60, 3, seed=12)
+    orc.gen_rotation_keys(TREE_ROTS)
+    gpu = F.Context(12, 3, 40, 60, 3, seed=12, keygen=False)
+    gpu.load_keys_from(orc, TREE_ROTS)
+    x = np.arange(1.0, 9.0)
+    ox = orc.encrypt(x, 8)
+    gx = gpu.from_oracle(ox)
+    tree = gpu.rotation_tree(8, TREE_ROTS, 0)
+    tree.build(-8, 8)
+    for r in range(-4, 5):
+        got = tree.rotate(gx, r)
+        ref = ox
+        for v, step in F.decompose(8, TREE_ROTS, r, 8, 0):
+            if v:
+                ref = orc.rotate(ref, step)
+        same(got, ref)
+        assert np.max(np.abs(gpu.decrypt(got) - np.roll(x, -r))) < 1e-6, r
+    st = tree.stats()
+    assert st['cache_hits'] > 0 and st['fast'] == st['total'] > 0
+
+
 def test_modup_moddown(pair):
     orc, gpu = pair
     rng = np.random.default_rng(2)
