@@ -50,7 +50,7 @@ def parse():
     ap.add_argument('--log-n', type=int, default=16)
     ap.add_argument('--seed', type=int, default=20250704)
     ap.add_argument('--scale-bits', type=int, default=50,
-                    help='scaling-prime size; 40 (the reference) leaves the N>=128 sort noise-limited, DESIGN.md §6')
+                    help='scaling-prime size; 40 (the reference) leaves the N>=128 sort noise-limited, DESIGN.md §3')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true', help='skip the instrumented roofline sort (PMC passes)')
     ap.add_argument('--cpu-sample-mults', type=int, default=0, help='override CPU sample size')

@@ -376,7 +376,7 @@ __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const
 // v P with v = round(sum_k y_k / p_k) (fp64, fixed order; oracle: moddown), so
 // ModDown rounds x / P to nearest instead of flooring with a 0..K overshoot --
 // that overshoot is a biased error which, multiplied by s, concentrates in a
-// few slots.
+// few slots (numeric specification).
 template <int KT>
 __device__ __forceinline__ u64 centre_count(const u64 (&y)[KT], const double *pinvd) {
     double t = 0.0;
