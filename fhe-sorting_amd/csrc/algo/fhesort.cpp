@@ -657,6 +657,40 @@ void DirectSortN::reducePartial(CtPtr &acc, int slots) {
     fhe::reducePartial(cc, sh, acc, slots);
 }
 
+// The np baby-step rotations x, rot(x,1), ..., rot(x,np-1) of vecRotsOpt
+// (src/sort_algo.h:383-416) feed every comparator batch, so every rank needs all
+// of them.  One rank computes them (hoisted: one ModUp) when unsharded; sharded,
+// rank r computes steps i = r mod world and the rest arrive through one
+// all-reduce of the stacked steps (zeros where another rank owns the step, so
+// the u64 sum is a gather) -- the 32 top-level rotations were the largest
+// replicated cost of a sharded sort.  Same words either way.
+std::vector<CtPtr> DirectSortN::babySteps(const Ciphertext &x, int np) {
+    std::vector<int> idx;
+    for (int i = 0; i < np; ++i)
+        if (shard_world <= 1 || !allreduce || i % shard_world == shard_rank) idx.push_back(i);
+    std::vector<CtPtr> own = rot.rotateMany(x, idx);
+    if ((int)idx.size() == np) return own;
+    std::vector<CtPtr> all(np);
+    for (size_t j = 0; j < idx.size(); ++j) all[idx[j]] = own[j];
+    CtPtr zero;
+    std::vector<const Ciphertext *> ptrs;
+    for (int i = 0; i < np; ++i) {
+        if (!all[i]) {
+            if (!zero) zero = cc.zero_like(x.level, x.slots);
+            all[i] = zero;
+        }
+        ptrs.push_back(all[i].get());
+    }
+    CtPtr g = cc.stack(ptrs);
+    own.clear();
+    all.clear();
+    allreduce(g->data, 2 * (size_t)g->batch * g->limbs * cc.n());
+    cc.reduce_after_allreduce(*g);
+    std::vector<CtPtr> out;
+    for (int i = 0; i < np; ++i) out.push_back(cc.member(*g, i));
+    return out;
+}
+
 CtPtr DirectSortN::vecRotsOpt(Lane L, const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np,
                               int is) {
     CtPtr result;
@@ -682,9 +716,7 @@ CtPtr DirectSortN::vecRotsOpt(Lane L, const std::vector<CtPtr> &baby, int num_pa
 // accumulation (src/sort_algo.h:474-491) word for word.
 CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg) {
     const SortShape s = rankShape(N, max_batch);
-    std::vector<int> idx(s.np);
-    for (int i = 0; i < s.np; ++i) idx[i] = i;
-    std::vector<CtPtr> baby = rot.rotateMany(x, idx);
+    std::vector<CtPtr> baby = babySteps(x, s.np);
     for (auto &b : baby) b->slots = s.num_slots;
     std::vector<int> mine;
     for (int b = 0; b < s.num_batch; ++b)

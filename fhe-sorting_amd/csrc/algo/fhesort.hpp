@@ -200,6 +200,7 @@ class DirectSortN {
     CtPtr blindRotationStacked(Lane L, const std::vector<CtPtr> &masked, int num_slots, int np,
                                const std::vector<int> &ibs, int num_partition);
     void reducePartial(CtPtr &acc, int slots);
+    std::vector<CtPtr> babySteps(const Ciphertext &x, int np);
     // encoded on the calling lane's engine, published once complete (thread-safe)
     const Plaintext &mask(Engine &E, int kind, int num_slots, int k, int rot, int level);
     std::map<std::tuple<int, int, int, int, int>, PtPtr> mask_cache;
