@@ -145,6 +145,8 @@ struct SortShape {
     int N, num_partition, num_batch, num_slots, np;
 };
 void directSortSizeParameters(int N, int &multDepth, std::vector<int> &rotations);
+// the hybrid sort test's parameters (tests/DirectSortHTest.cpp:23-104, ring 2^17)
+void hybridSortSizeParameters(int N, int &multDepth, std::vector<int> &rotations);
 SortShape rankShape(int N, int max_batch);
 SortShape checkShape(int N, int max_batch);
 
@@ -171,6 +173,13 @@ class DirectSortN {
     CtPtr constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
     CtPtr rotationIndexCheckN(const Ciphertext &rank, const Ciphertext &x);
     CtPtr sort(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+    // sort_hybrid (src/sort_algo.h:1050-1064): constructRank, then the MEHP24-style
+    // matrix index check rotationIndexCheckHybrid (:893-1047); its num_batch^2
+    // masks run stacked, blocks b shard over ranks like the rank-sort batches
+    CtPtr rotationIndexCheckHybrid(const Ciphertext &rank, const Ciphertext &x);
+    CtPtr sort_hybrid(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+    int hybrid_max_array = 256;  // maxArraySize (:899)
+    int hybrid_mask = 0;         // 0: by N as the reference; 1: scaled-sinc PS; 2: indicator (3,4,2); 3: (3,5,2)
     const std::vector<double> &sincCoefficients() const;
 
     int shard_rank = 0, shard_world = 1;
@@ -265,5 +274,6 @@ Parameters parameters(size_t N);
 // coefficient tables (generated offline by data/gen_doubled_sinc.py)
 void setCoefficientDir(const std::string &dir);
 const std::vector<double> &doubledSincCoefficients(int N);
+const std::vector<double> &scaledSincCoefficients(int N);  // selectCoefficients<N>()
 
 }  // namespace fhe

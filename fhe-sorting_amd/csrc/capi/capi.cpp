@@ -395,6 +395,45 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
     });
 }
 
+int fhe_sort_hybrid(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, const int32_t *rots, int nrot, int n,
+                    int dg, int df, int mode, int max_array, int mask_mode, int shard_rank, int shard_world,
+                    fhe_allreduce_fn fn, void *user, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(x);
+        if (max_array < 1 || (max_array & (max_array - 1))) throw std::invalid_argument("sort_hybrid: bad max_array");
+        if (mask_mode < 0 || mask_mode > 3) throw std::invalid_argument("sort_hybrid: mask_mode must be 0..3");
+        if (shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world)
+            throw std::invalid_argument("sort_hybrid: bad shard");
+        auto key = std::make_pair(N, std::vector<int>(rots, rots + nrot));
+        auto &slot = ctx->sorters[key];
+        if (!slot) slot = std::make_unique<DirectSortN>(*ctx->eng, N, key.second);
+        DirectSortN &ds = *slot;
+        ds.max_stack = ctx->sort_stack;
+        ds.lanes = ctx->sort_lanes;
+        ds.shard_rank = shard_rank;
+        ds.shard_world = shard_world;
+        ds.allreduce = make_allreduce(ctx, shard_world, fn, user);
+        ds.hybrid_max_array = max_array;
+        ds.hybrid_mask = mask_mode;
+        if (mode == 1) {
+            NEED(rank);
+            *out = wrap(ds.rotationIndexCheckHybrid(*rank->p, *x->p));
+        } else {
+            *out = wrap(ds.sort_hybrid(*x->p, SignFunc::CompositeSign, cfgof(n, dg, df)));
+        }
+    });
+}
+int fhe_hybrid_parameters(int N, int *mult_depth, int32_t *rots, int max_rots) {
+    int count = -1;
+    int rc = guard([&] {
+        std::vector<int> r;
+        hybridSortSizeParameters(N, *mult_depth, r);
+        count = (int)r.size();
+        for (int i = 0; i < count && i < max_rots; ++i) rots[i] = r[i];
+    });
+    return rc == FHE_OK ? count : -rc;
+}
 int fhe_mehp24_parameters(int N, int *depth, int *log_ring, int *scale_bits, int *dnum, int cfg[3], int *dg_i,
                           int *df_i, int *sub_length, int32_t *rots, int max_rots) {
     int count = -1;

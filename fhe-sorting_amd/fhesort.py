@@ -93,6 +93,9 @@ _SIGS = {
     'fhe_size_parameters': (C.c_int, [C.c_int, ip, ip, C.c_int]),
     'fhe_direct_sort': (C.c_int, [vp, vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_int, vp, vp, PP]),
+    'fhe_sort_hybrid': (C.c_int, [vp, vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.c_int, C.c_int, vp, vp, PP]),
+    'fhe_hybrid_parameters': (C.c_int, [C.c_int, ip, ip, C.c_int]),
     'fhe_mehp24_parameters': (C.c_int, [C.c_int, ip, ip, ip, ip, ip, ip, ip, ip, ip, C.c_int]),
     'fhe_mehp24_rotation_indices': (C.c_int, [C.c_int, C.c_int, ip, C.c_int]),
     'fhe_mehp24_sort': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, PP]),
@@ -409,6 +412,15 @@ class Context:
                          cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1],
                          C.cast(cb, C.c_void_p) if cb else None, None)
 
+    def sort_hybrid(self, x, N, rots, cfg, mode=0, rank=None, max_array=256, mask=0, shard=(0, 1), allreduce=None):
+        """DirectSort::sort_hybrid (mode 0) or rotationIndexCheckHybrid(rank, x) (mode 1)."""
+        r = np.asarray(rots, dtype=np.int32)
+        cb = ALLREDUCE_FN(allreduce) if allreduce else None
+        self._cb = cb
+        return self._new(lib().fhe_sort_hybrid, x.h, rank.h if rank is not None else None, N, _int(r), len(r),
+                         cfg[0], cfg[1], cfg[2], mode, max_array, mask, shard[0], shard[1],
+                         C.cast(cb, C.c_void_p) if cb else None, None)
+
     def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0, shard=(0, 1), allreduce=None):
         """mehp24::sortFG (sub 0; x holds N values in N*N slots) or
         sortLargeArrayFG with parts of `sub` values (x in sub*sub slots).
@@ -544,6 +556,16 @@ def mehp24_parameters(N):
     depth, log_ring, scale, dnum, dg_i, df_i, sub = (x.value for x in v)
     return dict(depth=depth, log_ring=log_ring, scale_bits=scale, dnum=dnum, cfg=tuple(int(c) for c in cfg), dg_i=dg_i,
                 df_i=df_i, sub=sub, rots=[int(x) for x in rots[:m]])
+
+
+def hybrid_parameters(N):
+    """The hybrid sort test's (depth, rotations) for N (tests/DirectSortHTest.cpp:23-104)."""
+    d = C.c_int()
+    rots = np.zeros(256, dtype=np.int32)
+    m = lib().fhe_hybrid_parameters(N, C.byref(d), _int(rots), 256)
+    if m < 0:
+        raise FheError(-m, lib().fhe_last_error().decode())
+    return d.value, [int(x) for x in rots[:m]]
 
 
 def mehp24_rotation_indices(N, sub=256):

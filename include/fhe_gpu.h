@@ -190,6 +190,22 @@ int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack);
  * so independent batch stacks overlap on the GPU.  Results do not depend on it. */
 int fhe_set_sort_lanes(fhe_ctx *ctx, int lanes);
 
+/* ------------------------------------------------------------ hybrid sort */
+/* DirectSort<N>::sort_hybrid (src/sort_algo.h:1050-1064; mode 0) or
+ * rotationIndexCheckHybrid(rank, x) (:893-1047; mode 1): constructRank, then the
+ * MEHP24-style matrix index check.  max_array = maxArraySize (the reference's 256;
+ * smaller values exercise the multi-block path on small rings: max_array^2 must
+ * equal the slot count when N > max_array); mask_mode 0 = the reference's choice
+ * by N (scaled-sinc PS below 256, Comparison::indicator with (3,4,2) below 512,
+ * (3,5,2) above), 1/2/3 force one of them.  Blocks shard over ranks like
+ * fhe_direct_sort (one all-reduce of the partial outputs). */
+int fhe_sort_hybrid(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, const int32_t *rots, int nrot, int n,
+                    int dg, int df, int mode, int max_array, int mask_mode, int shard_rank, int shard_world,
+                    fhe_allreduce_fn allreduce, void *user, fhe_ct **out);
+/* the hybrid test's depth and rotation list (tests/DirectSortHTest.cpp:23-104,
+ * ring 2^17); returns #rotations */
+int fhe_hybrid_parameters(int N, int *mult_depth, int32_t *rots, int max_rots);
+
 /* ------------------------------------------------------------ MEHP24 sort */
 /* the reference's MEHP24 test parameters for N (tests/mehp24/Mehp24SortTest.cpp:26-128)
  * and mehp24::utils::getRotationIndices(N) (src/mehp24/mehp24_utils.cpp:197-225):

@@ -298,6 +298,12 @@ class DirectSort {
     CtPtr constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
     CtPtr rotationIndexCheckN(const Ciphertext &rank, const Ciphertext &x);
     CtPtr sort(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+    // sort_hybrid (src/sort_algo.h:1050-1064): constructRank, then the MEHP24-style
+    // matrix index check rotationIndexCheckHybrid (:893-1047)
+    CtPtr rotationIndexCheckHybrid(const Ciphertext &rank, const Ciphertext &x);
+    CtPtr sort_hybrid(const Ciphertext &x, SignFunc f, const SignConfig &cfg);
+    int hybrid_max_array = 256;  // maxArraySize (:899)
+    int hybrid_mask = 0;         // 0: by N as the reference; 1: scaled-sinc PS; 2: indicator (3,4,2); 3: (3,5,2)
     // sharding over ranks (batch b handled iff b % world == rank)
     int shard_rank = 0, shard_world = 1;
     CtAllReduce allreduce;
@@ -316,8 +322,9 @@ class DirectSort {
     void reduce_partial(CtPtr &acc, int level, int slots);
 };
 
-// Doubled-sinc Chebyshev coefficients (generated offline, data file).
+// Doubled-sinc / scaled-sinc Chebyshev coefficients (generated offline, data files).
 const std::vector<double> &doubled_sinc_coefficients(int N);
+const std::vector<double> &scaled_sinc_coefficients(int N);
 void set_coefficient_dir(const std::string &dir);
 
 // MEHP24 (Mazzone et al.) ranking / sorting, src/mehp24/*

@@ -254,6 +254,19 @@ void *orc_direct_sort(void *c, void *x, void *rank, int N, const int *rots, int 
     }, (void *)nullptr);
 }
 
+// sort_hybrid (mode 0) / rotationIndexCheckHybrid(rank, x) (mode 1),
+// src/sort_algo.h:893-1064; max_array = maxArraySize (256), mask_mode 0 = by N
+void *orc_sort_hybrid(void *c, void *x, void *rank, int N, const int *rots, int nrot, int n, int dg, int df,
+                      int mode, int max_array, int mask_mode) {
+    return guard([&]() -> void * {
+        DirectSort ds(*CTX, N, std::vector<int>(rots, rots + nrot));
+        ds.hybrid_max_array = max_array;
+        ds.hybrid_mask = mask_mode;
+        if (mode == 1) return wrap(ds.rotationIndexCheckHybrid(CT(rank), CT(x)));
+        return wrap(ds.sort_hybrid(CT(x), SignFunc::CompositeSign, cfg3(n, dg, df)));
+    }, (void *)nullptr);
+}
+
 // MEHP24: sub == 0 -> sortFG on one ciphertext; otherwise sortLargeArrayFG
 // with parts of `sub` values (mehp24_sort.h sortFG / sortLargeArrayFG)
 void *orc_mehp24_sort_sharded(void *c, void *x, int N, int sub, int n, int dg, int df, int dg_i, int df_i,

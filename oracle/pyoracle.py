@@ -76,6 +76,8 @@ def lib():
             'orc_direct_sort': (vp, [vp, vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int,
                                      C.c_int, C.c_int, C.c_int, vp, vp]),
             'orc_size_parameters': (C.c_int, [C.c_int, ip, ip, C.c_int]),
+            'orc_sort_hybrid': (vp, [vp, vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_int]),
             'orc_mehp24_sort': (vp, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
             'orc_mehp24_sort_sharded': (vp, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                              C.c_int, C.c_int, vp, vp]),
@@ -315,6 +317,12 @@ class Context:
                                   cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1],
                                   C.cast(cb, C.c_void_p) if cb else None, None)
         return Ct(self, h)
+
+    def sort_hybrid(self, x, N, rots, cfg, mode=0, rank=None, max_array=256, mask=0):
+        """DirectSort::sort_hybrid (mode 0) or rotationIndexCheckHybrid(rank, x) (mode 1)."""
+        r = np.asarray(rots, dtype=np.int32)
+        return Ct(self, lib().orc_sort_hybrid(self.h, x.h, rank.h if rank is not None else None, N, _int(r), len(r),
+                                              cfg[0], cfg[1], cfg[2], mode, max_array, mask))
 
     def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0, shard=(0, 1), allreduce=None):
         if shard == (0, 1) and allreduce is None:
