@@ -1,0 +1,105 @@
+"""The reference's hot-path GoogleTest suites, restated on the GPU engine with
+their own assertions and tolerances:
+
+* DirectSortNTest (tests/DirectSortNTest.cpp): ConstructRank with
+  CompositeSign(3,6,3) -> ranks within 1e-4 (:61-128); RotationIndexCheck on
+  exact ranks -> sorted within 0.01 (:130-203); ...WithNoise, ranks +-0.001
+  (:205-285).  Ring 2^13 as the reference (it uses HEStd_NotSet), with 50-bit
+  scaling primes: at the reference's 40 bits the rank error is noise-limited
+  at 5e-4 for N=64 (the same precision decision as the bench).
+* RotationTest (tests/RotationTest.cpp): RotationComposer (NAF) rotate(+r) then
+  rotate(-r) == identity within 1e-5 for r in [-128, 128] (:111-130);
+  rotate-and-add over N^2 slots for rotations 8192 and 256 (:132-174).
+* SincTest (tests/SincTest.cpp): on the lattice {k / 2N}, the scaled-sinc PS
+  (selectCoefficients<N>) and Comparison::indicator(x, 0.5 / 2N) with
+  CompositeSign(3,4,2) both within 0.1 of [x == 0] (:75-229).
+
+Inputs are seeded (the reference's random_device makes its runs unrepeatable).
+All calls go through the C ABI via fhesort.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import fhesort as F
+
+pytestmark = pytest.mark.gpu
+DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'fhe-sorting_amd', 'data')
+
+
+def ranks_of(x):
+    return np.array([np.sum(x < v) for v in x], dtype=float)
+
+
+@pytest.fixture(scope='module', params=[8, 64])
+def nctx(request):
+    N = request.param
+    depth, rots = F.size_parameters(N)
+    ctx = F.Context(13, max(depth, 30), 50, 60, 3, seed=N)
+    ctx.gen_rotation_keys(rots)
+    return N, rots, ctx
+
+
+def test_construct_rank_cfg363(nctx):
+    N, rots, ctx = nctx
+    x = np.random.default_rng(N).permutation(N) / N
+    r = ctx.direct_sort(ctx.encrypt(x, N), N, rots, (3, 6, 3), mode=1)
+    assert np.max(np.abs(ctx.decrypt(r)[:N] - ranks_of(x))) < 1e-4
+
+
+@pytest.mark.parametrize('noise', [0.0, 0.001])
+def test_rotation_index_check_given_ranks(nctx, noise):
+    N, rots, ctx = nctx
+    rng = np.random.default_rng(N + 1)
+    x = rng.permutation(N) / N
+    rk = ranks_of(x) + rng.uniform(-noise, noise, N)
+    out = ctx.direct_sort(ctx.encrypt(x, N), N, rots, (3, 6, 3), mode=2, rank=ctx.encrypt(rk, N))
+    assert np.max(np.abs(ctx.decrypt(out)[:N] - np.sort(x))) < 0.01
+
+
+ROT_KEYS = [-1, -2, -4, -8, -16, -32, 1, 2, 4, 8, 16, 32, 64, 512]  # tests/RotationTest.cpp:43
+
+
+@pytest.fixture(scope='module')
+def rctx():
+    ctx = F.Context(15, 4, 50, 60, 3, seed=3)
+    ctx.gen_rotation_keys(ROT_KEYS)
+    return ctx
+
+
+def test_rotate_forward_and_backward(rctx):
+    N = 128
+    x = np.random.default_rng(7).permutation(25500)[:N] * 0.01  # getVectorWithMinDiff(N), RotationTest.cpp:16-31
+    ct = rctx.encrypt(x, N)
+    for r in range(-128, 129, 3):
+        back = rctx.compose_rotate(rctx.compose_rotate(ct, N, ROT_KEYS, 0, r), N, ROT_KEYS, 0, -r)
+        assert np.max(np.abs(rctx.decrypt(back)[:N] - x)) < 1e-5, r
+
+
+def test_rotate_larger_than_n_with_mask(rctx):
+    N = 128
+    x = np.random.default_rng(8).permutation(25500)[:N] * 0.01
+    big = np.tile(x, N)
+    ct = rctx.encrypt(big, N * N)
+    for i in (1, 6):
+        rot = N * N // (1 << i)
+        summed = rctx.add(ct, rctx.compose_rotate(ct, N, ROT_KEYS, 0, rot))
+        want = big + np.roll(big, -rot)
+        assert np.max(np.abs(rctx.decrypt(summed)[:N * N] - want)) < 1e-5 * (i + 1), i
+
+
+@pytest.mark.parametrize('N', [8, 32])
+def test_sinc_ps_and_indicator_on_lattice(N):
+    ctx = F.Context(13, 30, 50, 60, 3, seed=N)
+    L = min(2 * N * N, ctx.n // 2)
+    rng = np.random.default_rng(N)
+    x = rng.integers(-2 * N, 2 * N + 1, L) / (2.0 * N)
+    x[rng.integers(L)] = 0.0
+    want = (np.abs(x) < 1e-10).astype(float)
+    ct = ctx.encrypt(x, L)
+    coeffs = np.fromfile(os.path.join(DATA, f'scaled_sinc_{N}.f64'), dtype='<f8')
+    cheb = ctx.decrypt(ctx.cheb(ct, coeffs, -1.0, 1.0))[:L]
+    ind = ctx.decrypt(ctx.indicator(ct, 0.5 / (2 * N), 3, 4, 2))[:L]
+    assert np.max(np.abs(cheb - want)) < 0.1
+    assert np.max(np.abs(ind - want)) < 0.1
