@@ -335,12 +335,14 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
 // fold (HMult tail, may be null): on limb t = ell-1 the accumulators start at
 // P * (d0, d1)[ell-1] of the member, so the fused ModDown+rescale sees
 // x = d P + acc there.
+template <int D>  // D = digits: the 3 D loads of a thread are all issued before the first product
 __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
-                                                 int ell, int W, int nall, int alpha, int digits,
+                                                 int ell, int W, int nall, int alpha,
                                                  const uint32_t *perm, const int *pmap_ext, const Mod *mods,
                                                  int logN, KsStrides st, KsFold fold) {
     // grid: x = member (fastest: the blocks reading one key block for all
-    // members run back to back and share it in L2), y = coefficient block, z = target
+    // members run back to back and share it in L2), y = coefficient block, z = target.
+    // (An XCD-aware swizzle keeping those runs on one L2 measured 12% slower.)
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.y * NT + threadIdx.x;
     if (k >= n) return;
@@ -352,19 +354,24 @@ __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const
     const int pt = pmap_ext[t];
     const Mod m = mods[pt];
     const size_t kk = perm ? perm[k] : k;
+    u64 x[D], kb[D], ka[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
+        x[j] = (t >= lo && t < hi) ? dntt[(size_t)t * n + kk] : ext[((size_t)j * W + t) * n + kk];
+        kb[j] = key[(((size_t)j * 2 + 0) * nall + pt) * n + k];
+        ka[j] = key[(((size_t)j * 2 + 1) * nall + pt) * n + k];
+    }
     u64 a0 = 0, a1 = 0;
     if (fold.d && t == ell - 1) {
         const u64 *fd = fold.d + mb * fold.member;
         a0 = mul_shoup(fd[k], fold.w, fold.ws, m.q);
         a1 = mul_shoup(fd[fold.seg + k], fold.w, fold.ws, m.q);
     }
-    for (int j = 0; j < digits; ++j) {
-        const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
-        const u64 x = (t >= lo && t < hi) ? dntt[(size_t)t * n + kk] : ext[((size_t)j * W + t) * n + kk];
-        const u64 kb = key[(((size_t)j * 2 + 0) * nall + pt) * n + k];
-        const u64 ka = key[(((size_t)j * 2 + 1) * nall + pt) * n + k];
-        a0 = add_mod(a0, mul_barrett(x, kb, m), m.q);
-        a1 = add_mod(a1, mul_barrett(x, ka, m), m.q);
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        a0 = add_mod(a0, mul_barrett(x[j], kb[j], m), m.q);
+        a1 = add_mod(a1, mul_barrett(x[j], ka[j], m), m.q);
     }
     acc[(size_t)t * n + k] = a0;
     acc[((size_t)W + t) * n + k] = a1;
@@ -667,8 +674,11 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
     // ext (+ own digit) and 2 accumulators per member; the key once
     const double B = 8.0 * ((double)members * (digits * W + 2.0 * W) + 2.0 * digits * W) * ((size_t)1 << logN);
     const dim3 grid((unsigned)members, (unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
-    launch_clocked("k_ks_inner", B, k_ks_inner, grid, dim3(NT), st, acc, ext, dntt, key, ell, W, nall, alpha, digits,
-                   perm, pmap_ext, mods, logN, str, fold);
+    dispatch_int<1, 8>(digits, [&](auto c) {
+        constexpr int D = decltype(c)::value;
+        launch_clocked("k_ks_inner", B, k_ks_inner<D>, grid, dim3(NT), st, acc, ext, dntt, key, ell, W, nall, alpha,
+                       perm, pmap_ext, mods, logN, str, fold);
+    });
 }
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
