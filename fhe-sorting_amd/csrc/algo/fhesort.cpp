@@ -658,37 +658,15 @@ void DirectSortN::reducePartial(CtPtr &acc, int slots) {
 }
 
 // The np baby-step rotations x, rot(x,1), ..., rot(x,np-1) of vecRotsOpt
-// (src/sort_algo.h:383-416) feed every comparator batch, so every rank needs all
-// of them.  One rank computes them (hoisted: one ModUp) when unsharded; sharded,
-// rank r computes steps i = r mod world and the rest arrive through one
-// all-reduce of the stacked steps (zeros where another rank owns the step, so
-// the u64 sum is a gather) -- the 32 top-level rotations were the largest
-// replicated cost of a sharded sort.  Same words either way.
+// (src/sort_algo.h:383-416) feed every comparator batch, so every rank computes
+// all of them (hoisted: one ModUp).  Sharding them (rank r computes steps
+// r mod world, one all-reduce of the zero-padded stack gathers them) saved 7 ms
+// of compute per rank at world 8 but moves 1.3 GB through the collective --
+// about as long over xGMI -- so they stay replicated.
 std::vector<CtPtr> DirectSortN::babySteps(const Ciphertext &x, int np) {
-    std::vector<int> idx;
-    for (int i = 0; i < np; ++i)
-        if (shard_world <= 1 || !allreduce || i % shard_world == shard_rank) idx.push_back(i);
-    std::vector<CtPtr> own = rot.rotateMany(x, idx);
-    if ((int)idx.size() == np) return own;
-    std::vector<CtPtr> all(np);
-    for (size_t j = 0; j < idx.size(); ++j) all[idx[j]] = own[j];
-    CtPtr zero;
-    std::vector<const Ciphertext *> ptrs;
-    for (int i = 0; i < np; ++i) {
-        if (!all[i]) {
-            if (!zero) zero = cc.zero_like(x.level, x.slots);
-            all[i] = zero;
-        }
-        ptrs.push_back(all[i].get());
-    }
-    CtPtr g = cc.stack(ptrs);
-    own.clear();
-    all.clear();
-    allreduce(g->data, 2 * (size_t)g->batch * g->limbs * cc.n());
-    cc.reduce_after_allreduce(*g);
-    std::vector<CtPtr> out;
-    for (int i = 0; i < np; ++i) out.push_back(cc.member(*g, i));
-    return out;
+    std::vector<int> idx(np);
+    for (int i = 0; i < np; ++i) idx[i] = i;
+    return rot.rotateMany(x, idx);
 }
 
 CtPtr DirectSortN::vecRotsOpt(Lane L, const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np,
