@@ -149,6 +149,22 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
             x[r] = valid ? a[off] : 0;
         }
     }
+    // fused row-pass epilogues: their operands (the rescale input / the HMult
+    // accumulators and d) are loaded now, so the loads overlap the butterflies
+    // instead of stalling the store loop (the tile's LDS bounds occupancy, the
+    // extra VGPRs do not)
+    constexpr bool EPI_X = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL);
+    constexpr bool EPI_D = !COLS && MODE == NTT_MULTAIL;
+    u64 ex[EPI_X ? E : 1], ed[EPI_D ? E : 1];
+    if (EPI_X) {
+        const size_t lo = (size_t)limb * n + tid_global * LEN;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int idx = t + T * r;
+            ex[r] = valid ? F.x[(size_t)blockIdx.x * F.seg_x + lo + idx] : 0;
+            if (EPI_D) ed[EPI_D ? r : 0] = valid ? F.d[(size_t)blockIdx.x * F.seg_d + lo + idx] : 0;
+        }
+    }
     // ---- round 1: local stages 0..EB-1
 #pragma unroll
     for (int s = 0; s < EB; ++s) {
@@ -202,8 +218,9 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int r = 0; r < T; ++r)
-                tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] = canon4(x[g * T + r], q, q2);
+            for (int r = 0; r < T; ++r)  // fused epilogues take the lazy [0, 4q) value
+                tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] =
+                    MODE == NTT_PLAIN ? canon4(x[g * T + r], q, q2) : x[g * T + r];
         __syncthreads();
         const size_t z = blockIdx.x, lo = (size_t)limb * n + tid_global * LEN;
         const Mod mp = Tb.mods[p];
@@ -214,15 +231,23 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
             const int idx = t + T * r;
             const u64 v = tile[lds_at<PB, NB, COLS>(tr, idx)];
             if (!valid) continue;
+            // lazy epilogues: v in [0, 4q), every intermediate < 2^64, one final
+            // conditional subtraction (Shoup products of the fold are in [0, 2q))
             if (MODE == NTT_RESCALE) {
-                const u64 xin = F.x[z * F.seg_x + lo + idx];
-                F.out[z * F.seg_out + lo + idx] =
-                    F.scalar ? sub_mod(mul_barrett(xin, kq, mp), mul_shoup(v, F.c1[limb], F.c1s[limb], q), q)
-                             : mul_shoup(sub_mod(xin, v, q), F.c1[limb], F.c1s[limb], q);
-            } else if (MODE == NTT_MULTAIL) {
-                const u64 acc = F.x[z * F.seg_x + lo + idx], dd = F.d[z * F.seg_d + lo + idx];
-                const u64 tt = add_mod(acc, mul_shoup(dd, F.c2[limb], F.c2s[limb], q), q);
-                F.out[z * F.seg_out + lo + idx] = mul_shoup(sub_mod(tt, v, q), F.c1[limb], F.c1s[limb], q);
+                const u64 xin = ex[EPI_X ? r : 0];
+                u64 o;
+                if (F.scalar) {  // (K x - v) q_last^-1 = x kq - v c1: [0, q) + 2q - [0, 2q)
+                    o = mul_barrett(xin, kq, mp) + q2 - shoup_fold(v, F.c1[limb], F.c1s[limb], nq);
+                    o = o >= q2 ? o - q2 : o;
+                } else {  // (x - v) q_last^-1
+                    o = shoup_fold(xin + 2 * q2 - v, F.c1[limb], F.c1s[limb], nq);
+                }
+                F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
+            } else if (MODE == NTT_MULTAIL) {  // (acc + d c2 - v) c1, acc + d c2 + 4q - v < 7q
+                const u64 acc = ex[EPI_X ? r : 0], dd = ed[EPI_D ? r : 0];
+                const u64 tt = acc + shoup_fold(dd, F.c2[limb], F.c2s[limb], nq) + 2 * q2 - v;
+                const u64 o = shoup_fold(tt, F.c1[limb], F.c1s[limb], nq);
+                F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
             } else {
                 a[tid_global * LEN + idx] = v;
             }
