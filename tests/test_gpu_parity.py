@@ -354,3 +354,25 @@ def test_ring_2_17_ops_match_oracle():
             raise AssertionError(f'{name}: {e}')
     r = gpu.rotate(g, -32768)
     assert np.max(np.abs(gpu.decrypt(r) - np.roll(x, 32768))) < 1e-5
+
+
+def test_config2_direct_sort_full_size_bit_exact():
+    """BASELINE config 2 at its full size: DirectSort N=128 at ring 2^16, depth 30,
+    the reference's 40-bit scaling primes, 30 rotation keys, CompositeSign(3,3,2)
+    (src/sort_algo.h:117-123, tests/DirectSortTest.cpp:107-108): the GPU sort
+    equals the CPU oracle's word for word on identical keys (the oracle's keys are
+    generated on the host here: 31 limbs x 2^16, ~40 s of CPU work), and meets the
+    reference's own bound (sorted within 0.01 at output level == multDepth)."""
+    N = 128
+    depth, rots = O.size_parameters(N)
+    assert depth == 30 and len(rots) == 30
+    orc = O.Context(16, depth, 40, 60, 3, seed=2)
+    orc.gen_rotation_keys(rots)
+    gpu = F.Context(16, depth, 40, 60, 3, seed=2, keygen=False)
+    gpu.load_keys_from(orc, rots)
+    x = np.random.default_rng(20250704).permutation(N) / N
+    ox = orc.encrypt(x, N)
+    gout = gpu.direct_sort(gpu.from_oracle(ox), N, rots, (3, 3, 2))
+    same(gout, orc.direct_sort(ox, N, rots, (3, 3, 2)))
+    assert gout.level == depth
+    assert np.max(np.abs(gpu.decrypt(gout) - np.sort(x))) < 0.01
