@@ -178,6 +178,22 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
             ct_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2, nq);
         }
     }
+    // round-2 twiddles (G == 1: stage s needs 2^(s-EB) of them per lane, index
+    // t 2^(s-EB) + (r0 >> (PB-s))), loaded before the exchange so their latency
+    // overlaps the LDS round trip and barrier instead of stalling round 2
+    // (row passes only: in the column pass the extra VGPRs cost a wave of occupancy)
+    constexpr bool PRE = G == 1 && !COLS;
+    constexpr int NT2 = (1 << RB) - 1;
+    ulonglong2 tw2[PRE ? NT2 : 1];
+    if (PRE) {
+#pragma unroll
+        for (int s = EB, o = 0; s < PB; ++s)
+#pragma unroll
+            for (int u = 0; u < (1 << (s - EB)); ++u, ++o) {
+                const size_t i = (COLS ? 0 : (tid_global << s)) + ((size_t)t << (s - EB)) + (size_t)u;
+                tw2[PRE ? o : 0] = tw[((size_t)1 << (S0 + s)) + i];
+            }
+    }
     // ---- exchange through LDS: L1 -> L2 (idx = (t*G + g) * 2^RB + r)
 #pragma unroll
     for (int r = 0; r < E; ++r) tile[lds_at<PB, NB, COLS>(tr, t + T * r)] = x[r];
@@ -198,7 +214,9 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
                 const int idx0 = (t * G + g) * T + r0;
                 const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
                 const size_t wi = ((size_t)1 << (S0 + s)) + i;
-                ct_bfly(x[g * T + r0], x[g * T + r0 + (1 << hb)], tw[wi], q2, nq);
+                const ulonglong2 w =
+                    PRE ? tw2[PRE ? ((1 << (s - EB)) - 1) + (r0 >> (PB - s)) : 0] : tw[wi];
+                ct_bfly(x[g * T + r0], x[g * T + r0 + (1 << hb)], w, q2, nq);
             }
     }
     // ---- store.  COLS: layout L2 is already lane-contiguous in memory
@@ -224,8 +242,13 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         __syncthreads();
         const size_t z = blockIdx.x, lo = (size_t)limb * n + tid_global * LEN;
         const Mod mp = Tb.mods[p];
+        // per-limb epilogue constants, read once (the output stores may alias them
+        // as far as the compiler knows, so in the loop they were re-read per element)
+        const bool EPI = MODE == NTT_RESCALE || MODE == NTT_MULTAIL;
+        const u64 c1 = EPI ? F.c1[limb] : 0, c1s = EPI ? F.c1s[limb] : 0;
+        const u64 c2 = MODE == NTT_MULTAIL ? F.c2[limb] : 0, c2s = MODE == NTT_MULTAIL ? F.c2s[limb] : 0;
         // scaled rescale: out = (K x - v) q_last^-1 = x (K q_last^-1) - v q_last^-1
-        const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, mp), F.c1[limb], F.c1s[limb], q) : 0;
+        const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, mp), c1, c1s, q) : 0;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int idx = t + T * r;
@@ -237,16 +260,16 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
                 const u64 xin = ex[EPI_X ? r : 0];
                 u64 o;
                 if (F.scalar) {  // (K x - v) q_last^-1 = x kq - v c1: [0, q) + 2q - [0, 2q)
-                    o = mul_barrett(xin, kq, mp) + q2 - shoup_fold(v, F.c1[limb], F.c1s[limb], nq);
+                    o = mul_barrett(xin, kq, mp) + q2 - shoup_fold(v, c1, c1s, nq);
                     o = o >= q2 ? o - q2 : o;
                 } else {  // (x - v) q_last^-1
-                    o = shoup_fold(xin + 2 * q2 - v, F.c1[limb], F.c1s[limb], nq);
+                    o = shoup_fold(xin + 2 * q2 - v, c1, c1s, nq);
                 }
                 F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
             } else if (MODE == NTT_MULTAIL) {  // (acc + d c2 - v) c1, acc + d c2 + 4q - v < 7q
                 const u64 acc = ex[EPI_X ? r : 0], dd = ed[EPI_D ? r : 0];
-                const u64 tt = acc + shoup_fold(dd, F.c2[limb], F.c2s[limb], nq) + 2 * q2 - v;
-                const u64 o = shoup_fold(tt, F.c1[limb], F.c1s[limb], nq);
+                const u64 tt = acc + shoup_fold(dd, c2, c2s, nq) + 2 * q2 - v;
+                const u64 o = shoup_fold(tt, c1, c1s, nq);
                 F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
             } else {
                 a[tid_global * LEN + idx] = v;
