@@ -290,9 +290,9 @@ __global__ __launch_bounds__(NT) void k_reduce(u64 *x, Seg S, const Mod *mods, i
 
 // ------------------------------------------------------------ keyswitch ----
 struct ModUpArgs {
-    const u64 *qhinv[8], *qhinv_s[8], *qhat[8];  // per digit; qhat [W][AT] (zero-padded rows)
+    const u64 *qhinv[8], *qhinv_s[8], *qhat[8];  // per digit; qhat [W][qstride] (zero-padded rows)
     int lo[8], hi[8];
-    int digits;
+    int digits, qstride;
     size_t coef_stride, ext_stride;
 };
 
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
         const Mod mt = mods[pmap_ext[t]];
         Acc4 acc;  // lazy: one reduction per output
 #pragma unroll
-        for (int i = 0; i < AT; ++i) mac4(acc, y[i], split30(qh[(size_t)t * AT + i]));
+        for (int i = 0; i < AT; ++i) mac4(acc, y[i], split30(qh[(size_t)t * A.qstride + i]));
         ext[((size_t)j * W + t) * n + k] = reduce4(acc, mt);
     }
 }
@@ -657,14 +657,40 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
         A.hi[j] = std::min((j + 1) * alpha, ell);
     }
     A.digits = digits;
+    A.qstride = alpha;
     A.coef_stride = coef_stride;
     A.ext_stride = ext_stride;
-    const double B = 8.0 * members * (double)((size_t)digits * W) * ((size_t)1 << logN);  // ell in + (dW - ell) out
-    dispatch_int<1, 16>(alpha, [&](auto c) {
-        constexpr int AT = decltype(c)::value;
-        launch_clocked("k_modup_convert", B, k_modup_convert<AT>, pt_grid(logN, (W + TCH - 1) / TCH, digits * members),
-                       dim3(NT), st, ext, coef, W, ell, A, pmap_ext, mods, logN);
-    });
+    // a partial last digit (ell % alpha sources) runs in its own launch with a
+    // straight-line source loop of its true length, instead of alpha terms of
+    // which most multiply a zero constant (at the PS levels, ell ~ 17-25 with
+    // alpha 14, that was up to 4x the MACs of that digit)
+    const int last = ell - (digits - 1) * alpha;
+    const int full = last == alpha ? digits : digits - 1;
+    const size_t n = (size_t)1 << logN;
+    auto launch = [&](int nd, int at, const ModUpArgs &Ar, u64 *ext0) {
+        const double B = 8.0 * members * (double)((size_t)nd * W) * (double)n;  // sources in + targets out
+        dispatch_int<1, 16>(at, [&](auto c) {
+            constexpr int AT = decltype(c)::value;
+            launch_clocked("k_modup_convert", B, k_modup_convert<AT>, pt_grid(logN, (W + TCH - 1) / TCH, nd * members),
+                           dim3(NT), st, ext0, coef, W, ell, Ar, pmap_ext, mods, logN);
+        });
+    };
+    if (full > 0) {
+        ModUpArgs Af = A;
+        Af.digits = full;
+        launch(full, alpha, Af, ext);
+    }
+    if (full < digits) {
+        const int j = digits - 1;
+        ModUpArgs Al = A;
+        Al.digits = 1;
+        Al.qhinv[0] = A.qhinv[j];
+        Al.qhinv_s[0] = A.qhinv_s[j];
+        Al.qhat[0] = A.qhat[j];
+        Al.lo[0] = A.lo[j];
+        Al.hi[0] = A.hi[j];
+        launch(1, last, Al, ext + (size_t)j * W * n);
+    }
 }
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
