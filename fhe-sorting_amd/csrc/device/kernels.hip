@@ -377,6 +377,62 @@ __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const
     acc[((size_t)W + t) * n + k] = a1;
 }
 
+// Member-blocked variant: a thread owns one (coefficient, target) and MC
+// members; the 2D key words it needs are loaded once into registers and reused
+// for every member (no reliance on L2 for key reuse), and the D x-words of all
+// its members are loaded before the products.  grid: x = coefficient block,
+// y = target, z = member group.
+template <int D, int MC>
+__global__ __launch_bounds__(NT) void k_ks_inner_mc(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
+                                                    int ell, int W, int nall, int alpha, int members,
+                                                    const uint32_t *perm, const int *pmap_ext, const Mod *mods,
+                                                    int logN, KsStrides st, KsFold fold) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const int t = blockIdx.y;
+    const int m0 = blockIdx.z * MC;
+    const int pt = pmap_ext[t];
+    const Mod m = mods[pt];
+    const size_t kk = perm ? perm[k] : k;
+    u64 kb[D], ka[D], x[MC][D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        kb[j] = key[(((size_t)j * 2 + 0) * nall + pt) * n + k];
+        ka[j] = key[(((size_t)j * 2 + 1) * nall + pt) * n + k];
+    }
+#pragma unroll
+    for (int u = 0; u < MC; ++u) {
+        const size_t mb = (size_t)(m0 + u);
+        if (m0 + u >= members) break;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
+            x[u][j] = (t >= lo && t < hi) ? dntt[mb * st.d + (size_t)t * n + kk]
+                                          : ext[mb * st.ext + ((size_t)j * W + t) * n + kk];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < MC; ++u) {
+        const size_t mb = (size_t)(m0 + u);
+        if (m0 + u >= members) break;
+        u64 a0 = 0, a1 = 0;
+        if (fold.d && t == ell - 1) {
+            const u64 *fd = fold.d + mb * fold.member;
+            a0 = mul_shoup(fd[k], fold.w, fold.ws, m.q);
+            a1 = mul_shoup(fd[fold.seg + k], fold.w, fold.ws, m.q);
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            a0 = add_mod(a0, mul_barrett(x[u][j], kb[j], m), m.q);
+            a1 = add_mod(a1, mul_barrett(x[u][j], ka[j], m), m.q);
+        }
+        u64 *ac = acc + mb * st.acc;
+        ac[(size_t)t * n + k] = a0;
+        ac[((size_t)W + t) * n + k] = a1;
+    }
+}
+
 // grid: x = n / NT, y = ceil(ell / TCH), z = segment.  KT = K special primes;
 // phat [nq][KT] (the constants of one target contiguous: one scalar burst)
 // Exact centred conversion: y_k = [x P_k^-1]_{p_k}, x mod P = sum_k y_k P_k -
@@ -699,6 +755,16 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
     const int W = ell + K;
     // ext (+ own digit) and 2 accumulators per member; the key once
     const double B = 8.0 * ((double)members * (digits * W + 2.0 * W) + 2.0 * digits * W) * ((size_t)1 << logN);
+    if (members >= 4) {  // member groups of 4 (8 measured the same): the key words stay in registers
+        constexpr int MC = 4;
+        const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W, (unsigned)((members + MC - 1) / MC));
+        dispatch_int<1, 8>(digits, [&](auto c) {
+            constexpr int D = decltype(c)::value;
+            launch_clocked("k_ks_inner", B, k_ks_inner_mc<D, MC>, grid, dim3(NT), st, acc, ext, dntt, key, ell, W,
+                           nall, alpha, members, perm, pmap_ext, mods, logN, str, fold);
+        });
+        return;
+    }
     const dim3 grid((unsigned)members, (unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
     dispatch_int<1, 8>(digits, [&](auto c) {
         constexpr int D = decltype(c)::value;
