@@ -512,7 +512,8 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict_
                                                                 size_t seg_acc, size_t seg_corr, const u64 *phinv,
                                                                 const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                                                                 const u64 *pinv_s, const u64 *pmod, const double *pinvd,
-                                                                const Mod *mods, int logN) {
+                                                                const u64 *ninv, const u64 *ninv_s, const Mod *mods,
+                                                                int logN) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
@@ -535,7 +536,10 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict_
     for (int kk = 0; kk < KT; ++kk) mac4(cacc, v[kk], split30(phat[(size_t)last * KT + kk]));
     mac4(cacc, cnt, split30(ql - pmod[last]));
     const u64 cl = reduce4(cacc, ml);
-    const u64 y = mul_shoup(sub_mod(src[k], cl, ql), pinv[last], pinv_s[last], ql);
+    // the limbs arrive from an unscaled inverse NTT (n x, in [0, 2q)): phinv
+    // carries n^-1 for the special limbs, x_last takes it here
+    const u64 xl = mul_shoup(src[k], ninv[last], ninv_s[last], ql);
+    const u64 y = mul_shoup(sub_mod(xl, cl, ql), pinv[last], pinv_s[last], ql);
     const bool neg = y > (ql >> 1);
     const int i0 = blockIdx.y * TCH;
     for (int i = i0; i < i0 + TCH && i < last; ++i) {
@@ -774,15 +778,15 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
 }
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
-                             const u64 *pinv_s, const u64 *pmod, const double *pinvd, const Mod *mods, int logN,
-                             hipStream_t st) {
+                             const u64 *pinv_s, const u64 *pmod, const double *pinvd, const u64 *ninv,
+                             const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st) {
     if (ell <= 1) return;
     const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
     dispatch_int<1, 15>(K, [&](auto c) {
         constexpr int KT = decltype(c)::value;
         launch_clocked("k_moddown_rescale_convert", B, k_moddown_rescale_convert<KT>,
                        pt_grid(logN, (ell - 1 + TCH - 1) / TCH, segs), dim3(NT), st, corr, acc, ell, nq, seg_acc,
-                       seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, pinvd, mods, logN);
+                       seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, pinvd, ninv, ninv_s, mods, logN);
     });
 }
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,

@@ -55,8 +55,11 @@ inline void launch_clocked(const char *name, double bytes, Kern kernel, dim3 gri
 // forward / inverse negacyclic NTT of `limbs` limbs x `segs` segments
 void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
                  hipStream_t st);
+// raw = true: the inverse omits its final n^-1 scaling and leaves values in
+// [0, 2q) -- for the ModUp / ModDown conversions, whose first constant
+// (q-hat^-1, P-hat^-1) carries n^-1 instead (host::LevelTables)
 void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T,
-                 hipStream_t st);
+                 hipStream_t st, bool raw = false);
 // Operands of the fused forward NTTs (ntt.hip): the column pass can load the
 // centred lift of a coefficient-form limb; the row pass can finish a rescale
 // or an HMult tail in its store instead of writing the transform back.
@@ -75,10 +78,11 @@ struct NttFuse {
     const u64 *src = nullptr;  // inverse: out-of-place input of the first pass
     size_t seg_src = 0;
     int64_t scalar = 0;  // rescale: multiply the input by this integer first (0 = none)
+    bool raw = false;    // inverse: skip the n^-1 scaling of the last pass
 };
 // inverse NTT reading the input from `src` (segment z, limb l at src + z*seg_src + l*n), writing dst
 void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int segs, size_t seg, const int *pmap,
-                      const NttTables &T, hipStream_t st);
+                      const NttTables &T, hipStream_t st, bool raw = false);
 // rescale of `segs` polys: out = (x - NTT(lift(last))) * c1 over `limbs` = ell-1 limbs (tmp: scratch)
 void ntt_forward_rescale(u64 *tmp, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
 // HMult tail: out = (x + d * c2 - NTT(corr)) * c1 (corr is overwritten by the first pass only)
@@ -138,7 +142,8 @@ void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap,
 
 // ---------------------------------------------------------------- keyswitch
 // ext[m][j][t][k] for every member m, digit j and target t not in digit j
-// (coefficient in, NTT NOT applied); coef member stride coef_stride, ext member stride ext_stride
+// (coefficient in, unscaled: the q-hat^-1 constants carry n^-1; NTT NOT applied);
+// coef member stride coef_stride, ext member stride ext_stride
 void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
                    size_t coef_stride, size_t ext_stride, const int *pmap_ext,
                    const u64 *tabs /* packed, see engine */, const size_t *tab_off, const Mod *mods, int logN,
@@ -157,13 +162,15 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
               hipStream_t st, int members, KsStrides str, KsFold fold = KsFold());
 // fused ModDown + rescale of an HMult (see kernels.hip): corr [segs][ell-1][n]
-// from acc [segs][W][n] whose limbs ell-1 .. W-1 are in coefficient form
+// from acc [segs][W][n] whose limbs ell-1 .. W-1 are in coefficient form,
+// unscaled (ntt_inverse raw: n x); ninv [nall]: n^-1 mod each prime
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
-                             const u64 *pinv_s, const u64 *pmod, const double *pinvd, const Mod *mods, int logN,
-                             hipStream_t st);
+                             const u64 *pinv_s, const u64 *pmod, const double *pinvd, const u64 *ninv,
+                             const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st);
 // conv[s][i][k] = (sum_k' y_k' phat[i][k'] - v P) mod q_i for i < ell, y_k' =
-// pc[s][k'] * phinv_k', v = round(sum_k' y_k' pinvd_k'): the centred Conv_{P->q_i}
+// pc[s][k'] * phinv_k' (pc: unscaled inverse NTT, phinv carries n^-1),
+// v = round(sum_k' y_k' pinvd_k'): the centred Conv_{P->q_i}
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
                      const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pmod, const double *pinvd,
                      const Mod *mods, int logN, hipStream_t st);

@@ -382,13 +382,14 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
             gs_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2, nq);
         }
     }
-    // ---- store, layout L1 (COLS: times n^-1)
+    // ---- store, layout L1 (COLS: times n^-1 unless F.raw)
     const u64 ni = Tb.ninv[p], nis = Tb.ninv_s[p];
+    const bool scale = COLS && !F.raw;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const int idx = t + T * r;
         const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
-        if (valid) a[off] = COLS ? mul_shoup(x[r], ni, nis, q) : x[r];
+        if (valid) a[off] = scale ? mul_shoup(x[r], ni, nis, q) : x[r];
     }
 }
 
@@ -460,23 +461,26 @@ void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     dispatch<false, true, NTT_PLAIN>(k2, data, limbs, segs, seg, pmap, nullptr, T, F, st);
 }
 
-void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {
+void ntt_inverse(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st,
+                 bool raw) {
     if (limbs <= 0 || segs <= 0) return;
     const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
-    const NttFuse F;
+    NttFuse F;
+    F.raw = raw;
     dispatch<false, false, NTT_PLAIN>(k2, data, limbs, segs, seg, pmap, nullptr, T, F, st);
     dispatch<true, false, NTT_PLAIN>(k1, data, limbs, segs, seg, pmap, nullptr, T, F, st);
 }
 
 void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int segs, size_t seg, const int *pmap,
-                      const NttTables &T, hipStream_t st) {
+                      const NttTables &T, hipStream_t st, bool raw) {
     if (limbs <= 0 || segs <= 0) return;
     const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
     NttFuse F;
     F.src = src;
     F.seg_src = seg_src;
     dispatch<false, false, NTT_PLAIN>(k2, dst, limbs, segs, seg, pmap, nullptr, T, F, st);
-    const NttFuse G;
+    NttFuse G;
+    G.raw = raw;
     dispatch<true, false, NTT_PLAIN>(k1, dst, limbs, segs, seg, pmap, nullptr, T, G, st);
 }
 

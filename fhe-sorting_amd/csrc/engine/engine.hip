@@ -200,7 +200,7 @@ struct Engine::Impl {
         const int digits = P.digits_at(ell);
         auto coef = alloc((size_t)members * ell * nn * 8);
         u64 *c = static_cast<u64 *>(coef->p);
-        dev::ntt_inverse_from(c, d, d_stride, (int)ell, members, ell * nn, nullptr, T, st);
+        dev::ntt_inverse_from(c, d, d_stride, (int)ell, members, ell * nn, nullptr, T, st, /*raw*/ true);
         const size_t es = (size_t)digits * W * nn;
         auto extm = alloc((size_t)members * es * 8);
         u64 *e = static_cast<u64 *>(extm->p);
@@ -227,7 +227,7 @@ struct Engine::Impl {
         dev::ks_inner(acc, e, d, key, (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha, digits, pm, ext(ell), mods,
                       P.logN, st, members, str);
         // ModDown of both accumulators of every member
-        dev::ntt_inverse(acc + ell * nn, (int)K, segs, W * nn, ext(ell) + ell, T, st);
+        dev::ntt_inverse(acc + ell * nn, (int)K, segs, W * nn, ext(ell) + ell, T, st, /*raw*/ true);
         auto convm = alloc((size_t)segs * ell * nn * 8);
         u64 *conv = static_cast<u64 *>(convm->p);
         dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, segs, phinv, phinv_s,
@@ -261,11 +261,11 @@ struct Engine::Impl {
         fold.ws = LT.pmod_s[ell - 1];
         dev::ks_inner(acc, e, d2, static_cast<u64 *>(relin->p), (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha,
                       digits, nullptr, ext(ell), mods, P.logN, st, members, str, fold);
-        dev::ntt_inverse(acc + (ell - 1) * nn, (int)K + 1, segs, W * nn, ext(ell) + (ell - 1), T, st);
+        dev::ntt_inverse(acc + (ell - 1) * nn, (int)K + 1, segs, W * nn, ext(ell) + (ell - 1), T, st, /*raw*/ true);
         auto corrm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *corr = static_cast<u64 *>(corrm->p);
         dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, segs, phinv,
-                                     phinv_s, phat, pinv, pinv_s, pmod, pinvd, mods, P.logN, st);
+                                     phinv_s, phat, pinv, pinv_s, pmod, pinvd, T.ninv, T.ninv_s, mods, P.logN, st);
         // forward NTT of corr whose row pass finishes (acc + d P - corr) (P q_last)^-1 into `out`
         dev::NttFuse F;
         F.out = out;
@@ -1200,7 +1200,7 @@ void Engine::moddown_host(const u64 *in, size_t ell, u64 *out) {
     auto im = I.alloc(W * nn * 8);
     u64 *x = static_cast<u64 *>(im->p);
     HIP_OK(hipMemcpyAsync(x, in, W * nn * 8, hipMemcpyHostToDevice, ST));
-    dev::ntt_inverse(x + ell * nn, (int)K, 1, 0, I.ext(ell) + ell, I.T, ST);
+    dev::ntt_inverse(x + ell * nn, (int)K, 1, 0, I.ext(ell) + ell, I.T, ST, /*raw*/ true);
     auto cm = I.alloc(ell * nn * 8);
     u64 *conv = static_cast<u64 *>(cm->p);
     dev::moddown_convert(conv, x + ell * nn, (int)ell, (int)K, (int)I.P.nq(), W * nn, ell * nn, 1, I.phinv,

@@ -388,7 +388,9 @@ LevelTables make_level_tables(const Params &P) {
                 u64 prod = 1;
                 for (size_t s = lo; s < hi; ++s)
                     if (s != i) prod = mulmod(prod, P.primes[s] % P.primes[i], mods[i]);
-                qhinv[i - lo] = invmod(prod, mods[i]);
+                // times n^-1: the inverse NTT feeding the conversion is unscaled
+                qhinv[i - lo] = mulmod(invmod(prod, mods[i]), invmod(((u64)1 << P.logN) % P.primes[i], mods[i]),
+                                       mods[i]);
                 qhinv_s[i - lo] = shoup(qhinv[i - lo], P.primes[i]);
             }
             for (size_t t = 0; t < W; ++t) {
@@ -422,7 +424,7 @@ LevelTables make_level_tables(const Params &P) {
         u64 prod = 1;
         for (size_t s = 0; s < K; ++s)
             if (s != k) prod = mulmod(prod, P.primes[nq + s] % mk.q, mk);
-        T.phinv[k] = invmod(prod, mk);
+        T.phinv[k] = mulmod(invmod(prod, mk), invmod(((u64)1 << P.logN) % mk.q, mk), mk);  // times n^-1 (as qhinv)
         T.phinv_s[k] = shoup(T.phinv[k], mk.q);
     }
     for (size_t i = 0; i < nq; ++i) {

@@ -82,7 +82,8 @@ inline u64 enc_e1(u64 c) { return 0x80000000ULL + 3 * c + 2; }
 
 // Precomputed key-switching / rescale constants for every level.
 struct LevelTables {
-    // ModUp, per ell (1..nq) and digit: [qhinv(alpha), qhinv_s(alpha), qhat(W*alpha) as [t][i]]
+    // ModUp, per ell (1..nq) and digit: [qhinv(alpha), qhinv_s(alpha), qhat(W*alpha) as [t][i]];
+    // qhinv and phinv include n^-1 (their inputs come from unscaled inverse NTTs)
     std::vector<u64> modup;             // packed
     std::vector<std::vector<size_t>> modup_off;  // [ell][digit] offset into modup
     // ModDown (level independent)
