@@ -1,0 +1,435 @@
+// k-way sorting network (reference: src/k-way/*.cpp, src/kway_adapter.h);
+// see kway.hpp for the map.  Every ciphertext operation runs on the GPU
+// through fhe::Engine; masks are encoded at the level of the ciphertext they
+// meet (FLEXIBLEAUTO re-encodes a plaintext at its operand's level).
+#include "kway.hpp"
+
+#include <cmath>
+#include <stdexcept>
+
+namespace fhe {
+namespace kwaySort {
+
+namespace {
+long ipow(long b, long e) {
+    long r = 1;
+    while (e-- > 0) r *= b;
+    return r;
+}
+long nextPow2(long n) {
+    long p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+}  // namespace
+
+// Masking.cpp:25-48: stage -> (m, logDist, slope).  Rounds r = 0, 1, ... have
+// 1 + r * ceil(k/2) stages; f(r) = r + r(r-1)/2 * ceil(k/2) stages precede round r.
+std::tuple<int, int, int> sortType(int k, int M, int stage) {
+    (void)M;
+    const int up = (k + 1) / 2;
+    int r = 0;
+    while (stage >= r + 1 + r * (r + 1) / 2 * up) ++r;
+    const int n = stage - (r + r * (r - 1) / 2 * up);
+    const int m = (n + up - 1) / up;
+    const int slope = n == 0 ? 0 : (n - 1) % up + 1;
+    return std::make_tuple(m, r - m, slope);
+}
+
+int stageCount(int k, int M) { return M + M * (M - 1) / 2 * ((k + 1) / 2); }
+
+// Masking.cpp:50-146.  res[0][slot] = size of the sorting group the slot takes
+// part in (0: none), res[1][slot] = its position (1-based) in that group.
+std::vector<std::vector<int>> genIndices(long numSlots, long k, long M, long m, long logDist, long slope) {
+    std::vector<std::vector<int>> res(2, std::vector<int>((size_t)numSlots, 0));
+    const long km = ipow(k, m), dist = ipow(k, logDist), next = ipow(k, m + 1), total = ipow(k, M);
+    auto put = [&](long here, int a, int b) {
+        res[0][(size_t)here] = a;
+        res[1][(size_t)here] = b;
+    };
+    // one anti-diagonal walk starting at (row, col): positions loc = 1, 2, ...;
+    // when the walk ends, the whole chain is re-labelled from its far end
+    auto diagonal = [&](long start, long row0, long col0) {
+        long row = row0, col = col0;
+        int loc = 1;
+        while (row < km && col >= 0) {
+            for (long d = 0; d < dist; ++d) {
+                const long here = start + dist * (col + k * row) + d;
+                res[0][(size_t)here] = loc;
+                if (row == km - 1 || col - slope < 0) {
+                    for (int i = 0; i < loc; ++i) {
+                        const long h2 = start + dist * ((col + i * slope) + k * (row - i)) + d;
+                        res[1][(size_t)h2] = loc - i;
+                        res[0][(size_t)h2] += i;
+                    }
+                }
+            }
+            ++loc;
+            ++row;
+            col -= slope;
+        }
+    };
+    for (long start = 0; start < total; start += dist * next) {
+        if (slope == 0) {
+            for (long s = 0; s < km; ++s)
+                for (long col = 0; col < k; ++col)  // row stays s: loc = col + 1
+                    for (long d = 0; d < dist; ++d) put(start + dist * (s + km * col) + d, (int)k, (int)col + 1);
+        } else if (slope > k / 2) {
+            for (long t = 0; t + 1 < km; ++t) {
+                const long col = k - k / 2;
+                for (long loc = 1; loc < k; ++loc)
+                    for (long d = 0; d < dist; ++d)
+                        put(start + dist * (col + k * t + loc - 1) + d, (int)(k - 1), (int)loc);
+            }
+        } else {
+            for (long t = slope; t < k; ++t) diagonal(start, 0, t);
+            for (long s = 1; s + 1 < km; ++s)
+                for (long t = k - slope; t < k; ++t) diagonal(start, s, t);
+        }
+    }
+    return res;
+}
+
+void genMask(const std::vector<std::vector<int>> &indices, long index0, long index1, std::vector<double> &mask) {
+    const size_t ns = indices[0].size();
+    mask.assign(ns, 0.0);
+    for (size_t i = 0; i < ns; ++i)
+        if (indices[0][i] == index0 && indices[1][i] == index1) mask[i] = 1.0;
+}
+
+long getRotateDistance(long k, long logDist, long slope) {  // Masking.cpp:155-165
+    const long dist = ipow(k, logDist);
+    return (slope == 0 || slope == k / 2 + 1) ? dist : dist * (k - slope);
+}
+
+std::vector<int> rotationIndices(int N) {  // kway_adapter.h:45-49
+    std::vector<int> r;
+    for (int i = 1; i < N; i *= 2) {
+        r.push_back(i);
+        r.push_back(-i);
+    }
+    return r;
+}
+
+// ------------------------------------------------------------- Sorter ----
+Sorter::Sorter(Engine &cc_, long numSlots_, long k_, long M_)
+    : cc(cc_), numSlots(numSlots_), k(k_), M(M_), level{0, 1, 3, 5, 6, 7} {
+    if (k != 2 && k != 3 && k != 5) throw std::invalid_argument("k-way: only k = 2, 3, 5 are supported");
+    if (M < 1 || ipow(k, M) != numSlots) throw std::invalid_argument("k-way: k^M must equal the input length");
+}
+
+const Plaintext &Sorter::mask(const std::vector<double> &v, const Ciphertext &like) {
+    auto key = std::make_pair(v, like.level);
+    auto it = masks.find(key);
+    if (it != masks.end()) return *it->second;
+    return *(masks[key] = cc.encode(v, like.slots, like.level));
+}
+
+// EvalUtils::checkLevelAndBoot (EvalUtils.cpp:59-86): the reference bootstraps
+// when fewer than need + 1 levels remain; without bootstrapping that is an error
+void Sorter::checkLevel(const Ciphertext &c, int need) const {
+    if (cc.params().L - c.level < need + 1)
+        throw std::runtime_error("k-way: no levels left (the reference bootstraps here; bootstrapping is not built)");
+}
+
+// EvalUtils.cpp:113-146: binary decomposition, ascending powers of two
+CtPtr Sorter::leftRotate(const CtPtr &c, long r) {
+    CtPtr o = c;
+    for (long p = 1; r > 0; p <<= 1, r >>= 1)
+        if (r & 1) o = cc.rotate(*o, p);
+    return o;
+}
+CtPtr Sorter::rightRotate(const CtPtr &c, long r) {
+    CtPtr o = c;
+    for (long p = 1; r > 0; p <<= 1, r >>= 1)
+        if (r & 1) o = cc.rotate(*o, -p);
+    return o;
+}
+// EvalUtils::flipCtxt(ctxt, mask) = mask - ctxt (EvalUtils.cpp:102-105)
+CtPtr Sorter::flip(const CtPtr &c, const std::vector<double> &m) { return cc.plain_sub(mask(m, *c), *c); }
+CtPtr Sorter::maskMul(const CtPtr &c, const std::vector<double> &m) { return cc.mul_plain(*c, mask(m, *c)); }
+
+// SortUtils.cpp:5-16: cmp * (a - b) + b  (= max(a, b) when cmp = [a > b])
+CtPtr Sorter::fcnL(const CtPtr &a, const CtPtr &b, const CtPtr &cmp) {
+    return cc.add(*cc.mul(*cc.sub(*a, *b), *cmp), *b);
+}
+// SortUtils.cpp:32-54: out = [min, max]
+void Sorter::twoSorter(const CtPtr &a, const CtPtr &b, const CtPtr &cmp, CtPtr *out) {
+    out[1] = fcnL(a, b, cmp);
+    out[0] = cc.sub(*cc.add(*a, *b), *out[1]);
+}
+// SortUtils.cpp:56-77; cmp = [a>b, a>c, b>c]
+void Sorter::threeSorter(const CtPtr *x, const CtPtr *cmp, CtPtr *out) {
+    CtPtr ab[2], abc[2];
+    twoSorter(x[0], x[1], cmp[0], ab);
+    twoSorter(cmp[1], cmp[2], cmp[0], abc);     // [min(a,b) > c, max(a,b) > c]
+    out[2] = fcnL(ab[1], x[2], abc[1]);          // compareMax
+    out[0] = fcnL(x[2], ab[0], abc[0]);          // compareMin
+    out[1] = cc.sub(*cc.sub(*cc.add(*cc.add(*x[0], *x[1]), *x[2]), *out[0]), *out[2]);
+}
+// SortUtils.cpp:79-129; cmp = [a>b, a>c, a>d, b>c, b>d, c>d]
+void Sorter::fourSorter(const CtPtr *x, const CtPtr *cmp, CtPtr *out) {
+    CtPtr ab[2], cd[2], vsC[2], vsD[2], Mx[2], mn[2];
+    twoSorter(x[0], x[1], cmp[0], ab);
+    twoSorter(x[2], x[3], cmp[5], cd);
+    twoSorter(cmp[1], cmp[3], cmp[0], vsC);
+    twoSorter(cmp[2], cmp[4], cmp[0], vsD);
+    twoSorter(vsC[1], vsD[1], cmp[5], Mx);
+    twoSorter(vsC[0], vsD[0], cmp[5], mn);
+    out[3] = fcnL(ab[1], cd[1], Mx[1]);
+    const CtPtr left = fcnL(ab[0], cd[1], mn[1]), right = fcnL(ab[1], cd[0], Mx[0]);
+    out[2] = fcnL(left, right, Mx[1]);
+    out[0] = fcnL(cd[0], ab[0], mn[0]);
+    CtPtr s = x[0];
+    for (int i = 1; i < 4; ++i) s = cc.add(*s, *x[i]);
+    for (int i : {0, 2, 3}) s = cc.sub(*s, *out[i]);
+    out[1] = s;
+}
+// SortUtils.cpp:131-208; cmp = [a>b a>c a>d a>e b>c b>d b>e c>d c>e d>e]
+void Sorter::fiveSorter(const CtPtr *x, const CtPtr *cmp, CtPtr *out) {
+    const CtPtr abcIn[3] = {x[0], x[1], x[2]}, abcCmp[3] = {cmp[0], cmp[1], cmp[4]};
+    CtPtr abc[3], de[2];
+    threeSorter(abcIn, abcCmp, abc);
+    twoSorter(x[3], x[4], cmp[9], de);
+    const CtPtr vsDIn[3] = {cmp[2], cmp[5], cmp[7]}, vsEIn[3] = {cmp[3], cmp[6], cmp[8]};
+    CtPtr vsD[3], vsE[3];
+    threeSorter(vsDIn, abcCmp, vsD);
+    threeSorter(vsEIn, abcCmp, vsE);
+    CtPtr hi[2], mid[2], lo[2];
+    twoSorter(vsD[2], vsE[2], cmp[9], hi);
+    twoSorter(vsD[1], vsE[1], cmp[9], mid);
+    twoSorter(vsD[0], vsE[0], cmp[9], lo);
+    out[4] = fcnL(abc[2], de[1], hi[1]);
+    out[0] = fcnL(de[0], abc[0], lo[0]);
+    CtPtr left = fcnL(abc[1], de[1], mid[1]), right = fcnL(abc[2], de[0], hi[0]);
+    out[3] = fcnL(left, right, hi[1]);
+    left = fcnL(de[0], abc[1], mid[0]);
+    right = fcnL(de[1], abc[0], lo[1]);
+    out[1] = fcnL(right, left, lo[0]);
+    CtPtr s = x[0];
+    for (int i = 1; i < 5; ++i) s = cc.add(*s, *x[i]);
+    for (int i : {0, 1, 3, 4}) s = cc.sub(*s, *out[i]);
+    out[2] = s;
+}
+// SortUtils.cpp:424-433
+CtPtr Sorter::slotAssemble(const CtPtr *s, long num, long shift) {
+    CtPtr o = s[0];
+    for (long i = 1; i < num; ++i) o = cc.add(*o, *rightRotate(s[i], i * shift));
+    return o;
+}
+
+namespace {
+std::vector<double> groupMask(const std::vector<std::vector<int>> &ind, long size) {
+    std::vector<double> m;
+    genMask(ind, size, 1, m);
+    return m;
+}
+}  // namespace
+
+// Sorter.cpp:9-36 (+ slotMatching2, SortUtils.cpp:210-217)
+CtPtr Sorter::runTwoSorter(const CtPtr &x, const std::vector<std::vector<int>> &ind, long shift, const CtPtr &c) {
+    const auto m2 = groupMask(ind, 2);
+    CtPtr s[2];
+    twoSorter(x, leftRotate(x, shift), c, s);
+    for (auto &v : s) v = maskMul(v, m2);
+    return cc.add(*s[0], *rightRotate(s[1], shift));
+}
+// Sorter.cpp:38-68 (+ slotMatching3, SortUtils.cpp:219-241)
+CtPtr Sorter::runThreeSorter(const CtPtr &x, const std::vector<std::vector<int>> &ind, long shift, const CtPtr &c) {
+    const auto m3 = groupMask(ind, 3);
+    const CtPtr xs[3] = {x, leftRotate(x, shift), leftRotate(x, 2 * shift)};
+    const CtPtr cs[3] = {flip(leftRotate(c, shift), m3), c, flip(leftRotate(c, 2 * shift), m3)};
+    CtPtr s[3];
+    threeSorter(xs, cs, s);
+    for (auto &v : s) v = maskMul(v, m3);
+    return cc.add(*cc.add(*s[0], *rightRotate(s[1], shift)), *rightRotate(s[2], 2 * shift));
+}
+// Sorter.cpp:70-85 (+ slotMatching4, SortUtils.cpp:243-287; the reference's
+// masked products at :262-267 are overwritten before use and are skipped)
+CtPtr Sorter::runFourSorter(const CtPtr &x, const std::vector<std::vector<int>> &ind, long shift, const CtPtr &c1,
+                            const CtPtr &c2) {
+    std::vector<double> m41;
+    genMask(ind, 4, 1, m41);
+    CtPtr cs[6];
+    cs[2] = c1;
+    cs[0] = flip(leftRotate(c1, shift), m41);
+    cs[3] = flip(leftRotate(c1, 2 * shift), m41);
+    cs[5] = flip(leftRotate(c1, 3 * shift), m41);
+    cs[1] = c2;
+    cs[4] = leftRotate(c2, shift);
+    CtPtr xs[4];
+    for (int i = 0; i < 4; ++i) xs[i] = maskMul(leftRotate(x, i * shift), m41);
+    CtPtr s[4];
+    fourSorter(xs, cs, s);
+    return slotAssemble(s, 4, shift);
+}
+// Sorter.cpp:87-115 (+ slotMatching5, SortUtils.cpp:289-323)
+CtPtr Sorter::runFiveSorter(const CtPtr &x, const std::vector<std::vector<int>> &ind, long shift, const CtPtr &c1,
+                            const CtPtr &c2) {
+    const auto m5 = groupMask(ind, 5);
+    CtPtr xs[5], cs[10];
+    for (int i = 0; i < 5; ++i) xs[i] = leftRotate(x, i * shift);
+    cs[3] = c1;
+    cs[0] = leftRotate(c1, shift);
+    cs[4] = leftRotate(c1, 2 * shift);
+    cs[7] = leftRotate(c1, 3 * shift);
+    cs[9] = leftRotate(c1, 4 * shift);
+    cs[2] = c2;
+    cs[6] = leftRotate(c2, shift);
+    cs[1] = leftRotate(c2, 2 * shift);
+    cs[5] = leftRotate(c2, 3 * shift);
+    cs[8] = leftRotate(c2, 4 * shift);
+    for (int i : {0, 1, 4, 5, 7, 8, 9}) cs[i] = flip(cs[i], m5);
+    CtPtr s[5];
+    fiveSorter(xs, cs, s);
+    for (auto &v : s) v = maskMul(v, m5);
+    return slotAssemble(s, 5, shift);
+}
+// Sorter.cpp:117-185 (+ slotMatching2345, SortUtils.cpp:325-422)
+CtPtr Sorter::run2345Sorter(const CtPtr &x, const std::vector<std::vector<int>> &ind, long shift, const CtPtr &c1,
+                            const CtPtr &c2) {
+    const size_t ns = ind[0].size();
+    std::vector<double> m2345(ns, 0.0), m45(ns, 0.0), m345(ns, 0.0), m3(ns, 0.0), m4(ns, 0.0), m5(ns, 0.0);
+    for (size_t i = 0; i < ns; ++i) {
+        if (ind[1][i] != 1) continue;
+        const int g = ind[0][i];
+        if (g >= 2 && g <= 5) m2345[i] = 1.0;
+        if (g >= 3 && g <= 5) m345[i] = 1.0;
+        if (g == 4 || g == 5) m45[i] = 1.0;
+        if (g == 3) m3[i] = 1.0;
+        if (g == 4) m4[i] = 1.0;
+        if (g == 5) m5[i] = 1.0;
+    }
+    CtPtr xs[5], cs[10];
+    for (int i = 0; i < 5; ++i) xs[i] = leftRotate(x, i * shift);
+    cs[0] = flip(leftRotate(c1, shift), m2345);
+    cs[1] = cc.add(*maskMul(c1, m3), *flip(maskMul(leftRotate(c2, 2 * shift), m45), m45));
+    cs[2] = cc.add(*maskMul(c1, m4), *maskMul(c2, m5));
+    cs[3] = maskMul(c1, m5);
+    cs[4] = flip(maskMul(leftRotate(c1, 2 * shift), m345), m345);
+    cs[5] = flip(maskMul(leftRotate(c2, 3 * shift), m45), m45);
+    cs[6] = maskMul(leftRotate(c2, shift), m5);
+    cs[7] = flip(maskMul(leftRotate(c1, 3 * shift), m45), m45);
+    cs[8] = flip(maskMul(leftRotate(c2, 4 * shift), m5), m5);
+    cs[9] = flip(maskMul(leftRotate(c1, 4 * shift), m5), m5);
+    CtPtr s[5];
+    fiveSorter(xs, cs, s);
+    s[0] = maskMul(s[0], m2345);
+    s[1] = maskMul(s[1], m2345);
+    s[2] = maskMul(s[2], m345);
+    s[3] = maskMul(s[3], m45);
+    s[4] = maskMul(s[4], m5);
+    return slotAssemble(s, 5, shift);
+}
+
+// Sorter.cpp:187-256.  rot = the input moved so that every slot meets its
+// comparison partner; fix (optional) = the slots outside every group.
+void Sorter::rightRotateForSort(const CtPtr &x, const std::vector<std::vector<int>> &ind, long logDist, long slope,
+                                CtPtr &rot, CtPtr *fix) {
+    const size_t ns = (size_t)numSlots;
+    std::vector<double> left(ns, 0.0);
+    std::vector<std::vector<double>> right((size_t)k, std::vector<double>(ns, 0.0));
+    for (size_t i = 0; i < ns; ++i) {
+        if (ind[1][i] < ind[0][i]) left[i] = 1.0;
+        if (ind[0][i] > 0 && ind[0][i] == ind[1][i]) right[(size_t)ind[0][i] - 1][i] = 1.0;
+    }
+    const CtPtr xl = maskMul(x, left);
+    const long r = getRotateDistance(k, logDist, slope);
+    if (slope == 0 || slope == k / 2 + 1) {
+        const long g = slope == 0 ? k - 1 : k - 2;  // the one group size present
+        const CtPtr xr = maskMul(x, right[(size_t)g]);
+        if (slope != 0 && fix) *fix = cc.sub(*cc.sub(*x, *xl), *xr);
+        rot = cc.add(*rightRotate(xl, r), *leftRotate(xr, g * r));
+        return;
+    }
+    std::vector<CtPtr> xr((size_t)k);
+    for (long i = 0; i < k; ++i) xr[(size_t)i] = maskMul(x, right[(size_t)i]);
+    if (fix) {
+        CtPtr f = cc.sub(*x, *xl);
+        for (long i = 0; i < k; ++i) f = cc.sub(*f, *xr[(size_t)i]);
+        *fix = f;
+    }
+    rot = rightRotate(xl, r);
+    for (long i = 1; i < k; ++i) rot = cc.add(*rot, *leftRotate(xr[(size_t)i], i * r));
+}
+
+// Sorter.cpp:258-268: comp = [x > rot(x)]
+CtPtr Sorter::comparisonForSort(const CtPtr &x, const std::vector<std::vector<int>> &ind, long logDist, long slope,
+                                CtPtr &fix, const SignConfig &cfg) {
+    CtPtr rot;
+    rightRotateForSort(x, ind, logDist, slope, rot, &fix);
+    return comp.compare(cc, *x, *rot, SignFunc::CompositeSign, cfg);
+}
+// Sorter.cpp:270-287 (the second rotation's fix part is unused and not formed)
+void Sorter::comparisonForSort2(const CtPtr &x, const std::vector<std::vector<int>> &ind, long logDist, long slope,
+                                CtPtr &c1, CtPtr &c2, CtPtr &fix, const SignConfig &cfg) {
+    CtPtr r1, r2;
+    rightRotateForSort(x, ind, logDist, slope, r1, &fix);
+    rightRotateForSort(r1, ind, logDist, slope, r2, nullptr);
+    c1 = comp.compare(cc, *x, *r1, SignFunc::CompositeSign, cfg);
+    c2 = comp.compare(cc, *x, *r2, SignFunc::CompositeSign, cfg);
+}
+
+// Sorter.cpp:289-404
+CtPtr Sorter::sorter(const Ciphertext &input, const SignConfig &cfg) {
+    CtPtr ct = cc.clone(input), fix, c1, c2;
+    const int stages = stageCount((int)k, (int)M);
+    stagesRun = 0;
+    for (int stage = 0; stage < stages; ++stage) {
+        int m, logDist, slope;
+        std::tie(m, logDist, slope) = sortType((int)k, (int)M, stage);
+        const long shift = getRotateDistance(k, logDist, slope);
+        const auto ind = genIndices(numSlots, k, M, m, logDist, slope);
+        if (slope == 0) {
+            checkLevel(*ct, level[(size_t)k]);
+            if (k == 5) {
+                comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
+                checkLevel(*c1, level[5]);
+                checkLevel(*c2, level[5]);
+                ct = runFiveSorter(ct, ind, shift, c1, c2);
+            } else {
+                c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
+                checkLevel(*c1, level[(size_t)k]);
+                ct = k == 2 ? runTwoSorter(ct, ind, shift, c1) : runThreeSorter(ct, ind, shift, c1);
+            }
+        } else if (slope == k / 2 + 1) {  // k = 3 or 5 (k = 2 has slopes 0, 1 only)
+            checkLevel(*ct, level[(size_t)k - 1]);
+            if (k == 3) {
+                c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
+                checkLevel(*c1, level[2]);
+                ct = runTwoSorter(ct, ind, shift, c1);
+            } else {
+                comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
+                checkLevel(*c1, level[4]);
+                checkLevel(*c2, level[4]);
+                ct = runFourSorter(ct, ind, shift, c1, c2);
+            }
+            ct = cc.add(*ct, *fix);
+        } else if (k == 5 && slope == 1) {
+            checkLevel(*ct, level[5]);
+            comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
+            checkLevel(*c1, level[5]);
+            checkLevel(*c2, level[5]);
+            ct = cc.add(*run2345Sorter(ct, ind, shift, c1, c2), *fix);
+        } else if ((k == 5 && slope == 2) || (k == 3 && slope == 1)) {
+            checkLevel(*ct, level[3]);
+            c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
+            checkLevel(*c1, level[3]);
+            const CtPtr two = runTwoSorter(ct, ind, shift, c1);
+            const CtPtr three = runThreeSorter(ct, ind, shift, c1);
+            ct = cc.add(*cc.add(*two, *fix), *three);
+        } else if (k == 2 && slope == 1) {
+            checkLevel(*ct, level[2]);
+            c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
+            checkLevel(*c1, level[2]);
+            ct = cc.add(*runTwoSorter(ct, ind, shift, c1), *fix);
+        } else {
+            throw std::invalid_argument("k-way: no matching k and slope");
+        }
+        ++stagesRun;
+    }
+    return ct;
+}
+
+}  // namespace kwaySort
+}  // namespace fhe

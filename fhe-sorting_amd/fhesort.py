@@ -102,6 +102,14 @@ _SIGS = {
     'fhe_mehp24_sort_sharded': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                           C.c_int, C.c_int, vp, vp, PP]),
     'fhe_mehp24_indicator': (C.c_int, [vp, vp, C.c_double, C.c_int, C.c_int, PP]),
+    'fhe_kway_sort': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_kway_sort_type': (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                     C.POINTER(C.c_int)]),
+    'fhe_kway_stage_count': (C.c_int, [C.c_int, C.c_int]),
+    'fhe_kway_rotate_distance': (C.c_int, [C.c_int, C.c_int, C.c_int]),
+    'fhe_kway_gen_indices': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    'fhe_kway_rotation_indices': (C.c_int, [C.c_int, C.POINTER(C.c_int32), C.c_int]),
     'fhe_comm_get_unique_id': (C.c_int, [C.POINTER(C.c_uint8)]),
     'fhe_comm_init': (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_int, C.c_int]),
     'fhe_comm_destroy': (C.c_int, [vp]),
@@ -436,6 +444,11 @@ class Context:
     def mehp24_indicator(self, x, b, dg, df):
         return self._new(lib().fhe_mehp24_indicator, x.h, b, dg, df)
 
+    def kway_sort(self, x, k, M, cfg):
+        """kwaySort::Sorter::sorter via KWayAdapter<k^M>::sort (no bootstrapping);
+        cfg = (3, dg, df)."""
+        return self._new(lib().fhe_kway_sort, x.h, k, M, cfg[1], cfg[2])
+
     # multi-GPU -----------------------------------------------------------
     @staticmethod
     def comm_unique_id():
@@ -574,6 +587,35 @@ def mehp24_rotation_indices(N, sub=256):
     if m < 0:
         raise FheError(-m, lib().fhe_last_error().decode())
     return [int(x) for x in rots[:m]]
+
+
+def kway_rotation_indices(N):
+    rots = np.zeros(64, dtype=np.int32)
+    m = lib().fhe_kway_rotation_indices(N, _int(rots), 64)
+    if m < 0:
+        raise FheError(-m, lib().fhe_last_error().decode())
+    return [int(x) for x in rots[:m]]
+
+
+def kway_stage_count(k, M):
+    return int(lib().fhe_kway_stage_count(k, M))
+
+
+def kway_sort_type(k, M, stage):
+    v = [C.c_int() for _ in range(3)]
+    _chk(lib().fhe_kway_sort_type(k, M, stage, *[C.byref(a) for a in v]))
+    return tuple(a.value for a in v)
+
+
+def kway_rotate_distance(k, log_dist, slope):
+    return int(lib().fhe_kway_rotate_distance(k, log_dist, slope))
+
+
+def kway_gen_indices(num_slots, k, M, m, log_dist, slope):
+    g = np.zeros(num_slots, dtype=np.int32)
+    p = np.zeros(num_slots, dtype=np.int32)
+    _chk(lib().fhe_kway_gen_indices(num_slots, k, M, m, log_dist, slope, _int(g), _int(p)))
+    return g, p
 
 
 def decompose(N, rots, rotation, wrapN, algo):

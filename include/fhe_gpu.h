@@ -236,6 +236,30 @@ int fhe_mehp24_sort_sharded(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n
 /* mehp24::utils::indicatorAdv(c, b, dg, df) (src/mehp24/mehp24_utils.cpp:166-174) */
 int fhe_mehp24_indicator(fhe_ctx *ctx, const fhe_ct *x, double b, int dg, int df, fhe_ct **out);
 
+/* ------------------------------------------------ k-way sorting network */
+/* kwaySort::Sorter::sorter (src/k-way/Sorter.cpp:289-404) as called by
+ * KWayAdapter<N>::sort (src/kway_adapter.h:65-71): sorts the N = k^M values in
+ * the first slots of x (k in {2, 3, 5}; x holds next_pow2(N) slots), comparator
+ * CompositeSign(3, dg, df) (the reference tests' CompositeSignConfig(3, d_f, d_g)
+ * order: tests/k-way/KWaySort2Test.cpp:149).  Bootstrapping is not built: where
+ * the reference calls EvalBootstrap (EvalUtils::checkLevelAndBoot,
+ * src/k-way/EvalUtils.cpp:59-86) the context must still hold the levels,
+ * otherwise FHE_EDEPTH.  Rotation keys: fhe_kway_rotation_indices(N). */
+int fhe_kway_sort(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int df, fhe_ct **out);
+/* kwaySort::sortType(k, M, stage) -> (m, logDist, slope) (src/k-way/Masking.cpp:25-48) */
+int fhe_kway_sort_type(int k, int M, int stage, int *m, int *log_dist, int *slope);
+/* number of stages, M + M(M-1)/2 * ceil(k/2) (src/k-way/Sorter.cpp:290); < 0 on error */
+int fhe_kway_stage_count(int k, int M);
+/* kwaySort::getRotateDistance (src/k-way/Masking.cpp:155-165); < 0 on error */
+int fhe_kway_rotate_distance(int k, int log_dist, int slope);
+/* kwaySort::genIndices (src/k-way/Masking.cpp:50-146): group[i] = indices[0][i],
+ * position[i] = indices[1][i] for i < num_slots */
+int fhe_kway_gen_indices(int num_slots, int k, int M, int m, int log_dist, int slope, int32_t *group,
+                         int32_t *position);
+/* KWayAdapter<N>::getSizeParameters rotation set (+-2^i < N, src/kway_adapter.h:45-49);
+ * returns the count (< 0: error) */
+int fhe_kway_rotation_indices(int N, int32_t *rots, int max_rots);
+
 /* ------------------------------------------------------ multi-GPU (RCCL) */
 int fhe_comm_get_unique_id(uint8_t id[128]);
 int fhe_comm_init(fhe_ctx *ctx, const uint8_t id[128], int rank, int world);

@@ -342,4 +342,15 @@ CtPtr sort_large_fg(Context &cc, const Ciphertext &c, size_t total, size_t sub, 
                     size_t dg_i, size_t df_i, const Shard &sh = Shard());
 }  // namespace mehp24
 
+// k-way sorting network without bootstrapping (oracle_kway.cpp; src/k-way/*)
+namespace kway {
+int stage_count(int k, int M);
+void sort_type(int k, int stage, int &m, int &log_dist, int &slope);
+long rotate_distance(long k, long log_dist, long slope);
+void gen_indices(long ns, long k, long M, long m, long log_dist, long slope, std::vector<int> &grp,
+                 std::vector<int> &pos);
+std::vector<int> rotation_indices(int N);
+CtPtr sort(Context &cc, const Ciphertext &x, int k, int M, const SignConfig &cfg);
+}  // namespace kway
+
 }  // namespace oracle

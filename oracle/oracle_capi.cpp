@@ -9,6 +9,8 @@
 #include <omp.h>
 #endif
 
+#include <stdexcept>
+
 #include "oracle.h"
 
 using namespace oracle;
@@ -296,6 +298,29 @@ int orc_mehp24_rotation_indices(int N, int sub, int *rots, int maxr) {
         return (int)r.size();
     }, -1);
 }
+
+// k-way network (src/k-way/Sorter.cpp:289-404), CompositeSign(3, dg, df)
+void *orc_kway_sort(void *c, void *x, int k, int M, int dg, int df) {
+    return guard([&]() -> void * { return wrap(kway::sort(*CTX, CT(x), k, M, cfg3(3, dg, df))); },
+                 (void *)nullptr);
+}
+int orc_kway_sort_type(int k, int M, int stage, int *out3) {
+    return guard([&]() {
+        if (k < 2 || M < 1 || stage < 0 || stage >= kway::stage_count(k, M)) throw std::invalid_argument("stage");
+        kway::sort_type(k, stage, out3[0], out3[1], out3[2]);
+        return 0;
+    }, -1);
+}
+int orc_kway_gen_indices(int ns, int k, int M, int m, int log_dist, int slope, int *grp, int *pos) {
+    return guard([&]() {
+        std::vector<int> g, p;
+        kway::gen_indices(ns, k, M, m, log_dist, slope, g, p);
+        std::copy(g.begin(), g.end(), grp);
+        std::copy(p.begin(), p.end(), pos);
+        return 0;
+    }, -1);
+}
+int orc_kway_rotate_distance(int k, int log_dist, int slope) { return (int)kway::rotate_distance(k, log_dist, slope); }
 
 int orc_size_parameters(int N, int *multDepth, int *rots, int maxr) {
     return guard([&]() {

@@ -83,6 +83,10 @@ def lib():
                                              C.c_int, C.c_int, vp, vp]),
             'orc_mehp24_indicator': (vp, [vp, vp, C.c_double, C.c_int, C.c_int]),
             'orc_mehp24_rotation_indices': (C.c_int, [C.c_int, C.c_int, ip, C.c_int]),
+            'orc_kway_sort': (vp, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int]),
+            'orc_kway_sort_type': (C.c_int, [C.c_int, C.c_int, C.c_int, ip]),
+            'orc_kway_gen_indices': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip]),
+            'orc_kway_rotate_distance': (C.c_int, [C.c_int, C.c_int, C.c_int]),
             'orc_decompose': (C.c_int, [C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip, C.c_int]),
             'orc_set_coeff_dir': (None, [C.c_char_p]),
             'orc_doubled_sinc': (C.c_int, [C.c_int, dp, C.c_int]),
@@ -336,6 +340,10 @@ class Context:
     def mehp24_indicator(self, a, b, dg, df):
         return Ct(self, lib().orc_mehp24_indicator(self.h, a.h, b, dg, df))
 
+    def kway_sort(self, x, k, M, cfg):
+        """k-way network; cfg = (n, dg, df) with n = 3"""
+        return Ct(self, lib().orc_kway_sort(self.h, x.h, k, M, cfg[1], cfg[2]))
+
     # kernel level -----------------------------------------------------
     def ntt(self, prime_index, data, inverse=False):
         d = np.ascontiguousarray(data, dtype=np.uint64).copy()
@@ -394,6 +402,25 @@ def mehp24_rotation_indices(N, sub=256):
     if m < 0:
         raise ValueError(lib().orc_last_error().decode())
     return [int(x) for x in rots[:m]]
+
+
+def kway_sort_type(k, M, stage):
+    out = np.zeros(3, dtype=np.int32)
+    if lib().orc_kway_sort_type(k, M, stage, _int(out)) < 0:
+        raise ValueError(lib().orc_last_error().decode())
+    return tuple(int(v) for v in out)
+
+
+def kway_gen_indices(num_slots, k, M, m, log_dist, slope):
+    g = np.zeros(num_slots, dtype=np.int32)
+    p = np.zeros(num_slots, dtype=np.int32)
+    if lib().orc_kway_gen_indices(num_slots, k, M, m, log_dist, slope, _int(g), _int(p)) < 0:
+        raise ValueError(lib().orc_last_error().decode())
+    return g, p
+
+
+def kway_rotate_distance(k, log_dist, slope):
+    return int(lib().orc_kway_rotate_distance(k, log_dist, slope))
 
 
 def decompose(N, rots, rotation, wrapN, algo):

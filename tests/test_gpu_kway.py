@@ -1,0 +1,64 @@
+"""k-way sorting network on the GPU engine (src/k-way/*, no bootstrapping):
+bit-exact with the CPU oracle on identical keys for k = 2, 3 (N = 4, 8, 9), and
+the reference test's property (decrypted == sorted input within 0.01,
+tests/k-way/KWaySort5Test.cpp) for k = 5, N = 25.  A context too shallow for
+the network fails with FHE_EDEPTH where the reference would bootstrap.
+
+All calls go through the C ABI (include/fhe_gpu.h) via fhesort.py.
+"""
+import numpy as np
+import pytest
+
+import fhesort as F
+import pyoracle as O
+from test_gpu_hybrid import same
+
+pytestmark = pytest.mark.gpu
+
+
+def _dnum(depth):  # the engine takes digits of <= 16 primes: deep chains need more digits
+    return -(-(depth + 1) // 15)
+
+
+def _slots(N):
+    s = 1
+    while s < N:
+        s *= 2
+    return s
+
+
+@pytest.mark.parametrize('k,M,depth,used', [(2, 2, 52, 48), (3, 2, 70, 67), (2, 3, 100, 96)])
+def test_kway_matches_oracle(k, M, depth, used):
+    N = k ** M
+    rots = F.kway_rotation_indices(N)
+    orc = O.Context(11, depth, 40, 60, _dnum(depth), seed=41)
+    orc.gen_rotation_keys(rots)
+    gpu = F.Context(11, depth, 40, 60, _dnum(depth), seed=41, keygen=False)
+    gpu.load_keys_from(orc, rots)
+    x = np.random.default_rng(N).permutation(N) * (1 - 1e-8) / N
+    ox = orc.encrypt(x, _slots(N))
+    g = gpu.kway_sort(gpu.from_oracle(ox), k, M, (3, 2, 2))
+    o = orc.kway_sort(ox, k, M, (3, 2, 2))
+    same(g, o)
+    assert g.info()['level'] == used
+    assert np.max(np.abs(gpu.decrypt(g)[:N] - np.sort(x))) < 0.01
+
+
+def test_kway_five_way_sorts():
+    k, M = 5, 2
+    N = k ** M
+    gpu = F.Context(11, 104, 40, 60, _dnum(104), seed=42)
+    gpu.gen_rotation_keys(F.kway_rotation_indices(N))
+    x = np.random.default_rng(7).permutation(N) * (1 - 1e-8) / N
+    out = gpu.kway_sort(gpu.encrypt(x, _slots(N)), k, M, (3, 2, 2))
+    assert out.info()['level'] == 100
+    assert np.max(np.abs(gpu.decrypt(out)[:N] - np.sort(x))) < 0.01
+
+
+def test_kway_too_shallow_is_edepth():
+    gpu = F.Context(11, 30, 40, 60, 3, seed=43)
+    gpu.gen_rotation_keys(F.kway_rotation_indices(4))
+    ct = gpu.encrypt(np.array([0.5, 0.25, 0.75, 0.0]), 4)
+    with pytest.raises(F.FheError) as e:
+        gpu.kway_sort(ct, 2, 2, (3, 2, 2))
+    assert e.value.code == 3  # FHE_EDEPTH
