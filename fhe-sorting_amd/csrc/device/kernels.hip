@@ -205,12 +205,16 @@ __global__ __launch_bounds__(NT) void k_linear_sum_multi(MultiLinArgs A, size_t 
         u64 xv[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) xv[u] = base + u < end ? A.x[base + u][(size_t)blockIdx.z * A.xseg[base + u] + ln] : 0;
+        // fully unrolled (a `break` here kept the loop rolled: xv[] indexed at
+        // run time and one exposed LDS round trip per baby step); the guard is
+        // wave-uniform
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-            if (base + u >= end) break;
-            const Split30 x = split30(xv[u]);
+            if (base + u < end) {
+                const Split30 x = split30(xv[u]);
 #pragma unroll
-            for (int g = 0; g < G; ++g) mac4(s[g], x, w[g * MLS_M + base + u]);
+                for (int g = 0; g < G; ++g) mac4(s[g], x, w[g * MLS_M + base + u]);
+            }
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) run[g] = add_mod(run[g], reduce4(s[g], md), md.q);
