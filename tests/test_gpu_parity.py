@@ -376,3 +376,33 @@ def test_config2_direct_sort_full_size_bit_exact():
     same(gout, orc.direct_sort(ox, N, rots, (3, 3, 2)))
     assert gout.level == depth
     assert np.max(np.abs(gpu.decrypt(gout) - np.sort(x))) < 0.01
+
+
+def test_config3_direct_sort_full_size():
+    """The BASELINE metric's own configuration at full size: DirectSort N=1024 at ring
+    2^16, depth 39, 161 rotation keys, CompositeSign(3,5,2), scale 2^50
+    -- the bench workload.  The oracle needs ~30 min for this sort, so parity here is
+    through size-independent properties: the reference's bound (sorted within 0.01,
+    output level == multDepth; tests/DirectSortTest.cpp:128,169), and the same
+    ciphertext word for word whether the 32 comparator / index-check batches run as
+    one stack on three concurrent lanes (the bench's setting) or in stacks of 5 on one
+    lane."""
+    N = 1024
+    depth, rots = F.size_parameters(N)
+    assert depth == 39 and len(rots) == 161
+    gpu = F.Context(16, depth, 50, 60, 3, seed=20250704)
+    gpu.gen_rotation_keys(rots)
+    x = np.random.default_rng(20250704).permutation(N) / N
+    ct = gpu.encrypt(x, N)
+    gpu.set_sort_lanes(3)
+    gpu.set_sort_stack(32)
+    a = gpu.direct_sort(ct, N, rots, (3, 5, 2))
+    gpu.set_sort_lanes(1)
+    gpu.set_sort_stack(5)
+    try:
+        b = gpu.direct_sort(ct, N, rots, (3, 5, 2))
+    finally:
+        gpu.set_sort_stack(32)
+    assert a.level == depth
+    assert np.max(np.abs(gpu.decrypt(a) - np.sort(x))) < 0.01
+    assert np.array_equal(a.data(), b.data())
