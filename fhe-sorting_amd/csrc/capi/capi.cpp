@@ -509,9 +509,10 @@ int fhe_kway_sort(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int df, f
         NEED(ctx);
         NEED(x);
         NEED(out);
+        if (k < 2 || M < 1) throw std::invalid_argument("k-way: k >= 2 and M >= 1 required");
         long N = 1;
-        for (int i = 0; i < M; ++i) N *= k;
-        if (M < 1 || N > x->p->slots) throw std::invalid_argument("k-way: k^M exceeds the ciphertext's slots");
+        for (int i = 0; i < M && N <= x->p->slots; ++i) N *= k;
+        if (N > x->p->slots) throw std::invalid_argument("k-way: k^M exceeds the ciphertext's slots");
         kwaySort::Sorter s(*ctx->eng, N, k, M);
         *out = wrap(s.sorter(*x->p, SignConfig(CompositeSignConfig(3, dg, df), ctx->eng->params().L)));
     });
@@ -522,17 +523,22 @@ int fhe_kway_sort_type(int k, int M, int stage, int *m, int *log_dist, int *slop
         NEED(m);
         NEED(log_dist);
         NEED(slope);
-        if (k < 2 || M < 1 || stage < 0 || stage >= kwaySort::stageCount(k, M))
+        if (k < 2 || k > 16 || M < 1 || M > 30 || stage < 0 || stage >= kwaySort::stageCount(k, M))
             throw std::invalid_argument("k-way: stage out of range");
         std::tie(*m, *log_dist, *slope) = kwaySort::sortType(k, M, stage);
     });
 }
 
-int fhe_kway_stage_count(int k, int M) { return (k < 2 || M < 1) ? -FHE_EINVAL : kwaySort::stageCount(k, M); }
+int fhe_kway_stage_count(int k, int M) {
+    return (k < 2 || k > 16 || M < 1 || M > 30) ? -FHE_EINVAL : kwaySort::stageCount(k, M);
+}
 
 int fhe_kway_rotate_distance(int k, int log_dist, int slope) {
-    return (k < 2 || log_dist < 0 || slope < 0) ? -FHE_EINVAL
-                                                 : (int)kwaySort::getRotateDistance(k, log_dist, slope);
+    if (k < 2 || k > 16 || log_dist < 0 || slope < 0 || slope > k) return -FHE_EINVAL;
+    long d = 1;
+    for (int i = 0; i < log_dist; ++i)
+        if ((d *= k) > (1L << 30)) return -FHE_EINVAL;
+    return (int)kwaySort::getRotateDistance(k, log_dist, slope);
 }
 
 int fhe_kway_gen_indices(int num_slots, int k, int M, int m, int log_dist, int slope, int32_t *group,
@@ -540,9 +546,10 @@ int fhe_kway_gen_indices(int num_slots, int k, int M, int m, int log_dist, int s
     return guard([&] {
         NEED(group);
         NEED(position);
-        if (k < 2 || M < 1 || m < 0 || log_dist < 0 || m + 1 + log_dist > 30) throw std::invalid_argument("k-way: bad index layout");
+        if (k < 2 || k > 16 || M < 1 || M > 30 || m < 0 || log_dist < 0 || m + 1 + log_dist > 30 || num_slots < 1)
+            throw std::invalid_argument("k-way: bad index layout");
         long N = 1, blk = 1;
-        for (int i = 0; i < M; ++i) N *= k;
+        for (int i = 0; i < M && N <= num_slots; ++i) N *= k;
         for (int i = 0; i < m + 1 + log_dist; ++i) blk *= k;  // dist * k^(m+1): one group block
         if (num_slots < (N + blk - 1) / blk * blk) throw std::invalid_argument("k-way: layout exceeds num_slots");
         auto ind = kwaySort::genIndices(num_slots, k, M, m, log_dist, slope);
@@ -556,7 +563,7 @@ int fhe_kway_gen_indices(int num_slots, int k, int M, int m, int log_dist, int s
 int fhe_kway_rotation_indices(int N, int32_t *rots, int max_rots) {
     int count = -1;
     int rc = guard([&] {
-        if (N < 1) throw std::invalid_argument("k-way: N must be positive");
+        if (N < 1 || N > (1 << 30)) throw std::invalid_argument("k-way: N must be in 1..2^30");
         auto r = kwaySort::rotationIndices(N);
         count = (int)r.size();
         for (int i = 0; i < count && i < max_rots; ++i) rots[i] = r[(size_t)i];
