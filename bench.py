@@ -192,10 +192,24 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json'):
     top = sorted(stats.items(), key=lambda kv: -kv[1]['ms'])[:8]
     table = {k: {'share': round(v['ms'] / total_ms, 3), 'avg_us': round(v['ms'] / v['launches'] * 1e3, 1),
                  'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1)} for k, v in top}
+    run_bytes = sum(v['bytes'] for v in stats.values())
     return {'kernel': name, 'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_source': src,
             'avg_us': round(avg_s * 1e6, 2), 'launches': st['launches'],
-            'algorithmic_bytes_per_launch': per_launch, 'clocked_ms_per_sort': round(total_ms, 1), 'kernels': table}
+            'algorithmic_bytes_per_launch': per_launch, 'clocked_ms_per_sort': round(total_ms, 1), 'kernels': table,
+            # whole sort: every clocked kernel's algorithmic bytes,
+            # over its summed kernel time here and over the timed wall in with_run()
+            'run': {'algorithmic_bytes_per_sort': run_bytes,
+                    'GBps_over_kernel_time': round(run_bytes / (total_ms * 1e-3) / 1e9, 1)}}
+
+
+def with_run(roof, ms_per_step, world):
+    """whole-run fraction: all ranks' algorithmic bytes of one sort / wall / (world x peak)"""
+    if roof and 'run' in roof:
+        gbps = roof['run']['algorithmic_bytes_per_sort'] / (ms_per_step * 1e-3) / 1e9
+        roof['run']['GBps_over_wall'] = round(gbps, 1)
+        roof['run']['frac_over_wall'] = round(gbps / (world * HBM_PEAK_GBS), 4)
+    return roof
 
 
 def cpu_baseline(logN, depth, N, sample_mults, scale_bits, dnum=3):
@@ -315,7 +329,8 @@ def run_mehp24(a, d):
         if not a.no_roofline and d.world == 1:
             try:
                 ctx.pool_trim()
-                res['roofline'] = roofline(ctx, run, a.clock_json, 'pmc_traffic_mehp24.json')
+                res['roofline'] = with_run(roofline(ctx, run, a.clock_json, 'pmc_traffic_mehp24.json'),
+                                           res['ms_per_step'], 1)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
         if d.world == 1 and not a.no_cpu_baseline:
@@ -404,7 +419,9 @@ def main():
         if not a.no_roofline:
             try:
                 ctx.set_sort_lanes(1)
-                res['roofline'] = roofline(ctx, lambda: ctx.direct_sort(ct, N, rots, cfg, shard=(0, 1)), a.clock_json)
+                res['roofline'] = with_run(
+                    roofline(ctx, lambda: ctx.direct_sort(ct, N, rots, cfg, shard=(0, 1)), a.clock_json),
+                    res['ms_per_step'], d.world)
                 ctx.set_sort_lanes(a.lanes)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
