@@ -34,6 +34,39 @@ void trim_zeros(std::vector<double> &a) {
     while (a.size() > 1 && a.back() == 0.0) a.pop_back();
 }
 
+// Levels OpenFHE's EvalChebyshevSeriesPS consumes for a degree-d series: the
+// reference's multDepth tables (src/sort_algo.h:87-201) budget these, and its
+// tests assert the output level (tests/DirectSortTest.cpp:128).  Degrees < 5
+// go through EvalChebyshevSeriesLinear (T_1..T_d, then one constant product);
+// up to 2204 OpenFHE picks (k, m) from a fixed table whose depth bands are the
+// published ones below; above, ComputeDegreesPS's heuristic: minimise
+// k + 2m + 2^(m-1) - 4 over k*(2^m - 1) > d with floor(log2 k) within 1 of
+// floor(log2 sqrt(d/2)); depth ceil(log2 k) + m.  The evaluation itself stays
+// depth-optimal; a series whose optimal depth is below this one is evaluated
+// to the lower output level (its leaves absorb the extra rescale).
+int openfhe_ps_depth(int d) {
+    if (d < 5) return ceil_log2(d) + 1;
+    static const int band_top[] = {5, 13, 27, 59, 119, 247, 495, 1007, 2031, 2204};
+    for (int i = 0; i < 10; ++i)
+        if (d <= band_top[i]) return 3 + i;
+    const double f = std::floor(std::log2(std::sqrt(d / 2.0)));
+    long best = -1;
+    int depth = 0;
+    for (long k = 1; k <= d; ++k) {
+        if (std::fabs(std::floor(std::log2((double)k)) - f) > 1) continue;
+        const int mmax = (int)std::ceil(std::log2((double)d / k) + 1) + 1;
+        for (int m = 1; m <= mmax; ++m)
+            if ((long)d - k * ((1L << m) - 1) < 0) {
+                const long mult = k + 2 * m + (1L << (m - 1)) - 4;
+                if (best < 0 || mult < best) {
+                    best = mult;
+                    depth = ceil_log2(k) + m;
+                }
+            }
+    }
+    return depth;
+}
+
 // Leaves are sum_{i<=B} a_i T_i (depth log2(B)+1); a node p = q T_G + r with
 // G a power of two; capacity at depth D is 2^D - B, so a degree-d series
 // costs ceil(log2(d+1)) levels.
@@ -210,7 +243,7 @@ CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<
     if (d == 0) return cc.add_const(*cc.trivial_const(0.0, x->level, x->slots, x->batch), s[0]);
     PSEval ev(cc, *x, d);
     ev.build_baby();
-    return ev.run(s, x->level + ev.D);
+    return ev.run(s, x->level + std::max(ev.D, openfhe_ps_depth(d)));
 }
 
 // ====================================================== composite sign =====
@@ -635,17 +668,42 @@ const Plaintext &DirectSortN::mask(Engine &E, int kind, int num_slots, int k, in
     return *p;
 }
 
+void checkShardWorld(const host::Params &P, int world) {
+    u64 qmax = 0;
+    for (size_t i = 0; i < P.nq(); ++i) qmax = std::max(qmax, P.primes[i]);
+    if (world < 1 || (u64)world > ~0ULL / qmax)
+        throw std::invalid_argument("sharded run: world " + std::to_string(world) +
+                                    " ranks would overflow the u64 sum of residues (world * q_max >= 2^64)");
+}
+ShardHeader checkShardHeader(const u64 h[4]) {
+    const u64 present = h[0], s1 = h[1], s2 = h[2], limbs = h[3];
+    if (present == 0) throw std::runtime_error("sharded run: no shard produced a partial");
+    // all present partials share one level iff sum(l)^2 == present * sum(l^2)
+    if ((unsigned __int128)s1 * s1 != (unsigned __int128)present * s2 || s1 % present || limbs % present)
+        throw std::runtime_error("sharded run: ranks' partials differ in level or limb count");
+    return ShardHeader{(int)(s1 / present) - 1, (size_t)(limbs / present)};
+}
+
 void reducePartial(Engine &cc, const Shard &sh, CtPtr &acc, int slots) {
-    if (sh.world <= 1) return;
-    if (!sh.allreduce) throw std::runtime_error("sharded run without an allreduce hook");
-    auto hdr = cc.alloc_u64(2);
-    u64 h[2] = {acc ? (u64)(acc->level + 1) : 0, acc ? 1ULL : 0ULL};
-    cc.h2d(hdr.ptr, h, 2);
-    sh.allreduce(hdr.ptr, 2);
-    cc.d2h(h, hdr.ptr, 2);
-    if (h[1] == 0) throw std::runtime_error("sharded run: no shard produced a partial");
-    const int level = (int)(h[0] / h[1]) - 1;
-    if (!acc) acc = cc.zero_like(level, slots);
+    // a single rank reduces only when the caller gave it a collective (an
+    // RCCL communicator of world 1 still runs the all-reduce)
+    if (!sh.allreduce) {
+        if (sh.world > 1) throw std::runtime_error("sharded run without an allreduce hook");
+        return;
+    }
+    checkShardWorld(cc.params(), sh.world);
+    if (acc && acc->batch != 1) throw std::invalid_argument("sharded run: a partial must be a single ciphertext");
+    // header: presence, level + 1, (level + 1)^2, limbs -- summed over ranks.
+    // Every rank sees the same sums, so every rank takes the same branch below.
+    auto hdr = cc.alloc_u64(4);
+    const u64 l1 = acc ? (u64)(acc->level + 1) : 0;
+    u64 h[4] = {acc ? 1ULL : 0ULL, l1, l1 * l1, acc ? (u64)acc->limbs : 0};
+    cc.h2d(hdr.ptr, h, 4);
+    sh.allreduce(hdr.ptr, 4);
+    cc.d2h(h, hdr.ptr, 4);
+    const ShardHeader H = checkShardHeader(h);
+    if (!acc) acc = cc.zero_like(H.level, slots);
+    if (acc->limbs != H.limbs) throw std::runtime_error("sharded run: partial limb count differs from the header");
     sh.allreduce(acc->data, 2 * acc->limbs * cc.n());
     cc.reduce_after_allreduce(*acc);
 }

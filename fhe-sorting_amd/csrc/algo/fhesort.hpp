@@ -161,11 +161,22 @@ struct Shard {
     CtAllReduce allreduce;
     bool mine(size_t i) const { return world <= 1 || (int)(i % (size_t)world) == rank; }
 };
-// Combines per-rank partial sums of one ciphertext: a 2-word header (level + 1,
-// presence) is summed first so ranks that hold no partial agree on the level
-// and contribute a zero ciphertext, then the limbs are summed as u64 and
-// reduced mod q.  No-op for one rank.
+// Combines per-rank partial sums of one ciphertext: a 4-word header
+// (presence, level + 1, (level + 1)^2, limbs) is summed first so ranks that
+// hold no partial agree on the level and contribute a zero ciphertext, and
+// ranks whose partials disagree on level or limbs all fail with the same error
+// instead of entering mismatched collectives; then the limbs are summed as u64
+// and reduced mod q.  No-op for one rank.
 void reducePartial(Engine &cc, const Shard &sh, CtPtr &acc, int slots);
+
+// The u64 sum of `world` residues, each < q_max, must not wrap: world * q_max
+// < 2^64 (world <= 16 for the 60-bit first prime).  Throws otherwise.
+void checkShardWorld(const host::Params &P, int world);
+struct ShardHeader {
+    int level;
+    size_t limbs;
+};
+ShardHeader checkShardHeader(const u64 h[4]);
 
 class DirectSortN {
   public:

@@ -351,6 +351,7 @@ int fhe_size_parameters(int N, int *depth, int32_t *rots, int max_rots) {
 // The reduction a sharded sort uses: the caller's hook if given, else RCCL on
 // the context's communicator (fhe_comm_init), on the engine stream.
 static CtAllReduce make_allreduce(fhe_ctx *ctx, int shard_world, fhe_allreduce_fn fn, void *user) {
+    if (shard_world > 1) checkShardWorld(ctx->eng->params(), shard_world);  // before any work
     if (fn) {
         // the partial sums are produced asynchronously on the context stream:
         // drain it so the callback sees finished data (it must complete the
@@ -358,11 +359,16 @@ static CtAllReduce make_allreduce(fhe_ctx *ctx, int shard_world, fhe_allreduce_f
         Engine *eng = ctx->eng.get();
         return [fn, user, eng](u64 *d, size_t c) {
             eng->sync();
-            fn(d, (uint64_t)c, user);
+            const int rc = fn(d, (uint64_t)c, user);
+            if (rc != 0) throw std::runtime_error("HIP error: allreduce hook returned " + std::to_string(rc));
         };
     }
-    if (shard_world <= 1) return nullptr;
-    if (!ctx->comm) throw std::runtime_error("sharded sort needs fhe_comm_init or an allreduce hook");
+    if (!ctx->comm) {
+        if (shard_world > 1) throw std::runtime_error("sharded sort needs fhe_comm_init or an allreduce hook");
+        return nullptr;
+    }
+    if (shard_world != ctx->world)
+        throw std::invalid_argument("sharded sort: shard world differs from the communicator's world");
     ncclComm_t comm = ctx->comm;
     hipStream_t st = static_cast<hipStream_t>(ctx->eng->stream_handle());
     return [comm, st](u64 *d, size_t c) {
@@ -618,8 +624,9 @@ int fhe_ct_allreduce(fhe_ctx *ctx, fhe_ct *ct) {
         return FHE_ENOCOMM;
     }
     return guard([&] {
+        NEED(ct);
         hipStream_t st = static_cast<hipStream_t>(ctx->eng->stream_handle());
-        const size_t cnt = 2 * ct->p->limbs * ctx->eng->n();
+        const size_t cnt = 2 * (size_t)ct->p->batch * ct->p->limbs * ctx->eng->n();
         if (ncclAllReduce(ct->p->data, ct->p->data, cnt, ncclUint64, ncclSum, ctx->comm, st) != ncclSuccess)
             throw std::runtime_error("HIP error: ncclAllReduce failed");
         ctx->eng->reduce_after_allreduce(*ct->p);

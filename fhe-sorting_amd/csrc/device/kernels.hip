@@ -67,19 +67,26 @@ __device__ __forceinline__ u64 smod(int64_t v, const Mod &m) {
     const u64 r = reduce64((u64)0 - (u64)v, m);
     return r ? m.q - r : 0;
 }
-__global__ __launch_bounds__(NT) void k_mul_scalar(u64 *out, const u64 *a, int64_t K, Seg S, const Mod *mods,
-                                                   int logN) {
+// (v * 2^sh) mod q: a constant too large for 62 bits is carried as a rounded
+// mantissa and a power of two (host::SConst)
+__device__ __forceinline__ u64 smod(int64_t v, int sh, const Mod &m) {
+    u64 r = smod(v, m);
+    for (int i = 0; i < sh; ++i) r = add_mod(r, r, m.q);
+    return r;
+}
+__global__ __launch_bounds__(NT) void k_mul_scalar(u64 *out, const u64 *a, int64_t K, int sh, Seg S,
+                                                   const Mod *mods, int logN) {
     EW_PROLOGUE
     const Mod m = mods[l];
-    const u64 w = smod(K, m);
+    const u64 w = smod(K, sh, m);
     (void)q;
     const ulonglong2 x = ld2(a + oa);
     st2(out + oo, make_ulonglong2(mul_barrett(x.x, w, m), mul_barrett(x.y, w, m)));
 }
-__global__ __launch_bounds__(NT) void k_add_scalar(u64 *out, const u64 *a, int64_t K, Seg S, const Mod *mods,
-                                                   int logN) {
+__global__ __launch_bounds__(NT) void k_add_scalar(u64 *out, const u64 *a, int64_t K, int sh, Seg S,
+                                                   const Mod *mods, int logN) {
     EW_PROLOGUE
-    const u64 w = smod(K, mods[l]);
+    const u64 w = smod(K, sh, mods[l]);
     const ulonglong2 x = ld2(a + oa);
     st2(out + oo, make_ulonglong2(add_mod(x.x, w, q), add_mod(x.y, w, q)));
 }
@@ -136,6 +143,7 @@ constexpr int LIN_MAX = 32;
 struct LinArgs {
     const u64 *x[LIN_MAX];
     int64_t K[LIN_MAX];
+    uint8_t sh[LIN_MAX];  // K[i] * 2^sh[i]
     int m, accumulate;
     size_t xseg;
 };
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(NT) void k_linear_sum(u64 *out, LinArgs A, size_t s
     const size_t n = (size_t)1 << logN;
     const int l = blockIdx.y;
     const Mod md = mods[l];
-    if ((int)threadIdx.x < A.m) w[threadIdx.x] = smod(A.K[threadIdx.x], md);
+    if ((int)threadIdx.x < A.m) w[threadIdx.x] = smod(A.K[threadIdx.x], A.sh[threadIdx.x], md);
     __syncthreads();
     const size_t off = (size_t)blockIdx.z * seg + (size_t)l * n;
     const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
@@ -176,6 +184,7 @@ struct MultiLinArgs {
     const u64 *x[MLS_M];
     size_t xseg[MLS_M];
     int64_t K[MLS_G * MLS_M];  // [g][i]
+    uint8_t sh[MLS_G * MLS_M];  // K[t] * 2^sh[t]
     int m, G, accumulate;
 };
 // One coefficient per lane, G outputs.  Every residue and constant is < 2^60,
@@ -190,7 +199,7 @@ __global__ __launch_bounds__(NT) void k_linear_sum_multi(MultiLinArgs A, size_t 
     const size_t n = (size_t)1 << logN;
     const int l = blockIdx.y;
     const Mod md = mods[l];
-    for (int t = threadIdx.x; t < G * MLS_M; t += NT) w[t] = split30((t % MLS_M) < A.m ? smod(A.K[t], md) : 0);
+    for (int t = threadIdx.x; t < G * MLS_M; t += NT) w[t] = split30((t % MLS_M) < A.m ? smod(A.K[t], A.sh[t], md) : 0);
     __syncthreads();
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
@@ -586,15 +595,16 @@ void ew_neg(u64 *out, const u64 *a, int limbs, int segs, Seg S, const Mod *mods,
     hipLaunchKernelGGL(k_neg, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, S, mods, logN);
 }
 void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
-                   hipStream_t st) {
+                   hipStream_t st, int sh) {
     if (limbs <= 0 || segs <= 0) return;
     const double B = 8.0 * 2 * limbs * segs * ((size_t)1 << logN);
-    launch_clocked("k_mul_scalar", B, k_mul_scalar, ew_grid(logN, limbs, segs), dim3(NT), st, out, a, K, S, mods, logN);
+    launch_clocked("k_mul_scalar", B, k_mul_scalar, ew_grid(logN, limbs, segs), dim3(NT), st, out, a, K, sh, S, mods,
+                   logN);
 }
 void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
-                   hipStream_t st) {
+                   hipStream_t st, int sh) {
     if (limbs <= 0 || segs <= 0) return;
-    hipLaunchKernelGGL(k_add_scalar, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, K, S, mods, logN);
+    hipLaunchKernelGGL(k_add_scalar, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, K, sh, S, mods, logN);
 }
 void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, Seg S, const Mod *mods, int logN,
                   hipStream_t st) {
@@ -615,7 +625,7 @@ void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *
     hipLaunchKernelGGL(k_sum_members, ew_grid(logN, limbs, 2), dim3(NT), 0, st, out, in, members, ln_all, mods, logN);
 }
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
-                   size_t xseg, const Mod *mods, int logN, hipStream_t st, bool accumulate) {
+                   size_t xseg, const Mod *mods, int logN, hipStream_t st, bool accumulate, const uint8_t *sh) {
     if (limbs <= 0) return;
     for (int base = 0; base < m || (m == 0 && base == 0); base += LIN_MAX) {
         LinArgs A{};
@@ -625,6 +635,7 @@ void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int 
         for (int i = 0; i < A.m; ++i) {
             A.x[i] = xs[base + i];
             A.K[i] = K[base + i];
+            A.sh[i] = sh ? sh[base + i] : 0;
         }
         const double B = 8.0 * (A.m + A.accumulate + 1) * limbs * segs * ((size_t)1 << logN);
         launch_clocked("k_linear_sum", B, k_linear_sum, ew_grid(logN, limbs, segs), dim3(NT), st, out, A, seg, mods,
@@ -633,7 +644,8 @@ void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int 
     }
 }
 void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,
-                         int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st) {
+                         int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st,
+                         const uint8_t *sh) {
     if (limbs <= 0 || segs <= 0 || G <= 0 || m <= 0) return;
     if (G > MLS_G) throw std::invalid_argument("ew_linear_sum_multi: at most 8 outputs per pass");
     for (int base = 0; base < m; base += MLS_M) {
@@ -645,7 +657,10 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
         for (int i = 0; i < A.m; ++i) {
             A.x[i] = xs[base + i];
             A.xseg[i] = xseg[base + i];
-            for (int g = 0; g < G; ++g) A.K[g * MLS_M + i] = K[(size_t)g * m + base + i];
+            for (int g = 0; g < G; ++g) {
+                A.K[g * MLS_M + i] = K[(size_t)g * m + base + i];
+                A.sh[g * MLS_M + i] = sh ? sh[(size_t)g * m + base + i] : 0;
+            }
         }
         const double B = 8.0 * (A.m + (double)G * (1 + A.accumulate)) * limbs * segs * ((size_t)1 << logN);
         const dim3 grid = pt_grid(logN, limbs, segs);

@@ -77,7 +77,8 @@ struct NttFuse {
     const u64 *c2 = nullptr, *c2s = nullptr;  // per limb: P mod q_i (HMult)
     const u64 *src = nullptr;  // inverse: out-of-place input of the first pass
     size_t seg_src = 0;
-    int64_t scalar = 0;  // rescale: multiply the input by this integer first (0 = none)
+    int64_t scalar = 0;  // rescale: multiply the input by scalar * 2^scalar_sh first (0 = none)
+    int scalar_sh = 0;
     bool raw = false;    // inverse: skip the n^-1 scaling of the last pass
 };
 // inverse NTT reading the input from `src` (segment z, limb l at src + z*seg_src + l*n), writing dst
@@ -107,12 +108,12 @@ void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, co
 void ew_sub(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, const Mod *mods, int logN,
             hipStream_t st);
 void ew_neg(u64 *out, const u64 *a, int limbs, int segs, Seg S, const Mod *mods, int logN, hipStream_t st);
-// out = a * (K mod q_l)   (K: signed integer constant, reduced in-kernel)
+// out = a * (K 2^sh mod q_l)   (K: signed integer constant, reduced in-kernel)
 void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
-                   hipStream_t st);
-// out = a + (K mod q_l)
+                   hipStream_t st, int sh = 0);
+// out = a + (K 2^sh mod q_l)
 void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
-                   hipStream_t st);
+                   hipStream_t st, int sh = 0);
 // out[s] = a[s] * p[s]  (Barrett; S.b = 0 broadcasts one plaintext)
 void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, Seg S, const Mod *mods, int logN,
                   hipStream_t st);
@@ -122,13 +123,15 @@ void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int mem
                const Mod *mods, int logN, hipStream_t st);
 // out [2][limbs][n] = sum_m in [m][2][limbs][n]
 void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st);
-// out (+)= sum_i (K_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride)
+// out (+)= sum_i (K_i 2^sh_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride; sh may be null)
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
-                   size_t xseg, const Mod *mods, int logN, hipStream_t st, bool accumulate = false);
+                   size_t xseg, const Mod *mods, int logN, hipStream_t st, bool accumulate = false,
+                   const uint8_t *sh = nullptr);
 // outs[g] = sum_i (K[g*m + i] mod q_l) * x_i for g < G <= 8 in one pass over the
 // inputs (x_i: [segs][limbs][n] with segment stride xseg[i]; outs: stride seg)
 void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,
-                         int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st);
+                         int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st,
+                         const uint8_t *sh = nullptr);
 // out [members][2][limbs][n] = sum_i ct_i * pt_i  (ct_i member stride cmember, 0 = broadcast;
 // c1 at + cpoly; pt_i [limbs][n] shared), lazy 128-bit accumulation
 void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, int m, int limbs, int members,

@@ -76,6 +76,11 @@ __device__ __forceinline__ u64 smod64(int64_t v, const Mod &m) {  // signed inte
     const u64 r = reduce64((u64)0 - (u64)v, m);
     return r ? m.q - r : 0;
 }
+__device__ __forceinline__ u64 smod64(int64_t v, int sh, const Mod &m) {  // v * 2^sh -> [0, q)
+    u64 r = smod64(v, m);
+    for (int i = 0; i < sh; ++i) r = r + r >= m.q ? r + r - m.q : r + r;
+    return r;
+}
 __device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0, q)
     x = x >= q2 ? x - q2 : x;
     return x >= q ? x - q : x;
@@ -132,7 +137,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         // context creation), so c or q_p - (q_last - c) is already reduced
         const Mod ml = Tb.mods[F.lastp];
         const u64 ql = ml.q, qh = ql >> 1;
-        const u64 kl = F.scalar ? smod64(F.scalar, ml) : 0;  // K mod q_last (scaled rescale)
+        const u64 kl = F.scalar ? smod64(F.scalar, F.scalar_sh, ml) : 0;  // K mod q_last (scaled rescale)
         const u64 *src = F.last + (size_t)blockIdx.x * F.seg_last;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
@@ -248,7 +253,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         const u64 c1 = EPI ? F.c1[limb] : 0, c1s = EPI ? F.c1s[limb] : 0;
         const u64 c2 = MODE == NTT_MULTAIL ? F.c2[limb] : 0, c2s = MODE == NTT_MULTAIL ? F.c2s[limb] : 0;
         // scaled rescale: out = (K x - v) q_last^-1 = x (K q_last^-1) - v q_last^-1
-        const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, mp), c1, c1s, q) : 0;
+        const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, F.scalar_sh, mp), c1, c1s, q) : 0;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int idx = t + T * r;

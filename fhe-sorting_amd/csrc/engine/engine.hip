@@ -156,8 +156,13 @@ struct Engine::Impl {
     int *modup_smap = nullptr, *modup_pmap = nullptr;
 
     // keys
-    std::shared_ptr<DevMem> s_ntt, pk, relin;
-    std::map<u64, std::shared_ptr<DevMem>> rotkeys;
+    // key material, shared by an engine and its forks (sort lanes): a key load
+    // on the parent replaces the members in place, so every fork sees it
+    struct KeySet {
+        std::shared_ptr<DevMem> s_ntt, pk, relin;
+        std::map<u64, std::shared_ptr<DevMem>> rotkeys;
+    };
+    std::shared_ptr<KeySet> ks = std::make_shared<KeySet>();
     std::map<u64, std::shared_ptr<DevMem>> perms;
     int key_digits = 0;
 
@@ -259,7 +264,7 @@ struct Engine::Impl {
         fold.member = 2 * ell * nn;
         fold.w = LT.pmod[ell - 1];
         fold.ws = LT.pmod_s[ell - 1];
-        dev::ks_inner(acc, e, d2, static_cast<u64 *>(relin->p), (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha,
+        dev::ks_inner(acc, e, d2, static_cast<u64 *>(ks->relin->p), (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha,
                       digits, nullptr, ext(ell), mods, P.logN, st, members, str, fold);
         dev::ntt_inverse(acc + (ell - 1) * nn, (int)K + 1, segs, W * nn, ext(ell) + (ell - 1), T, st, /*raw*/ true);
         auto corrm = alloc((size_t)segs * (ell - 1) * nn * 8);
@@ -282,7 +287,7 @@ struct Engine::Impl {
     }
     // out [segs][ell-1][n] = Rescale(K * in) from the first ell limbs of
     // in [segs][.][n] (segment stride seg_in); K = 0 means no scalar
-    void rescale(const u64 *in, size_t ell, size_t seg_in, int segs, u64 *out, int64_t K = 0) {
+    void rescale(const u64 *in, size_t ell, size_t seg_in, int segs, u64 *out, host::SConst K = {}) {
         Phase phase_("rescale");
         const size_t nn = n();
         auto lastm = alloc((size_t)segs * nn * 8);
@@ -303,7 +308,8 @@ struct Engine::Impl {
         F.seg_x = seg_in;
         F.c1 = qlinv + ell * P.nq();
         F.c1s = qlinv_s + ell * P.nq();
-        F.scalar = K;
+        F.scalar = K.k;
+        F.scalar_sh = K.sh;
         dev::ntt_forward_rescale(tmp, (int)(ell - 1), segs, F, T, st);
     }
 };
@@ -412,11 +418,8 @@ void Engine::wait_for(const Engine &other) {
 Engine::~Engine() {
     if (impl && impl->st) {
         (void)hipStreamSynchronize(impl->st);
-        impl->rotkeys.clear();
+        impl->ks.reset();  // the last engine sharing the key set frees it
         impl->perms.clear();
-        impl->relin.reset();
-        impl->pk.reset();
-        impl->s_ntt.reset();
         impl->keep.clear();
         (void)hipStreamDestroy(impl->st);
     }
@@ -473,8 +476,8 @@ void Engine::keygen() {
     auto s = sample_coeffs(I.seed, host::tags::secret, n, true);
     auto coef = I.alloc(n * 8);
     HIP_OK(hipMemcpyAsync(coef->p, s.data(), n * 8, hipMemcpyHostToDevice, I.st));
-    I.s_ntt = I.alloc(nall * n * 8);
-    u64 *S = static_cast<u64 *>(I.s_ntt->p);
+    I.ks->s_ntt = I.alloc(nall * n * 8);
+    u64 *S = static_cast<u64 *>(I.ks->s_ntt->p);
     dev::ew_signed_to_rns(S, static_cast<int64_t *>(coef->p), (int)nall, nullptr, I.mods, I.P.logN, I.st);
     dev::ntt_forward(S, (int)nall, 1, 0, nullptr, I.T, I.st);
     // public key
@@ -485,8 +488,8 @@ void Engine::keygen() {
             for (size_t k = 0; k < n; ++k) a[l * n + k] = host::sample_uniform_mod(g, I.P.primes[l]);
     }
     auto e = sample_coeffs(I.seed, host::tags::pk_e, n, false);
-    I.pk = I.alloc(2 * nq * n * 8);
-    u64 *pk = static_cast<u64 *>(I.pk->p);
+    I.ks->pk = I.alloc(2 * nq * n * 8);
+    u64 *pk = static_cast<u64 *>(I.ks->pk->p);
     HIP_OK(hipMemcpyAsync(pk + nq * n, a.data(), nq * n * 8, hipMemcpyHostToDevice, I.st));
     auto ec = I.alloc(n * 8);
     HIP_OK(hipMemcpyAsync(ec->p, e.data(), n * 8, hipMemcpyHostToDevice, I.st));
@@ -500,16 +503,16 @@ void Engine::keygen() {
     // relinearisation key: s' = s^2
     auto s2 = I.alloc(nq * n * 8);
     dev::ew_mul_plain(static_cast<u64 *>(s2->p), S, S, (int)nq, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
-    I.relin = I.alloc((size_t)I.key_digits * 2 * nall * n * 8);
+    I.ks->relin = I.alloc((size_t)I.key_digits * 2 * nall * n * 8);
     // (key material generated by the shared helper below)
     extern void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out);
-    gen_switch_key_impl(I, static_cast<u64 *>(s2->p), 0, static_cast<u64 *>(I.relin->p));
+    gen_switch_key_impl(I, static_cast<u64 *>(s2->p), 0, static_cast<u64 *>(I.ks->relin->p));
     HIP_OK(hipStreamSynchronize(I.st));
 }
 
 void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out) {
     const size_t n = I.n(), nall = I.P.nall(), nq = I.P.nq();
-    const u64 *S = static_cast<const u64 *>(I.s_ntt->p);
+    const u64 *S = static_cast<const u64 *>(I.ks->s_ntt->p);
     const int digits = I.key_digits;
     // P mod q_i
     std::vector<int64_t> Pmod(nq);
@@ -560,16 +563,16 @@ void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out) {
 void Engine::gen_rotation_keys(const std::vector<int> &rot) {
     auto &I = *impl;
     const size_t n = I.n(), nq = I.P.nq(), nall = I.P.nall();
-    if (!I.s_ntt) throw std::runtime_error("gen_rotation_keys: no secret key (call keygen)");
+    if (!I.ks->s_ntt) throw std::runtime_error("gen_rotation_keys: no secret key (call keygen)");
     auto sp = I.alloc(nq * n * 8);
     for (int k : rot) {
         const u64 g = host::galois_for_rotation(I.P.logN, k);
-        if (g == 1 || I.rotkeys.count(g)) continue;
-        dev::ew_permute(static_cast<u64 *>(sp->p), static_cast<const u64 *>(I.s_ntt->p), I.perm(g), (int)nq, 1, dev::Seg{0, 0, 0},
+        if (g == 1 || I.ks->rotkeys.count(g)) continue;
+        dev::ew_permute(static_cast<u64 *>(sp->p), static_cast<const u64 *>(I.ks->s_ntt->p), I.perm(g), (int)nq, 1, dev::Seg{0, 0, 0},
                         I.P.logN, I.st);
         auto key = I.alloc((size_t)I.key_digits * 2 * nall * n * 8);
         gen_switch_key_impl(I, static_cast<u64 *>(sp->p), g, static_cast<u64 *>(key->p));
-        I.rotkeys[g] = key;
+        I.ks->rotkeys[g] = key;
     }
     HIP_OK(hipStreamSynchronize(I.st));
 }
@@ -577,20 +580,20 @@ void Engine::gen_rotation_keys(const std::vector<int> &rot) {
 void Engine::load_secret(const u64 *s) {
     auto &I = *impl;
     const size_t bytes = I.P.nall() * I.n() * 8;
-    I.s_ntt = I.alloc(bytes);
-    HIP_OK(hipMemcpy(I.s_ntt->p, s, bytes, hipMemcpyHostToDevice));
+    I.ks->s_ntt = I.alloc(bytes);
+    HIP_OK(hipMemcpy(I.ks->s_ntt->p, s, bytes, hipMemcpyHostToDevice));
 }
 void Engine::load_public(const u64 *pk) {
     auto &I = *impl;
     const size_t bytes = 2 * I.P.nq() * I.n() * 8;
-    I.pk = I.alloc(bytes);
-    HIP_OK(hipMemcpy(I.pk->p, pk, bytes, hipMemcpyHostToDevice));
+    I.ks->pk = I.alloc(bytes);
+    HIP_OK(hipMemcpy(I.ks->pk->p, pk, bytes, hipMemcpyHostToDevice));
 }
 void Engine::load_relin(const u64 *key) {
     auto &I = *impl;
     const size_t bytes = (size_t)I.key_digits * 2 * I.P.nall() * I.n() * 8;
-    I.relin = I.alloc(bytes);
-    HIP_OK(hipMemcpy(I.relin->p, key, bytes, hipMemcpyHostToDevice));
+    I.ks->relin = I.alloc(bytes);
+    HIP_OK(hipMemcpy(I.ks->relin->p, key, bytes, hipMemcpyHostToDevice));
 }
 void Engine::load_rotation(long k, const u64 *key) {
     auto &I = *impl;
@@ -598,14 +601,14 @@ void Engine::load_rotation(long k, const u64 *key) {
     const u64 g = host::galois_for_rotation(I.P.logN, k);
     auto m = I.alloc(bytes);
     HIP_OK(hipMemcpy(m->p, key, bytes, hipMemcpyHostToDevice));
-    I.rotkeys[g] = m;
+    I.ks->rotkeys[g] = m;
 }
 bool Engine::has_rotation_key(long k) const {
-    return impl->rotkeys.count(host::galois_for_rotation(impl->P.logN, k)) > 0;
+    return impl->ks->rotkeys.count(host::galois_for_rotation(impl->P.logN, k)) > 0;
 }
 size_t Engine::key_bytes() const {
-    size_t b = impl->relin ? impl->relin->bytes : 0;
-    for (auto &kv : impl->rotkeys) b += kv.second->bytes;
+    size_t b = impl->ks->relin ? impl->ks->relin->bytes : 0;
+    for (auto &kv : impl->ks->rotkeys) b += kv.second->bytes;
     return b;
 }
 
@@ -634,7 +637,7 @@ PtPtr Engine::encode_scaled(const std::vector<double> &v, int slots, int level, 
 
 CtPtr Engine::encrypt_pt(const Plaintext &pt) {
     auto &I = *impl;
-    if (!I.pk) throw std::runtime_error("encrypt: no public key");
+    if (!I.ks->pk) throw std::runtime_error("encrypt: no public key");
     const size_t n = I.n(), nq = I.P.nq(), ell = pt.limbs;
     const u64 c = I.enc_counter++;
     std::vector<int64_t> smp(3 * n);
@@ -655,7 +658,7 @@ CtPtr Engine::encrypt_pt(const Plaintext &pt) {
                               I.P.logN, I.st);
     dev::ntt_forward(r, (int)ell, 3, ell * n, nullptr, I.T, I.st);
     auto ct = new_ct(pt.level, pt.slots, pt.scale, ell);
-    const u64 *pk = static_cast<const u64 *>(I.pk->p);
+    const u64 *pk = static_cast<const u64 *>(I.ks->pk->p);
     u64 *c0 = ct->data, *c1 = ct->data + ell * n;
     dev::ew_mul_plain(c0, r, pk, (int)ell, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
     dev::ew_add(c0, c0, r + ell * n, (int)ell, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
@@ -689,12 +692,12 @@ CtPtr Engine::encrypt_ext(const std::vector<double> &v, int slots) {
 std::vector<double> Engine::decrypt(const Ciphertext &ct) {
     auto &I = *impl;
     if (ct.batch != 1) throw std::invalid_argument("decrypt: one ciphertext at a time (use member())");
-    if (!I.s_ntt) throw std::runtime_error("decrypt: no secret key");
+    if (!I.ks->s_ntt) throw std::runtime_error("decrypt: no secret key");
     const size_t n = I.n();
     const int L2 = ct.limbs >= 2 ? 2 : 1;  // m = c0 + c1 s on the first one or two limbs
     auto mm = I.alloc(L2 * n * 8);
     u64 *m = static_cast<u64 *>(mm->p);
-    dev::ew_mul_plain(m, ct.data + ct.limbs * n, static_cast<const u64 *>(I.s_ntt->p), L2, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN,
+    dev::ew_mul_plain(m, ct.data + ct.limbs * n, static_cast<const u64 *>(I.ks->s_ntt->p), L2, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN,
                       I.st);
     dev::ew_add(m, m, ct.data, L2, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
     dev::ntt_inverse(m, L2, 1, 0, nullptr, I.T, I.st);
@@ -827,9 +830,9 @@ CtPtr Engine::plain_sub(const Plaintext &p, const Ciphertext &a) {
 }
 CtPtr Engine::add_const(const Ciphertext &a, double c) {
     auto r = clone(a);
-    const i64 K = host::const_at_scale(c, a.scale);
+    const host::SConst K = host::const_at_scale(c, a.scale);
     const size_t l2 = 2 * a.limbs * n();
-    dev::ew_add_scalar(r->data, r->data, K, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
+    dev::ew_add_scalar(r->data, r->data, K.k, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST, K.sh);
     return r;
 }
 CtPtr Engine::mul_int(const Ciphertext &a, i64 K) {
@@ -845,10 +848,10 @@ CtPtr Engine::mul_const_to(const Ciphertext &a, double c, int target) {
     ctr.constmult += a.batch;
     ctr.rescale += a.batch;
     const size_t nn = n(), ell = I.P.limbs_at(target - 1);
-    const i64 K = host::const_to_target(c, I.P.delta[target], I.P.primes[I.P.L - target + 1], a.scale);
+    const host::SConst K = host::const_to_target(c, I.P.delta[target], I.P.primes[I.P.L - target + 1], a.scale);
     const int segs = 2 * a.batch;
     auto r = new_ct(target, a.slots, I.P.delta[target], ell - 1, a.batch);
-    if (K == 0) {  // rescale(0 * a) = 0
+    if (K.k == 0) {  // rescale(0 * a) = 0
         HIP_OK(hipMemsetAsync(r->data, 0, (size_t)segs * (ell - 1) * nn * 8, ST));
         return r;
     }
@@ -927,7 +930,7 @@ CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vec
     auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
     match_levels(a, b);
     if (a->level >= I.P.L) throw std::runtime_error("mul: no levels left");
-    if (!I.relin) throw std::runtime_error("mul: no relinearisation key");
+    if (!I.ks->relin) throw std::runtime_error("mul: no relinearisation key");
     const int B = a->batch;
     ctr.hmult += B;
     ctr.keyswitch += B;
@@ -940,17 +943,24 @@ CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vec
     if (!xs.empty()) {
         const int target = a->level + 1;
         const u64 qd = I.P.primes[I.P.L - target + 1];
-        std::map<size_t, std::pair<std::vector<const u64 *>, std::vector<int64_t>>> by_limbs;
+        struct Group {
+            std::vector<const u64 *> x;
+            std::vector<int64_t> k;
+            std::vector<uint8_t> sh;
+        };
+        std::map<size_t, Group> by_limbs;
         for (size_t i = 0; i < xs.size(); ++i) {
             if (xs[i]->level > a->level) throw std::invalid_argument("mul_add: summand level too high");
             if (xs[i]->batch != B) throw std::invalid_argument("mul_add: batch size mismatch");
             auto &g = by_limbs[xs[i]->limbs];
-            g.first.push_back(xs[i]->data);
-            g.second.push_back(host::const_to_target(cs[i], I.P.delta[target], qd, xs[i]->scale));
+            const host::SConst K = host::const_to_target(cs[i], I.P.delta[target], qd, xs[i]->scale);
+            g.x.push_back(xs[i]->data);
+            g.k.push_back(K.k);
+            g.sh.push_back((uint8_t)K.sh);
         }
         for (auto &kv : by_limbs)
-            dev::ew_linear_sum(d01, kv.second.first.data(), kv.second.second.data(), (int)kv.second.first.size(),
-                               (int)ell, 2 * B, ell * nn, kv.first * nn, MODS, LOGN, ST, true);
+            dev::ew_linear_sum(d01, kv.second.x.data(), kv.second.k.data(), (int)kv.second.x.size(), (int)ell, 2 * B,
+                               ell * nn, kv.first * nn, MODS, LOGN, ST, true, kv.second.sh.data());
         ctr.constmult += xs.size() * B;
     }
     if (raw) {
@@ -981,8 +991,8 @@ std::vector<CtPtr> Engine::rotate_hoisted(const Ciphertext &a, const std::vector
             outs.push_back(clone(a));
             continue;
         }
-        auto it = I.rotkeys.find(g);
-        if (it == I.rotkeys.end()) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
+        auto it = I.ks->rotkeys.find(g);
+        if (it == I.ks->rotkeys.end()) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
         if (!extm) extm = I.modup(a.data + ln, ell, B, 2 * ln);  // c1 of every member
         ctr.keyswitch += B;
         ctr.rotations += B;
@@ -1021,20 +1031,23 @@ CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std
     for (auto &kv : by_limbs) {
         std::vector<const u64 *> p;
         std::vector<int64_t> k;
+        std::vector<uint8_t> sh;
         for (size_t i : kv.second) {
+            const host::SConst K = host::const_to_target(c[i], I.P.delta[target], (u64)qd, xs[i]->scale);
             p.push_back(xs[i]->data);
-            k.push_back(host::const_to_target(c[i], I.P.delta[target], (u64)qd, xs[i]->scale));
+            k.push_back(K.k);
+            sh.push_back((uint8_t)K.sh);
         }
         // accumulate: first group writes, later groups add
         if (first) {
             dev::ew_linear_sum(t, p.data(), k.data(), (int)p.size(), (int)ell, segs, ell * nn, kv.first * nn, MODS,
-                               LOGN, ST);
+                               LOGN, ST, false, sh.data());
             first = false;
         } else {
             auto sm = I.alloc((size_t)segs * ell * nn * 8);
             u64 *s = static_cast<u64 *>(sm->p);
             dev::ew_linear_sum(s, p.data(), k.data(), (int)p.size(), (int)ell, segs, ell * nn, kv.first * nn, MODS,
-                               LOGN, ST);
+                               LOGN, ST, false, sh.data());
             dev::ew_add(t, t, s, (int)ell, segs, seg3(ell * nn, ell * nn, ell * nn), MODS, LOGN, ST);
         }
     }
@@ -1067,17 +1080,21 @@ std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> 
     for (size_t g0 = 0; g0 < c.size(); g0 += 8) {
         const int G = (int)std::min<size_t>(8, c.size() - g0);
         std::vector<int64_t> K((size_t)G * m);
+        std::vector<uint8_t> sh((size_t)G * m);
         for (int g = 0; g < G; ++g) {
             if (c[g0 + g].size() != m) throw std::invalid_argument("linear_sums_to: coefficient row size");
-            for (size_t i = 0; i < m; ++i)
-                K[(size_t)g * m + i] = host::const_to_target(c[g0 + g][i], I.P.delta[target], qd, xs[i]->scale);
+            for (size_t i = 0; i < m; ++i) {
+                const host::SConst k = host::const_to_target(c[g0 + g][i], I.P.delta[target], qd, xs[i]->scale);
+                K[(size_t)g * m + i] = k.k;
+                sh[(size_t)g * m + i] = (uint8_t)k.sh;
+            }
         }
         auto tm = I.alloc((size_t)G * segs * ell * nn * 8);
         u64 *t = static_cast<u64 *>(tm->p);
         std::vector<u64 *> op(G);
         for (int g = 0; g < G; ++g) op[g] = t + (size_t)g * segs * ell * nn;
         dev::ew_linear_sum_multi(op.data(), G, xp.data(), xseg.data(), K.data(), (int)m, (int)ell, segs, ell * nn,
-                                 MODS, LOGN, ST);
+                                 MODS, LOGN, ST, sh.data());
         if (!rescale) {  // raw sums at the pre-rescale scale, views into one allocation
             for (int g = 0; g < G; ++g) {
                 auto r = std::make_shared<Ciphertext>();
@@ -1114,9 +1131,9 @@ std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> 
 
 CtPtr Engine::trivial_const(double c, int level, int slots, int batch) {
     auto r = zero_like(level, slots, batch);
-    const i64 K = host::const_at_scale(c, impl->P.delta[level]);
+    const host::SConst K = host::const_at_scale(c, impl->P.delta[level]);
     const size_t l2 = 2 * r->limbs * n();
-    dev::ew_add_scalar(r->data, r->data, K, (int)r->limbs, batch, seg3(l2, l2, 0), MODS, LOGN, ST);
+    dev::ew_add_scalar(r->data, r->data, K.k, (int)r->limbs, batch, seg3(l2, l2, 0), MODS, LOGN, ST, K.sh);
     return r;
 }
 CtPtr Engine::zero_like(int level, int slots, int batch) {
@@ -1313,7 +1330,7 @@ void Engine::time_kernel(const std::string &name, size_t ell, int iters, double 
     const size_t nn = n(), K = (size_t)I.P.K, W = ell + K, B = nn * 8;
     const int digits = I.P.digits_at(ell);
     if (ell < 1 || ell > I.P.nq()) throw std::invalid_argument("time_kernel: bad limb count");
-    if (!I.relin) throw std::runtime_error("time_kernel: needs the relinearisation key");
+    if (!I.ks->relin) throw std::runtime_error("time_kernel: needs the relinearisation key");
     // operands with random-looking contents (reduced residues)
     auto dm = I.alloc(3 * ell * nn * 8);
     auto em = I.alloc((size_t)digits * W * nn * 8);
@@ -1329,7 +1346,7 @@ void Engine::time_kernel(const std::string &name, size_t ell, int iters, double 
         str.ext = (size_t)digits * W * nn;
         str.d = ell * nn;
         launch = [&, str] {
-            dev::ks_inner(acc, e, d, static_cast<u64 *>(I.relin->p), (int)ell, (int)K, (int)I.P.nq(), (int)I.P.nall(),
+            dev::ks_inner(acc, e, d, static_cast<u64 *>(I.ks->relin->p), (int)ell, (int)K, (int)I.P.nq(), (int)I.P.nall(),
                           I.P.alpha, digits, nullptr, I.ext(ell), MODS, LOGN, ST, 1, str);
         };
         bytes = (double)((size_t)digits * W * 3 + 2 * W) * B;  // ext + key(b,a) read, 2 accumulators written

@@ -73,7 +73,10 @@ bool is_prime(u64 n) {
 // ---------------------------------------------------------------- params --
 Params make_params(int logN, int L, int scale_bits, int first_bits, int dnum) {
     if (logN < 4 || logN > 17) throw std::invalid_argument("logN out of range [4,17]");
-    if (scale_bits < 20 || scale_bits > 58 || first_bits > 61 || first_bits <= scale_bits)
+    // every prime < 2^60 keeps the 30-bit split sums of the basis conversions
+    // and linear sums exact (16 products of 30-bit halves per 64-bit partial);
+    // scaling primes are the primes nearest 2^scale_bits, so scale_bits <= 59
+    if (scale_bits < 20 || scale_bits > 59 || first_bits > 60 || first_bits <= scale_bits)
         throw std::invalid_argument("unsupported modulus sizes");
     Params P;
     P.logN = logN;
@@ -314,10 +317,17 @@ std::vector<double> decode_coeffs(const u64 *m0, const u64 *m1, size_t n, u64 q0
     return out;
 }
 
-i64 const_to_target(double c, double delta_target, u64 q_dropped, double scale_in) {
-    return std::llround(c * delta_target * (double)q_dropped / scale_in);
+SConst scaled_const(double x) {
+    if (!std::isfinite(x)) throw std::invalid_argument("scaled constant is not finite");
+    const double ax = std::fabs(x);
+    if (ax <= 0x1p62) return SConst{std::llround(x), 0};
+    const int sh = (int)std::ceil(std::log2(ax)) - 62;
+    return SConst{std::llround(std::ldexp(x, -sh)), sh};
 }
-i64 const_at_scale(double c, double scale) { return std::llround(c * scale); }
+SConst const_to_target(double c, double delta_target, u64 q_dropped, double scale_in) {
+    return scaled_const(c * delta_target * (double)q_dropped / scale_in);
+}
+SConst const_at_scale(double c, double scale) { return scaled_const(c * scale); }
 
 // -------------------------------------------------------------- sampling --
 SplitMix64::SplitMix64(u64 seed, u64 tag) : s(seed ^ (tag * 0xD1B54A32D192ED03ULL)) { next(); }

@@ -58,9 +58,18 @@ std::vector<i64> encode_coeffs(const std::vector<double> &v, size_t n, int slots
 std::vector<double> decode_coeffs(const u64 *m0, const u64 *m1, size_t n, u64 q0, u64 q1, int slots,
                                   double scale);
 
-// constants of the scale bookkeeping
-i64 const_to_target(double c, double delta_target, u64 q_dropped, double scale_in);
-i64 const_at_scale(double c, double scale);
+// constants of the scale bookkeeping.  A scaled constant
+// x = c * scale is carried as k * 2^sh: k = llround(x) while |x| <= 2^62,
+// beyond that k = llround(x / 2^sh) with sh = ceil(log2 |x|) - 62 (OpenFHE's
+// large-constant approximation, MAX_BITS_IN_WORD = 62), so 59- and 60-bit
+// scales take constants such as g3's 25614/1024.
+struct SConst {
+    i64 k = 0;
+    int sh = 0;
+};
+SConst scaled_const(double x);
+SConst const_to_target(double c, double delta_target, u64 q_dropped, double scale_in);
+SConst const_at_scale(double c, double scale);
 
 // seeded sampling
 struct SplitMix64 {

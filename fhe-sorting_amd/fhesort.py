@@ -38,7 +38,33 @@ class Params(C.Structure):
 _lib = None
 vp, ip, dp, u64p = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_uint64)
 PP = C.POINTER(C.c_void_p)
-ALLREDUCE_FN = C.CFUNCTYPE(None, C.POINTER(C.c_uint64), C.c_uint64, C.c_void_p)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_uint64), C.c_uint64, C.c_void_p)
+
+
+class _Hook:
+    """ctypes wrapper of a Python all-reduce callback f(dev_ptr, count, user):
+    an exception inside it is recorded and reported as a non-zero return (the
+    C side then aborts the sort); the caller re-raises it after the C call."""
+
+    def __init__(self, f):
+        self.exc = None
+
+        def call(ptr, count, user):
+            try:
+                r = f(ptr, count, user)
+                return 0 if r is None else int(r)
+            except BaseException as e:  # noqa: BLE001 -- must not unwind through C
+                self.exc = e
+                return 1
+        self.fn = ALLREDUCE_FN(call) if f else None
+
+    def ptr(self):
+        return C.cast(self.fn, C.c_void_p) if self.fn else None
+
+    def reraise(self, err):
+        if self.exc is not None:
+            raise self.exc from err
+        raise err
 
 _SIGS = {
     'fhe_last_error': (C.c_char_p, []),
@@ -414,20 +440,22 @@ class Context:
 
     def direct_sort(self, x, N, rots, cfg, mode=0, rank=None, shard=(0, 1), allreduce=None):
         r = np.asarray(rots, dtype=np.int32)
-        cb = ALLREDUCE_FN(allreduce) if allreduce else None
-        self._cb = cb  # keep alive for the duration of the call
-        return self._new(lib().fhe_direct_sort, x.h, rank.h if rank is not None else None, N, _int(r), len(r),
-                         cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1],
-                         C.cast(cb, C.c_void_p) if cb else None, None)
+        hk = _Hook(allreduce)
+        try:
+            return self._new(lib().fhe_direct_sort, x.h, rank.h if rank is not None else None, N, _int(r), len(r),
+                             cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1], hk.ptr(), None)
+        except FheError as e:
+            hk.reraise(e)
 
     def sort_hybrid(self, x, N, rots, cfg, mode=0, rank=None, max_array=256, mask=0, shard=(0, 1), allreduce=None):
         """DirectSort::sort_hybrid (mode 0) or rotationIndexCheckHybrid(rank, x) (mode 1)."""
         r = np.asarray(rots, dtype=np.int32)
-        cb = ALLREDUCE_FN(allreduce) if allreduce else None
-        self._cb = cb
-        return self._new(lib().fhe_sort_hybrid, x.h, rank.h if rank is not None else None, N, _int(r), len(r),
-                         cfg[0], cfg[1], cfg[2], mode, max_array, mask, shard[0], shard[1],
-                         C.cast(cb, C.c_void_p) if cb else None, None)
+        hk = _Hook(allreduce)
+        try:
+            return self._new(lib().fhe_sort_hybrid, x.h, rank.h if rank is not None else None, N, _int(r), len(r),
+                             cfg[0], cfg[1], cfg[2], mode, max_array, mask, shard[0], shard[1], hk.ptr(), None)
+        except FheError as e:
+            hk.reraise(e)
 
     def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0, shard=(0, 1), allreduce=None):
         """mehp24::sortFG (sub 0; x holds N values in N*N slots) or
@@ -436,10 +464,12 @@ class Context:
         ranks and combined by `allreduce` (or RCCL after comm_init)."""
         if shard == (0, 1) and allreduce is None:
             return self._new(lib().fhe_mehp24_sort, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i)
-        cb = ALLREDUCE_FN(allreduce) if allreduce else None
-        self._cb = cb  # keep alive for the duration of the call
-        return self._new(lib().fhe_mehp24_sort_sharded, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i,
-                         shard[0], shard[1], C.cast(cb, C.c_void_p) if cb else None, None)
+        hk = _Hook(allreduce)
+        try:
+            return self._new(lib().fhe_mehp24_sort_sharded, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i,
+                             shard[0], shard[1], hk.ptr(), None)
+        except FheError as e:
+            hk.reraise(e)
 
     def mehp24_indicator(self, x, b, dg, df):
         return self._new(lib().fhe_mehp24_indicator, x.h, b, dg, df)

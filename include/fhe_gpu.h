@@ -170,8 +170,11 @@ int fhe_decompose(int N, const int32_t *rots, int nrot, int rotation, int wrap_n
 /* DirectSort<N>::getSizeParameters (src/sort_algo.h:87-201); returns #rotations */
 int fhe_size_parameters(int N, int *mult_depth, int32_t *rots, int max_rots);
 /* u64 sum of `count` device words over all ranks, in place (RCCL, MPI, ...).
- * Called with the context stream drained; the sum must be complete on return. */
-typedef void (*fhe_allreduce_fn)(uint64_t *dev_data, uint64_t count, void *user);
+ * Called with the context stream drained; the sum must be complete on return.
+ * Returns 0 on success; any other value aborts the sort with FHE_EHIP.  Sums
+ * are exact while world * q_max < 2^64 (world <= 16 at a 60-bit q0): a larger
+ * world is refused with FHE_EINVAL before any work. */
+typedef int (*fhe_allreduce_fn)(uint64_t *dev_data, uint64_t count, void *user);
 /* DirectSort<N>(cc, pk, rots, enc).{sort | constructRank | rotationIndexCheckN}
  * (src/sort_algo.h:752-774 / 368-506 / 658-750); mode 0 sort, 1 rank, 2 index
  * check (then `rank` is the rank ciphertext).  Batches b with b % world == rank

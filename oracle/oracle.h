@@ -72,6 +72,16 @@ inline u64 mul_shoup(u64 a, u64 w, u64 wp, u64 q) {
 }
 u64 signed_to_mod(i64 v, u64 q);
 u64 i128_to_mod(i128 v, u64 q);
+// A scaled constant x = c * scale as k * 2^sh: k = llround(x) while |x| <=
+// 2^62, else sh = ceil(log2 |x|) - 62 and k = llround(x / 2^sh) -- OpenFHE's
+// large-constant approximation (MAX_BITS_IN_WORD = 62), needed at 59/60-bit
+// scales.
+struct ScaledConst {
+    i64 k = 0;
+    int sh = 0;
+    u64 mod(u64 q) const { return i128_to_mod((i128)k * ((i128)1 << sh), q); }
+};
+ScaledConst scaled_const(double x);
 bool is_prime(u64 n);
 
 // ---------------------------------------------------------------- params ----
@@ -197,6 +207,7 @@ class Context {
     CtPtr plain_sub(const Plaintext &p, const Ciphertext &a) const;   // p - a
     CtPtr add_const(const Ciphertext &a, double c) const;
     CtPtr mul_int(const Ciphertext &a, i64 k) const;                 // no rescale
+    CtPtr mul_int(const Ciphertext &a, const ScaledConst &k) const;  // no rescale
     CtPtr mul_const(const Ciphertext &a, double c);                  // -> level+1
     CtPtr mul_const_to(const Ciphertext &a, double c, int target);   // -> target (> a.level)
     CtPtr mul_plain(const Ciphertext &a, const Plaintext &p);        // -> level+1

@@ -33,6 +33,39 @@ void trim(std::vector<double> &a) {
     while (a.size() > 1 && a.back() == 0.0) a.pop_back();
 }
 
+// Levels OpenFHE's EvalChebyshevSeriesPS consumes for a degree-d series: the
+// reference's multDepth tables (src/sort_algo.h:87-201) budget these, and its
+// tests assert the output level (tests/DirectSortTest.cpp:128).  Degrees < 5
+// go through EvalChebyshevSeriesLinear (T_1..T_d, then one constant product);
+// up to 2204 OpenFHE picks (k, m) from a fixed table whose depth bands are the
+// published ones below; above, ComputeDegreesPS's heuristic: minimise
+// k + 2m + 2^(m-1) - 4 over k*(2^m - 1) > d with floor(log2 k) within 1 of
+// floor(log2 sqrt(d/2)); depth ceil(log2 k) + m.  The evaluation itself stays
+// depth-optimal; a series whose optimal depth is below this one is evaluated
+// to the lower output level (its leaves absorb the extra rescale).
+int openfhe_ps_depth(int d) {
+    if (d < 5) return ceil_log2(d) + 1;
+    static const int band_top[] = {5, 13, 27, 59, 119, 247, 495, 1007, 2031, 2204};
+    for (int i = 0; i < 10; ++i)
+        if (d <= band_top[i]) return 3 + i;
+    const double f = std::floor(std::log2(std::sqrt(d / 2.0)));
+    long best = -1;
+    int depth = 0;
+    for (long k = 1; k <= d; ++k) {
+        if (std::fabs(std::floor(std::log2((double)k)) - f) > 1) continue;
+        const int mmax = (int)std::ceil(std::log2((double)d / k) + 1) + 1;
+        for (int m = 1; m <= mmax; ++m)
+            if ((long)d - k * ((1L << m) - 1) < 0) {
+                const long mult = k + 2 * m + (1L << (m - 1)) - 4;
+                if (best < 0 || mult < best) {
+                    best = mult;
+                    depth = ceil_log2(k) + m;
+                }
+            }
+    }
+    return depth;
+}
+
 struct PSPlan {
     int B = 1;      // baby-step count (power of two): leaves use T_0..T_B
     int beta = 1;   // log2(B) + 1 = depth of a leaf
@@ -155,7 +188,7 @@ CtPtr cheb_series_ps(Context &cc, const Ciphertext &x0, const std::vector<double
     PSPlan plan = plan_ps(d);
     PSEval ev(cc, *x, plan);
     ev.build_baby();
-    return ev.eval(std_c, x->level + plan.D);
+    return ev.eval(std_c, x->level + std::max(plan.D, openfhe_ps_depth(d)));
 }
 
 // ====================================================== composite sign =====
@@ -466,11 +499,23 @@ void DirectSort::reduce_partial(CtPtr &acc, int level_hint, int slots) {
 void reduce_partial(Context &cc, const Shard &sh, CtPtr &acc, int slots) {
     if (sh.world <= 1) return;
     if (!sh.allreduce) throw std::runtime_error("sharded run without an allreduce hook");
-    u64 hdr[2] = {acc ? (u64)(acc->level + 1) : 0, acc ? 1ULL : 0ULL};
-    sh.allreduce(hdr, 2);
-    if (hdr[1] == 0) throw std::runtime_error("sharded run: no shard produced a partial");
-    int level = (int)(hdr[0] / hdr[1]) - 1;
+    // residues < q_max summed over `world` ranks must not wrap in u64
+    u64 qmax = 0;
+    for (size_t i = 0; i <= (size_t)cc.P.L; ++i) qmax = std::max(qmax, cc.P.primes[i]);
+    if ((u64)sh.world > ~0ULL / qmax)
+        throw std::invalid_argument("sharded run: world * q_max >= 2^64 would overflow the u64 sum");
+    // header: presence, level + 1, (level + 1)^2, limbs; equal levels on every
+    // present rank iff sum(l)^2 == present * sum(l^2)
+    const u64 l1 = acc ? (u64)(acc->level + 1) : 0;
+    u64 hdr[4] = {acc ? 1ULL : 0ULL, l1, l1 * l1, acc ? (u64)acc->limbs : 0};
+    sh.allreduce(hdr, 4);
+    if (hdr[0] == 0) throw std::runtime_error("sharded run: no shard produced a partial");
+    if ((unsigned __int128)hdr[1] * hdr[1] != (unsigned __int128)hdr[0] * hdr[2] || hdr[1] % hdr[0] ||
+        hdr[3] % hdr[0])
+        throw std::runtime_error("sharded run: ranks' partials differ in level or limb count");
+    int level = (int)(hdr[1] / hdr[0]) - 1;
     if (!acc) acc = cc.zero_like(level, slots);
+    if (acc->limbs != hdr[3] / hdr[0]) throw std::runtime_error("sharded run: partial limb count differs");
     sh.allreduce(acc->c.data(), acc->c.size());
     const size_t n = cc.P.n;
     for (int p = 0; p < 2; ++p)

@@ -239,7 +239,7 @@ void *orc_compose_rotate(void *c, void *a, int N, const int *rots, int nrot, int
     }, (void *)nullptr);
 }
 
-typedef void (*orc_allreduce_fn)(uint64_t *data, uint64_t count, void *user);
+typedef int (*orc_allreduce_fn)(uint64_t *data, uint64_t count, void *user);
 
 // mode: 0 = sort, 1 = constructRank, 2 = rotationIndexCheckN(rank=b)
 void *orc_direct_sort(void *c, void *x, void *rank, int N, const int *rots, int nrot, int n, int dg, int df,
@@ -248,7 +248,9 @@ void *orc_direct_sort(void *c, void *x, void *rank, int N, const int *rots, int 
         DirectSort ds(*CTX, N, std::vector<int>(rots, rots + nrot));
         ds.shard_rank = shard_rank;
         ds.shard_world = shard_world;
-        if (fn) ds.allreduce = [fn, user](uint64_t *d, size_t cnt) { fn(d, (uint64_t)cnt, user); };
+        if (fn) ds.allreduce = [fn, user](uint64_t *d, size_t cnt) {
+            if (fn(d, (uint64_t)cnt, user) != 0) throw std::runtime_error("allreduce hook failed");
+        };
         auto cfg = cfg3(n, dg, df);
         if (mode == 1) return wrap(ds.constructRank(CT(x), SignFunc::CompositeSign, cfg));
         if (mode == 2) return wrap(ds.rotationIndexCheckN(CT(rank), CT(x)));
@@ -279,7 +281,9 @@ void *orc_mehp24_sort_sharded(void *c, void *x, int N, int sub, int n, int dg, i
         Shard sh;
         sh.rank = shard_rank;
         sh.world = shard_world;
-        if (fn) sh.allreduce = [fn, user](uint64_t *d, size_t cnt) { fn(d, (uint64_t)cnt, user); };
+        if (fn) sh.allreduce = [fn, user](uint64_t *d, size_t cnt) {
+            if (fn(d, (uint64_t)cnt, user) != 0) throw std::runtime_error("allreduce hook failed");
+        };
         return wrap(mehp24::sort_large_fg(*CTX, CT(x), N, sub, SignFunc::CompositeSign, cfg, dg_i, df_i, sh));
     }, (void *)nullptr);
 }

@@ -59,6 +59,12 @@ u64 i128_to_mod(i128 v, u64 q) {
     r = (r + 1) % q;
     return r == 0 ? 0 : (u64)(q - r);
 }
+ScaledConst scaled_const(double x) {
+    if (!std::isfinite(x)) throw std::invalid_argument("scaled constant is not finite");
+    if (std::fabs(x) <= 0x1p62) return ScaledConst{std::llround(x), 0};
+    const int sh = (int)std::ceil(std::log2(std::fabs(x))) - 62;
+    return ScaledConst{std::llround(std::ldexp(x, -sh)), sh};
+}
 
 static u64 powmod_plain(u64 a, u64 e, u64 q) {
     u128 r = 1, b = a % q;
@@ -737,21 +743,22 @@ CtPtr Context::plain_sub(const Plaintext &p, const Ciphertext &a) const {
 CtPtr Context::add_const(const Ciphertext &a, double c) const {
     auto r = clone(a);
     const size_t n = P.n;
-    i64 K = std::llround(c * a.scale);
+    const ScaledConst K = scaled_const(c * a.scale);
     for (size_t l = 0; l < a.limbs; ++l) {
-        u64 kv = signed_to_mod(K, P.primes[l]);
+        u64 kv = K.mod(P.primes[l]);
         u64 *x = r->poly(0, n) + l * n;
         for (size_t k = 0; k < n; ++k) x[k] = mod_add(x[k], kv, P.primes[l]);
     }
     return r;
 }
 
-CtPtr Context::mul_int(const Ciphertext &a, i64 K) const {
+CtPtr Context::mul_int(const Ciphertext &a, i64 K) const { return mul_int(a, ScaledConst{K, 0}); }
+CtPtr Context::mul_int(const Ciphertext &a, const ScaledConst &K) const {
     auto r = clone(a);
     const size_t n = P.n;
 #pragma omp parallel for
     for (size_t l = 0; l < a.limbs; ++l) {
-        u64 kv = signed_to_mod(K, P.primes[l]);
+        u64 kv = K.mod(P.primes[l]);
         for (int i = 0; i < 2; ++i) {
             u64 *x = r->poly(i, n) + l * n;
             for (size_t k = 0; k < n; ++k) x[k] = mod_mul(x[k], kv, tab[l].mod);
@@ -766,7 +773,7 @@ CtPtr Context::mul_const_to(const Ciphertext &a, double c, int target) {
     ctr.constmult++;
     auto d = drop_to(a, target - 1);
     const double qd = (double)P.primes[P.L - target + 1];
-    i64 K = std::llround(c * P.delta[target] * qd / a.scale);
+    const ScaledConst K = scaled_const(c * P.delta[target] * qd / a.scale);
     auto m = mul_int(*d, K);
     auto r = rescale(*m);
     r->scale = P.delta[target];
@@ -1031,8 +1038,8 @@ CtPtr Context::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::ve
         std::vector<std::vector<u64>> Kmod(xs.size(), std::vector<u64>(ell));
         for (size_t i = 0; i < xs.size(); ++i) {
             if (xs[i]->level > a->level) throw std::invalid_argument("mul_add: summand level too high");
-            const i64 K = std::llround(cs[i] * P.delta[target] * qd / xs[i]->scale);
-            for (size_t l = 0; l < ell; ++l) Kmod[i][l] = signed_to_mod(K, P.primes[l]);
+            const ScaledConst K = scaled_const(cs[i] * P.delta[target] * qd / xs[i]->scale);
+            for (size_t l = 0; l < ell; ++l) Kmod[i][l] = K.mod(P.primes[l]);
         }
         ctr.constmult += xs.size();
 #pragma omp parallel for
@@ -1113,8 +1120,8 @@ CtPtr Context::linear_sum_to(const std::vector<const Ciphertext *> &xs, const st
     std::vector<std::vector<u64>> Kmod(xs.size(), std::vector<u64>(ell));
     for (size_t i = 0; i < xs.size(); ++i) {
         if (xs[i]->level > target - 1) throw std::invalid_argument("linear_sum_to: input level too high");
-        i64 K = std::llround(c[i] * P.delta[target] * qd / xs[i]->scale);
-        for (size_t l = 0; l < ell; ++l) Kmod[i][l] = signed_to_mod(K, P.primes[l]);
+        const ScaledConst K = scaled_const(c[i] * P.delta[target] * qd / xs[i]->scale);
+        for (size_t l = 0; l < ell; ++l) Kmod[i][l] = K.mod(P.primes[l]);
     }
     ctr.constmult += xs.size();
 #pragma omp parallel for
@@ -1137,9 +1144,9 @@ CtPtr Context::linear_sum_to(const std::vector<const Ciphertext *> &xs, const st
 CtPtr Context::trivial_const(double c, int level, int slots) const {
     const size_t n = P.n, ell = P.limbs_at(level);
     auto r = make_ct(level, slots, P.delta[level], ell, n);
-    i64 K = std::llround(c * P.delta[level]);
+    const ScaledConst K = scaled_const(c * P.delta[level]);
     for (size_t l = 0; l < ell; ++l) {
-        u64 kv = signed_to_mod(K, P.primes[l]);
+        u64 kv = K.mod(P.primes[l]);
         u64 *x = r->poly(0, n) + l * n;
         for (size_t k = 0; k < n; ++k) x[k] = kv;
     }

@@ -109,7 +109,33 @@ def lib():
     return _lib
 
 
-ALLREDUCE_FN = C.CFUNCTYPE(None, C.POINTER(C.c_uint64), C.c_uint64, C.c_void_p)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_uint64), C.c_uint64, C.c_void_p)
+
+
+class _Hook:
+    """ctypes wrapper of a Python all-reduce callback f(dev_ptr, count, user):
+    an exception inside it is recorded and reported as a non-zero return (the
+    C side then aborts the sort); the caller re-raises it after the C call."""
+
+    def __init__(self, f):
+        self.exc = None
+
+        def call(ptr, count, user):
+            try:
+                r = f(ptr, count, user)
+                return 0 if r is None else int(r)
+            except BaseException as e:  # noqa: BLE001 -- must not unwind through C
+                self.exc = e
+                return 1
+        self.fn = ALLREDUCE_FN(call) if f else None
+
+    def ptr(self):
+        return C.cast(self.fn, C.c_void_p) if self.fn else None
+
+    def reraise(self, err):
+        if self.exc is not None:
+            raise self.exc from err
+        raise err
 
 
 def _u64(a):
@@ -316,11 +342,13 @@ class Context:
 
     def direct_sort(self, x, N, rots, cfg, mode=0, rank=None, shard=(0, 1), allreduce=None):
         r = np.asarray(rots, dtype=np.int32)
-        cb = ALLREDUCE_FN(allreduce) if allreduce else None
+        hk = _Hook(allreduce)
         h = lib().orc_direct_sort(self.h, x.h, rank.h if rank is not None else None, N, _int(r), len(r),
-                                  cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1],
-                                  C.cast(cb, C.c_void_p) if cb else None, None)
-        return Ct(self, h)
+                                  cfg[0], cfg[1], cfg[2], mode, shard[0], shard[1], hk.ptr(), None)
+        try:
+            return Ct(self, h)
+        except RuntimeError as e:
+            hk.reraise(e)
 
     def sort_hybrid(self, x, N, rots, cfg, mode=0, rank=None, max_array=256, mask=0):
         """DirectSort::sort_hybrid (mode 0) or rotationIndexCheckHybrid(rank, x) (mode 1)."""
@@ -331,11 +359,13 @@ class Context:
     def mehp24_sort(self, x, N, cfg, dg_i, df_i, sub=0, shard=(0, 1), allreduce=None):
         if shard == (0, 1) and allreduce is None:
             return Ct(self, lib().orc_mehp24_sort(self.h, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i))
-        cb = ALLREDUCE_FN(allreduce) if allreduce else None
-        self._cb = cb
-        return Ct(self, lib().orc_mehp24_sort_sharded(self.h, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i,
-                                                      shard[0], shard[1], C.cast(cb, C.c_void_p) if cb else None,
-                                                      None))
+        hk = _Hook(allreduce)
+        h = lib().orc_mehp24_sort_sharded(self.h, x.h, N, sub, cfg[0], cfg[1], cfg[2], dg_i, df_i,
+                                          shard[0], shard[1], hk.ptr(), None)
+        try:
+            return Ct(self, h)
+        except RuntimeError as e:
+            hk.reraise(e)
 
     def mehp24_indicator(self, a, b, dg, df):
         return Ct(self, lib().orc_mehp24_indicator(self.h, a.h, b, dg, df))

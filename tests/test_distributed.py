@@ -98,3 +98,53 @@ def test_sharded_sort_world2_matches_unsharded(tmp_path, kind):
     x = np.load(tmp_path / 'x.npy')
     y = np.load(tmp_path / 'decrypted.npy')[:len(x)]
     assert np.max(np.abs(y - np.sort(x))) < 0.01
+
+
+# ---- all-reduce protocol checks: overflow bound, header
+# consistency, errors raised inside the hook.  One process; the hook plays the
+# other ranks.
+
+def _one_rank_direct():
+    c = _context('direct')
+    x, ct = _input(c, 'direct')
+    return c, ct
+
+
+def test_world_beyond_u64_bound_is_refused():
+    """17 ranks x a 60-bit q0 could wrap the u64 sum of residues: refused."""
+    c, ct = _one_rank_direct()
+    with pytest.raises(RuntimeError, match='overflow'):
+        _run(c, 'direct', ct, shard=(0, 17), allreduce=lambda p, n, u: None)
+
+
+def test_mismatched_partial_levels_fail_cleanly():
+    """A peer whose partial sits at another level makes every rank fail with
+    the same error before the data all-reduce (no mismatched collectives)."""
+    import ctypes as C
+    c, ct = _one_rank_direct()
+    calls = []
+
+    def peer_at_other_level(ptr, count, _user):
+        arr = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint64)), shape=(count,))
+        calls.append(int(count))
+        if count == 4 and arr[0] == 1:  # header of a present partial: add a peer one level up
+            l1 = int(arr[1]) + 1
+            arr[0] += 1
+            arr[1] += l1
+            arr[2] += l1 * l1
+            arr[3] += int(arr[3]) - 1
+    with pytest.raises(RuntimeError, match='differ in level'):
+        _run(c, 'direct', ct, shard=(0, 2), allreduce=peer_at_other_level)
+    assert calls and all(n == 4 for n in calls), 'the data all-reduce must not start'
+
+
+def test_exception_in_hook_propagates():
+    c, ct = _one_rank_direct()
+
+    class Boom(Exception):
+        pass
+
+    def failing(ptr, count, _user):
+        raise Boom('transport down')
+    with pytest.raises(Boom):
+        _run(c, 'direct', ct, shard=(0, 2), allreduce=failing)

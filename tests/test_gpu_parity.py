@@ -227,6 +227,45 @@ def test_composite_sign_and_compare():
     same(gi, orc.indicator(a, 0.05, 3, 2, 1))
 
 
+@pytest.fixture(scope='module')
+def pair59():
+    """CompareTest's context (tests/CompareTest.cpp:13-22): depth 50, 59-bit
+    scaling primes; ring 2^12 here (the reference's ring is chosen by OpenFHE);
+    dnum 4 keeps digits within the engine's 16 primes."""
+    orc = O.Context(12, 50, 59, 60, 4, seed=12)
+    gpu = F.Context(12, 50, 59, 60, 4, seed=12, keygen=False)
+    gpu.load_keys_from(orc)
+    return orc, gpu
+
+
+def test_composite_sign4_bit_exact(pair59):
+    """compositeSign<4>(3, 3) (src/sign.cpp:62-158: g4 = degree-27 Chebyshev PS,
+    f4 = degree 15), the reference CLI's sign (src/sort.h:76-95) and SignTest's
+    small inputs (tests/SignTest.cpp:82-122, within 0.1)."""
+    orc, gpu = pair59
+    x = np.array([0.02, -0.02, 0.01, -0.01, 0.009, -0.009, 1, -1])
+    ox = orc.encrypt(x, 8)
+    gy = gpu.sign(gpu.from_oracle(ox), 4, 3, 3)
+    same(gy, orc.sign(ox, 4, 3, 3))
+    assert np.max(np.abs(gpu.decrypt(gy) - np.sign(x))) < 0.1
+
+
+def test_compare_vectors_scale59_bit_exact(pair59):
+    """CompareTest's vectors with compositeSign(4, 3, 3) at 59-bit scaling
+    (tests/CompareTest.cpp:43-63): [1,5,3,4] vs [2,4,3,3] -> [0,1,0.5,1] +- 0.1.
+    The 59-bit scale makes f4's and g3's constants exceed 2^62 (mantissa +
+    power-of-two path of host::SConst)."""
+    orc, gpu = pair59
+    a = orc.encrypt([1.0, 5.0, 3.0, 4.0], 4)
+    b = orc.encrypt([2.0, 4.0, 3.0, 3.0], 4)
+    gc = gpu.compare(gpu.from_oracle(a), gpu.from_oracle(b), 4, 3, 3)
+    same(gc, orc.compare(a, b, 4, 3, 3))
+    assert np.max(np.abs(gpu.decrypt(gc) - [0.0, 1.0, 0.5, 1.0])) < 0.1
+    x = orc.encrypt([0.5, -0.3, 0.1, -0.7], 4)
+    gs = gpu.sign(gpu.from_oracle(x), 3, 2, 2)  # g3's 25614/1024 at 2^59 > 2^63
+    same(gs, orc.sign(x, 3, 2, 2))
+
+
 def test_keygen_and_encrypt_parity():
     """GPU key generation + encryption == oracle's for the same seed (bit-exact)."""
     orc = O.Context(12, 6, 40, 60, 3, seed=77)
@@ -257,7 +296,7 @@ def test_direct_sort_bit_exact(N, cfg):
     same(gout, oout)
     y = gpu.decrypt(gout)
     assert np.max(np.abs(y - np.sort(x))) < 0.01
-    assert gout.level <= depth
+    assert gout.level == depth  # EXPECT_EQ(level, multDepth), tests/DirectSortTest.cpp:128
 
 
 def test_batched_ops_match_members(pair):
