@@ -211,6 +211,20 @@ void Sorter::fiveSorter(const CtPtr *x, const CtPtr *cmp, CtPtr *out) {
     for (int i : {0, 1, 3, 4}) s = cc.sub(*s, *out[i]);
     out[2] = s;
 }
+std::vector<CtPtr> Sorter::kSorter(int kk, const std::vector<CtPtr> &x, const std::vector<CtPtr> &cmp) {
+    const size_t nx = kk == 1 ? 2 : (size_t)kk, nc = kk == 1 ? 1 : (size_t)(kk * (kk - 1) / 2);
+    if (kk < 1 || kk > 5 || x.size() != nx || cmp.size() != nc)
+        throw std::invalid_argument("kway sorter: kk in 1..5 with kk (2 for fcnL) inputs and kk(kk-1)/2 comparisons");
+    std::vector<CtPtr> out(kk == 1 ? 1 : (size_t)kk);
+    switch (kk) {
+    case 1: out[0] = fcnL(x[0], x[1], cmp[0]); break;
+    case 2: twoSorter(x[0], x[1], cmp[0], out.data()); break;
+    case 3: threeSorter(x.data(), cmp.data(), out.data()); break;
+    case 4: fourSorter(x.data(), cmp.data(), out.data()); break;
+    default: fiveSorter(x.data(), cmp.data(), out.data()); break;
+    }
+    return out;
+}
 // SortUtils.cpp:424-433
 CtPtr Sorter::slotAssemble(const CtPtr *s, long num, long shift) {
     CtPtr o = s[0];

@@ -41,6 +41,9 @@ class Sorter {
     Sorter(Engine &cc, long numSlots, long k, long M);
     CtPtr sorter(const Ciphertext &x, const SignConfig &cfg);
     int stagesRun = 0;  // stages completed by the last sorter() call
+    // SortUtils::fcnL (kk = 1: returns {fcnL(x0, x1, c0)}) or the kk-sorter,
+    // kk = 2..5 (SortUtils.cpp:5-208), on their own: SortUtilsTest's cases
+    std::vector<CtPtr> kSorter(int kk, const std::vector<CtPtr> &x, const std::vector<CtPtr> &cmp);
 
   private:
     Engine &cc;

@@ -524,6 +524,28 @@ int fhe_kway_sort(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int df, f
     });
 }
 
+int fhe_kway_sorter(fhe_ctx *ctx, int kk, const fhe_ct *const *x, int nx, const fhe_ct *const *cmp, int ncmp,
+                    fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(x);
+        NEED(cmp);
+        NEED(out);
+        std::vector<CtPtr> xv, cv;
+        for (int i = 0; i < nx; ++i) {
+            NEED(x[i]);
+            xv.push_back(x[i]->p);
+        }
+        for (int i = 0; i < ncmp; ++i) {
+            NEED(cmp[i]);
+            cv.push_back(cmp[i]->p);
+        }
+        if (xv.empty()) throw std::invalid_argument("fhe_kway_sorter: no inputs");
+        kwaySort::Sorter s(*ctx->eng, 25, 5, 2);  // the network shape is unused here
+        auto o = s.kSorter(kk, xv, cv);
+        for (size_t i = 0; i < o.size(); ++i) out[i] = wrap(o[i]);
+    });
+}
 int fhe_kway_sort_type(int k, int M, int stage, int *m, int *log_dist, int *slope) {
     return guard([&] {
         NEED(m);
@@ -645,7 +667,7 @@ int fhe_moddown(fhe_ctx *ctx, const uint64_t *in, int ell, uint64_t *out) {
 int fhe_automorph(fhe_ctx *ctx, const uint64_t *in, int limbs, uint64_t g, uint64_t *out) {
     return guard([&] { ctx->eng->automorph_host(in, (size_t)limbs, g, out); });
 }
-int fhe_counters(fhe_ctx *ctx, uint64_t out[6]) {
+int fhe_counters(fhe_ctx *ctx, uint64_t out[7]) {
     return guard([&] {
         const auto &c = ctx->eng->ctr;
         out[0] = c.hmult;
@@ -654,6 +676,7 @@ int fhe_counters(fhe_ctx *ctx, uint64_t out[6]) {
         out[3] = c.rescale;
         out[4] = c.ptmult;
         out[5] = c.constmult;
+        out[6] = c.opbytes;
     });
 }
 int fhe_reset_counters(fhe_ctx *ctx) {

@@ -762,6 +762,13 @@ CtPtr Engine::drop_to(const Ciphertext &a, int level) {
     return r;
 }
 
+// op-level byte model (Counters::opbytes): `limb_units` limbs of n words per ciphertext, times members
+void Engine::count_bytes(double limb_units, int members) { ctr.opbytes += (u64)(limb_units * members * 8.0 * n()); }
+double Engine::ks_units(size_t ell) const {  // 2 digits(l) (l + K): the key read of one key switch
+    const auto &P = impl->P;
+    return 2.0 * P.digits_at(ell) * (double)(ell + P.K);
+}
+
 void Engine::match_levels(CtPtr &a, CtPtr &b) {
     if (a->level < b->level)
         a = level_adjust(*a, b->level);
@@ -776,6 +783,7 @@ CtPtr Engine::add(const Ciphertext &a0, const Ciphertext &b0) {
     const size_t ln = a->limbs * n();
     auto r = new_ct(a->level, a->slots, a->scale, a->limbs, a->batch);
     dev::ew_add(r->data, a->data, b->data, (int)a->limbs, 2 * a->batch, seg3(ln, ln, ln), MODS, LOGN, ST);
+    count_bytes(6.0 * a->limbs, a->batch);
     return r;
 }
 CtPtr Engine::sub(const Ciphertext &a0, const Ciphertext &b0) {
@@ -785,6 +793,7 @@ CtPtr Engine::sub(const Ciphertext &a0, const Ciphertext &b0) {
     const size_t ln = a->limbs * n();
     auto r = new_ct(a->level, a->slots, a->scale, a->limbs, a->batch);
     dev::ew_sub(r->data, a->data, b->data, (int)a->limbs, 2 * a->batch, seg3(ln, ln, ln), MODS, LOGN, ST);
+    count_bytes(6.0 * a->limbs, a->batch);
     return r;
 }
 void Engine::add_inplace(CtPtr &acc, const Ciphertext &b) {
@@ -796,6 +805,7 @@ void Engine::add_inplace(CtPtr &acc, const Ciphertext &b) {
     if (acc->level == b.level && acc.use_count() == 1) {
         const size_t ln = b.limbs * n();
         dev::ew_add(acc->data, acc->data, b.data, (int)b.limbs, 2 * b.batch, seg3(ln, ln, ln), MODS, LOGN, ST);
+        count_bytes(6.0 * b.limbs, b.batch);
         return;
     }
     acc = add(*acc, b);
@@ -804,6 +814,7 @@ CtPtr Engine::negate(const Ciphertext &a) {
     const size_t ln = a.limbs * n();
     auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
     dev::ew_neg(r->data, a.data, (int)a.limbs, 2 * a.batch, seg3(ln, ln, 0), MODS, LOGN, ST);
+    count_bytes(4.0 * a.limbs, a.batch);
     return r;
 }
 // plaintext ops touch c0 of every member: segments 0, 2, 4, ... (stride 2 limbs n)
@@ -812,6 +823,7 @@ CtPtr Engine::add_plain(const Ciphertext &a, const Plaintext &p) {
     auto r = clone(a);
     const size_t l2 = 2 * a.limbs * n();
     dev::ew_add(r->data, r->data, p.data, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
+    count_bytes(5.0 * a.limbs, a.batch);
     return r;
 }
 CtPtr Engine::sub_plain(const Ciphertext &a, const Plaintext &p) {
@@ -819,6 +831,7 @@ CtPtr Engine::sub_plain(const Ciphertext &a, const Plaintext &p) {
     auto r = clone(a);
     const size_t l2 = 2 * a.limbs * n();
     dev::ew_sub(r->data, r->data, p.data, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
+    count_bytes(5.0 * a.limbs, a.batch);
     return r;
 }
 CtPtr Engine::plain_sub(const Plaintext &p, const Ciphertext &a) {
@@ -833,12 +846,14 @@ CtPtr Engine::add_const(const Ciphertext &a, double c) {
     const host::SConst K = host::const_at_scale(c, a.scale);
     const size_t l2 = 2 * a.limbs * n();
     dev::ew_add_scalar(r->data, r->data, K.k, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST, K.sh);
+    count_bytes(4.0 * a.limbs, a.batch);
     return r;
 }
 CtPtr Engine::mul_int(const Ciphertext &a, i64 K) {
     const size_t ln = a.limbs * n();
     auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
     dev::ew_mul_scalar(r->data, a.data, K, (int)a.limbs, 2 * a.batch, seg3(ln, ln, 0), MODS, LOGN, ST);
+    count_bytes(4.0 * a.limbs, a.batch);
     return r;
 }
 CtPtr Engine::mul_const_to(const Ciphertext &a, double c, int target) {
@@ -848,6 +863,7 @@ CtPtr Engine::mul_const_to(const Ciphertext &a, double c, int target) {
     ctr.constmult += a.batch;
     ctr.rescale += a.batch;
     const size_t nn = n(), ell = I.P.limbs_at(target - 1);
+    count_bytes(4.0 * ell, a.batch);
     const host::SConst K = host::const_to_target(c, I.P.delta[target], I.P.primes[I.P.L - target + 1], a.scale);
     const int segs = 2 * a.batch;
     auto r = new_ct(target, a.slots, I.P.delta[target], ell - 1, a.batch);
@@ -868,6 +884,7 @@ CtPtr Engine::rescale(const Ciphertext &a) {
     auto &I = *impl;
     if (a.level >= I.P.L) throw std::runtime_error("rescale: no levels left");
     ctr.rescale += a.batch;
+    count_bytes(4.0 * a.limbs, a.batch);
     auto r = new_ct(a.level + 1, a.slots, a.scale / (double)I.P.primes[a.limbs - 1], a.limbs - 1, a.batch);
     I.rescale(a.data, a.limbs, a.limbs * n(), 2 * a.batch, r->data);
     return r;
@@ -879,6 +896,7 @@ CtPtr Engine::mul_plain(const Ciphertext &a, const Plaintext &p) {
     ctr.ptmult += a.batch;
     ctr.rescale += a.batch;
     const size_t nn = n(), ell = a.limbs;
+    count_bytes(5.0 * ell, a.batch);
     const int segs = 2 * a.batch;
     auto tm = I.alloc((size_t)segs * ell * nn * 8);
     u64 *t = static_cast<u64 *>(tm->p);
@@ -903,6 +921,8 @@ CtPtr Engine::mul_plain_sum(const std::vector<const Ciphertext *> &a, const std:
     ctr.ptmult += a.size() * B;
     ctr.rescale += B;
     const size_t nn = n(), ell = a[0]->limbs;
+    count_bytes(2.0 * ell * a.size() + 2.0 * ell, B);  // the ct reads and the output
+    count_bytes((double)ell * a.size(), 1);            // the shared plaintexts
     std::vector<const u64 *> cp, pp;
     for (size_t i = 0; i < a.size(); ++i) {
         cp.push_back(a[i]->data);
@@ -936,6 +956,7 @@ CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vec
     ctr.keyswitch += B;
     ctr.rescale += B;
     const size_t nn = n(), ell = a->limbs;
+    count_bytes(6.0 * ell + ks_units(ell) + 2.0 * ell * xs.size(), B);
     auto d01m = I.alloc((size_t)B * 2 * ell * nn * 8), d2m = I.alloc((size_t)B * ell * nn * 8);
     u64 *d01 = static_cast<u64 *>(d01m->p), *d2 = static_cast<u64 *>(d2m->p);
     dev::ew_tensor(d01, d2, a->data, b->data, (int)ell, B, 2 * ell * nn, b->batch == 1 ? 0 : 2 * ell * nn, MODS,
@@ -996,6 +1017,7 @@ std::vector<CtPtr> Engine::rotate_hoisted(const Ciphertext &a, const std::vector
         if (!extm) extm = I.modup(a.data + ln, ell, B, 2 * ln);  // c1 of every member
         ctr.keyswitch += B;
         ctr.rotations += B;
+        count_bytes(4.0 * ell + ks_units(ell), B);
         const uint32_t *pm = I.perm(g);
         auto c0m = I.alloc((size_t)B * ln * 8);
         u64 *c0p = static_cast<u64 *>(c0m->p);
@@ -1017,6 +1039,7 @@ CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std
     const int segs = 2 * B;
     const size_t nn = n(), ell = I.P.limbs_at(target - 1);
     const double qd = (double)I.P.primes[I.P.L - target + 1];
+    count_bytes(2.0 * ell * xs.size() + 2.0 * ell, B);
     auto tm = I.alloc((size_t)segs * ell * nn * 8);
     u64 *t = static_cast<u64 *>(tm->p);
     // group inputs by their limb count (segment stride) so each launch has one xseg
@@ -1068,6 +1091,7 @@ std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> 
     const int B = xs[0]->batch, segs = 2 * B;
     const size_t nn = n(), ell = I.P.limbs_at(target - 1), m = xs.size();
     const u64 qd = I.P.primes[I.P.L - target + 1];
+    count_bytes((2.0 * ell * m + 2.0 * ell) * c.size(), B);  // op model: one linear sum per output
     std::vector<const u64 *> xp(m);
     std::vector<size_t> xseg(m);
     for (size_t i = 0; i < m; ++i) {

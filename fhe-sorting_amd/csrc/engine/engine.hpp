@@ -55,7 +55,13 @@ using PtPtr = std::shared_ptr<Plaintext>;
 
 struct Counters {
     u64 hmult = 0, keyswitch = 0, rotations = 0, rescale = 0, ptmult = 0, constmult = 0;
+    // op-level algorithmic HBM bytes (SURVEY §8(d)'s per-op formulas, each op
+    // at its own level; B = 8n per limb): HMult (4l + 2 digits(l)(l+K) + 2l) B,
+    // rotation (2l + 2 digits(l)(l+K) + 2l) B, ct x pt 5l B, ct x const 4l B,
+    // add 6l B, linear sum of m terms (2l m + 2l) B -- per ciphertext
+    u64 opbytes = 0;
     Counters &operator+=(const Counters &o) {
+        opbytes += o.opbytes;
         hmult += o.hmult;
         keyswitch += o.keyswitch;
         rotations += o.rotations;
@@ -121,6 +127,8 @@ class Engine {
     CtPtr mul_const_to(const Ciphertext &a, double c, int target);
     CtPtr level_adjust(const Ciphertext &a, int target);
     void match_levels(CtPtr &a, CtPtr &b);
+    void count_bytes(double limb_units, int members);
+    double ks_units(size_t ell) const;
     CtPtr mul_plain(const Ciphertext &a, const Plaintext &p);
     // sum_i a_i * p_i with one rescale (masked sums of src/sort_algo.h:341-346, 573-577)
     CtPtr mul_plain_sum(const std::vector<const Ciphertext *> &a, const std::vector<const Plaintext *> &p);

@@ -129,6 +129,7 @@ _SIGS = {
                                           C.c_int, C.c_int, vp, vp, PP]),
     'fhe_mehp24_indicator': (C.c_int, [vp, vp, C.c_double, C.c_int, C.c_int, PP]),
     'fhe_kway_sort': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_kway_sorter': (C.c_int, [vp, C.c_int, PP, C.c_int, PP, C.c_int, PP]),
     'fhe_kway_sort_type': (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                      C.POINTER(C.c_int)]),
     'fhe_kway_stage_count': (C.c_int, [C.c_int, C.c_int]),
@@ -479,6 +480,15 @@ class Context:
         cfg = (3, dg, df)."""
         return self._new(lib().fhe_kway_sort, x.h, k, M, cfg[1], cfg[2])
 
+    def kway_sorter(self, kk, xs, cmps):
+        """SortUtils::fcnL (kk = 1) or the kk-sorter (kk = 2..5): ascending outputs."""
+        xa = (C.c_void_p * len(xs))(*[x.h for x in xs])
+        ca = (C.c_void_p * len(cmps))(*[c.h for c in cmps])
+        nout = 1 if kk == 1 else kk
+        outs = (C.c_void_p * nout)()
+        _chk(lib().fhe_kway_sorter(self.h, kk, xa, len(xs), ca, len(cmps), outs))
+        return [Ct(self, outs[i]) for i in range(nout)]
+
     # multi-GPU -----------------------------------------------------------
     @staticmethod
     def comm_unique_id():
@@ -536,9 +546,10 @@ class Context:
         return out
 
     def counters(self):
-        out = np.zeros(6, dtype=np.uint64)
+        out = np.zeros(7, dtype=np.uint64)
         _chk(lib().fhe_counters(self.h, _u64(out)))
-        return dict(zip(['hmult', 'keyswitch', 'rotations', 'rescale', 'ptmult', 'constmult'], map(int, out)))
+        return dict(zip(['hmult', 'keyswitch', 'rotations', 'rescale', 'ptmult', 'constmult', 'opbytes'],
+                        map(int, out)))
 
     def reset_counters(self):
         _chk(lib().fhe_reset_counters(self.h))

@@ -249,6 +249,13 @@ int fhe_mehp24_indicator(fhe_ctx *ctx, const fhe_ct *x, double b, int dg, int df
  * src/k-way/EvalUtils.cpp:59-86) the context must still hold the levels,
  * otherwise FHE_EDEPTH.  Rotation keys: fhe_kway_rotation_indices(N). */
 int fhe_kway_sort(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int df, fhe_ct **out);
+/* SortUtils::fcnL (kk = 1: out[0] = fcnL(x0, x1, cmp0) = cmp*(x0-x1)+x1,
+ * src/k-way/SortUtils.cpp:5-16) or the kk-sorter for kk = 2..5
+ * (SortUtils.cpp:32-208): nx = kk inputs, ncmp = kk(kk-1)/2 comparison
+ * ciphertexts in SortUtilsTest's order (a>b, a>c, ..., tests/k-way/
+ * SortUtilsTest.cpp:68-260); out receives kk ciphertexts in ascending order. */
+int fhe_kway_sorter(fhe_ctx *ctx, int kk, const fhe_ct *const *x, int nx, const fhe_ct *const *cmp, int ncmp,
+                    fhe_ct **out);
 /* kwaySort::sortType(k, M, stage) -> (m, logDist, slope) (src/k-way/Masking.cpp:25-48) */
 int fhe_kway_sort_type(int k, int M, int stage, int *m, int *log_dist, int *slope);
 /* number of stages, M + M(M-1)/2 * ceil(k/2) (src/k-way/Sorter.cpp:290); < 0 on error */
@@ -275,8 +282,10 @@ int fhe_ntt(fhe_ctx *ctx, uint64_t *host, int prime_index, int limbs, int invers
 int fhe_modup(fhe_ctx *ctx, const uint64_t *d, int ell, uint64_t *ext);
 int fhe_moddown(fhe_ctx *ctx, const uint64_t *in, int ell, uint64_t *out);
 int fhe_automorph(fhe_ctx *ctx, const uint64_t *in, int limbs, uint64_t galois, uint64_t *out);
-/* op counters: hmult, keyswitch, rotations, rescale, ptmult, constmult */
-int fhe_counters(fhe_ctx *ctx, uint64_t out[6]);
+/* op counters: hmult, keyswitch, rotations, rescale, ptmult, constmult, and
+ * the op-level algorithmic HBM bytes of SURVEY §8(d) (HMult, rotation, ct x pt,
+ * ct x const, add, linear sum formulas, each op at its own level) */
+int fhe_counters(fhe_ctx *ctx, uint64_t out[7]);
 int fhe_reset_counters(fhe_ctx *ctx);
 int fhe_sync(fhe_ctx *ctx);
 /* opaque hipStream_t of the context (for event timing by the caller) */

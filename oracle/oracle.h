@@ -362,6 +362,7 @@ void gen_indices(long ns, long k, long M, long m, long log_dist, long slope, std
                  std::vector<int> &pos);
 std::vector<int> rotation_indices(int N);
 CtPtr sort(Context &cc, const Ciphertext &x, int k, int M, const SignConfig &cfg);
+std::vector<CtPtr> sorter(Context &cc, int kk, const std::vector<CtPtr> &x, const std::vector<CtPtr> &s);
 }  // namespace kway
 
 }  // namespace oracle

@@ -421,6 +421,26 @@ void direct_sort_size_parameters(int N, int &multDepth, std::vector<int> &rotati
                      834, 835, 864, 865, 866, 867, 896, 897, 898, 899, 928, 929, 930, 931, 960, 961, 962, 963, 992,
                      993, 994, 995, 1024, 2048, 4096, 8192, 16384, 32768};
         break;
+    case 2048:
+        multDepth = 52;
+        rotations = {
+            1, 2, 4, 8, 16, 31, 32, 64, 115, 128, 179, 211, 227, 241, 242, 243, 256, 307, 339, 355, 369, 370,
+            371, 403, 419, 433, 434, 435, 451, 465, 466, 467, 481, 482, 483, 496, 497, 498, 499, 512, 563, 595,
+            611, 625, 626, 627, 659, 675, 689, 690, 691, 707, 721, 722, 723, 737, 738, 739, 752, 753, 754, 755,
+            787, 803, 817, 818, 819, 835, 849, 850, 851, 865, 866, 867, 880, 881, 882, 883, 899, 913, 914, 915,
+            929, 930, 931, 944, 945, 946, 947, 961, 962, 963, 976, 977, 978, 979, 992, 993, 994, 995, 1008,
+            1009, 1010, 1011, 1024, 1075, 1107, 1123, 1137, 1138, 1139, 1171, 1187, 1201, 1202, 1203, 1219,
+            1233, 1234, 1235, 1249, 1250, 1251, 1264, 1265, 1266, 1267, 1299, 1315, 1329, 1330, 1331, 1347,
+            1361, 1362, 1363, 1377, 1378, 1379, 1392, 1393, 1394, 1395, 1411, 1425, 1426, 1427, 1441, 1442,
+            1443, 1456, 1457, 1458, 1459, 1473, 1474, 1475, 1488, 1489, 1490, 1491, 1504, 1505, 1506, 1507,
+            1520, 1521, 1522, 1523, 1555, 1571, 1585, 1586, 1587, 1603, 1617, 1618, 1619, 1633, 1634, 1635,
+            1648, 1649, 1650, 1651, 1667, 1681, 1682, 1683, 1697, 1698, 1699, 1712, 1713, 1714, 1715, 1729,
+            1730, 1731, 1744, 1745, 1746, 1747, 1760, 1761, 1762, 1763, 1776, 1777, 1778, 1779, 1795, 1809,
+            1810, 1811, 1825, 1826, 1827, 1840, 1841, 1842, 1843, 1857, 1858, 1859, 1872, 1873, 1874, 1875,
+            1888, 1889, 1890, 1891, 1904, 1905, 1906, 1907, 1921, 1922, 1923, 1937, 1938, 1939, 1953, 1954,
+            1955, 1968, 1969, 1970, 1971, 1985, 1986, 1987, 2000, 2001, 2002, 2003, 2016, 2017, 2018, 2019,
+            2032, 2033, 2034, 2035, 2048, 4096, 8192, 16384, 32768};
+        break;
     default: throw std::invalid_argument("direct_sort_size_parameters: unsupported N");
     }
 }

@@ -308,6 +308,17 @@ void *orc_kway_sort(void *c, void *x, int k, int M, int dg, int df) {
     return guard([&]() -> void * { return wrap(kway::sort(*CTX, CT(x), k, M, cfg3(3, dg, df))); },
                  (void *)nullptr);
 }
+// kk = 1: fcnL(x0, x1, s0); kk = 2..5: the kk-sorter; outs[] receives 1 or kk handles
+int orc_kway_sorter(void *c, int kk, void **x, int nx, void **s, int ns, void **outs) {
+    return guard([&]() -> int {
+        std::vector<CtPtr> xv, sv;
+        for (int i = 0; i < nx; ++i) xv.push_back(CTX->clone(CT(x[i])));
+        for (int i = 0; i < ns; ++i) sv.push_back(CTX->clone(CT(s[i])));
+        auto o = kway::sorter(*CTX, kk, xv, sv);
+        for (size_t i = 0; i < o.size(); ++i) outs[i] = wrap(o[i]);
+        return 0;
+    }, -1);
+}
 int orc_kway_sort_type(int k, int M, int stage, int *out3) {
     return guard([&]() {
         if (k < 2 || M < 1 || stage < 0 || stage >= kway::stage_count(k, M)) throw std::invalid_argument("stage");

@@ -353,6 +353,26 @@ struct Net {
 
 }  // namespace
 
+// SortUtils::fcnL (kk = 1: out[0] = fcnL(x0, x1, s0)) and the 2/3/4/5-sorters
+// (SortUtils.cpp:5-208) on their own, for SortUtilsTest's known answers
+std::vector<CtPtr> sorter(Context &cc, int kk, const std::vector<CtPtr> &x, const std::vector<CtPtr> &s) {
+    const size_t nx = kk == 1 ? 2 : (size_t)kk, ns = kk == 1 ? 1 : (size_t)(kk * (kk - 1) / 2);
+    if (kk < 1 || kk > 5 || x.size() != nx || s.size() != ns) throw std::invalid_argument("k-way sorter: bad arity");
+    Net net{cc, (long)x[0]->slots, 5, 2, SignConfig{}, {}, {}, {}, {}};
+    std::vector<CtPtr> out(kk == 1 ? 1 : (size_t)kk);
+    if (kk == 1)
+        out[0] = net.fcn(x[0], x[1], s[0]);
+    else if (kk == 2)
+        net.sort2(x[0], x[1], s[0], out[0], out[1]);
+    else if (kk == 3)
+        net.sort3(x.data(), s.data(), out.data());
+    else if (kk == 4)
+        net.sort4(x.data(), s.data(), out.data());
+    else
+        net.sort5(x.data(), s.data(), out.data());
+    return out;
+}
+
 CtPtr sort(Context &cc, const Ciphertext &x, int k, int M, const SignConfig &cfg) {
     if (k != 2 && k != 3 && k != 5) throw std::invalid_argument("k-way: only k = 2, 3, 5 are supported");
     if (M < 1 || pw(k, M) > x.slots) throw std::invalid_argument("k-way: k^M exceeds the slots");

@@ -28,6 +28,7 @@ def lib():
             build()
         L = C.CDLL(LIB_PATH)
         vp, ip, dp, u64p = C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_uint64)
+        PP = C.POINTER(C.c_void_p)
         sig = {
             'orc_last_error': (C.c_char_p, []),
             'orc_ctx_new': (vp, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]),
@@ -84,6 +85,7 @@ def lib():
             'orc_mehp24_indicator': (vp, [vp, vp, C.c_double, C.c_int, C.c_int]),
             'orc_mehp24_rotation_indices': (C.c_int, [C.c_int, C.c_int, ip, C.c_int]),
             'orc_kway_sort': (vp, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int]),
+            'orc_kway_sorter': (C.c_int, [vp, C.c_int, PP, C.c_int, PP, C.c_int, PP]),
             'orc_kway_sort_type': (C.c_int, [C.c_int, C.c_int, C.c_int, ip]),
             'orc_kway_gen_indices': (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip]),
             'orc_kway_rotate_distance': (C.c_int, [C.c_int, C.c_int, C.c_int]),
@@ -373,6 +375,16 @@ class Context:
     def kway_sort(self, x, k, M, cfg):
         """k-way network; cfg = (n, dg, df) with n = 3"""
         return Ct(self, lib().orc_kway_sort(self.h, x.h, k, M, cfg[1], cfg[2]))
+
+    def kway_sorter(self, kk, xs, cmps):
+        """SortUtils::fcnL (kk = 1) or the kk-sorter (kk = 2..5): ascending outputs."""
+        xa = (C.c_void_p * len(xs))(*[x.h for x in xs])
+        ca = (C.c_void_p * len(cmps))(*[c.h for c in cmps])
+        nout = 1 if kk == 1 else kk
+        outs = (C.c_void_p * nout)()
+        if lib().orc_kway_sorter(self.h, kk, xa, len(xs), ca, len(cmps), outs) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return [Ct(self, outs[i]) for i in range(nout)]
 
     # kernel level -----------------------------------------------------
     def ntt(self, prime_index, data, inverse=False):

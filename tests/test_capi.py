@@ -48,7 +48,7 @@ def test_binding_loads_without_gpu():
     F.lib()  # binds every signature; no HIP call issued
 
 
-@pytest.mark.parametrize('N', [4, 8, 16, 32, 64, 128, 256, 512, 1024])
+@pytest.mark.parametrize('N', [4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048])
 def test_size_parameters_match_oracle(N):
     assert F.size_parameters(N) == O.size_parameters(N)
 

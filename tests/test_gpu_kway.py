@@ -62,3 +62,22 @@ def test_kway_too_shallow_is_edepth():
     with pytest.raises(F.FheError) as e:
         gpu.kway_sort(ct, 2, 2, (3, 2, 2))
     assert e.value.code == 3  # FHE_EDEPTH
+
+
+@pytest.mark.parametrize('kk', [1, 2, 3, 4, 5])
+def test_sortutils_sorters_bit_exact(kk):
+    """fcnL and the 2/3/4/5-sorters (src/k-way/SortUtils.cpp:5-208) on the GPU
+    == the oracle word for word, and SortUtilsTest's known answers within 0.1
+    (tests/k-way/SortUtilsTest.cpp:68-260; depth 50, 59-bit scaling)."""
+    from test_kway import SORTUTILS_KATS
+    _, xs, cs, expected = SORTUTILS_KATS[kk - 1]
+    orc = O.Context(12, 50, 59, 60, 4, seed=16)
+    gpu = F.Context(12, 50, 59, 60, 4, seed=16, keygen=False)
+    gpu.load_keys_from(orc)
+    ox = [orc.encrypt(np.array(v, dtype=float), 16) for v in xs]
+    oc = [orc.encrypt(np.array(v, dtype=float), 16) for v in cs]
+    oo = orc.kway_sorter(kk, ox, oc)
+    go = gpu.kway_sorter(kk, [gpu.from_oracle(c) for c in ox], [gpu.from_oracle(c) for c in oc])
+    for g, o, e in zip(go, oo, expected):
+        assert np.array_equal(g.data(), o.data())
+        assert np.max(np.abs(gpu.decrypt(g)[:len(e)] - e)) < 0.1

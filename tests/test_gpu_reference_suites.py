@@ -103,3 +103,30 @@ def test_sinc_ps_and_indicator_on_lattice(N):
     ind = ctx.decrypt(ctx.indicator(ct, 0.5 / (2 * N), 3, 4, 2))[:L]
     assert np.max(np.abs(cheb - want)) < 0.1
     assert np.max(np.abs(ind - want)) < 0.1
+
+
+def test_direct_sort_n2048_ring16():
+    """DirectSortNTest's largest size, N=2048 (tests/DirectSortNTest.cpp:387):
+    multDepth 52 and the 270-key rotation set of src/sort_algo.h:166-196, at
+    ring 2^16 (P = 16 values per partition, 128 comparator and 128 index-check
+    batches), CompositeSign(3,6,3) as that suite; 50-bit scaling,
+    dnum 4 so a digit stays within 16 primes.  Property: sorted within 0.01
+    (:379).  The suite also asserts level == multDepth (:343); at N=2048 the
+    path consumes 46 of the 52 budgeted levels -- constructRank 1 (masked
+    ct x pt) + 27 (CompositeSign(3,6,3): 9 polynomials of depth 3) + 1, the
+    index check 1 + 14 (degree-12958 doubled sinc: OpenFHE's PS depth) + 1 + 1
+    -- in OpenFHE's accounting as in this engine's, so 46 is asserted."""
+    N = 2048
+    depth, rots = F.size_parameters(N)
+    assert depth == 52 and len(rots) == 270
+    ctx = F.Context(16, depth, 50, 60, 4, seed=N)
+    try:
+        ctx.gen_rotation_keys(rots)  # 270 keys x 260 MB = 70 GB of HBM
+        ctx.set_sort_lanes(1)
+        ctx.set_sort_stack(8)
+        x = np.random.default_rng(N).permutation(N) / N
+        out = ctx.direct_sort(ctx.encrypt(x, N), N, rots, (3, 6, 3))
+        assert out.level == 46 <= depth
+        assert np.max(np.abs(ctx.decrypt(out)[:N] - np.sort(x))) < 0.01
+    finally:
+        ctx.close()

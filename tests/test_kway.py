@@ -94,3 +94,38 @@ def test_oracle_network_needs_levels():
     ct = ctx.encrypt(np.array([0.5, 0.25, 0.75, 0.0]), 4)
     with pytest.raises(RuntimeError, match='no levels left'):
         ctx.kway_sort(ct, 2, 2, (3, 2, 2))
+
+
+# ---- SortUtilsTest known answers (tests/k-way/SortUtilsTest.cpp:68-260):
+# fcnL and the 2/3/4/5-sorters on plain-value inputs and given comparison
+# bits, at the suite's depth 50 / 59-bit scaling (ring 2^12; dnum 4), within 0.1.
+SORTUTILS_KATS = [
+    # (kk, inputs, comparisons, expected outputs ascending)
+    (1, [[2, 4, 6, 8], [1, 5, 3, 7]], [[1, 0, 1, 1]], [[2, 5, 6, 8]]),
+    (2, [[5, 2, 8, 1], [3, 6, 4, 7]], [[1, 0, 1, 0]], [[3, 2, 4, 1], [5, 6, 8, 7]]),
+    (3, [[5, 9, 3, 7], [2, 4, 8, 1], [6, 1, 4, 5]],
+     [[1, 1, 0, 1], [0, 1, 0, 1], [0, 1, 1, 0]],
+     [[2, 1, 3, 1], [5, 4, 4, 5], [6, 9, 8, 7]]),
+    (4, [[9, 7, 5], [6, 4, 8], [3, 8, 2], [7, 2, 6]],
+     [[1, 1, 0], [1, 0, 1], [1, 1, 0], [1, 0, 1], [0, 1, 1], [0, 1, 0]],
+     [[3, 2, 2], [6, 4, 5], [7, 7, 6], [9, 8, 8]]),
+    (5, [[9, 7, 5], [6, 4, 8], [3, 8, 2], [7, 2, 6], [5, 6, 4]],
+     [[1, 1, 0], [1, 0, 1], [1, 1, 0], [1, 1, 1], [1, 0, 1], [0, 1, 1], [1, 0, 1], [0, 1, 0], [0, 1, 0],
+      [1, 0, 1]],
+     [[3, 2, 2], [5, 4, 4], [6, 6, 5], [7, 7, 6], [9, 8, 8]]),
+]
+
+
+@pytest.fixture(scope='module')
+def sortutils_ctx():
+    return O.Context(12, 50, 59, 60, 4, seed=16)
+
+
+@pytest.mark.parametrize('kat', SORTUTILS_KATS, ids=['fcnL', 'twoSorter', 'threeSorter', 'fourSorter', 'fiveSorter'])
+def test_sortutils_known_answers(sortutils_ctx, kat):
+    c = sortutils_ctx
+    kk, xs, cs, expected = kat
+    enc = lambda v: c.encrypt(np.array(v, dtype=float), 16)
+    outs = c.kway_sorter(kk, [enc(v) for v in xs], [enc(v) for v in cs])
+    for o, e in zip(outs, expected):
+        assert np.max(np.abs(c.decrypt(o)[:len(e)] - e)) < 0.1
