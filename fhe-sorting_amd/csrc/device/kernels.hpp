@@ -80,6 +80,7 @@ struct NttFuse {
     int64_t scalar = 0;  // rescale: multiply the input by scalar * 2^scalar_sh first (0 = none)
     int scalar_sh = 0;
     bool raw = false;    // inverse: skip the n^-1 scaling of the last pass
+    int lsegb = 0, segs = 0;  // shuffle row passes: log2 segments per block, segment count (set at launch)
 };
 // inverse NTT reading the input from `src` (segment z, limb l at src + z*seg_src + l*n), writing dst
 void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int segs, size_t seg, const int *pmap,
@@ -88,6 +89,9 @@ void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int s
 void ntt_forward_rescale(u64 *tmp, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
 // HMult tail: out = (x + d * c2 - NTT(corr)) * c1 (corr is overwritten by the first pass only)
 void ntt_forward_multail(u64 *corr, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
+// one row pass (forward: the second pass; inverse: the first) alone, for kernel timing
+void ntt_row_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st,
+                  bool forward);
 // forward NTT of `count` limbs scattered in each of `segs` segments: limb y
 // of segment z sits at data + z * seg + smap[y] * n and belongs to prime
 // pmap[y] (ModUp: every digit of every member at once)

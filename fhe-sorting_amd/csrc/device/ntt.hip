@@ -16,6 +16,7 @@
 // low bits first) and folds n^-1 into the final store.
 #include <hip/hip_ext.h>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
@@ -86,6 +87,158 @@ __device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0,
     return x >= q ? x - q : x;
 }
 
+// ---------------------------------------------------------------------------
+// Register-only 256-point row passes (PB = 8, 16 lanes x 16 coefficients).
+//
+// A coefficient's 8-bit in-row index is split into 4 lane bits and 4 register
+// bits; a butterfly stage needs its bit among the register bits.  Instead of
+// re-dealing the whole transform through LDS, a stage whose bit sits in a lane
+// bit swaps that lane bit with a register bit whose stage is done: lanes t and
+// t ^ 2^m exchange half of their registers with DPP moves (no LDS, no
+// barrier).  The schedules below need 5 such swaps per pass, all against
+// register bit 3 (slots j and j + 8), and start and end in the layout
+//   idx = lane_index(t) + 16 * r      (lane bits = index bits 0..3),
+// so loads and stores are fully coalesced: the 16 lanes of a transform cover
+// one 128-B line per instruction.
+struct RowLayout {
+    int lane[4];  // index bit held by lane bit m
+    int reg[4];   // index bit held by register bit p
+};
+struct RowSwap {
+    int m, p;  // swap lane bit m with register bit p before the stage (m < 0: none)
+};
+// GS inverse: stages take index bits 0, 1, ..., 7
+__device__ constexpr RowSwap inv_swap(int s) {
+    return s <= 3 ? RowSwap{s, 3} : s == 7 ? RowSwap{0, 3} : RowSwap{-1, 0};
+}
+// CT forward: stages take index bits 7, 6, ..., 0; stage 8 is the final
+// fix-up swap (no butterfly) back to lane bits = index bits 0..3
+__device__ constexpr RowSwap fwd_swap(int s) {
+    return s < 4 ? RowSwap{-1, 0} : s < 8 ? RowSwap{7 - s, 3} : RowSwap{3, 3};
+}
+template <bool FWD>
+__device__ constexpr RowLayout row_layout(int s) {  // layout in effect during stage s (after its swap)
+    RowLayout L{{0, 1, 2, 3}, {4, 5, 6, 7}};
+    for (int k = 0; k <= s; ++k) {
+        const RowSwap w = FWD ? fwd_swap(k) : inv_swap(k);
+        if (w.m >= 0) {
+            const int t = L.lane[w.m];
+            L.lane[w.m] = L.reg[w.p];
+            L.reg[w.p] = t;
+        }
+    }
+    return L;
+}
+__device__ __forceinline__ int lane_index(const RowLayout &L, int t) {
+    int v = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) v |= ((t >> m) & 1) << L.lane[m];
+    return v;
+}
+__device__ constexpr int reg_index(const RowLayout &L, int r) {
+    int v = 0;
+    for (int p = 0; p < 4; ++p) v |= ((r >> p) & 1) << L.reg[p];
+    return v;
+}
+// value of lane t ^ 2^m within the 16-lane row (DPP, VALU only)
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
+    int x = (int)v;
+    if (M == 0) x = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);        // quad_perm [1,0,3,2]
+    else if (M == 1) x = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    else if (M == 2) {                                                               // ^7 then ^3
+        x = __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);               // row_half_mirror
+        x = __builtin_amdgcn_update_dpp(0, x, 0x1B, 0xF, 0xF, false);                // quad_perm [3,2,1,0]
+    } else x = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);            // row_ror:8
+    return (uint32_t)x;
+}
+template <int M>
+__device__ __forceinline__ u64 xor_lane(u64 v) {
+    return (u64)xor_lane32<M>((uint32_t)v) | ((u64)xor_lane32<M>((uint32_t)(v >> 32)) << 32);
+}
+// swap lane bit M with register bit P for the pair (x[j], x[j + 2^P]), bit P of j clear:
+// afterwards x[j] holds the element whose (new) register bit P is 0
+template <int M, int P>
+__device__ __forceinline__ void swap_pair(u64 &lo, u64 &hi, int t) {
+    const u64 r0 = xor_lane<M>(lo), r1 = xor_lane<M>(hi);
+    const bool up = (t >> M) & 1;
+    const u64 nlo = up ? r1 : lo, nhi = up ? hi : r0;
+    lo = nlo;
+    hi = nhi;
+}
+template <int P>
+__device__ __forceinline__ void swap_regs(u64 *x, int t, int m) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (j & (1 << P)) continue;
+        switch (m) {
+        case 0: swap_pair<0, P>(x[j], x[j + (1 << P)], t); break;
+        case 1: swap_pair<1, P>(x[j], x[j + (1 << P)], t); break;
+        case 2: swap_pair<2, P>(x[j], x[j + (1 << P)], t); break;
+        default: swap_pair<3, P>(x[j], x[j + (1 << P)], t); break;
+        }
+    }
+}
+// the register bit holding index bit b in layout L
+__device__ constexpr int reg_of(const RowLayout &L, int b) {
+    int p = -1;
+    for (int k = 0; k < 4; ++k)
+        if (L.reg[k] == b) p = k;
+    return p;
+}
+template <bool FWD, int S>
+__device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulonglong2 *tw, size_t n, int S0,
+                                          u64 q2, u64 nq) {
+    constexpr RowSwap w = FWD ? fwd_swap(S) : inv_swap(S);
+    if (w.m >= 0) swap_regs<w.p>(x, t, w.m);
+    if (S >= 8) return;  // the forward pass's final fix-up swap
+    constexpr RowLayout L = row_layout<FWD>(S);
+    constexpr int b = FWD ? 7 - S : S;  // index bit of this stage
+    constexpr int P = reg_of(L, b);
+    const int li = lane_index(L, t);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (j & (1 << P)) continue;
+        const int idx0 = li + reg_index(L, j);
+        if (FWD) {
+            const size_t i = (row << S) + (size_t)(idx0 >> (8 - S));
+            ct_bfly(x[j], x[j + (1 << P)], tw[((size_t)1 << (S0 + S)) + i], q2, nq);
+        } else {
+            const size_t i = (row * 256 + (size_t)idx0) >> (S + 1);
+            gs_bfly(x[j], x[j + (1 << P)], tw[(n >> (S + 1)) + i], q2, nq);
+        }
+    }
+}
+template <bool FWD>
+__device__ __forceinline__ void row_pass_shfl(u64 *x, int t, size_t row, const ulonglong2 *tw, size_t n, int S0,
+                                              u64 q2, u64 nq) {
+    row_stage<FWD, 0>(x, t, row, tw, n, S0, q2, nq);
+    row_stage<FWD, 1>(x, t, row, tw, n, S0, q2, nq);
+    row_stage<FWD, 2>(x, t, row, tw, n, S0, q2, nq);
+    row_stage<FWD, 3>(x, t, row, tw, n, S0, q2, nq);
+    row_stage<FWD, 4>(x, t, row, tw, n, S0, q2, nq);
+    row_stage<FWD, 5>(x, t, row, tw, n, S0, q2, nq);
+    row_stage<FWD, 6>(x, t, row, tw, n, S0, q2, nq);
+    row_stage<FWD, 7>(x, t, row, tw, n, S0, q2, nq);
+    if (FWD) row_stage<FWD, 8>(x, t, row, tw, n, S0, q2, nq);
+}
+// in-row index of lane t's register r after a pass (both passes end in this layout)
+template <bool FWD>
+__device__ __forceinline__ int row_final_index(int t, int r) {
+    constexpr RowLayout L = row_layout<FWD>(FWD ? 8 : 7);
+    return lane_index(L, t) + reg_index(L, r);
+}
+// FHE_NTT_ROW_SHFL bit mask (A/B timing): 1 inverse row pass, 2 forward row
+// pass use the register-only DPP passes; 4 adds a waves-per-EU hint.  0 keeps
+// both on the LDS-exchange passes.
+int &row_shfl_enabled() {
+    static int v = [] {
+        const char *e = std::getenv("FHE_NTT_ROW_SHFL");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
 // Fused forward modes (MODE): 0 plain; 1 column pass loads the centred lift
 // of one coefficient-form limb (`last`, prime lastp) instead of `data`
 // (rescale: the lifted limb is never materialised per prime); 2 row pass
@@ -96,16 +249,19 @@ enum { NTT_PLAIN = 0, NTT_LIFT = 1, NTT_RESCALE = 2, NTT_MULTAIL = 3 };
 
 // COLS: the transform index is a column `col`, element idx sits at idx * 2^k2 + col.
 // ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
-template <int PB, int EB, bool COLS, int MODE>
-__global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
-                                                  NttTables Tb, NttFuse F) {
+// SH (row passes with PB = 8 only): register-only stages with DPP lane swaps
+// (row_pass_shfl) instead of the two LDS exchanges.
+template <int PB, int EB, bool COLS, int MODE, bool SH>
+__device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
+                                             const NttTables &Tb, const NttFuse &F) {
+    static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
     constexpr int E = 1 << EB;          // coefficients per lane
     constexpr int RB = PB - EB;         // bits of round 2
     constexpr int T = 1 << RB;          // lanes per transform
     constexpr int NB = NTB / T;         // transforms per block
     constexpr int G = E >> RB;          // round-2 groups per lane
     constexpr int LEN = 1 << PB;
-    __shared__ u64 tile[lds_words<PB, NB, COLS>()];
+    __shared__ u64 tile[SH ? 1 : lds_words<PB, NB, COLS>()];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
@@ -114,10 +270,6 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
     // L2), y = block within the limb, z = limb
     const int limb = blockIdx.z;
     const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (size_t)blockIdx.x * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
-    const u64 q = Tb.mods[p].q, q2 = 2 * q, nq = (u64)0 - q;
-    const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
-
     int t, tr;  // lane within its transform, transform within the block
     if (COLS) {
         tr = threadIdx.x % NB;
@@ -126,8 +278,15 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         tr = threadIdx.x / T;
         t = threadIdx.x % T;
     }
-    const size_t tid_global = (size_t)blockIdx.y * NB + tr;  // column or row index
-    const bool valid = tid_global < ((size_t)1 << (logN - PB));  // small rings: partial block
+    // SH: the block's transforms are one row of 2^F.lsegb segments (x 16 >> lsegb
+    // rows), so the per-row twiddles are loaded once per block and shared in L1
+    const int zseg = SH ? (int)blockIdx.x * (1 << F.lsegb) + (tr & ((1 << F.lsegb) - 1)) : (int)blockIdx.x;
+    const size_t tid_global = SH ? (size_t)blockIdx.y * (NB >> F.lsegb) + (tr >> F.lsegb)
+                                 : (size_t)blockIdx.y * NB + tr;  // column or row index
+    const bool valid = tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs);
+    u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
+    const u64 q = Tb.mods[p].q, q2 = 2 * q, nq = (u64)0 - q;
+    const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
     const int S0 = COLS ? 0 : logN - PB;                      // global stage of local stage 0
 
     u64 x[E];
@@ -138,7 +297,7 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         const Mod ml = Tb.mods[F.lastp];
         const u64 ql = ml.q, qh = ql >> 1;
         const u64 kl = F.scalar ? smod64(F.scalar, F.scalar_sh, ml) : 0;  // K mod q_last (scaled rescale)
-        const u64 *src = F.last + (size_t)blockIdx.x * F.seg_last;
+        const u64 *src = F.last + (size_t)zseg * F.seg_last;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int idx = t + T * r;
@@ -165,10 +324,48 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         const size_t lo = (size_t)limb * n + tid_global * LEN;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
-            const int idx = t + T * r;
-            ex[r] = valid ? F.x[(size_t)blockIdx.x * F.seg_x + lo + idx] : 0;
-            if (EPI_D) ed[EPI_D ? r : 0] = valid ? F.d[(size_t)blockIdx.x * F.seg_d + lo + idx] : 0;
+            const int idx = SH ? row_final_index<true>(t, r) : t + T * r;  // where the pass leaves element r
+            ex[r] = valid ? F.x[(size_t)zseg * F.seg_x + lo + idx] : 0;
+            if (EPI_D) ed[EPI_D ? r : 0] = valid ? F.d[(size_t)zseg * F.seg_d + lo + idx] : 0;
         }
+    }
+    // per-limb epilogue constants (fused row-pass modes)
+    const bool EPI = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL);
+    const Mod mp = Tb.mods[p];
+    const u64 c1 = EPI ? F.c1[limb] : 0, c1s = EPI ? F.c1s[limb] : 0;
+    const u64 c2 = MODE == NTT_MULTAIL ? F.c2[limb] : 0, c2s = MODE == NTT_MULTAIL ? F.c2s[limb] : 0;
+    // scaled rescale: out = (K x - v) q_last^-1 = x (K q_last^-1) - v q_last^-1
+    const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, F.scalar_sh, mp), c1, c1s, q) : 0;
+    // row-pass store of transform value v (lazy, [0, 4q)) for element r at in-row index idx
+    auto store_row = [&](int r, int idx, u64 v) {
+        const size_t z = (size_t)zseg, lo = (size_t)limb * n + tid_global * LEN;
+        // lazy epilogues: v in [0, 4q), every intermediate < 2^64, one final
+        // conditional subtraction (Shoup products of the fold are in [0, 2q))
+        if (MODE == NTT_RESCALE) {
+            const u64 xin = ex[EPI_X ? r : 0];
+            u64 o;
+            if (F.scalar) {  // (K x - v) q_last^-1 = x kq - v c1: [0, q) + 2q - [0, 2q)
+                o = mul_barrett(xin, kq, mp) + q2 - shoup_fold(v, c1, c1s, nq);
+                o = o >= q2 ? o - q2 : o;
+            } else {  // (x - v) q_last^-1
+                o = shoup_fold(xin + 2 * q2 - v, c1, c1s, nq);
+            }
+            F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
+        } else if (MODE == NTT_MULTAIL) {  // (acc + d c2 - v) c1, acc + d c2 + 4q - v < 7q
+            const u64 acc = ex[EPI_X ? r : 0], dd = ed[EPI_D ? r : 0];
+            const u64 tt = acc + shoup_fold(dd, c2, c2s, nq) + 2 * q2 - v;
+            const u64 o = shoup_fold(tt, c1, c1s, nq);
+            F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
+        } else {
+            a[tid_global * LEN + idx] = canon4(v, q, q2);
+        }
+    };
+    if constexpr (SH) {
+        row_pass_shfl<true>(x, t, tid_global, tw, n, S0, q2, nq);
+        if (!valid) return;
+#pragma unroll
+        for (int r = 0; r < E; ++r) store_row(r, row_final_index<true>(t, r), x[r]);
+        return;
     }
     // ---- round 1: local stages 0..EB-1
 #pragma unroll
@@ -242,43 +439,13 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int r = 0; r < T; ++r)  // fused epilogues take the lazy [0, 4q) value
-                tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] =
-                    MODE == NTT_PLAIN ? canon4(x[g * T + r], q, q2) : x[g * T + r];
+                tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] = x[g * T + r];
         __syncthreads();
-        const size_t z = blockIdx.x, lo = (size_t)limb * n + tid_global * LEN;
-        const Mod mp = Tb.mods[p];
-        // per-limb epilogue constants, read once (the output stores may alias them
-        // as far as the compiler knows, so in the loop they were re-read per element)
-        const bool EPI = MODE == NTT_RESCALE || MODE == NTT_MULTAIL;
-        const u64 c1 = EPI ? F.c1[limb] : 0, c1s = EPI ? F.c1s[limb] : 0;
-        const u64 c2 = MODE == NTT_MULTAIL ? F.c2[limb] : 0, c2s = MODE == NTT_MULTAIL ? F.c2s[limb] : 0;
-        // scaled rescale: out = (K x - v) q_last^-1 = x (K q_last^-1) - v q_last^-1
-        const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, F.scalar_sh, mp), c1, c1s, q) : 0;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int idx = t + T * r;
             const u64 v = tile[lds_at<PB, NB, COLS>(tr, idx)];
-            if (!valid) continue;
-            // lazy epilogues: v in [0, 4q), every intermediate < 2^64, one final
-            // conditional subtraction (Shoup products of the fold are in [0, 2q))
-            if (MODE == NTT_RESCALE) {
-                const u64 xin = ex[EPI_X ? r : 0];
-                u64 o;
-                if (F.scalar) {  // (K x - v) q_last^-1 = x kq - v c1: [0, q) + 2q - [0, 2q)
-                    o = mul_barrett(xin, kq, mp) + q2 - shoup_fold(v, c1, c1s, nq);
-                    o = o >= q2 ? o - q2 : o;
-                } else {  // (x - v) q_last^-1
-                    o = shoup_fold(xin + 2 * q2 - v, c1, c1s, nq);
-                }
-                F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
-            } else if (MODE == NTT_MULTAIL) {  // (acc + d c2 - v) c1, acc + d c2 + 4q - v < 7q
-                const u64 acc = ex[EPI_X ? r : 0], dd = ed[EPI_D ? r : 0];
-                const u64 tt = acc + shoup_fold(dd, c2, c2s, nq) + 2 * q2 - v;
-                const u64 o = shoup_fold(tt, c1, c1s, nq);
-                F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
-            } else {
-                a[tid_global * LEN + idx] = v;
-            }
+            if (valid) store_row(r, idx, v);
         }
     }
 }
@@ -288,16 +455,17 @@ __global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const in
 // COLS covers sg in [logN - PB, logN) and multiplies by n^-1 on the way out.
 // F.src (optional): read the input from there instead (out-of-place first
 // pass; segment z, limb l at F.src + z * F.seg_src + l * n)
-template <int PB, int EB, bool COLS>
-__global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
-                                                  NttTables Tb, NttFuse F) {
+template <int PB, int EB, bool COLS, bool SH>
+__device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
+                                             const NttTables &Tb, const NttFuse &F) {
+    static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
     constexpr int E = 1 << EB;
     constexpr int RB = PB - EB;
     constexpr int T = 1 << RB;
     constexpr int NB = NTB / T;
     constexpr int G = E >> RB;
     constexpr int LEN = 1 << PB;
-    __shared__ u64 tile[lds_words<PB, NB, COLS>()];
+    __shared__ u64 tile[SH ? 1 : lds_words<PB, NB, COLS>()];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
@@ -306,10 +474,6 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
     // L2), y = block within the limb, z = limb
     const int limb = blockIdx.z;
     const int p = pmap ? pmap[limb] : limb;
-    u64 *a = data + (size_t)blockIdx.x * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
-    const u64 q = Tb.mods[p].q, q2 = 2 * q, nq = (u64)0 - q;
-    const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
-
     int t, tr;
     if (COLS) {
         tr = threadIdx.x % NB;
@@ -318,12 +482,26 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
         tr = threadIdx.x / T;
         t = threadIdx.x % T;
     }
-    const size_t tid_global = (size_t)blockIdx.y * NB + tr;
-    const bool valid = tid_global < ((size_t)1 << (logN - PB));
+    // SH: one row of 2^F.lsegb segments per block (shared per-row twiddles)
+    const int zseg = SH ? (int)blockIdx.x * (1 << F.lsegb) + (tr & ((1 << F.lsegb) - 1)) : (int)blockIdx.x;
+    const size_t tid_global = SH ? (size_t)blockIdx.y * (NB >> F.lsegb) + (tr >> F.lsegb) : (size_t)blockIdx.y * NB + tr;
+    const bool valid = tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs);
+    u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
+    const u64 q = Tb.mods[p].q, q2 = 2 * q, nq = (u64)0 - q;
+    const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
     const int SG0 = COLS ? logN - PB : 0;  // global GS stage of local stage 0
 
-    const u64 *ain = F.src ? F.src + (size_t)blockIdx.x * F.seg_src + (size_t)limb * n : a;
+    const u64 *ain = F.src ? F.src + (size_t)zseg * F.seg_src + (size_t)limb * n : a;
     u64 x[E];
+    if constexpr (SH) {  // coalesced load (idx = t + 16 r), register-only stages, coalesced store
+#pragma unroll
+        for (int r = 0; r < E; ++r) x[r] = valid ? ain[tid_global * LEN + t + T * r] : 0;
+        row_pass_shfl<false>(x, t, tid_global, tw, n, 0, q2, nq);
+        if (!valid) return;
+#pragma unroll
+        for (int r = 0; r < E; ++r) a[tid_global * LEN + row_final_index<false>(t, r)] = x[r];
+        return;
+    }
     // ---- load, layout L2 (low bits within a lane group).  The ROWS pass's
     // per-lane runs of T consecutive words are read 16 B at a time (L1 serves
     // the rest of each line; routing them through LDS measured slower).
@@ -398,18 +576,66 @@ __global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const in
     }
 }
 
+template <int PB, int EB, bool COLS, int MODE>
+__global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
+                                                  NttTables Tb, NttFuse F) {
+    ntt_fwd_body<PB, EB, COLS, MODE, false>(data, seg, pmap, smap, logN, Tb, F);
+}
+template <int PB, int EB, bool COLS>
+__global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
+                                                  NttTables Tb, NttFuse F) {
+    ntt_inv_body<PB, EB, COLS, false>(data, seg, pmap, smap, logN, Tb, F);
+}
+// register-only row passes (PB = 8): OCC = requested waves per SIMD (0: compiler's choice)
+template <int MODE, int OCC>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, 8))) void k_ntt_fwd_row(
+    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
+    ntt_fwd_body<8, 4, false, MODE, true>(data, seg, pmap, smap, logN, Tb, F);
+}
+template <int OCC>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, 8))) void k_ntt_inv_row(
+    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
+    ntt_inv_body<8, 4, false, true>(data, seg, pmap, smap, logN, Tb, F);
+}
+
 template <int PB, int EB, bool COLS, bool FWD, int MODE>
 void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap, const NttTables &T,
                  const NttFuse &F, hipStream_t st) {
     constexpr int NB = NTB >> (PB - EB);
+    constexpr bool CAN_SH = !COLS && PB == 8 && EB == 4;
+    const int mode = row_shfl_enabled();
+    const bool sh = CAN_SH && (mode & (FWD ? 2 : 1)) != 0;
     const int count = 1 << (T.logN - PB);  // columns (COLS) or rows (ROWS)
-    const dim3 grid((unsigned)segs, (unsigned)((count + NB - 1) / NB), (unsigned)limbs);
+    dim3 grid((unsigned)segs, (unsigned)((count + NB - 1) / NB), (unsigned)limbs);
+    NttFuse Fs = F;
+    if (sh) {  // 2^lsegb segments of one row per block (lsegb <= 4: 16 transforms per block)
+        Fs.lsegb = 0;
+        while (Fs.lsegb < 4 && (2 << Fs.lsegb) <= segs) ++Fs.lsegb;
+        Fs.segs = segs;
+        const int rows_pb = NB >> Fs.lsegb;
+        grid = dim3((unsigned)((segs + (1 << Fs.lsegb) - 1) >> Fs.lsegb), (unsigned)((count + rows_pb - 1) / rows_pb),
+                    (unsigned)limbs);
+    }
     LaunchClock *clk = launch_clock();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const int slot = clk ? clk->events(e0, e1) : -1;
-    if (FWD)
+    const int occ = (mode & 4) ? 2 : 1;
+    constexpr int FWD_OCC = MODE == NTT_MULTAIL ? 4 : MODE == NTT_RESCALE ? 5 : 6;
+    if (FWD && sh && occ == 2)
+        hipExtLaunchKernelGGL((k_ntt_fwd_row<MODE, FWD_OCC>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
+                              T, Fs);
+    else if (FWD && sh)
+        hipExtLaunchKernelGGL((k_ntt_fwd_row<MODE, 0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
+                              T, Fs);
+    else if (FWD)
         hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
                               T.logN, T, F);
+    else if (sh && occ == 2)
+        hipExtLaunchKernelGGL((k_ntt_inv_row<5>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T,
+                              Fs);
+    else if (sh)
+        hipExtLaunchKernelGGL((k_ntt_inv_row<0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T,
+                              Fs);
     else
         hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
                               T.logN, T, F);
@@ -417,7 +643,8 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
         // same spelling as the demangled symbol rocprofv3 prints, plus the caller tag
         static const std::string base = std::string(FWD ? "k_ntt_fwd<" : "k_ntt_inv<") + std::to_string(PB) + ", " +
                                         std::to_string(EB) + (COLS ? ", true" : ", false") +
-                                        (FWD ? ", " + std::to_string(MODE) : std::string()) + ">";
+                                        (FWD ? ", " + std::to_string(MODE) : std::string()) +
+                                        (sh ? ", true>" : ">");
         static std::map<const char *, std::string> names;
         static std::mutex mu;
         const char *ph = launch_phase();
@@ -487,6 +714,17 @@ void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int s
     NttFuse G;
     G.raw = raw;
     dispatch<true, false, NTT_PLAIN>(k1, dst, limbs, segs, seg, pmap, nullptr, T, G, st);
+}
+
+void ntt_row_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st,
+                  bool forward) {  // one row pass alone (kernel timing)
+    if (limbs <= 0 || segs <= 0) return;
+    const int k2 = T.logN - (T.logN + 1) / 2;
+    const NttFuse F;
+    if (forward)
+        dispatch<false, true, NTT_PLAIN>(k2, data, limbs, segs, seg, pmap, nullptr, T, F, st);
+    else
+        dispatch<false, false, NTT_PLAIN>(k2, data, limbs, segs, seg, pmap, nullptr, T, F, st);
 }
 
 void ntt_forward_mapped(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,

@@ -1377,6 +1377,24 @@ void Engine::time_kernel(const std::string &name, size_t ell, int iters, double 
     } else if (name == "ntt_fwd") {
         launch = [&] { dev::ntt_forward(e, (int)W, digits, W * nn, I.ext(ell), I.T, ST); };
         bytes = 2.0 * 2.0 * (double)(W * digits) * B;  // two passes, each reads + writes every limb
+    } else if (name == "ntt_inv_row32" || name == "ntt_fwd_row32") {  // 32 ciphertext members of ell limbs
+        const bool fwd = name == "ntt_fwd_row32";
+        auto bm = I.alloc((size_t)32 * ell * nn * 8);
+        u64 *buf = static_cast<u64 *>(bm->p);
+        HIP_OK(hipMemsetAsync(buf, 0x33, (size_t)32 * ell * nn * 8, ST));
+        dev::ew_reduce(buf, (int)ell, 32, ell * nn, MODS, LOGN, ST);
+        em = bm;  // keep alive
+        launch = [&, buf, fwd] { dev::ntt_row_pass(buf, (int)ell, 32, ell * nn, nullptr, I.T, ST, fwd); };
+        bytes = 2.0 * 32.0 * (double)ell * B;
+    } else if (name == "ntt_inv" || name == "ntt_fwd_row" || name == "ntt_inv_row") {
+        const bool row = name != "ntt_inv", fwd = name == "ntt_fwd_row";
+        launch = [&, row, fwd] {
+            if (row)
+                dev::ntt_row_pass(e, (int)W, digits, W * nn, I.ext(ell), I.T, ST, fwd);
+            else
+                dev::ntt_inverse(e, (int)W, digits, W * nn, I.ext(ell), I.T, ST);
+        };
+        bytes = (row ? 2.0 : 4.0) * (double)(W * digits) * B;
     } else if (name == "modup_convert") {
         launch = [&] {
             dev::modup_convert(e, d, (int)ell, (int)K, I.P.alpha, digits, 1, ell * nn, (size_t)digits * W * nn,

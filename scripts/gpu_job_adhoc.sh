@@ -1,7 +1,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -k "sortutils or n2048 or digest or sign4 or scale59" > gpurun_out/tests_r2c.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/tests_r2c.log; exit 1; }
-tail -15 gpurun_out/tests_r2c.log
-timeout -k 10 600 python bench.py --no-cpu-baseline --clock-json gpurun_out/clock_r2c.json > gpurun_out/bench_r2c.json 2> gpurun_out/bench_r2c.err || { echo "bench failed"; tail -5 gpurun_out/bench_r2c.err; exit 1; }
-cat gpurun_out/bench_r2c.json
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > gpurun_out/tests_adhoc.log 2>&1 || { echo "tests failed"; tail -40 gpurun_out/tests_adhoc.log; exit 1; }
+tail -1 gpurun_out/tests_adhoc.log
+for V in 0 1 3 5 0 1; do
+FHE_NTT_ROW_SHFL=$V timeout -k 10 300 python bench.py --no-cpu-baseline --steps 4 > gpurun_out/bench_v$V.json 2>gpurun_out/bench_v$V.err || { echo "bench $V failed"; tail -5 gpurun_out/bench_v$V.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/bench_v$V.json'));r=d['roofline'];print('V$V', d['ms_per_step'], r['kernel'], r['frac'], {k:(v['avg_us'],v['GBps']) for k,v in list(r['kernels'].items())[:8]})"
+done
