@@ -33,6 +33,7 @@
 // ============================================================================
 #pragma once
 
+#include <complex>
 #include <cstdint>
 #include <cstddef>
 #include <functional>
@@ -189,6 +190,8 @@ class Context {
     // encode / decode
     Plaintext encode(const std::vector<double> &v, int slots, int level) const;
     Plaintext encode_scaled(const std::vector<double> &v, int slots, int level, double scale) const;
+    // complex slot values (bootstrapping's linear-transform diagonals)
+    Plaintext encode_complex(const std::vector<std::complex<double>> &v, int slots, int level, double scale) const;
     std::vector<double> decode(const std::vector<u64> &m0_coeff_limb0, int slots, double scale) const;
     std::vector<double> decode_real(const std::vector<double> &m_coeff, int slots, double scale) const;
     CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
@@ -221,6 +224,14 @@ class Context {
     CtPtr square(const Ciphertext &a);
     CtPtr rotate(const Ciphertext &a, long k);                       // keyed rotation
     std::vector<CtPtr> rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks);
+    // keyed automorphisms X -> X^g sharing one ModUp (rotations are g = 5^k)
+    std::vector<CtPtr> apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs);
+    CtPtr conjugate(const Ciphertext &a);                            // g = 2n - 1
+    void gen_galois_keys(const std::vector<u64> &gs);
+    // ModRaise (bootstrapping): a ciphertext at the last level (one limb, q0)
+    // re-read over every Q prime by the centred lift of its coefficients; the
+    // result decrypts to t = c0 + c1 s over Z (= m + q0 I) at level 0, scale Delta_0
+    CtPtr mod_raise(const Ciphertext &a);
     CtPtr rescale(const Ciphertext &a);                              // drop last prime
     CtPtr drop_to(const Ciphertext &a, int level) const;             // discard limbs
     CtPtr level_adjust(const Ciphertext &a, int target);             // scalar-1 + rescale
@@ -248,6 +259,9 @@ class Context {
 enum class SignFunc { CompositeSign = 0, SignumPolycircuit = 1, Tanh = 2, NaiveDiscrete = 3 };
 struct SignConfig {
     int n = 3, dg = 0, df = 0;
+    // compositeSign's lazy bootstrap (src/sign.cpp:164-170): when set, g_n / f_n
+    // run on a bootstrapped input whenever fewer than depth + 2 levels remain
+    std::function<CtPtr(const Ciphertext &)> boot;
 };
 
 CtPtr cheb_series_ps(Context &cc, const Ciphertext &x, const std::vector<double> &coeffs,
@@ -337,6 +351,8 @@ class DirectSort {
 const std::vector<double> &doubled_sinc_coefficients(int N);
 const std::vector<double> &scaled_sinc_coefficients(int N);
 void set_coefficient_dir(const std::string &dir);
+// EvalMod cosine series (data/gen_evalmod.py): evalmod_k<K>r<r>_<degree>.f64
+const std::vector<double> &evalmod_coefficients(int K, int r, int degree);
 
 // MEHP24 (Mazzone et al.) ranking / sorting, src/mehp24/*
 namespace mehp24 {
@@ -364,5 +380,53 @@ std::vector<int> rotation_indices(int N);
 CtPtr sort(Context &cc, const Ciphertext &x, int k, int M, const SignConfig &cfg);
 std::vector<CtPtr> sorter(Context &cc, int kk, const std::vector<CtPtr> &x, const std::vector<CtPtr> &s);
 }  // namespace kway
+
+// ---------------------------------------------- CKKS bootstrapping --------
+// oracle_boot.cpp: OpenFHE's EvalBootstrapSetup / EvalBootstrapKeyGen /
+// EvalBootstrap as the reference uses them (tests/k-way/KWaySort235Test.cpp:
+// 46-48, src/k-way/EvalUtils.cpp:76, src/sign.cpp:164-170), restated for
+// sparse packing (slots s <= n/4): ModRaise, partial trace to the slot
+// subring, CoeffsToSlots as budget_enc BSGS linear transforms, real-part
+// extraction by conjugation, EvalMod (Chebyshev cosine + r double angles),
+// SlotsToCoeffs as budget_dec BSGS linear transforms.  DESIGN.md §9d.
+struct BootConfig {
+    int slots = 0;                        // s: power of two, 2 <= s <= n/4
+    int budget_enc = 4, budget_dec = 4;   // levelBudget {CoeffsToSlots, SlotsToCoeffs}
+    int K = 512;                          // EvalMod input range |t / q0| <= K
+    int r = 6;                            // double-angle iterations
+    int degree = 88;                      // Chebyshev degree of the cosine
+    int correction_bits = 11;             // message scaled to q0 2^-bits before ModRaise
+};
+class Bootstrapper {
+  public:
+    Bootstrapper(Context &cc, const BootConfig &cfg);
+    std::vector<int> rotation_indices() const;  // trace + BSGS steps (conjugation key separate)
+    void keygen();                              // rotation keys + conjugation key
+    int depth() const;                          // output level of a bootstrap
+    CtPtr bootstrap(const Ciphertext &ct);      // input level <= L-1, slots == cfg.slots
+    // the stages on their own (tests)
+    CtPtr coeffs_to_slots(const Ciphertext &raised);
+    CtPtr eval_mod(const Ciphertext &x);
+    CtPtr slots_to_coeffs(const Ciphertext &x);
+
+    Context &cc;
+    BootConfig cfg;
+    struct Giant {
+        long shift = 0;                                  // giant rotation (mod 2s)
+        std::vector<int> baby;                           // index into LinLevel::baby
+        std::vector<std::vector<std::complex<double>>> v;  // pre-rotated diagonals, 2s entries
+    };
+    struct LinLevel {
+        std::vector<long> baby;  // baby rotations (mod 2s), baby[0] == 0 when used
+        std::vector<Giant> giants;
+    };
+    std::vector<LinLevel> cts, stc;
+    std::vector<double> cheb;
+    long stc_int = 1;  // power-of-two part of the SlotsToCoeffs scale, applied as an integer product
+
+  private:
+    CtPtr linear(const Ciphertext &x, const LinLevel &lv, int tag);
+    std::map<std::pair<int, int>, std::vector<std::vector<Plaintext>>> pts;  // (tag, level) -> [giant][baby]
+};
 
 }  // namespace oracle

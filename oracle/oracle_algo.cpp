@@ -171,6 +171,8 @@ struct PSEval {
 
 }  // namespace
 
+int cheb_ps_depth(int d) { return std::max(std::max(1, ceil_log2((long)d + 1)), openfhe_ps_depth(d)); }
+
 CtPtr cheb_series_ps(Context &cc, const Ciphertext &x0, const std::vector<double> &coeffs, double a,
                      double b) {
     std::vector<double> c(coeffs);
@@ -254,9 +256,20 @@ CtPtr composite_sign(Context &cc, const Ciphertext &x, const SignConfig &cfg) {
     auto g = [&](const Ciphertext &v) { return cfg.n == 3 ? g3(cc, v) : g4(cc, v); };
     auto f = [&](const Ciphertext &v) { return cfg.n == 3 ? f3(cc, v) : f4(cc, v); };
     if (cfg.n != 3 && cfg.n != 4) throw std::invalid_argument("composite_sign: n must be 3 or 4");
-    CtPtr y = g(x);  // src/sign.cpp:173 applies g once unconditionally
-    for (int i = 1; i < cfg.dg; ++i) y = g(*y);
-    for (int i = 0; i < cfg.df; ++i) y = f(*y);
+    // lazyBootstrap (src/sign.cpp:164-170): g_depth = f_depth = n (3 or 4)
+    auto lazy = [&](const Ciphertext &c) -> CtPtr {
+        return (cfg.boot && cc.P.L - c.level < cfg.n + 2) ? cfg.boot(c) : nullptr;
+    };
+    CtPtr b = lazy(x);
+    CtPtr y = g(b ? *b : x);  // src/sign.cpp:173 applies g once unconditionally
+    for (int i = 1; i < cfg.dg; ++i) {
+        if ((b = lazy(*y))) y = b;
+        y = g(*y);
+    }
+    for (int i = 0; i < cfg.df; ++i) {
+        if ((b = lazy(*y))) y = b;
+        y = f(*y);
+    }
     return y;
 }
 
@@ -955,5 +968,8 @@ static const std::vector<double> &coefficient_table(const std::string &kind, int
 }
 const std::vector<double> &doubled_sinc_coefficients(int N) { return coefficient_table("doubled_sinc", N); }
 const std::vector<double> &scaled_sinc_coefficients(int N) { return coefficient_table("scaled_sinc", N); }
+const std::vector<double> &evalmod_coefficients(int K, int r, int degree) {
+    return coefficient_table("evalmod_k" + std::to_string(K) + "r" + std::to_string(r), degree);
+}
 
 }  // namespace oracle

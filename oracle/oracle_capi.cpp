@@ -319,6 +319,82 @@ int orc_kway_sorter(void *c, int kk, void **x, int nx, void **s, int ns, void **
         return 0;
     }, -1);
 }
+
+// ------------------------------------------------- bootstrapping ----------
+// EvalBootstrapSetup(levelBudget, {0,0}, slots) + EvalBootstrapKeyGen +
+// EvalBootstrap (tests/k-way/KWaySort235Test.cpp:46-48, EvalUtils.cpp:76)
+void *orc_boot_new(void *c, int slots, int budget_enc, int budget_dec, int K, int r, int degree,
+                   int correction_bits) {
+    return guard([&]() -> void * {
+        BootConfig b;
+        b.slots = slots;
+        b.budget_enc = budget_enc;
+        b.budget_dec = budget_dec;
+        b.K = K;
+        b.r = r;
+        b.degree = degree;
+        b.correction_bits = correction_bits;
+        return new Bootstrapper(*CTX, b);
+    }, (void *)nullptr);
+}
+void orc_boot_free(void *b) { delete static_cast<Bootstrapper *>(b); }
+int orc_boot_keygen(void *b) {
+    return guard([&]() { static_cast<Bootstrapper *>(b)->keygen(); return 0; }, -1);
+}
+int orc_boot_depth(void *b) { return static_cast<Bootstrapper *>(b)->depth(); }
+int orc_boot_rotations(void *b, int *out, int maxr) {
+    auto r = static_cast<Bootstrapper *>(b)->rotation_indices();
+    for (int i = 0; i < std::min((int)r.size(), maxr); ++i) out[i] = r[i];
+    return (int)r.size();
+}
+// stage: 0 = full bootstrap, 1 = CoeffsToSlots (input: a raised ciphertext),
+// 2 = EvalMod, 3 = SlotsToCoeffs, 4 = ModRaise (context op)
+void *orc_bootstrap(void *b, void *x, int stage) {
+    return guard([&]() -> void * {
+        auto *B = static_cast<Bootstrapper *>(b);
+        switch (stage) {
+            case 1: return wrap(B->coeffs_to_slots(CT(x)));
+            case 2: return wrap(B->eval_mod(CT(x)));
+            case 3: return wrap(B->slots_to_coeffs(CT(x)));
+            case 4: return wrap(B->cc.mod_raise(CT(x)));
+            default: return wrap(B->bootstrap(CT(x)));
+        }
+    }, (void *)nullptr);
+}
+void *orc_conjugate(void *c, void *a) { return guard([&]() -> void * { return wrap(CTX->conjugate(CT(a))); }, (void *)nullptr); }
+int orc_gen_galois_keys(void *c, const uint64_t *gs, int m) {
+    return guard([&]() { CTX->gen_galois_keys(std::vector<uint64_t>(gs, gs + m)); return 0; }, -1);
+}
+// key of galois element g (0 if absent, else g)
+uint64_t orc_galois_key(void *c, uint64_t g, uint64_t *out) {
+    auto it = CTX->rotkeys.find(g);
+    if (it == CTX->rotkeys.end()) return 0;
+    if (out) std::memcpy(out, it->second.data.data(), it->second.data.size() * 8);
+    return g;
+}
+void *orc_encode_complex(void *c, const double *re, const double *im, int len, int slots, int level, double scale) {
+    return guard([&]() -> void * {
+        std::vector<std::complex<double>> v;
+        for (int i = 0; i < len; ++i) v.emplace_back(re[i], im[i]);
+        return new PtH{CTX->encode_complex(v, slots, level, scale)};
+    }, (void *)nullptr);
+}
+// k-way sort / compare with a bootstrapper (b may be NULL: no bootstrapping)
+void *orc_kway_sort_boot(void *c, void *x, int k, int M, int dg, int df, void *b) {
+    return guard([&]() -> void * {
+        auto cfg = cfg3(3, dg, df);
+        if (b) cfg.boot = [b](const Ciphertext &ct) { return static_cast<Bootstrapper *>(b)->bootstrap(ct); };
+        return wrap(kway::sort(*CTX, CT(x), k, M, cfg));
+    }, (void *)nullptr);
+}
+void *orc_compare_boot(void *c, void *a, void *bb, int n, int dg, int df, void *b) {
+    return guard([&]() -> void * {
+        auto cfg = cfg3(n, dg, df);
+        if (b) cfg.boot = [b](const Ciphertext &ct) { return static_cast<Bootstrapper *>(b)->bootstrap(ct); };
+        return wrap(compare(*CTX, CT(a), CT(bb), SignFunc::CompositeSign, cfg));
+    }, (void *)nullptr);
+}
+
 int orc_kway_sort_type(int k, int M, int stage, int *out3) {
     return guard([&]() {
         if (k < 2 || M < 1 || stage < 0 || stage >= kway::stage_count(k, M)) throw std::invalid_argument("stage");

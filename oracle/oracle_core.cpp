@@ -394,18 +394,27 @@ Plaintext Context::encode(const std::vector<double> &v, int slots, int level) co
     return encode_scaled(v, slots, level, P.delta[level]);
 }
 Plaintext Context::encode_scaled(const std::vector<double> &v, int slots, int level, double scale) const {
+    std::vector<cd> z;
+    for (size_t i = 0; i < v.size() && i < (size_t)std::max(slots, 0); ++i) z.push_back(cd(v[i], 0));
+    return encode_complex(z, slots, level, scale);
+}
+Plaintext Context::encode_complex(const std::vector<cd> &v, int slots, int level, double scale) const {
     const size_t n = P.n;
     if (slots <= 0 || (slots & (slots - 1)) || (size_t)slots > n / 2)
         throw std::invalid_argument("encode: slots must be a power of two <= n/2");
     const EncTables &T = enc_tables(n);
     std::vector<cd> vals(slots, cd(0, 0));
-    for (size_t i = 0; i < v.size() && i < (size_t)slots; ++i) vals[i] = cd(v[i], 0);
+    for (size_t i = 0; i < v.size() && i < (size_t)slots; ++i) vals[i] = v[i];
     emb_inv(vals, T);
     const size_t gap = n / (2 * (size_t)slots);
     std::vector<i64> coef(n, 0);
+    auto rnd = [](double x) -> i64 {
+        if (!(std::fabs(x) < 9.2e18)) throw std::overflow_error("encode: scaled coefficient exceeds 63 bits");
+        return std::llround(x);
+    };
     for (size_t i = 0; i < (size_t)slots; ++i) {
-        coef[i * gap] = std::llround(vals[i].real() * scale);
-        coef[i * gap + n / 2] = std::llround(vals[i].imag() * scale);
+        coef[i * gap] = rnd(vals[i].real() * scale);
+        coef[i * gap + n / 2] = rnd(vals[i].imag() * scale);
     }
     Plaintext pt;
     pt.level = level;
@@ -518,9 +527,14 @@ void Context::gen_switch_key(const std::vector<u64> &sp, SwitchKey &out, u64 kid
 }
 
 void Context::gen_rotation_keys(const std::vector<int> &rot) {
+    std::vector<u64> gs;
+    for (int k : rot) gs.push_back(galois_for_rotation(P.logN, k));
+    gen_galois_keys(gs);
+}
+
+void Context::gen_galois_keys(const std::vector<u64> &gs) {
     const size_t n = P.n, nq = P.nq();
-    for (int k : rot) {
-        u64 g = galois_for_rotation(P.logN, k);
+    for (u64 g : gs) {
         if (g == 1 || rotkeys.count(g)) continue;
         auto perm = automorphism_perm(P.logN, g);
         std::vector<u64> sp(nq * n);
@@ -1072,18 +1086,25 @@ CtPtr Context::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::ve
 CtPtr Context::square(const Ciphertext &a) { return mul(a, a); }
 
 std::vector<CtPtr> Context::rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks) {
+    std::vector<u64> gs;
+    for (long k : ks) gs.push_back(galois_for_rotation(P.logN, k));
+    return apply_galois_hoisted(a, gs);
+}
+
+CtPtr Context::conjugate(const Ciphertext &a) { return apply_galois_hoisted(a, {2 * (u64)P.n - 1})[0]; }
+
+std::vector<CtPtr> Context::apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs) {
     const size_t n = P.n, ell = a.limbs;
     std::vector<CtPtr> outs;
     std::vector<u64> ext;
     bool have_ext = false;
-    for (long k : ks) {
-        u64 g = galois_for_rotation(P.logN, k);
+    for (u64 g : gs) {
         if (g == 1) {
             outs.push_back(clone(a));
             continue;
         }
         auto it = rotkeys.find(g);
-        if (it == rotkeys.end()) throw std::out_of_range("rotate: no rotation key for index " + std::to_string(k));
+        if (it == rotkeys.end()) throw std::out_of_range("rotate: no rotation key for galois element " + std::to_string(g));
         if (!have_ext) {
             modup(a.poly(1, n), ell, ext);
             have_ext = true;
@@ -1110,6 +1131,26 @@ std::vector<CtPtr> Context::rotate_hoisted(const Ciphertext &a, const std::vecto
 }
 
 CtPtr Context::rotate(const Ciphertext &a, long k) { return rotate_hoisted(a, {k})[0]; }
+
+CtPtr Context::mod_raise(const Ciphertext &a) {
+    if (a.limbs != 1) throw std::invalid_argument("mod_raise: input must be at the last level (one limb)");
+    const size_t n = P.n, nq = P.nq();
+    const u64 q0 = P.primes[0];
+    auto r = make_ct(0, a.slots, P.delta[0], nq, n);
+    for (int i = 0; i < 2; ++i) {
+        std::vector<u64> c(a.poly(i, n), a.poly(i, n) + n);
+        ntt_inverse(c.data(), tab[0], n);
+        std::vector<i64> t(n);
+        for (size_t k = 0; k < n; ++k) t[k] = c[k] > q0 / 2 ? (i64)c[k] - (i64)q0 : (i64)c[k];
+#pragma omp parallel for
+        for (size_t l = 0; l < nq; ++l) {
+            u64 *o = r->poly(i, n) + l * n;
+            for (size_t k = 0; k < n; ++k) o[k] = signed_to_mod(t[k], P.primes[l]);
+            ntt_forward(o, tab[l], n);
+        }
+    }
+    return r;
+}
 
 CtPtr Context::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c,
                              int target) {

@@ -107,7 +107,7 @@ struct Net {
     Context &cc;
     long ns, k, M;
     SignConfig cfg;
-    const int lv[6] = {0, 1, 3, 5, 6, 7};  // Sorter.h:85-93
+    static constexpr int lv[6] = {0, 1, 3, 5, 6, 7};  // Sorter.h:85-93
     std::map<std::pair<Mask, int>, Plaintext> cache;
     std::vector<int> grp, pos;
 
@@ -122,8 +122,12 @@ struct Net {
         for (size_t i = 0; i < (size_t)ns; ++i) m[i] = (grp[i] == g && pos[i] == p) ? 1.0 : 0.0;
         return m;
     }
-    void need(const Ciphertext &c, int l) const {
-        if (cc.P.L - c.level < l + 1) throw std::runtime_error("k-way: no levels left (bootstrapping not built)");
+    // EvalUtils::checkLevelAndBoot (EvalUtils.cpp:59-86): bootstrap when fewer
+    // than l + 1 levels remain (cfg.boot); without a bootstrapper that is an error
+    void need(CtPtr &c, int l) const {
+        if (cc.P.L - c->level >= l + 1) return;
+        if (!cfg.boot) throw std::runtime_error("k-way: no levels left (set up bootstrapping for this depth)");
+        c = cfg.boot(*c);
     }
     CtPtr rot(CtPtr c, long r, long sign) {  // EvalUtils::leftRotate / rightRotate
         for (long p = 1; r > 0; p *= 2, r /= 2)
@@ -304,18 +308,19 @@ struct Net {
             gen_indices(ns, k, M, m, ld, sl, grp, pos);
             CtPtr fix, c1, c2;
             auto one = [&](int before, int after) {
-                need(*ct, before);
+                need(ct, before);
                 c1 = cmp(ct, align(ct, ld, sl, &fix));
-                need(*c1, after);
+                need(c1, after);
             };
             auto two = [&](int before, int after) {
-                need(*ct, before);
+                need(ct, before);
                 const CtPtr r1 = align(ct, ld, sl, &fix);
                 const CtPtr r2 = align(r1, ld, sl, nullptr);
                 c1 = cmp(ct, r1);
                 c2 = cmp(ct, r2);
-                need(*c1, after);
-                need(*c2, after);
+                need(ct, before);  // Sorter.cpp:351 (k = 5, middle slope): a second check of ctxt
+                need(c1, after);
+                need(c2, after);
             };
             if (sl == 0) {
                 if (k == 5) {
@@ -337,8 +342,10 @@ struct Net {
                 two(lv[5], lv[5]);
                 ct = cc.add(*run2345(ct, sh, c1, c2), *fix);
             } else if ((k == 5 && sl == 2) || (k == 3 && sl == 1)) {
-                one(lv[3], lv[3]);
-                const CtPtr a = run2(ct, sh, c1), b = run3(ct, sh, c1);
+                one(lv[3], lv[2]);  // Sorter.cpp:370-378: c1 checked for 2, then for 3
+                const CtPtr a = run2(ct, sh, c1);
+                need(c1, lv[3]);
+                const CtPtr b = run3(ct, sh, c1);
                 ct = cc.add(*cc.add(*a, *fix), *b);
             } else if (k == 2 && sl == 1) {
                 one(lv[2], lv[2]);
@@ -358,7 +365,7 @@ struct Net {
 std::vector<CtPtr> sorter(Context &cc, int kk, const std::vector<CtPtr> &x, const std::vector<CtPtr> &s) {
     const size_t nx = kk == 1 ? 2 : (size_t)kk, ns = kk == 1 ? 1 : (size_t)(kk * (kk - 1) / 2);
     if (kk < 1 || kk > 5 || x.size() != nx || s.size() != ns) throw std::invalid_argument("k-way sorter: bad arity");
-    Net net{cc, (long)x[0]->slots, 5, 2, SignConfig{}, {}, {}, {}, {}};
+    Net net{cc, (long)x[0]->slots, 5, 2, SignConfig{}, {}, {}, {}};
     std::vector<CtPtr> out(kk == 1 ? 1 : (size_t)kk);
     if (kk == 1)
         out[0] = net.fcn(x[0], x[1], s[0]);
@@ -376,7 +383,7 @@ std::vector<CtPtr> sorter(Context &cc, int kk, const std::vector<CtPtr> &x, cons
 CtPtr sort(Context &cc, const Ciphertext &x, int k, int M, const SignConfig &cfg) {
     if (k != 2 && k != 3 && k != 5) throw std::invalid_argument("k-way: only k = 2, 3, 5 are supported");
     if (M < 1 || pw(k, M) > x.slots) throw std::invalid_argument("k-way: k^M exceeds the slots");
-    Net net{cc, pw(k, M), k, M, cfg, {}, {}, {}, {}};
+    Net net{cc, pw(k, M), k, M, cfg, {}, {}, {}};
     return net.run(x);
 }
 

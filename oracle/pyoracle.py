@@ -101,6 +101,18 @@ def lib():
             'orc_counters': (C.c_int, [vp, u64p]),
             'orc_reset_counters': (None, [vp]),
             'orc_num_threads': (C.c_int, []),
+            'orc_boot_new': (vp, [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+            'orc_boot_free': (None, [vp]),
+            'orc_boot_keygen': (C.c_int, [vp]),
+            'orc_boot_depth': (C.c_int, [vp]),
+            'orc_boot_rotations': (C.c_int, [vp, ip, C.c_int]),
+            'orc_bootstrap': (vp, [vp, vp, C.c_int]),
+            'orc_conjugate': (vp, [vp, vp]),
+            'orc_gen_galois_keys': (C.c_int, [vp, u64p, C.c_int]),
+            'orc_galois_key': (C.c_uint64, [vp, C.c_uint64, u64p]),
+            'orc_encode_complex': (vp, [vp, dp, dp, C.c_int, C.c_int, C.c_int, C.c_double]),
+            'orc_kway_sort_boot': (vp, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]),
+            'orc_compare_boot': (vp, [vp, vp, vp, C.c_int, C.c_int, C.c_int, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -372,9 +384,33 @@ class Context:
     def mehp24_indicator(self, a, b, dg, df):
         return Ct(self, lib().orc_mehp24_indicator(self.h, a.h, b, dg, df))
 
-    def kway_sort(self, x, k, M, cfg):
-        """k-way network; cfg = (n, dg, df) with n = 3"""
-        return Ct(self, lib().orc_kway_sort(self.h, x.h, k, M, cfg[1], cfg[2]))
+    def kway_sort(self, x, k, M, cfg, boot=None):
+        """k-way network; cfg = (n, dg, df) with n = 3; boot: a Bootstrapper (checkLevelAndBoot)"""
+        if boot is None:
+            return Ct(self, lib().orc_kway_sort(self.h, x.h, k, M, cfg[1], cfg[2]))
+        return Ct(self, lib().orc_kway_sort_boot(self.h, x.h, k, M, cfg[1], cfg[2], boot.h))
+
+    def compare_boot(self, a, b, n, dg, df, boot):
+        """Comparison::compare with compositeSign's lazy bootstrap (src/sign.cpp:164-170)"""
+        return Ct(self, lib().orc_compare_boot(self.h, a.h, b.h, n, dg, df, boot.h))
+
+    def conjugate(self, a): return Ct(self, lib().orc_conjugate(self.h, a.h))
+
+    def gen_galois_keys(self, gs):
+        g = np.asarray(gs, dtype=np.uint64)
+        if lib().orc_gen_galois_keys(self.h, _u64(g), len(g)) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def galois_key(self, g):
+        out = np.empty((self.digits, 2, self.nq + self.K, self.n), dtype=np.uint64)
+        r = lib().orc_galois_key(self.h, int(g), _u64(out))
+        return out if r else None
+
+    def encode_complex(self, v, slots, level, scale=None):
+        v = np.asarray(v, dtype=np.complex128)
+        re, im = np.ascontiguousarray(v.real), np.ascontiguousarray(v.imag)
+        scale = self.delta[level] if scale is None else scale
+        return Pt(self, lib().orc_encode_complex(self.h, _dbl(re), _dbl(im), len(v), slots, level, scale), level)
 
     def kway_sorter(self, kk, xs, cmps):
         """SortUtils::fcnL (kk = 1) or the kk-sorter (kk = 2..5): ascending outputs."""
@@ -417,6 +453,45 @@ class Context:
 
     def reset_counters(self):
         lib().orc_reset_counters(self.h)
+
+
+class Bootstrapper:
+    """EvalBootstrapSetup(levelBudget={budget_enc, budget_dec}, slots) +
+    EvalBootstrapKeyGen + EvalBootstrap (oracle_boot.cpp)."""
+
+    def __init__(self, ctx, slots, budget=(4, 4), K=512, r=6, degree=88, correction_bits=11, keygen=True):
+        self.ctx = ctx
+        self.cfg = dict(slots=slots, budget=tuple(budget), K=K, r=r, degree=degree, correction_bits=correction_bits)
+        self.h = _check(lib().orc_boot_new(ctx.h, slots, budget[0], budget[1], K, r, degree, correction_bits))
+        if keygen:
+            self.keygen()
+
+    def __del__(self):
+        try:
+            lib().orc_boot_free(self.h)
+        except Exception:
+            pass
+
+    def keygen(self):
+        if lib().orc_boot_keygen(self.h) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    @property
+    def depth(self):
+        return lib().orc_boot_depth(self.h)
+
+    def rotations(self):
+        out = np.zeros(4096, dtype=np.int32)
+        m = lib().orc_boot_rotations(self.h, _int(out), 4096)
+        return [int(x) for x in out[:m]]
+
+    def bootstrap(self, x, stage=0):
+        return Ct(self.ctx, lib().orc_bootstrap(self.h, x.h, stage))
+
+    def mod_raise(self, x): return self.bootstrap(x, 4)
+    def coeffs_to_slots(self, x): return self.bootstrap(x, 1)
+    def eval_mod(self, x): return self.bootstrap(x, 2)
+    def slots_to_coeffs(self, x): return self.bootstrap(x, 3)
 
 
 def automorph_perm(logN, g):
