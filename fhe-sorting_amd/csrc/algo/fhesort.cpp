@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <fstream>
 #include <map>
@@ -227,6 +228,8 @@ struct PSEval {
 
 }  // namespace
 
+int chebPSDepth(int d) { return std::max(std::max(1, ceil_log2((long)d + 1)), openfhe_ps_depth(d)); }
+
 CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<double> &coeffs, double a,
                             double b) {
     std::vector<double> c(coeffs);
@@ -306,9 +309,32 @@ CtPtr compositeSignN(Engine &cc, const Ciphertext &x, int n, const SignConfig &c
     if (n != 3 && n != 4) throw std::invalid_argument("compositeSign: n must be 3 or 4");
     auto g = [&](const Ciphertext &v) { return n == 3 ? g3(cc, v) : g4(cc, v); };
     auto f = [&](const Ciphertext &v) { return n == 3 ? f3(cc, v) : f4(cc, v); };
-    CtPtr y = g(x);  // applied once even when dg == 0 (src/sign.cpp:173)
-    for (int i = 1; i < cfg.compos.dg; ++i) y = g(*y);
-    for (int i = 0; i < cfg.compos.df; ++i) y = f(*y);
+    // lazyBootstrap (src/sign.cpp:164-170): g_depth = f_depth = n (3 or 4)
+    const int L = cc.params().L;
+    auto lazy = [&](const Ciphertext &c) -> CtPtr {
+        if (!(cfg.boot && L - c.level < n + 2)) return nullptr;
+        CtPtr b = cfg.boot(c);
+        if (std::getenv("FHE_KWAY_TRACE")) {  // diagnostics: lazy bootstrap error
+            const auto u = cc.decrypt(c), v = cc.decrypt(*b);
+            double e = 0, mx = 0;
+            for (size_t i = 0; i < u.size(); ++i) {
+                e = std::max(e, std::fabs(u[i] - v[i]));
+                mx = std::max(mx, std::fabs(u[i]));
+            }
+            std::fprintf(stderr, "  sign boot at level %d: max|in| %.6g, max|out - in| %.3g\n", c.level, mx, e);
+        }
+        return b;
+    };
+    CtPtr b = lazy(x);
+    CtPtr y = g(b ? *b : x);  // applied once even when dg == 0 (src/sign.cpp:173)
+    for (int i = 1; i < cfg.compos.dg; ++i) {
+        if ((b = lazy(*y))) y = b;
+        y = g(*y);
+    }
+    for (int i = 0; i < cfg.compos.df; ++i) {
+        if ((b = lazy(*y))) y = b;
+        y = f(*y);
+    }
     return y;
 }
 
@@ -320,6 +346,11 @@ CtPtr sign(const Ciphertext &x, Engine &cc, SignFunc func, const SignConfig &cfg
 
 CtPtr Comparison::compare(Engine &cc, const Ciphertext &a, const Ciphertext &b, SignFunc f, const SignConfig &cfg) {
     CtPtr diff = cc.sub(a, b);
+    if (cfg.boot && std::getenv("FHE_KWAY_TRACE")) {
+        double mx = 0;
+        for (double v : cc.decrypt(*diff)) mx = std::max(mx, std::fabs(v));
+        std::fprintf(stderr, "  compare: level %d, max|a - b| %.6g\n", diff->level, mx);
+    }
     CtPtr s = sign(*diff, cc, f, cfg);
     return cc.mul_const(*cc.add_const(*s, 1.0), 0.5);
 }
@@ -1402,6 +1433,9 @@ static const std::vector<double> &coefficientTable(const std::string &kind, int 
 }
 const std::vector<double> &doubledSincCoefficients(int N) { return coefficientTable("doubled_sinc", N); }
 const std::vector<double> &scaledSincCoefficients(int N) { return coefficientTable("scaled_sinc", N); }
+const std::vector<double> &evalModCoefficients(int K, int r, int degree) {
+    return coefficientTable("evalmod_k" + std::to_string(K) + "r" + std::to_string(r), degree);
+}
 const std::vector<double> &DirectSortN::sincCoefficients() const { return doubledSincCoefficients(N); }
 
 }  // namespace fhe

@@ -31,7 +31,11 @@ struct CompositeSignConfig {
 };
 struct SignConfig {
     CompositeSignConfig compos{0, 0, 0};
-    int multDepth = 100;  // src/sign.h:27-28: no bootstrapping on this path
+    int multDepth = 100;  // src/sign.h:27-28
+    // compositeSign's lazyBootstrap (src/sign.cpp:164-170): when set, g_n / f_n
+    // run on a bootstrapped input whenever fewer than depth + 2 levels remain
+    // (the context's depth is the reference's Cfg.multDepth)
+    std::function<CtPtr(const Ciphertext &)> boot;
     SignConfig() = default;
     explicit SignConfig(CompositeSignConfig c) : compos(c) {}
     SignConfig(CompositeSignConfig c, int depth) : compos(c), multDepth(depth) {}
@@ -41,6 +45,8 @@ struct SignConfig {
 // Paterson-Stockmeyer; replaces OpenFHE EvalChebyshevSeriesPS.
 CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x, const std::vector<double> &coeffs, double a,
                             double b);
+// levels evalChebyshevSeriesPS consumes for a degree-d series
+int chebPSDepth(int degree);
 
 CtPtr compositeSignN(Engine &cc, const Ciphertext &x, int n, const SignConfig &cfg);
 template <int n>
@@ -286,5 +292,7 @@ Parameters parameters(size_t N);
 void setCoefficientDir(const std::string &dir);
 const std::vector<double> &doubledSincCoefficients(int N);
 const std::vector<double> &scaledSincCoefficients(int N);  // selectCoefficients<N>()
+// bootstrapping's EvalMod cosine (data/gen_evalmod.py): evalmod_k<K>r<r>_<degree>.f64
+const std::vector<double> &evalModCoefficients(int K, int r, int degree);
 
 }  // namespace fhe

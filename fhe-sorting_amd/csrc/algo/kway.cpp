@@ -4,6 +4,9 @@
 // meet (FLEXIBLEAUTO re-encodes a plaintext at its operand's level).
 #include "kway.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <cmath>
 #include <stdexcept>
 
@@ -125,11 +128,23 @@ const Plaintext &Sorter::mask(const std::vector<double> &v, const Ciphertext &li
     return *(masks[key] = cc.encode(v, like.slots, like.level));
 }
 
-// EvalUtils::checkLevelAndBoot (EvalUtils.cpp:59-86): the reference bootstraps
-// when fewer than need + 1 levels remain; without bootstrapping that is an error
-void Sorter::checkLevel(const Ciphertext &c, int need) const {
-    if (cc.params().L - c.level < need + 1)
-        throw std::runtime_error("k-way: no levels left (the reference bootstraps here; bootstrapping is not built)");
+// EvalUtils::checkLevelAndBoot (EvalUtils.cpp:59-86): bootstrap when fewer
+// than need + 1 levels remain (cfg.boot); without a bootstrapper that is an error
+void Sorter::checkLevel(CtPtr &c, int need, const SignConfig &cfg) {
+    if (cc.params().L - c->level >= need + 1) return;
+    if (!cfg.boot) throw std::runtime_error("k-way: no levels left (set up bootstrapping for this depth)");
+    CtPtr in = c;
+    c = cfg.boot(*c);
+    ++bootstraps;
+    if (std::getenv("FHE_KWAY_TRACE")) {
+        const auto a = cc.decrypt(*in), b = cc.decrypt(*c);
+        double e = 0, mx = 0;
+        for (size_t i = 0; i < (size_t)numSlots && i < a.size(); ++i) {
+            e = std::max(e, std::fabs(a[i] - b[i]));
+            mx = std::max(mx, std::fabs(a[i]));
+        }
+        std::fprintf(stderr, "  boot %d at level %d: max|in| %.6g, max|out - in| %.3g\n", bootstraps, in->level, mx, e);
+    }
 }
 
 // EvalUtils.cpp:113-146: binary decomposition, ascending powers of two
@@ -389,58 +404,70 @@ CtPtr Sorter::sorter(const Ciphertext &input, const SignConfig &cfg) {
     CtPtr ct = cc.clone(input), fix, c1, c2;
     const int stages = stageCount((int)k, (int)M);
     stagesRun = 0;
+    bootstraps = 0;
     for (int stage = 0; stage < stages; ++stage) {
         int m, logDist, slope;
         std::tie(m, logDist, slope) = sortType((int)k, (int)M, stage);
         const long shift = getRotateDistance(k, logDist, slope);
         const auto ind = genIndices(numSlots, k, M, m, logDist, slope);
         if (slope == 0) {
-            checkLevel(*ct, level[(size_t)k]);
+            checkLevel(ct, level[(size_t)k], cfg);
             if (k == 5) {
                 comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
-                checkLevel(*c1, level[5]);
-                checkLevel(*c2, level[5]);
+                checkLevel(c1, level[5], cfg);
+                checkLevel(c2, level[5], cfg);
                 ct = runFiveSorter(ct, ind, shift, c1, c2);
             } else {
                 c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
-                checkLevel(*c1, level[(size_t)k]);
+                checkLevel(c1, level[(size_t)k], cfg);
                 ct = k == 2 ? runTwoSorter(ct, ind, shift, c1) : runThreeSorter(ct, ind, shift, c1);
             }
         } else if (slope == k / 2 + 1) {  // k = 3 or 5 (k = 2 has slopes 0, 1 only)
-            checkLevel(*ct, level[(size_t)k - 1]);
+            checkLevel(ct, level[(size_t)k - 1], cfg);
             if (k == 3) {
                 c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
-                checkLevel(*c1, level[2]);
+                checkLevel(c1, level[2], cfg);
                 ct = runTwoSorter(ct, ind, shift, c1);
             } else {
                 comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
-                checkLevel(*c1, level[4]);
-                checkLevel(*c2, level[4]);
+                checkLevel(c1, level[4], cfg);
+                checkLevel(c2, level[4], cfg);
                 ct = runFourSorter(ct, ind, shift, c1, c2);
             }
             ct = cc.add(*ct, *fix);
         } else if (k == 5 && slope == 1) {
-            checkLevel(*ct, level[5]);
+            checkLevel(ct, level[5], cfg);
             comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
-            checkLevel(*c1, level[5]);
-            checkLevel(*c2, level[5]);
+            checkLevel(c1, level[5], cfg);
+            checkLevel(c2, level[5], cfg);
             ct = cc.add(*run2345Sorter(ct, ind, shift, c1, c2), *fix);
         } else if ((k == 5 && slope == 2) || (k == 3 && slope == 1)) {
-            checkLevel(*ct, level[3]);
+            checkLevel(ct, level[3], cfg);
             c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
-            checkLevel(*c1, level[3]);
+            checkLevel(c1, level[2], cfg);  // Sorter.cpp:373-376: checked for 2, then for 3
             const CtPtr two = runTwoSorter(ct, ind, shift, c1);
+            checkLevel(c1, level[3], cfg);
             const CtPtr three = runThreeSorter(ct, ind, shift, c1);
             ct = cc.add(*cc.add(*two, *fix), *three);
         } else if (k == 2 && slope == 1) {
-            checkLevel(*ct, level[2]);
+            checkLevel(ct, level[2], cfg);
             c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
-            checkLevel(*c1, level[2]);
+            checkLevel(c1, level[2], cfg);
             ct = cc.add(*runTwoSorter(ct, ind, shift, c1), *fix);
         } else {
             throw std::invalid_argument("k-way: no matching k and slope");
         }
         ++stagesRun;
+        if (std::getenv("FHE_KWAY_TRACE")) {  // diagnostics: decrypted range after every stage
+            const auto v = cc.decrypt(*ct);
+            double lo = 1e300, hi = -1e300;
+            for (size_t i = 0; i < (size_t)numSlots && i < v.size(); ++i) {
+                lo = std::min(lo, v[i]);
+                hi = std::max(hi, v[i]);
+            }
+            std::fprintf(stderr, "kway stage %d (m %d dist %d slope %d): level %d, values [%.6g, %.6g], boots %d\n",
+                         stage, m, logDist, slope, ct->level, lo, hi, bootstraps);
+        }
     }
     return ct;
 }

@@ -10,11 +10,11 @@
 //            comparisonForSort(2), sorter}                 src/k-way/Sorter.cpp:9-404
 //   KWayAdapter<N>::getSizeParameters                      src/kway_adapter.h:38-62
 //
-// Bootstrapping is not built: where the reference calls EvalBootstrap
-// (checkLevelAndBoot), this implementation requires the context to still hold
-// the levels and otherwise fails with "no levels left" (FHE_EDEPTH at the
-// C-ABI).  A network therefore runs when the context depth covers all of its
-// stages (DESIGN.md §9c gives the depth per k and M).
+// Bootstrapping: where the reference calls EvalBootstrap (checkLevelAndBoot,
+// and compositeSign's lazy bootstrap inside every comparison) the sorter calls
+// cfg.boot -- an fhe::Bootstrapper (bootstrap.hpp) at the C-ABI.  Without one a
+// network runs only when the context depth covers all of its stages and
+// otherwise fails with "no levels left" (FHE_EDEPTH).
 #pragma once
 #include <map>
 #include <string>
@@ -40,7 +40,8 @@ class Sorter {
     // numSlots = k^M values; the ciphertext holds next_pow2(numSlots) slots
     Sorter(Engine &cc, long numSlots, long k, long M);
     CtPtr sorter(const Ciphertext &x, const SignConfig &cfg);
-    int stagesRun = 0;  // stages completed by the last sorter() call
+    int stagesRun = 0;   // stages completed by the last sorter() call
+    int bootstraps = 0;  // checkLevelAndBoot bootstraps of the last sorter() call
     // SortUtils::fcnL (kk = 1: returns {fcnL(x0, x1, c0)}) or the kk-sorter,
     // kk = 2..5 (SortUtils.cpp:5-208), on their own: SortUtilsTest's cases
     std::vector<CtPtr> kSorter(int kk, const std::vector<CtPtr> &x, const std::vector<CtPtr> &cmp);
@@ -53,7 +54,7 @@ class Sorter {
     std::map<std::pair<std::vector<double>, int>, PtPtr> masks;
 
     const Plaintext &mask(const std::vector<double> &v, const Ciphertext &like);
-    void checkLevel(const Ciphertext &c, int need) const;
+    void checkLevel(CtPtr &c, int need, const SignConfig &cfg);
     CtPtr leftRotate(const CtPtr &c, long r);
     CtPtr rightRotate(const CtPtr &c, long r);
     CtPtr flip(const CtPtr &c, const std::vector<double> &m);

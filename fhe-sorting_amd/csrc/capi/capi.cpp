@@ -9,6 +9,7 @@
 #include <string>
 
 #include "../../../include/fhe_gpu.h"
+#include "../algo/bootstrap.hpp"
 #include "../algo/fhesort.hpp"
 #include "../algo/kway.hpp"
 #include "../engine/engine.hpp"
@@ -30,6 +31,9 @@ struct fhe_ct {
 };
 struct fhe_pt {
     PtPtr p;
+};
+struct fhe_boot {
+    std::unique_ptr<Bootstrapper> b;
 };
 struct fhe_rot_tree {
     std::unique_ptr<RotationTreeN> t;
@@ -524,6 +528,28 @@ int fhe_kway_sort(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int df, f
     });
 }
 
+int fhe_kway_sort_boot(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int df, fhe_boot *boot,
+                       int *bootstraps, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(x);
+        NEED(out);
+        if (k < 2 || M < 1) throw std::invalid_argument("k-way: k >= 2 and M >= 1 required");
+        long N = 1;
+        for (int i = 0; i < M && N <= x->p->slots; ++i) N *= k;
+        if (N > x->p->slots) throw std::invalid_argument("k-way: k^M exceeds the ciphertext's slots");
+        if (boot && &boot->b->cc != ctx->eng.get()) throw std::invalid_argument("k-way: bootstrapper of another context");
+        kwaySort::Sorter s(*ctx->eng, N, k, M);
+        SignConfig cfg(CompositeSignConfig(3, dg, df), ctx->eng->params().L);
+        if (boot) {
+            Bootstrapper *B = boot->b.get();
+            cfg.boot = [B](const Ciphertext &c) { return B->evalBootstrap(c); };
+        }
+        *out = wrap(s.sorter(*x->p, cfg));
+        if (bootstraps) *bootstraps = s.bootstraps;
+    });
+}
+
 int fhe_kway_sorter(fhe_ctx *ctx, int kk, const fhe_ct *const *x, int nx, const fhe_ct *const *cmp, int ncmp,
                     fhe_ct **out) {
     return guard([&] {
@@ -546,6 +572,109 @@ int fhe_kway_sorter(fhe_ctx *ctx, int kk, const fhe_ct *const *x, int nx, const 
         for (size_t i = 0; i < o.size(); ++i) out[i] = wrap(o[i]);
     });
 }
+// ----------------------------------------------------- bootstrapping ----
+int fhe_boot_create(fhe_ctx *ctx, const fhe_boot_params *p, fhe_boot **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(p);
+        NEED(out);
+        BootstrapConfig c;
+        c.slots = p->slots;
+        if (p->level_budget_enc) c.budgetEnc = p->level_budget_enc;
+        if (p->level_budget_dec) c.budgetDec = p->level_budget_dec;
+        if (p->K) c.K = p->K;
+        if (p->r) c.r = p->r;
+        if (p->degree) c.degree = p->degree;
+        if (p->correction_bits) c.correctionBits = p->correction_bits;
+        auto b = std::make_unique<fhe_boot>();
+        b->b = std::make_unique<Bootstrapper>(*ctx->eng, c);
+        *out = b.release();
+    });
+}
+int fhe_boot_destroy(fhe_boot *b) {
+    return guard([&] { delete b; });
+}
+int fhe_boot_keygen(fhe_boot *b) {
+    return guard([&] {
+        NEED(b);
+        b->b->keyGen();
+    });
+}
+int fhe_boot_rotation_indices(const fhe_boot *b, int32_t *rots, int max_rots) {
+    int n = -1;
+    const int st = guard([&] {
+        NEED(b);
+        auto r = b->b->rotationIndices();
+        for (int i = 0; rots && i < std::min((int)r.size(), max_rots); ++i) rots[i] = r[(size_t)i];
+        n = (int)r.size();
+    });
+    return st == FHE_OK ? n : -st;
+}
+int fhe_boot_depth(const fhe_boot *b) { return b ? b->b->depth() : -FHE_EINVAL; }
+int fhe_bootstrap(fhe_boot *b, const fhe_ct *x, fhe_ct **out) {
+    return guard([&] {
+        NEED(b);
+        NEED(x);
+        NEED(out);
+        *out = wrap(b->b->evalBootstrap(*x->p));
+    });
+}
+int fhe_bootstrap_stage(fhe_boot *b, const fhe_ct *x, int stage, fhe_ct **out) {
+    return guard([&] {
+        NEED(b);
+        NEED(x);
+        NEED(out);
+        Bootstrapper &B = *b->b;
+        switch (stage) {
+            case 0: *out = wrap(B.evalBootstrap(*x->p)); break;
+            case 1: *out = wrap(B.coeffsToSlots(*x->p)); break;
+            case 2: *out = wrap(B.evalMod(*x->p)); break;
+            case 3: *out = wrap(B.slotsToCoeffs(*x->p)); break;
+            case 4: *out = wrap(B.cc.mod_raise(*x->p)); break;
+            default: throw std::invalid_argument("fhe_bootstrap_stage: stage 0..4");
+        }
+    });
+}
+int fhe_conjugate(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(a);
+        NEED(out);
+        *out = wrap(ctx->eng->conjugate(*a->p));
+    });
+}
+int fhe_gen_galois_keys(fhe_ctx *ctx, const uint64_t *g, int n) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(g);
+        const uint64_t m2 = 2 * (uint64_t)ctx->eng->params().n;
+        for (int i = 0; i < n; ++i)
+            if (!(g[i] & 1) || g[i] >= m2) throw std::invalid_argument("galois element must be odd and < 2n");
+        ctx->eng->gen_galois_keys(std::vector<uint64_t>(g, g + n));
+    });
+}
+int fhe_ctx_load_galois_key(fhe_ctx *ctx, uint64_t g, const uint64_t *key) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(key);
+        if (!(g & 1) || g >= 2 * (uint64_t)ctx->eng->params().n) throw std::invalid_argument("galois element must be odd and < 2n");
+        ctx->eng->load_galois(g, key);
+    });
+}
+int fhe_pt_encode_complex(fhe_ctx *ctx, const double *re, const double *im, int len, int slots, int level,
+                          double scale, fhe_pt **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(re);
+        NEED(im);
+        NEED(out);
+        if (level < 0 || level > ctx->eng->params().L) throw std::invalid_argument("level out of range");
+        std::vector<std::complex<double>> v;
+        for (int i = 0; i < len; ++i) v.emplace_back(re[i], im[i]);
+        *out = new fhe_pt{ctx->eng->encode_complex(v, slots, level, scale)};
+    });
+}
+
 int fhe_kway_sort_type(int k, int M, int stage, int *m, int *log_dist, int *slope) {
     return guard([&] {
         NEED(m);

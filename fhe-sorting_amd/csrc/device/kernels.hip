@@ -290,6 +290,27 @@ __global__ __launch_bounds__(NT) void k_signed_to_rns(u64 *out, const int64_t *c
     }
     out[(size_t)l * n + k] = r;
 }
+// ModRaise: out[z][l][k] = centred(in[z][k] mod q_src) mod q_l  (in: coefficient form,
+// values in [0, 2 q_src); the centred lift of x > q_src / 2 is x - q_src)
+__global__ __launch_bounds__(NT) void k_lift_centered(u64 *out, const u64 *in, size_t seg_in, size_t seg_out,
+                                                      int src, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const u64 qs = mods[src].q;
+    u64 x = in[(size_t)blockIdx.z * seg_in + k];
+    if (x >= qs) x -= qs;
+    const Mod m = mods[l];
+    u64 r;
+    if (x > qs / 2) {
+        r = reduce64(qs - x, m);
+        r = r ? m.q - r : 0;
+    } else {
+        r = reduce64(x, m);
+    }
+    out[(size_t)blockIdx.z * seg_out + (size_t)l * n + k] = r;
+}
 __global__ __launch_bounds__(NT) void k_reduce(u64 *x, Seg S, const Mod *mods, int logN) {
     EW_PROLOGUE
     const Mod m = mods[l];
@@ -703,6 +724,12 @@ void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap,
                       hipStream_t st) {
     if (limbs <= 0) return;
     hipLaunchKernelGGL(k_signed_to_rns, pt_grid(logN, limbs, 1), dim3(NT), 0, st, out, coef, pmap, mods, logN);
+}
+void ew_lift_centered(u64 *out, const u64 *in, int src, int limbs, int segs, size_t seg_in, size_t seg_out,
+                      const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    hipLaunchKernelGGL(k_lift_centered, pt_grid(logN, limbs, segs), dim3(NT), 0, st, out, in, seg_in, seg_out, src,
+                       mods, logN);
 }
 void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st) {
     if (limbs <= 0 || segs <= 0) return;

@@ -186,6 +186,10 @@ void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, i
                     size_t seg_acc, size_t seg_add, const u64 *pinv, const u64 *pinv_s, const Mod *mods, int logN,
                     hipStream_t st);
 
+// ModRaise: out[z][l][k] = centred lift of in[z][k] (a residue mod prime `src`,
+// coefficient form, < 2 q_src) reduced mod q_l for l < limbs
+void ew_lift_centered(u64 *out, const u64 *in, int src, int limbs, int segs, size_t seg_in, size_t seg_out,
+                      const Mod *mods, int logN, hipStream_t st);
 // u64 all-reduce fix-up: x mod q_l per limb
 void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st);
 

@@ -561,12 +561,17 @@ void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out) {
 }
 
 void Engine::gen_rotation_keys(const std::vector<int> &rot) {
+    std::vector<u64> gs;
+    for (int k : rot) gs.push_back(host::galois_for_rotation(impl->P.logN, k));
+    gen_galois_keys(gs);
+}
+
+void Engine::gen_galois_keys(const std::vector<u64> &gs) {
     auto &I = *impl;
     const size_t n = I.n(), nq = I.P.nq(), nall = I.P.nall();
     if (!I.ks->s_ntt) throw std::runtime_error("gen_rotation_keys: no secret key (call keygen)");
     auto sp = I.alloc(nq * n * 8);
-    for (int k : rot) {
-        const u64 g = host::galois_for_rotation(I.P.logN, k);
+    for (u64 g : gs) {
         if (g == 1 || I.ks->rotkeys.count(g)) continue;
         dev::ew_permute(static_cast<u64 *>(sp->p), static_cast<const u64 *>(I.ks->s_ntt->p), I.perm(g), (int)nq, 1, dev::Seg{0, 0, 0},
                         I.P.logN, I.st);
@@ -603,6 +608,14 @@ void Engine::load_rotation(long k, const u64 *key) {
     HIP_OK(hipMemcpy(m->p, key, bytes, hipMemcpyHostToDevice));
     I.ks->rotkeys[g] = m;
 }
+void Engine::load_galois(u64 g, const u64 *key) {
+    auto &I = *impl;
+    const size_t bytes = (size_t)I.key_digits * 2 * I.P.nall() * I.n() * 8;
+    auto m = I.alloc(bytes);
+    HIP_OK(hipMemcpy(m->p, key, bytes, hipMemcpyHostToDevice));
+    I.ks->rotkeys[g] = m;
+}
+bool Engine::has_galois_key(u64 g) const { return impl->ks->rotkeys.count(g) > 0; }
 bool Engine::has_rotation_key(long k) const {
     return impl->ks->rotkeys.count(host::galois_for_rotation(impl->P.logN, k)) > 0;
 }
@@ -620,6 +633,25 @@ PtPtr Engine::encode_scaled(const std::vector<double> &v, int slots, int level, 
     auto &I = *impl;
     const size_t n = I.n(), ell = I.P.limbs_at(level);
     auto coef = host::encode_coeffs(v, n, slots, scale);
+    auto cm = I.alloc(n * 8);
+    HIP_OK(hipMemcpyAsync(cm->p, coef.data(), n * 8, hipMemcpyHostToDevice, I.st));
+    auto pt = std::make_shared<Plaintext>();
+    pt->mem = I.alloc(ell * n * 8);
+    pt->data = static_cast<u64 *>(pt->mem->p);
+    pt->level = level;
+    pt->slots = slots;
+    pt->scale = scale;
+    pt->limbs = ell;
+    dev::ew_signed_to_rns(pt->data, static_cast<int64_t *>(cm->p), (int)ell, nullptr, I.mods, I.P.logN, I.st);
+    dev::ntt_forward(pt->data, (int)ell, 1, 0, nullptr, I.T, I.st);
+    HIP_OK(hipStreamSynchronize(I.st));  // `coef` (pageable host) must outlive the copy
+    return pt;
+}
+
+PtPtr Engine::encode_complex(const std::vector<std::complex<double>> &v, int slots, int level, double scale) {
+    auto &I = *impl;
+    const size_t n = I.n(), ell = I.P.limbs_at(level);
+    auto coef = host::encode_coeffs_complex(v, n, slots, scale);
     auto cm = I.alloc(n * 8);
     HIP_OK(hipMemcpyAsync(cm->p, coef.data(), n * 8, hipMemcpyHostToDevice, I.st));
     auto pt = std::make_shared<Plaintext>();
@@ -1002,18 +1034,29 @@ CtPtr Engine::square(const Ciphertext &a) { return mul(a, a); }
 
 std::vector<CtPtr> Engine::rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks) {
     auto &I = *impl;
+    std::vector<u64> gs;
+    for (long k : ks) {
+        const u64 g = host::galois_for_rotation(I.P.logN, k);
+        if (g != 1 && !I.ks->rotkeys.count(g)) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
+        gs.push_back(g);
+    }
+    return apply_galois_hoisted(a, gs);
+}
+CtPtr Engine::conjugate(const Ciphertext &a) { return apply_galois_hoisted(a, {2 * (u64)n() - 1})[0]; }
+
+std::vector<CtPtr> Engine::apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs) {
+    auto &I = *impl;
     const size_t nn = n(), ell = a.limbs, ln = ell * nn;
     const int B = a.batch;
     std::vector<CtPtr> outs;
     std::shared_ptr<DevMem> extm;
-    for (long k : ks) {
-        const u64 g = host::galois_for_rotation(I.P.logN, k);
+    for (u64 g : gs) {
         if (g == 1) {
             outs.push_back(clone(a));
             continue;
         }
         auto it = I.ks->rotkeys.find(g);
-        if (it == I.ks->rotkeys.end()) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
+        if (it == I.ks->rotkeys.end()) throw NoKeyError("rotate: no key for galois element " + std::to_string(g));
         if (!extm) extm = I.modup(a.data + ln, ell, B, 2 * ln);  // c1 of every member
         ctr.keyswitch += B;
         ctr.rotations += B;
@@ -1030,6 +1073,21 @@ std::vector<CtPtr> Engine::rotate_hoisted(const Ciphertext &a, const std::vector
     return outs;
 }
 CtPtr Engine::rotate(const Ciphertext &a, long k) { return rotate_hoisted(a, {k})[0]; }
+
+CtPtr Engine::mod_raise(const Ciphertext &a) {
+    auto &I = *impl;
+    if (a.limbs != 1) throw std::invalid_argument("mod_raise: input must be at the last level (one limb)");
+    const size_t nn = n(), nq = I.P.nq();
+    const int segs = 2 * a.batch;
+    auto cm = I.alloc((size_t)segs * nn * 8);
+    u64 *c = static_cast<u64 *>(cm->p);
+    dev::ntt_inverse_from(c, a.data, nn, 1, segs, nn, nullptr, I.T, ST);
+    auto r = new_ct(0, a.slots, I.P.delta[0], nq, a.batch);
+    dev::ew_lift_centered(r->data, c, 0, (int)nq, segs, nn, nq * nn, MODS, LOGN, ST);
+    dev::ntt_forward(r->data, (int)nq, segs, nq * nn, nullptr, I.T, ST);
+    count_bytes(2.0 + 2.0 * nq, a.batch);
+    return r;
+}
 
 CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c, int target) {
     auto &I = *impl;

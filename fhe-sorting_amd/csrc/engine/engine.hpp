@@ -12,6 +12,7 @@
 // EvalFastRotation/EvalChebyshevSeriesPS, called from src/sign.cpp,
 // src/comparison.cpp, src/rotation.h and src/sort_algo.h).
 #pragma once
+#include <complex>
 #include <cstddef>
 #include <cstdint>
 #include <memory>
@@ -97,11 +98,16 @@ class Engine {
     void load_relin(const u64 *key);              // [digits][2][nall][n]
     void load_rotation(long k, const u64 *key);   // [digits][2][nall][n]
     bool has_rotation_key(long k) const;
+    // keys of arbitrary automorphisms X -> X^g (rotations: g = 5^k; conjugation: 2n - 1)
+    void gen_galois_keys(const std::vector<u64> &gs);
+    void load_galois(u64 g, const u64 *key);      // [digits][2][nall][n]
+    bool has_galois_key(u64 g) const;
     size_t key_bytes() const;
 
     // ------------------------------------------------- encode / encrypt ---
     PtPtr encode(const std::vector<double> &v, int slots, int level);
     PtPtr encode_scaled(const std::vector<double> &v, int slots, int level, double scale);
+    PtPtr encode_complex(const std::vector<std::complex<double>> &v, int slots, int level, double scale);
     CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
     CtPtr encrypt_pt(const Plaintext &pt);
     // OpenFHE FLEXIBLEAUTOEXT-style encryption: one extra level absorbs the
@@ -141,6 +147,12 @@ class Engine {
     CtPtr square(const Ciphertext &a);
     CtPtr rotate(const Ciphertext &a, long k);
     std::vector<CtPtr> rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks);
+    // keyed automorphisms sharing one ModUp; conjugate = g 2n - 1
+    std::vector<CtPtr> apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs);
+    CtPtr conjugate(const Ciphertext &a);
+    // ModRaise (bootstrapping): last-level ciphertext (one limb) re-read over
+    // every Q prime by the centred lift; level 0, scale Delta_0
+    CtPtr mod_raise(const Ciphertext &a);
     CtPtr rescale(const Ciphertext &a);
     CtPtr drop_to(const Ciphertext &a, int level);
     CtPtr linear_sum_to(const std::vector<const Ciphertext *> &xs, const std::vector<double> &c, int target);

@@ -275,17 +275,28 @@ void special_fft(std::vector<cd> &v, const Emb &E, size_t n) {
 }  // namespace
 
 std::vector<i64> encode_coeffs(const std::vector<double> &v, size_t n, int slots, double scale) {
+    std::vector<cd> z;
+    for (size_t i = 0; i < v.size() && i < (size_t)std::max(slots, 0); ++i) z.push_back(cd(v[i], 0));
+    return encode_coeffs_complex(z, n, slots, scale);
+}
+
+std::vector<i64> encode_coeffs_complex(const std::vector<std::complex<double>> &v, size_t n, int slots,
+                                       double scale) {
     if (slots <= 0 || (slots & (slots - 1)) || (size_t)slots > n / 2)
         throw std::invalid_argument("encode: slots must be a power of two <= n/2");
     const Emb &E = emb_tables(n);
     std::vector<cd> z(slots, cd(0, 0));
-    for (size_t i = 0; i < v.size() && i < (size_t)slots; ++i) z[i] = cd(v[i], 0);
+    for (size_t i = 0; i < v.size() && i < (size_t)slots; ++i) z[i] = v[i];
     special_ifft(z, E, n);
     const size_t gap = n / (2 * (size_t)slots);
     std::vector<i64> coef(n, 0);
+    auto rnd = [](double x) -> i64 {
+        if (!(std::fabs(x) < 9.2e18)) throw std::overflow_error("encode: scaled coefficient exceeds 63 bits");
+        return std::llround(x);
+    };
     for (size_t i = 0; i < (size_t)slots; ++i) {
-        coef[i * gap] = std::llround(z[i].real() * scale);
-        coef[i * gap + n / 2] = std::llround(z[i].imag() * scale);
+        coef[i * gap] = rnd(z[i].real() * scale);
+        coef[i * gap + n / 2] = rnd(z[i].imag() * scale);
     }
     return coef;
 }

@@ -3,6 +3,7 @@
 // -ffp-contract=off so the fp64 encoder rounds deterministically (the spec in
 // DESIGN.md §3 fixes every floating-point step).
 #pragma once
+#include <complex>
 #include <cstddef>
 #include <cstdint>
 #include <map>
@@ -54,6 +55,8 @@ u64 galois_for_rotation(int logN, long k);
 
 // canonical embedding (special FFT, fp64) -> signed integer coefficients
 std::vector<i64> encode_coeffs(const std::vector<double> &v, size_t n, int slots, double scale);
+std::vector<i64> encode_coeffs_complex(const std::vector<std::complex<double>> &v, size_t n, int slots,
+                                       double scale);
 // m0 (and m1 when q1 != 0): message limbs in coefficient form; 2 limbs => CRT lift
 std::vector<double> decode_coeffs(const u64 *m0, const u64 *m1, size_t n, u64 q0, u64 q1, int slots,
                                   double scale);

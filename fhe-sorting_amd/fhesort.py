@@ -130,6 +130,18 @@ _SIGS = {
     'fhe_mehp24_indicator': (C.c_int, [vp, vp, C.c_double, C.c_int, C.c_int, PP]),
     'fhe_kway_sort': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, PP]),
     'fhe_kway_sorter': (C.c_int, [vp, C.c_int, PP, C.c_int, PP, C.c_int, PP]),
+    'fhe_kway_sort_boot': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.POINTER(C.c_int), PP]),
+    'fhe_boot_create': (C.c_int, [vp, vp, PP]),
+    'fhe_boot_destroy': (C.c_int, [vp]),
+    'fhe_boot_keygen': (C.c_int, [vp]),
+    'fhe_boot_rotation_indices': (C.c_int, [vp, C.POINTER(C.c_int32), C.c_int]),
+    'fhe_boot_depth': (C.c_int, [vp]),
+    'fhe_bootstrap': (C.c_int, [vp, vp, PP]),
+    'fhe_bootstrap_stage': (C.c_int, [vp, vp, C.c_int, PP]),
+    'fhe_conjugate': (C.c_int, [vp, vp, PP]),
+    'fhe_gen_galois_keys': (C.c_int, [vp, u64p, C.c_int]),
+    'fhe_ctx_load_galois_key': (C.c_int, [vp, C.c_uint64, u64p]),
+    'fhe_pt_encode_complex': (C.c_int, [vp, dp, dp, C.c_int, C.c_int, C.c_int, C.c_double, PP]),
     'fhe_kway_sort_type': (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                      C.POINTER(C.c_int)]),
     'fhe_kway_stage_count': (C.c_int, [C.c_int, C.c_int]),
@@ -228,6 +240,61 @@ class RotationTree:
         return dict(zip(('fast', 'normal', 'total', 'cache_hits', 'cache_misses'), (int(x) for x in v)))
 
 
+class BootParams(C.Structure):
+    """fhe_boot_params (include/fhe_gpu.h)"""
+    _fields_ = [('slots', C.c_int), ('level_budget_enc', C.c_int), ('level_budget_dec', C.c_int),
+                ('K', C.c_int), ('r', C.c_int), ('degree', C.c_int), ('correction_bits', C.c_int)]
+
+
+class Bootstrapper:
+    """EvalBootstrapSetup(levelBudget, {0, 0}, slots) / EvalBootstrapKeyGen /
+    EvalBootstrap on the GPU (fhe_boot_*; tests/k-way/KWaySort235Test.cpp:46-48)."""
+
+    def __init__(self, ctx, slots, budget=(4, 4), K=512, r=6, degree=88, correction_bits=11, keygen=True):
+        p = BootParams(slots, budget[0], budget[1], K, r, degree, correction_bits)
+        out = C.c_void_p()
+        _chk(lib().fhe_boot_create(ctx.h, C.byref(p), C.byref(out)))
+        self.ctx, self.h = ctx, out.value
+        ctx._boots.append(self)
+        if keygen:
+            self.keygen()
+
+    def close(self):
+        if getattr(self, 'h', None):
+            lib().fhe_boot_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def keygen(self):
+        _chk(lib().fhe_boot_keygen(self.h))
+
+    @property
+    def depth(self):
+        return lib().fhe_boot_depth(self.h)
+
+    def rotations(self):
+        out = np.zeros(4096, dtype=np.int32)
+        m = lib().fhe_boot_rotation_indices(self.h, out.ctypes.data_as(C.POINTER(C.c_int32)), 4096)
+        if m < 0:
+            _chk(-m)
+        return [int(x) for x in out[:m]]
+
+    def bootstrap(self, x, stage=0):
+        out = C.c_void_p()
+        _chk(lib().fhe_bootstrap_stage(self.h, x.h, stage, C.byref(out)))
+        return Ct(self.ctx, out.value)
+
+    def mod_raise(self, x): return self.bootstrap(x, 4)
+    def coeffs_to_slots(self, x): return self.bootstrap(x, 1)
+    def eval_mod(self, x): return self.bootstrap(x, 2)
+    def slots_to_coeffs(self, x): return self.bootstrap(x, 3)
+
+
 class Ct:
     def __init__(self, ctx, h):
         self.ctx, self.h = ctx, h
@@ -282,6 +349,7 @@ class Context:
 
     def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, device=0, keygen=True):
         self.logN, self.n, self.L = logN, 1 << logN, L
+        self._boots = []
         p = Params(logN, L, scale_bits, first_bits, dnum, seed)
         h = C.c_void_p()
         _chk(lib().fhe_ctx_create(C.byref(p), device, C.byref(h)))
@@ -296,6 +364,8 @@ class Context:
             self.keygen()
 
     def close(self):
+        for b in getattr(self, '_boots', []):  # bootstrappers refer to the context
+            b.close()
         if getattr(self, 'h', None):
             lib().fhe_ctx_destroy(self.h)
             self.h = None
@@ -340,8 +410,29 @@ class Context:
         ia = np.asarray(idx, dtype=np.int32)
         _chk(lib().fhe_ctx_load_keys(self.h, _u64(rl), _int(ia), arr, len(keys)))
 
+    def load_galois_keys_from(self, orc, gs):
+        """Upload the oracle's keys of galois elements gs (conjugation: 2n - 1)."""
+        for g in gs:
+            key = orc.galois_key(g)
+            if key is not None:
+                _chk(lib().fhe_ctx_load_galois_key(self.h, int(g), _u64(np.ascontiguousarray(key))))
+
+    def gen_galois_keys(self, gs):
+        g = np.asarray(gs, dtype=np.uint64)
+        _chk(lib().fhe_gen_galois_keys(self.h, _u64(g), len(g)))
+
     def key_bytes(self):
         return lib().fhe_key_bytes(self.h)
+
+    def encode_complex(self, v, slots, level, scale=None):
+        v = np.asarray(v, dtype=np.complex128)
+        re, im = np.ascontiguousarray(v.real), np.ascontiguousarray(v.imag)
+        scale = self.delta[level] if scale is None else scale
+        out = C.c_void_p()
+        _chk(lib().fhe_pt_encode_complex(self.h, _dbl(re), _dbl(im), len(v), slots, level, scale, C.byref(out)))
+        return Pt(self, out.value)
+
+    def conjugate(self, a): return self._new(lib().fhe_conjugate, a.h)
 
     # objects ------------------------------------------------------------
     def encode(self, v, slots, level=0):
@@ -475,10 +566,16 @@ class Context:
     def mehp24_indicator(self, x, b, dg, df):
         return self._new(lib().fhe_mehp24_indicator, x.h, b, dg, df)
 
-    def kway_sort(self, x, k, M, cfg):
-        """kwaySort::Sorter::sorter via KWayAdapter<k^M>::sort (no bootstrapping);
-        cfg = (3, dg, df)."""
-        return self._new(lib().fhe_kway_sort, x.h, k, M, cfg[1], cfg[2])
+    def kway_sort(self, x, k, M, cfg, boot=None):
+        """kwaySort::Sorter::sorter via KWayAdapter<k^M>::sort; cfg = (3, dg, df).
+        boot: a Bootstrapper (checkLevelAndBoot + compositeSign's lazy bootstrap);
+        the number of checkLevelAndBoot bootstraps is left in self.kway_bootstraps."""
+        if boot is None:
+            return self._new(lib().fhe_kway_sort, x.h, k, M, cfg[1], cfg[2])
+        nb = C.c_int()
+        out = self._new(lib().fhe_kway_sort_boot, x.h, k, M, cfg[1], cfg[2], boot.h, C.byref(nb))
+        self.kway_bootstraps = nb.value
+        return out
 
     def kway_sorter(self, kk, xs, cmps):
         """SortUtils::fcnL (kk = 1) or the kk-sorter (kk = 2..5): ascending outputs."""

@@ -39,6 +39,7 @@ enum {
 typedef struct fhe_ctx fhe_ctx;
 typedef struct fhe_ct fhe_ct;
 typedef struct fhe_pt fhe_pt;
+typedef struct fhe_boot fhe_boot;
 
 /* CCParams<CryptoContextCKKSRNS> subset used by the sort path
  * (tests/DirectSortTest.cpp:24-31; src/sort_algo.h:87-201) */
@@ -244,11 +245,17 @@ int fhe_mehp24_indicator(fhe_ctx *ctx, const fhe_ct *x, double b, int dg, int df
  * KWayAdapter<N>::sort (src/kway_adapter.h:65-71): sorts the N = k^M values in
  * the first slots of x (k in {2, 3, 5}; x holds next_pow2(N) slots), comparator
  * CompositeSign(3, dg, df) (the reference tests' CompositeSignConfig(3, d_f, d_g)
- * order: tests/k-way/KWaySort2Test.cpp:149).  Bootstrapping is not built: where
- * the reference calls EvalBootstrap (EvalUtils::checkLevelAndBoot,
- * src/k-way/EvalUtils.cpp:59-86) the context must still hold the levels,
- * otherwise FHE_EDEPTH.  Rotation keys: fhe_kway_rotation_indices(N). */
+ * order: tests/k-way/KWaySort2Test.cpp:149).  Without a bootstrapper the
+ * context must hold every level (no EvalBootstrap at EvalUtils::
+ * checkLevelAndBoot, src/k-way/EvalUtils.cpp:59-86), otherwise FHE_EDEPTH.
+ * Rotation keys: fhe_kway_rotation_indices(N). */
 int fhe_kway_sort(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int df, fhe_ct **out);
+/* the same with bootstrapping (KWaySort235Test's context, tests/k-way/
+ * KWaySort235Test.cpp:18-51): checkLevelAndBoot and compositeSign's lazy
+ * bootstrap (src/sign.cpp:164-170) call fhe_bootstrap(boot); boot's slots
+ * must equal x's.  bootstraps (may be NULL): checkLevelAndBoot bootstraps done. */
+int fhe_kway_sort_boot(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int df, fhe_boot *boot,
+                       int *bootstraps, fhe_ct **out);
 /* SortUtils::fcnL (kk = 1: out[0] = fcnL(x0, x1, cmp0) = cmp*(x0-x1)+x1,
  * src/k-way/SortUtils.cpp:5-16) or the kk-sorter for kk = 2..5
  * (SortUtils.cpp:32-208): nx = kk inputs, ncmp = kk(kk-1)/2 comparison
@@ -269,6 +276,45 @@ int fhe_kway_gen_indices(int num_slots, int k, int M, int m, int log_dist, int s
 /* KWayAdapter<N>::getSizeParameters rotation set (+-2^i < N, src/kway_adapter.h:45-49);
  * returns the count (< 0: error) */
 int fhe_kway_rotation_indices(int N, int32_t *rots, int max_rots);
+
+/* ---------------------------------------------------- CKKS bootstrapping */
+/* FHECKKSRNS::EvalBootstrapSetup(levelBudget, {0, 0}, numSlots) as the
+ * reference calls it (tests/k-way/KWaySort235Test.cpp:46-47, level budgets from
+ * KWayAdapter<N>::getSizeParameters, src/kway_adapter.h:55-62).  Sparse packing:
+ * slots a power of two in [2, n/4].  EvalMod range K (|t/q0| <= K; 512 for the
+ * uniform ternary secret), r double angles, cosine degree (EvalMod coefficients
+ * evalmod_k<K>r<r>_<degree>.f64 in the coefficient directory), correction_bits:
+ * the message is scaled to q0 2^-bits before ModRaise.  Zero fields take the
+ * defaults {budget 4/4, K 512, r 6, degree 88, bits 11}.  The bootstrapper
+ * refers to ctx: destroy it first. */
+typedef struct {
+    int slots;
+    int level_budget_enc, level_budget_dec;
+    int K, r, degree, correction_bits;
+} fhe_boot_params;
+int fhe_boot_create(fhe_ctx *ctx, const fhe_boot_params *p, fhe_boot **out);
+int fhe_boot_destroy(fhe_boot *b);
+/* EvalBootstrapKeyGen(sk, numSlots) (KWaySort235Test.cpp:48): the rotation keys
+ * of the trace and linear transforms plus the conjugation key, on the GPU */
+int fhe_boot_keygen(fhe_boot *b);
+/* the rotation indices fhe_boot_keygen generates (returns the count, < 0: error) */
+int fhe_boot_rotation_indices(const fhe_boot *b, int32_t *rots, int max_rots);
+/* output level of fhe_bootstrap (levels the bootstrap consumes from the top) */
+int fhe_boot_depth(const fhe_boot *b);
+/* CryptoContext::EvalBootstrap(ct) (src/k-way/EvalUtils.cpp:76, src/sign.cpp:168):
+ * x at level <= mult_depth - 1 with the setup's slots; out at fhe_boot_depth */
+int fhe_bootstrap(fhe_boot *b, const fhe_ct *x, fhe_ct **out);
+/* the stages alone (parity tests): 1 CoeffsToSlots of a raised ciphertext
+ * (+ conjugate-add), 2 EvalMod, 3 SlotsToCoeffs, 4 ModRaise */
+int fhe_bootstrap_stage(fhe_boot *b, const fhe_ct *x, int stage, fhe_ct **out);
+/* EvalConjugate-style keyed automorphism X -> X^(2n-1) */
+int fhe_conjugate(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out);
+/* keys of arbitrary galois elements g (odd, < 2n); load one generated elsewhere */
+int fhe_gen_galois_keys(fhe_ctx *ctx, const uint64_t *g, int n);
+int fhe_ctx_load_galois_key(fhe_ctx *ctx, uint64_t g, const uint64_t *key);
+/* MakeCKKSPackedPlaintext of complex slot values at an explicit scale */
+int fhe_pt_encode_complex(fhe_ctx *ctx, const double *re, const double *im, int len, int slots, int level,
+                          double scale, fhe_pt **out);
 
 /* ------------------------------------------------------ multi-GPU (RCCL) */
 int fhe_comm_get_unique_id(uint8_t id[128]);

@@ -21,7 +21,10 @@
 //   5. EvalMod: Chebyshev series of cos(2 pi (K u - 1/4) / 2^r), r double
 //      angles -> sin(2 pi t / q0)
 //   6. SlotsToCoeffs: (lo + i hi) and the butterflies of emb, merged into
-//      budget_dec levels, scaled by 2^b / (2 pi)
+//      budget_dec levels, scaled by 2^b / (4 pi), then x + conj(x): the
+//      output slots are real (OpenFHE's CKKS bootstrap handles real data;
+//      an imaginary part left in would be amplified by every later sign
+//      polynomial, which sees complex slots)
 //
 // Every plaintext diagonal is computed here in fp64 with a fixed operation
 // order; the engine's bootstrap (fhe-sorting_amd/csrc/algo/bootstrap.cpp)
@@ -203,7 +206,9 @@ Bootstrapper::Bootstrapper(Context &c, const BootConfig &cf) : cc(c), cfg(cf) {
     }
     const double q0 = (double)cc.P.primes[0];
     const double c_enc = cc.delta(0) / ((double)n * q0 * (double)cfg.K);
-    const double c_dec = std::ldexp(1.0, cfg.correction_bits) / (2.0 * M_PI);
+    // SlotsToCoeffs: sin(2 pi t / q0) ~ 2 pi 2^-b m -> m / 2 (the final
+    // x + conj(x) keeps the real part, as OpenFHE's bootstrap returns real slots)
+    const double c_dec = std::ldexp(1.0, cfg.correction_bits) / (4.0 * M_PI);
     const auto ge = split_levels(logs, cfg.budget_enc), gd = split_levels(logs, cfg.budget_dec);
     int t = 0;
     for (size_t li = 0; li < ge.size(); ++li) {
@@ -313,6 +318,7 @@ CtPtr Bootstrapper::eval_mod(const Ciphertext &x) {
 CtPtr Bootstrapper::slots_to_coeffs(const Ciphertext &x) {
     CtPtr y = stc_int > 1 ? cc.mul_int(x, stc_int) : cc.clone(x);
     for (size_t i = 0; i < stc.size(); ++i) y = linear(*y, stc[i], 100 + (int)i);
+    y = cc.add(*y, *cc.conjugate(*y));  // real part: imaginary noise must not reach the next polynomial
     y->slots = cfg.slots;
     return y;
 }
