@@ -17,6 +17,11 @@ summed by one RCCL all-reduce each (u64 sum + mod q) -- strong scaling.
 --workload mehp24: MEHP24 sortLargeArrayFG of N=4096 at ring 2^17 (BASELINE
 config 5), pair compares and indicators sharded over ranks.
 
+--workload kway: the k-way sorting network with bootstrapping, k=5, N=3125 at
+ring 2^16 (BASELINE config 4; KWaySort235Test's context: depth 40, scale 2^59,
+levelBudget {5,5}).  The network is one chain of stages on one ciphertext, so
+it does not shard: --gpus N runs N independent replicas (weak scaling).
+
 Output: one JSON line.  value = ciphertext-mults/s (relinearised ct x ct
 products, incl. those in the Chebyshev PS, summed over ranks / wall time);
 ms_per_step = sort wall time.  Also: roofline of the dominant kernel (HIP
@@ -43,9 +48,11 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--workload', choices=('direct', 'mehp24'), default='direct',
+    ap.add_argument('--workload', choices=('direct', 'mehp24', 'kway'), default='direct',
                     help='direct: DirectSort rank sort (the BASELINE metric); mehp24: MEHP24 sortLargeArrayFG '
-                         '(BASELINE config 5, ring 2^17)')
+                         '(BASELINE config 5, ring 2^17); kway: k-way network with bootstrapping (config 4)')
+    ap.add_argument('--kway-k', type=int, default=5)
+    ap.add_argument('--kway-m', type=int, default=5)
     ap.add_argument('--n-sort', type=int, default=None, help='values to sort (default 1024; mehp24: 4096)')
     ap.add_argument('--log-n', type=int, default=16)
     ap.add_argument('--seed', type=int, default=20250704)
@@ -369,11 +376,130 @@ def run_mehp24(a, d):
     d.barrier()
 
 
+def kway_dg(N):  # d_g of KWaySort235Test (tests/k-way/KWaySort235Test.cpp:97-222)
+    return 2 if N <= 16 else 3 if N <= 125 else 4 if N <= 512 else 5
+
+
+def cpu_bootstrap_baseline(logN, depth, slots, budget):
+    """CPU oracle on a bounded sample of the workload: the EvalMod step of one
+    bootstrap (Chebyshev degree 88 + 6 double angles: 26 relinearised products
+    from level budget_enc down) at the workload's parameters, host cores.  (A
+    whole bootstrap would first need ~50 rotation keys generated on the CPU.)"""
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import pyoracle as O
+    orc = O.Context(logN, depth, 59, 60, 3, seed=7)
+    B = O.Bootstrapper(orc, slots, budget, keygen=False)
+    x = orc.encrypt(np.random.default_rng(1).uniform(-0.5, 0.5, 2 * slots), 2 * slots, level=budget[0])
+    orc.reset_counters()
+    t = time.perf_counter()
+    B.eval_mod(x)
+    dt = time.perf_counter() - t
+    c = orc.counters()
+    return {'value': round(c['hmult'] / dt, 3), 'unit': 'ciphertext-mults/s', 'cores': O.lib().orc_num_threads(),
+            'kind': 'port', 'seconds': round(dt, 2), 'hmults': c['hmult'],
+            'sample': f'EvalMod of one bootstrap at ring 2^{logN}, depth {depth}, from level {budget[0]}'}
+
+
+def run_kway(a, d):
+    """kwaySort::Sorter::sorter via KWayAdapter<N>::sort with bootstrapping
+    (src/k-way/Sorter.cpp:289-404, EvalUtils.cpp:59-86, src/sign.cpp:164-170)
+    in KWaySort235Test's context (tests/k-way/KWaySort235Test.cpp:18-51,
+    src/kway_adapter.h:41-63) at ring 2^16 (BASELINE config 4).  Replicas only:
+    each rank sorts its own ciphertext."""
+    k, M = a.kway_k, a.kway_m
+    N = k ** M
+    s = 1
+    while s < N:
+        s *= 2
+    budget = (4, 4) if N <= 128 else (5, 5)
+    cfg = (3, 2, kway_dg(N))  # CompositeSignConfig(3, d_f, d_g): dg = d_f = 2, df = d_g
+    logN, depth = a.log_n, 40
+    t0 = time.time()
+    ctx = F.Context(logN, depth, 59, 60, 3, seed=a.seed + d.rank, device=d.device)
+    B = F.Bootstrapper(ctx, s, budget)
+    ctx.gen_rotation_keys(F.kway_rotation_indices(N))
+    x = np.random.default_rng(a.seed + d.rank).permutation(N) * (1 - 1e-8) / N  # getVectorWithMinDiff
+    ct = ctx.encrypt(x, s)
+    setup_s = time.time() - t0
+
+    def run():
+        return ctx.kway_sort(ct, k, M, cfg, boot=B)
+
+    out = None
+    for _ in range(a.warmup):
+        out = run()
+    device_sync(ctx)
+    d.barrier()
+    ctx.reset_counters()
+    device_sync(ctx)
+    d.barrier()
+    t = time.perf_counter()
+    for _ in range(a.steps):
+        out = run()
+    device_sync(ctx)
+    d.barrier()
+    dt = d.max(time.perf_counter() - t)
+    cnt = ctx.counters()
+    boots = ctx.kway_bootstraps
+    peak_gb = ctx.pool_stats()['peak'] / 1e9
+    hm_total = d.sum(cnt['hmult'])
+    ks_total = d.sum(cnt['keyswitch'])
+    op_total = d.sum(cnt['opbytes'])
+    y = ctx.decrypt(out)[:N]
+    err = d.max(float(np.max(np.abs(y - np.sort(x)))))
+    if d.rank == 0:
+        ms = dt / a.steps * 1e3
+        res = {
+            'metric': f'k-way encrypted sort seconds + ciphertext-mults/sec, k={k}, N={N} @ ringDim 2^{logN}',
+            'value': round(hm_total / dt, 2),
+            'unit': 'ciphertext-mults/s',
+            'n_gpus': d.world,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': round(ms, 2),
+            'sort_seconds': round(ms / 1e3, 4),
+            'sorts_per_s': round(d.world * a.steps / dt, 4),
+            'keyswitches_per_s': round(ks_total / dt, 2),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'u64',
+            'data': 'synthetic: seeded permutation of {k/N} per rank, keys and encryption from a seeded PRNG',
+            'config': {'workload': f'k-way network k={k}, M={M} (N={N}, {s} slots), ringDim 2^{logN}, depth {depth}, '
+                                   f'scale 2^59, levelBudget {budget}, CompositeSign{cfg}, bootstrapping',
+                       'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'slots': s,
+                       'parallelism': f'replicas x{d.world}', 'collective': 'none'},
+            'max_abs_err': err,
+            'output_level': out.level,
+            'hmult_per_sort': int(hm_total / a.steps / d.world),
+            'checklevel_bootstraps_per_sort': boots,
+            'bootstrap_depth': B.depth,
+            'setup_s': round(setup_s, 1),
+            'hbm_peak_gb_rank0': round(peak_gb, 1),
+            'roofline': None,
+        }
+        if not a.no_roofline:
+            try:
+                res['roofline'] = with_run(roofline(ctx, run, a.clock_json, 'pmc_traffic_kway.json'),
+                                           res['ms_per_step'], 1, op_total / a.steps / d.world)
+            except Exception as e:  # never hide the main number
+                res['roofline'] = {'error': str(e)}
+        if d.world == 1 and not a.no_cpu_baseline:
+            try:
+                res['cpu_baseline'] = cpu_bootstrap_baseline(logN, depth, s, budget)
+            except Exception as e:
+                res['cpu_baseline'] = {'error': str(e)}
+        print(json.dumps(res), flush=True)
+    d.barrier()
+
+
 def main():
     a = parse()
     d = Dist(a.gpus)
     if a.workload == 'mehp24':
         return run_mehp24(a, d)
+    if a.workload == 'kway':
+        return run_kway(a, d)
     N, logN = a.n_sort or 1024, a.log_n
     depth, rots = F.size_parameters(N)
     cfg = sign_cfg(N)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# k-way (config 4) bench line + rocprof kernel trace of one sort
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$R"
+TAG=${1:-kway}; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_bootstrap.py -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 600 python bench.py --workload kway --clock-json $O/clock.json "$@" > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/trace" -o run -- python3 "$R/bench.py" --workload kway --steps 1 --warmup 0 --no-cpu-baseline --no-roofline > $O/trace.log 2>&1 || { echo "trace failed"; tail -5 $O/trace.log; exit 1; }
+python scripts/trace_summary.py $O/trace/run_kernel_trace.csv > $O/trace_summary.txt && head -30 $O/trace_summary.txt
+gzip -f $O/trace/run_kernel_trace.csv
+echo ALLOK

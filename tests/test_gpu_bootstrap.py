@@ -129,3 +129,23 @@ def test_kway_with_bootstrap_sorts(k, M, cfg):
         assert np.max(np.abs(gpu.decrypt(out)[:N] - np.sort(x))) < 0.01
     finally:
         gpu.close()
+
+
+def test_config4_kway_k5_n3125_ring16():
+    """BASELINE config 4: k = 5, N = 3125 (KWaySort235Test's commented-out
+    case, tests/k-way/KWaySort235Test.cpp:88,213-218) at ring 2^16 with the
+    reference context (depth 40, scale 2^59, levelBudget {5,5}, d_g = 5)."""
+    k, M = 5, 5
+    N = k ** M
+    gpu = F.Context(16, 40, 59, 60, 3, seed=2025)
+    try:
+        B = F.Bootstrapper(gpu, 4096, (5, 5))
+        assert B.depth == 23
+        gpu.gen_rotation_keys(F.kway_rotation_indices(N))
+        x = np.random.default_rng(N).permutation(N) * (1 - 1e-8) / N
+        out = gpu.kway_sort(gpu.encrypt(x, 4096), k, M, (3, 2, 5), boot=B)
+        assert gpu.kway_bootstraps > 20
+        err = np.abs(gpu.decrypt(out)[:N] - np.sort(x))
+        assert np.max(err) < 0.01 and np.sum(err >= 0.01) == 0  # KWaySort235Test.cpp:291-292
+    finally:
+        gpu.close()
