@@ -3,7 +3,9 @@
 # two PMC passes (FETCH_SIZE, WRITE_SIZE) over every engine kernel.  The
 # profiled runs use one lane, like bench.py's roofline pass, so per-launch
 # durations and bytes match the live clock's.
-# usage: [PMCOUT=pmc_traffic_mehp24.json] gpu_job_profile.sh TAG [extra bench args]
+# usage: [PMCOUT=pmc_traffic_mehp24.json] [PMC_EXCLUDE=regex] gpu_job_profile.sh TAG [extra bench args]
+# (PMC_EXCLUDE: kernels left out of the counter passes -- the MEHP24 pass dies
+#  inside the profiler's dispatch interception on k_permute at ring 2^17)
 # (PMCOUT: the profiles/ file bench.py reads roofline.traffic from for this workload)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
@@ -18,7 +20,7 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O
 python scripts/trace_summary.py $O/trace/run_kernel_trace.csv > $O/trace_summary.txt && cat $O/trace_summary.txt || exit 1
 gzip -f $O/trace/run_kernel_trace.csv
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 900 rocprofv3 --pmc $C --kernel-include-regex 'k_[a-z]' --output-format csv -d "$R/$O/pmc_$C" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-roofline "$@" --lanes 1 > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -5 $O/pmc_$C.log; exit 1; }
+  timeout -s KILL 900 rocprofv3 --pmc $C --kernel-include-regex 'k_[a-z]' ${PMC_EXCLUDE:+--kernel-exclude-regex "$PMC_EXCLUDE"} --output-format csv -d "$R/$O/pmc_$C" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-roofline "$@" --lanes 1 > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -5 $O/pmc_$C.log; exit 1; }
 done
 python scripts/pmc_summary.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv $O/pmc_traffic.json || exit 1
 gzip -f $O/pmc_*/run_counter_collection.csv

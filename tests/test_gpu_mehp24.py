@@ -88,11 +88,12 @@ def _full(N):
     return x, y, out
 
 
-@pytest.mark.parametrize('N', [16, 256, 512])
+@pytest.mark.parametrize('N', [16, 256, 512, 4096])
 def test_reference_parameters_sort(N):
     """The reference test at its own parameters: N=16 and N=256 (sortFG) and
     N=512 (sortLargeArrayFG, two parts of 256) at ring 2^17, input encrypted
-    FLEXIBLEAUTOEXT-style (OpenFHE's default, which the reference runs under)."""
+    FLEXIBLEAUTOEXT-style (OpenFHE's default, which the reference runs under);
+    N=4096 is BASELINE config 5 (16 parts of 256, ~15 s on one MI355X)."""
     x, y, out = _full(N)
     err = np.max(np.abs(y - np.sort(x)))
     assert err < 0.01, err
