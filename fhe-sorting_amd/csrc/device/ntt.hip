@@ -57,20 +57,38 @@ __device__ __forceinline__ u64 shoup_fold(u64 a, u64 w, u64 wp, u64 nq) {
     const uint32_t cross = a0 * w1 + a1 * w0 + h0 * n1 + h1 * n0;
     return t + ((u64)cross << 32);
 }
-// Harvey lazy forward CT butterfly: x, y in [0, 4q) -> x, y in [0, 4q)
-__device__ __forceinline__ void ct_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2, u64 nq) {
-    u64 u = x;
-    u = u >= q2 ? u - q2 : u;                   // [0, 2q)
-    const u64 v = shoup_fold(y, w.x, w.y, nq);  // [0, 2q)
-    x = u + v;
-    y = u + q2 - v;
+// Butterfly twiddle product with an approximate Shoup quotient: the high half
+// of a * w' drops the a0*w'0 product and the carries of the two cross terms, so
+// the quotient is short by 0..2 and the product lands in [0, 4q) instead of
+// [0, 2q) -- 4 v_mad_u64_u32 + 2 v_mul_hi_u32 instead of 6 + 1 (and fewer
+// moves): the butterfly is VALU-bound, and every prime < 2^60
+// leaves room for the wider lazy ranges below (8q < 2^63).
+__device__ __forceinline__ u64 mulhi_approx(u64 a, u64 b) {
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    return (u64)a1 * b1 + (((u64)a1 * b0) >> 32) + (((u64)a0 * b1) >> 32);
 }
-// lazy inverse GS butterfly: x, y in [0, 2q) -> x, y in [0, 2q)
-__device__ __forceinline__ void gs_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q2, u64 nq) {
+__device__ __forceinline__ u64 shoup_fold4(u64 a, u64 w, u64 wp, u64 nq) {  // [0, 4q) for any a < 2^64
+    const u64 h = mulhi_approx(a, wp);
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+    const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32), n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
+    const u64 t = (u64)a0 * w0 + (u64)h0 * n0;
+    const uint32_t cross = a0 * w1 + a1 * w0 + h0 * n1 + h1 * n0;
+    return t + ((u64)cross << 32);
+}
+// lazy forward CT butterfly: x, y in [0, 8q) -> x, y in [0, 8q)   (q4 = 4q)
+__device__ __forceinline__ void ct_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q4, u64 nq) {
+    u64 u = x;
+    u = u >= q4 ? u - q4 : u;                    // [0, 4q)
+    const u64 v = shoup_fold4(y, w.x, w.y, nq);  // [0, 4q)
+    x = u + v;
+    y = u + q4 - v;
+}
+// lazy inverse GS butterfly: x, y in [0, 4q) -> x, y in [0, 4q)
+__device__ __forceinline__ void gs_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q4, u64 nq) {
     const u64 u = x, v = y;
     u64 s = u + v;
-    x = s >= q2 ? s - q2 : s;
-    y = shoup_fold(u + q2 - v, w.x, w.y, nq);
+    x = s >= q4 ? s - q4 : s;
+    y = shoup_fold4(u + q4 - v, w.x, w.y, nq);
 }
 __device__ __forceinline__ u64 smod64(int64_t v, const Mod &m) {  // signed integer -> [0, q)
     if (v >= 0) return reduce64((u64)v, m);
@@ -82,7 +100,8 @@ __device__ __forceinline__ u64 smod64(int64_t v, int sh, const Mod &m) {  // v *
     for (int i = 0; i < sh; ++i) r = r + r >= m.q ? r + r - m.q : r + r;
     return r;
 }
-__device__ __forceinline__ u64 canon4(u64 x, u64 q, u64 q2) {  // [0, 4q) -> [0, q)
+__device__ __forceinline__ u64 canon8(u64 x, u64 q, u64 q2) {  // [0, 8q) -> [0, q)
+    x = x >= 2 * q2 ? x - 2 * q2 : x;
     x = x >= q2 ? x - q2 : x;
     return x >= q ? x - q : x;
 }
@@ -188,7 +207,7 @@ __device__ constexpr int reg_of(const RowLayout &L, int b) {
 }
 template <bool FWD, int S>
 __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulonglong2 *tw, size_t n, int S0,
-                                          u64 q2, u64 nq) {
+                                          u64 q4, u64 nq) {
     constexpr RowSwap w = FWD ? fwd_swap(S) : inv_swap(S);
     if (w.m >= 0) swap_regs<w.p>(x, t, w.m);
     if (S >= 8) return;  // the forward pass's final fix-up swap
@@ -202,25 +221,25 @@ __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulong
         const int idx0 = li + reg_index(L, j);
         if (FWD) {
             const size_t i = (row << S) + (size_t)(idx0 >> (8 - S));
-            ct_bfly(x[j], x[j + (1 << P)], tw[((size_t)1 << (S0 + S)) + i], q2, nq);
+            ct_bfly(x[j], x[j + (1 << P)], tw[((size_t)1 << (S0 + S)) + i], q4, nq);
         } else {
             const size_t i = (row * 256 + (size_t)idx0) >> (S + 1);
-            gs_bfly(x[j], x[j + (1 << P)], tw[(n >> (S + 1)) + i], q2, nq);
+            gs_bfly(x[j], x[j + (1 << P)], tw[(n >> (S + 1)) + i], q4, nq);
         }
     }
 }
 template <bool FWD>
 __device__ __forceinline__ void row_pass_shfl(u64 *x, int t, size_t row, const ulonglong2 *tw, size_t n, int S0,
-                                              u64 q2, u64 nq) {
-    row_stage<FWD, 0>(x, t, row, tw, n, S0, q2, nq);
-    row_stage<FWD, 1>(x, t, row, tw, n, S0, q2, nq);
-    row_stage<FWD, 2>(x, t, row, tw, n, S0, q2, nq);
-    row_stage<FWD, 3>(x, t, row, tw, n, S0, q2, nq);
-    row_stage<FWD, 4>(x, t, row, tw, n, S0, q2, nq);
-    row_stage<FWD, 5>(x, t, row, tw, n, S0, q2, nq);
-    row_stage<FWD, 6>(x, t, row, tw, n, S0, q2, nq);
-    row_stage<FWD, 7>(x, t, row, tw, n, S0, q2, nq);
-    if (FWD) row_stage<FWD, 8>(x, t, row, tw, n, S0, q2, nq);
+                                              u64 q4, u64 nq) {
+    row_stage<FWD, 0>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 1>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 2>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 3>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 4>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 5>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 6>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 7>(x, t, row, tw, n, S0, q4, nq);
+    if (FWD) row_stage<FWD, 8>(x, t, row, tw, n, S0, q4, nq);
 }
 // in-row index of lane t's register r after a pass (both passes end in this layout)
 template <bool FWD>
@@ -251,7 +270,7 @@ enum { NTT_PLAIN = 0, NTT_LIFT = 1, NTT_RESCALE = 2, NTT_MULTAIL = 3 };
 // ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
 // SH (row passes with PB = 8 only): register-only stages with DPP lane swaps
 // (row_pass_shfl) instead of the two LDS exchanges.
-template <int PB, int EB, bool COLS, int MODE, bool SH>
+template <int PB, int EB, bool COLS, int MODE, bool SH, bool LEAN = false>
 __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
                                              const NttTables &Tb, const NttFuse &F) {
     static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
@@ -285,7 +304,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
                                  : (size_t)blockIdx.y * NB + tr;  // column or row index
     const bool valid = tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs);
     u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
-    const u64 q = Tb.mods[p].q, q2 = 2 * q, nq = (u64)0 - q;
+    const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
     const int S0 = COLS ? 0 : logN - PB;                      // global stage of local stage 0
 
@@ -317,8 +336,9 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // accumulators and d) are loaded now, so the loads overlap the butterflies
     // instead of stalling the store loop (the tile's LDS bounds occupancy, the
     // extra VGPRs do not)
-    constexpr bool EPI_X = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL);
-    constexpr bool EPI_D = !COLS && MODE == NTT_MULTAIL;
+    // LEAN: the operands are loaded in the store loop instead (fewer VGPRs)
+    constexpr bool EPI_X = !LEAN && !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL);
+    constexpr bool EPI_D = !LEAN && !COLS && MODE == NTT_MULTAIL;
     u64 ex[EPI_X ? E : 1], ed[EPI_D ? E : 1];
     if (EPI_X) {
         const size_t lo = (size_t)limb * n + tid_global * LEN;
@@ -336,32 +356,33 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     const u64 c2 = MODE == NTT_MULTAIL ? F.c2[limb] : 0, c2s = MODE == NTT_MULTAIL ? F.c2s[limb] : 0;
     // scaled rescale: out = (K x - v) q_last^-1 = x (K q_last^-1) - v q_last^-1
     const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, F.scalar_sh, mp), c1, c1s, q) : 0;
-    // row-pass store of transform value v (lazy, [0, 4q)) for element r at in-row index idx
+    // row-pass store of transform value v (lazy, [0, 8q)) for element r at in-row index idx
     auto store_row = [&](int r, int idx, u64 v) {
         const size_t z = (size_t)zseg, lo = (size_t)limb * n + tid_global * LEN;
-        // lazy epilogues: v in [0, 4q), every intermediate < 2^64, one final
-        // conditional subtraction (Shoup products of the fold are in [0, 2q))
+        // lazy epilogues: v in [0, 8q), every intermediate < 2^64 (q < 2^60), one
+        // final conditional subtraction (the exact Shoup products are in [0, 2q))
         if (MODE == NTT_RESCALE) {
-            const u64 xin = ex[EPI_X ? r : 0];
+            const u64 xin = EPI_X ? ex[EPI_X ? r : 0] : F.x[z * F.seg_x + lo + idx];
             u64 o;
             if (F.scalar) {  // (K x - v) q_last^-1 = x kq - v c1: [0, q) + 2q - [0, 2q)
                 o = mul_barrett(xin, kq, mp) + q2 - shoup_fold(v, c1, c1s, nq);
                 o = o >= q2 ? o - q2 : o;
-            } else {  // (x - v) q_last^-1
-                o = shoup_fold(xin + 2 * q2 - v, c1, c1s, nq);
+            } else {  // (x - v) q_last^-1, x + 8q - v < 9q
+                o = shoup_fold(xin + 2 * q4 - v, c1, c1s, nq);
             }
             F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
-        } else if (MODE == NTT_MULTAIL) {  // (acc + d c2 - v) c1, acc + d c2 + 4q - v < 7q
-            const u64 acc = ex[EPI_X ? r : 0], dd = ed[EPI_D ? r : 0];
-            const u64 tt = acc + shoup_fold(dd, c2, c2s, nq) + 2 * q2 - v;
+        } else if (MODE == NTT_MULTAIL) {  // (acc + d c2 - v) c1, acc + d c2 + 8q - v < 11q
+            const u64 acc = EPI_X ? ex[EPI_X ? r : 0] : F.x[z * F.seg_x + lo + idx];
+            const u64 dd = EPI_D ? ed[EPI_D ? r : 0] : F.d[z * F.seg_d + lo + idx];
+            const u64 tt = acc + shoup_fold(dd, c2, c2s, nq) + 2 * q4 - v;
             const u64 o = shoup_fold(tt, c1, c1s, nq);
             F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
         } else {
-            a[tid_global * LEN + idx] = canon4(v, q, q2);
+            a[tid_global * LEN + idx] = canon8(v, q, q2);
         }
     };
     if constexpr (SH) {
-        row_pass_shfl<true>(x, t, tid_global, tw, n, S0, q2, nq);
+        row_pass_shfl<true>(x, t, tid_global, tw, n, S0, q4, nq);
         if (!valid) return;
 #pragma unroll
         for (int r = 0; r < E; ++r) store_row(r, row_final_index<true>(t, r), x[r]);
@@ -377,14 +398,14 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
             const int idx0 = t + T * r0;
             const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
             const size_t wi = ((size_t)1 << (S0 + s)) + i;
-            ct_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2, nq);
+            ct_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q4, nq);
         }
     }
     // round-2 twiddles (G == 1: stage s needs 2^(s-EB) of them per lane, index
     // t 2^(s-EB) + (r0 >> (PB-s))), loaded before the exchange so their latency
     // overlaps the LDS round trip and barrier instead of stalling round 2
     // (row passes only: in the column pass the extra VGPRs cost a wave of occupancy)
-    constexpr bool PRE = G == 1 && !COLS;
+    constexpr bool PRE = G == 1 && !COLS && !LEAN;
     constexpr int NT2 = (1 << RB) - 1;
     ulonglong2 tw2[PRE ? NT2 : 1];
     if (PRE) {
@@ -418,7 +439,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
                 const size_t wi = ((size_t)1 << (S0 + s)) + i;
                 const ulonglong2 w =
                     PRE ? tw2[PRE ? ((1 << (s - EB)) - 1) + (r0 >> (PB - s)) : 0] : tw[wi];
-                ct_bfly(x[g * T + r0], x[g * T + r0 + (1 << hb)], w, q2, nq);
+                ct_bfly(x[g * T + r0], x[g * T + r0 + (1 << hb)], w, q4, nq);
             }
     }
     // ---- store.  COLS: layout L2 is already lane-contiguous in memory
@@ -487,7 +508,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     const size_t tid_global = SH ? (size_t)blockIdx.y * (NB >> F.lsegb) + (tr >> F.lsegb) : (size_t)blockIdx.y * NB + tr;
     const bool valid = tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs);
     u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
-    const u64 q = Tb.mods[p].q, q2 = 2 * q, nq = (u64)0 - q;
+    const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
     const int SG0 = COLS ? logN - PB : 0;  // global GS stage of local stage 0
 
@@ -496,7 +517,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     if constexpr (SH) {  // coalesced load (idx = t + 16 r), register-only stages, coalesced store
 #pragma unroll
         for (int r = 0; r < E; ++r) x[r] = valid ? ain[tid_global * LEN + t + T * r] : 0;
-        row_pass_shfl<false>(x, t, tid_global, tw, n, 0, q2, nq);
+        row_pass_shfl<false>(x, t, tid_global, tw, n, 0, q4, nq);
         if (!valid) return;
 #pragma unroll
         for (int r = 0; r < E; ++r) a[tid_global * LEN + row_final_index<false>(t, r)] = x[r];
@@ -539,7 +560,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
                 const size_t j = COLS ? 0 : tid_global * LEN;  // row offset (COLS: column bits vanish)
                 const size_t i = (j + (size_t)idx0 * (COLS ? ((size_t)1 << k2) : 1)) >> (sg + 1);
                 const size_t wi = (n >> (sg + 1)) + i;
-                gs_bfly(x[g * T + r0], x[g * T + r0 + (1 << s)], tw[wi], q2, nq);
+                gs_bfly(x[g * T + r0], x[g * T + r0 + (1 << s)], tw[wi], q4, nq);
             }
     }
     // ---- exchange L2 -> L1 (idx = t + T * r)
@@ -560,31 +581,58 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
             const int idx0 = t + T * r0;
             const int sg = SG0 + s;
             const size_t j = COLS ? 0 : tid_global * LEN;
-            const size_t i = (j + (size_t)idx0 * (COLS ? ((size_t)1 << k2) : 1)) >> (sg + 1);
+            // COLS: i = idx0 >> (s + 1) with t < T <= 2^(s+1), i.e. (T r0) >> (s + 1):
+            // a compile-time offset from a wave-uniform base -> scalar loads, no VGPRs
+            const size_t i = COLS ? ((size_t)T * r0) >> (s + 1)
+                                  : (j + (size_t)idx0) >> (sg + 1);
             const size_t wi = (n >> (sg + 1)) + i;
-            gs_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q2, nq);
+            gs_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q4, nq);
         }
     }
-    // ---- store, layout L1 (COLS: times n^-1 unless F.raw)
+    // ---- store, layout L1 (COLS: times n^-1, or raw: reduced to [0, 2q) for
+    // the conversions' 30-bit operand split; ROWS: lazy [0, 4q))
     const u64 ni = Tb.ninv[p], nis = Tb.ninv_s[p];
     const bool scale = COLS && !F.raw;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const int idx = t + T * r;
         const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
-        if (valid) a[off] = scale ? mul_shoup(x[r], ni, nis, q) : x[r];
+        const u64 v = scale ? mul_shoup(x[r], ni, nis, q) : COLS ? (x[r] >= q2 ? x[r] - q2 : x[r]) : x[r];
+        if (valid) a[off] = v;
     }
 }
 
-template <int PB, int EB, bool COLS, int MODE>
-__global__ __launch_bounds__(NTB) void k_ntt_fwd(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
-                                                  NttTables Tb, NttFuse F) {
-    ntt_fwd_body<PB, EB, COLS, MODE, false>(data, seg, pmap, smap, logN, Tb, F);
+// OCC: requested waves per SIMD (0: the compiler's choice).  The LDS tile of a
+// 256-point pass (34 KiB per block) already caps a CU at 4 blocks = 4 waves per
+// SIMD; asking for 4 keeps the compiler from hoisting every twiddle load into
+// registers (the inverse column pass otherwise takes 232 VGPRs = 2 waves).
+template <int PB, int EB, bool COLS, int MODE, int OCC, bool LEAN = false>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, 8))) void k_ntt_fwd(
+    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
+    ntt_fwd_body<PB, EB, COLS, MODE, false, LEAN>(data, seg, pmap, smap, logN, Tb, F);
 }
-template <int PB, int EB, bool COLS>
-__global__ __launch_bounds__(NTB) void k_ntt_inv(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
-                                                  NttTables Tb, NttFuse F) {
+// FHE_NTT_LEAN (A/B timing) bit mask: 1 = the HMult-tail row pass (mode 3),
+// 2 = the rescale row pass (mode 2) load their epilogue operands in the store
+// loop and skip the round-2 twiddle prefetch
+int &ntt_lean() {
+    static int v = [] {
+        const char *e = std::getenv("FHE_NTT_LEAN");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+template <int PB, int EB, bool COLS, int OCC>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, 8))) void k_ntt_inv(
+    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
     ntt_inv_body<PB, EB, COLS, false>(data, seg, pmap, smap, logN, Tb, F);
+}
+// FHE_NTT_OCC (A/B timing): waves-per-SIMD hint of the LDS-exchange passes (0 = none)
+int &ntt_occ() {
+    static int v = [] {
+        const char *e = std::getenv("FHE_NTT_OCC");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
 }
 // register-only row passes (PB = 8): OCC = requested waves per SIMD (0: compiler's choice)
 template <int MODE, int OCC>
@@ -627,8 +675,17 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     else if (FWD && sh)
         hipExtLaunchKernelGGL((k_ntt_fwd_row<MODE, 0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
                               T, Fs);
+    else if (FWD && !COLS && PB == 8 && MODE == NTT_MULTAIL && (ntt_lean() & 1))
+        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE, 0, true>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg,
+                              pmap, smap, T.logN, T, F);
+    else if (FWD && !COLS && PB == 8 && MODE == NTT_RESCALE && (ntt_lean() & 2))
+        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE, 0, true>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg,
+                              pmap, smap, T.logN, T, F);
+    else if (FWD && ntt_occ() == 4 && PB == 8)
+        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE, 4>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap,
+                              smap, T.logN, T, F);
     else if (FWD)
-        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
+        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE, 0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
                               T.logN, T, F);
     else if (sh && occ == 2)
         hipExtLaunchKernelGGL((k_ntt_inv_row<5>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T,
@@ -636,8 +693,11 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     else if (sh)
         hipExtLaunchKernelGGL((k_ntt_inv_row<0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T,
                               Fs);
+    else if (ntt_occ() == 4 && PB == 8)
+        hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS, 4>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
+                              T.logN, T, F);
     else
-        hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
+        hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS, 0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
                               T.logN, T, F);
     if (clk) {
         // same spelling as the demangled symbol rocprofv3 prints, plus the caller tag
