@@ -1,5 +1,6 @@
 """GPU precision diagnostic: rank error, index-check error with exact ranks,
-and end-to-end sort error for DirectSort at ring 2^16, per scale size."""
+and end-to-end sort error for DirectSort, per scale size and ring.
+usage: diag_precision.py N:scale_bits[:logN] ..."""
 import os, sys, time, json
 import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -23,7 +24,7 @@ def run(N, sb, logN=16, cfg=None):
     rk = c.encrypt(exp, N, level=rank.level)
     o1 = c.direct_sort(ct, N, rots, cfg, mode=2, rank=rk)
     o2 = c.direct_sort(ct, N, rots, cfg, mode=2, rank=rank)
-    res = dict(N=N, scale_bits=sb, cfg=cfg, rank_err=float(np.max(np.abs(r - exp))),
+    res = dict(N=N, scale_bits=sb, logN=logN, cfg=cfg, rank_err=float(np.max(np.abs(r - exp))),
                check_exact_rank_err=float(np.max(np.abs(c.decrypt(o1) - np.sort(x)))),
                sort_err=float(np.max(np.abs(c.decrypt(o2) - np.sort(x)))), level=o2.level, depth=depth,
                secs=round(time.time() - t, 2))
@@ -31,5 +32,5 @@ def run(N, sb, logN=16, cfg=None):
 
 if __name__ == '__main__':
     for spec in sys.argv[1:]:
-        N, sb = spec.split(':')
-        run(int(N), int(sb))
+        f = [int(v) for v in spec.split(':')]
+        run(f[0], f[1], f[2] if len(f) > 2 else 16)
