@@ -241,8 +241,11 @@ CtPtr Bootstrapper::transform(const Ciphertext &x, const Level &lv, int tag) {
         }
         it = pts.emplace(key, std::move(enc_pts)).first;
     }
-    const auto babies = cc.rotate_hoisted(x, lv.baby);  // one ModUp for every baby step
+    // baby steps: one ModUp, all key switches in the same launches
+    const auto babies = cc.rotate_hoisted(x, lv.baby);
     CtPtr acc;
+    std::vector<CtPtr> shifted;
+    std::vector<long> shifts;
     for (size_t gi = 0; gi < lv.giants.size(); ++gi) {
         const GiantStep &g = lv.giants[gi];
         std::vector<const Ciphertext *> a;
@@ -252,11 +255,27 @@ CtPtr Bootstrapper::transform(const Ciphertext &x, const Level &lv, int tag) {
             p.push_back(it->second[gi][j].get());
         }
         CtPtr inner = cc.mul_plain_sum(a, p);
-        if (g.shift) inner = cc.rotate(*inner, g.shift);
-        if (acc)
-            cc.add_inplace(acc, *inner);
-        else
+        if (g.shift) {
+            shifted.push_back(inner);
+            shifts.push_back(g.shift);
+        } else {
             acc = inner;
+        }
+    }
+    if (shifted.size() == 1) {
+        CtPtr r = cc.rotate(*shifted[0], shifts[0]);
+        if (acc)
+            cc.add_inplace(acc, *r);
+        else
+            acc = r;
+    } else if (!shifted.empty()) {  // giant steps: one batch, one rotation per member, summed
+        std::vector<const Ciphertext *> ptrs;
+        for (auto &c : shifted) ptrs.push_back(c.get());
+        CtPtr r = cc.sum_members(*cc.rotate_members(*cc.stack(ptrs), shifts));
+        if (acc)
+            cc.add_inplace(acc, *r);
+        else
+            acc = r;
     }
     return acc;
 }

@@ -467,6 +467,52 @@ __global__ __launch_bounds__(NT) void k_ks_inner_mc(u64 *acc, const u64 *ext, co
     }
 }
 
+// Multi-key variant (hoisted rotations by several amounts / per-member
+// rotations): grid x = member (fastest), y = coefficient block, z = target.
+template <int D>
+__global__ __launch_bounds__(NT) void k_ks_inner_mk(u64 *acc, const u64 *ext, const u64 *dntt, KsKeys KK, int ell,
+                                                    int W, int nall, int alpha, const int *pmap_ext, const Mod *mods,
+                                                    int logN, KsStrides st) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.y * NT + threadIdx.x;
+    if (k >= n) return;
+    const int t = blockIdx.z;
+    const size_t mb = blockIdx.x;
+    acc += mb * st.acc;
+    ext += mb * st.ext;
+    dntt += mb * st.d;
+    const u64 *key = KK.key[mb];
+    const uint32_t *perm = KK.perm[mb];
+    const int pt = pmap_ext[t];
+    const Mod m = mods[pt];
+    const size_t kk = perm ? perm[k] : k;
+    u64 x[D], kb[D], ka[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
+        x[j] = (t >= lo && t < hi) ? dntt[(size_t)t * n + kk] : ext[((size_t)j * W + t) * n + kk];
+        kb[j] = key[(((size_t)j * 2 + 0) * nall + pt) * n + k];
+        ka[j] = key[(((size_t)j * 2 + 1) * nall + pt) * n + k];
+    }
+    u64 a0 = 0, a1 = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        a0 = add_mod(a0, mul_barrett(x[j], kb[j], m), m.q);
+        a1 = add_mod(a1, mul_barrett(x[j], ka[j], m), m.q);
+    }
+    acc[(size_t)t * n + k] = a0;
+    acc[((size_t)W + t) * n + k] = a1;
+}
+// grid: x = n / NT, y = limb, z = member
+__global__ __launch_bounds__(NT) void k_permute_mk(u64 *out, const u64 *in, KsKeys KK, Seg S, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t ln = (size_t)blockIdx.y * n;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t *perm = KK.perm[blockIdx.z];
+    out[(size_t)blockIdx.z * S.o + ln + k] = in[(size_t)blockIdx.z * S.a + ln + perm[k]];
+}
+
 // grid: x = n / NT, y = ceil(ell / TCH), z = segment.  KT = K special primes;
 // phat [nq][KT] (the constants of one target contiguous: one scalar burst)
 // Exact centred conversion: y_k = [x P_k^-1]_{p_k}, x mod P = sum_k y_k P_k -
@@ -821,6 +867,29 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
         launch_clocked("k_ks_inner", B, k_ks_inner<D>, grid, dim3(NT), st, acc, ext, dntt, key, ell, W, nall, alpha,
                        perm, pmap_ext, mods, logN, str, fold);
     });
+}
+void ks_inner_multikey(u64 *acc, const u64 *ext, const u64 *dntt, const KsKeys &keys, int count, int ell, int K,
+                       int nall, int alpha, int digits, const int *pmap_ext, const Mod *mods, int logN,
+                       hipStream_t st, KsStrides str) {
+    if (count <= 0) return;
+    if (count > KS_MAXKEYS) throw std::invalid_argument("ks_inner_multikey: too many keys");
+    const int W = ell + K;
+    // ext (shared or per member), the accumulators and every member's key
+    const double shared = str.ext ? 0.0 : 1.0;
+    const double B = 8.0 * ((shared + (1 - shared) * count) * digits * W + count * (2.0 * W + 2.0 * digits * W)) *
+                     ((size_t)1 << logN);
+    const dim3 grid((unsigned)count, (unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
+    dispatch_int<1, 8>(digits, [&](auto c) {
+        constexpr int D = decltype(c)::value;
+        launch_clocked("k_ks_inner", B, k_ks_inner_mk<D>, grid, dim3(NT), st, acc, ext, dntt, keys, ell, W, nall,
+                       alpha, pmap_ext, mods, logN, str);
+    });
+}
+void ew_permute_multi(u64 *out, const u64 *in, const KsKeys &keys, int limbs, int count, Seg S, int logN,
+                      hipStream_t st) {
+    if (limbs <= 0 || count <= 0) return;
+    if (count > KS_MAXKEYS) throw std::invalid_argument("ew_permute_multi: too many keys");
+    hipLaunchKernelGGL(k_permute_mk, pt_grid(logN, limbs, count), dim3(NT), 0, st, out, in, keys, S, logN);
 }
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,

@@ -168,6 +168,20 @@ struct KsFold {
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
               hipStream_t st, int members, KsStrides str, KsFold fold = KsFold());
+// several key switches in one launch (hoisted rotations by different
+// amounts, or one rotation per member of a batch): member m < count uses key
+// keys[m] and reads ext through perm[m]; strides in `str` (0 = shared input)
+constexpr int KS_MAXKEYS = 16;
+struct KsKeys {
+    const u64 *key[KS_MAXKEYS];
+    const uint32_t *perm[KS_MAXKEYS];
+};
+void ks_inner_multikey(u64 *acc, const u64 *ext, const u64 *dntt, const KsKeys &keys, int count, int ell, int K,
+                       int nall, int alpha, int digits, const int *pmap_ext, const Mod *mods, int logN,
+                       hipStream_t st, KsStrides str);
+// out[m][l][k] = in[m][l][perms[m][k]] for m < count (in stride S.a, 0 = shared; out stride S.o)
+void ew_permute_multi(u64 *out, const u64 *in, const KsKeys &keys, int limbs, int count, Seg S, int logN,
+                      hipStream_t st);
 // fused ModDown + rescale of an HMult (see kernels.hip): corr [segs][ell-1][n]
 // from acc [segs][W][n] whose limbs ell-1 .. W-1 are in coefficient form,
 // unscaled (ntt_inverse raw: n x); ninv [nall]: n^-1 mod each prime

@@ -241,6 +241,32 @@ struct Engine::Impl {
         dev::moddown_finish(out, acc, conv, add, (int)ell, segs, ell * nn, W * nn, add_stride, pinv, pinv_s, mods,
                             P.logN, st);
     }
+    // `count` key switches in the same launches: switch m uses keys.key[m] and
+    // reads its ext (stride e_stride; 0 = one hoisted ModUp shared by all)
+    // through keys.perm[m]; out[m] ([2][ell][n]) = ModDown(acc_m) + (add[m], 0)
+    void ks_apply_multi(const u64 *e, size_t e_stride, const u64 *d, size_t d_stride, size_t ell, int count,
+                        const dev::KsKeys &keys, u64 *out, const u64 *add, size_t add_stride) {
+        Phase phase_("ks_moddown");
+        const size_t nn = n(), K = (size_t)P.K, W = ell + K;
+        const int digits = P.digits_at(ell);
+        const int segs = 2 * count;
+        auto accm = alloc((size_t)segs * W * nn * 8);
+        u64 *acc = static_cast<u64 *>(accm->p);
+        dev::KsStrides str;
+        str.acc = 2 * W * nn;
+        str.ext = e_stride;
+        str.d = d_stride;
+        dev::ks_inner_multikey(acc, e, d, keys, count, (int)ell, P.K, (int)P.nall(), P.alpha, digits, ext(ell), mods,
+                               P.logN, st, str);
+        dev::ntt_inverse(acc + ell * nn, (int)K, segs, W * nn, ext(ell) + ell, T, st, /*raw*/ true);
+        auto convm = alloc((size_t)segs * ell * nn * 8);
+        u64 *conv = static_cast<u64 *>(convm->p);
+        dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, segs, phinv, phinv_s,
+                             phat, pmod, pinvd, mods, P.logN, st);
+        dev::ntt_forward(conv, (int)ell, segs, ell * nn, nullptr, T, st);
+        dev::moddown_finish(out, acc, conv, add, (int)ell, segs, ell * nn, W * nn, add_stride, pinv, pinv_s, mods,
+                            P.logN, st);
+    }
     // HMult tail, fused: out[m] ([2][ell-1][n]) = Rescale(d01[m] + ModDown(Sum_j ext_j * key_j)).
     // Bit-identical to a ModDown with d01 added followed by rescale(): both
     // compute ((acc - Conv(acc_P)) P^-1 + d - [y_last]) q_last^-1 mod q_i, but
@@ -1050,6 +1076,41 @@ std::vector<CtPtr> Engine::apply_galois_hoisted(const Ciphertext &a, const std::
     const int B = a.batch;
     std::vector<CtPtr> outs;
     std::shared_ptr<DevMem> extm;
+    size_t keyed = 0;
+    for (u64 g : gs) keyed += g != 1;
+    if (B == 1 && keyed >= 2) {
+        // one ModUp, then every key switch, c0 permutation and ModDown of the
+        // set in the same launches (outputs are members of one batch)
+        std::vector<size_t> slot(gs.size(), (size_t)-1);
+        std::vector<u64> kg;
+        for (size_t i = 0; i < gs.size(); ++i) {
+            if (gs[i] == 1) continue;
+            if (!I.ks->rotkeys.count(gs[i]))
+                throw NoKeyError("rotate: no key for galois element " + std::to_string(gs[i]));
+            slot[i] = kg.size();
+            kg.push_back(gs[i]);
+        }
+        extm = I.modup(a.data + ln, ell, 1, 2 * ln);
+        auto r = new_ct(a.level, a.slots, a.scale, ell, (int)kg.size());
+        auto c0m = I.alloc(kg.size() * ln * 8);
+        u64 *c0p = static_cast<u64 *>(c0m->p);
+        for (size_t c0 = 0; c0 < kg.size(); c0 += dev::KS_MAXKEYS) {
+            const int cnt = (int)std::min<size_t>(dev::KS_MAXKEYS, kg.size() - c0);
+            dev::KsKeys KK{};
+            for (int i = 0; i < cnt; ++i) {
+                KK.key[i] = static_cast<const u64 *>(I.ks->rotkeys.at(kg[c0 + i])->p);
+                KK.perm[i] = I.perm(kg[c0 + i]);
+            }
+            dev::ew_permute_multi(c0p + c0 * ln, a.data, KK, (int)ell, cnt, seg3(ln, 0, 0), LOGN, ST);
+            I.ks_apply_multi(static_cast<u64 *>(extm->p), 0, a.data + ln, 0, ell, cnt, KK, r->data + c0 * 2 * ln,
+                             c0p + c0 * ln, ln);
+        }
+        ctr.keyswitch += kg.size();
+        ctr.rotations += kg.size();
+        count_bytes((4.0 * ell + ks_units(ell)) * (double)kg.size(), 1);
+        for (size_t i = 0; i < gs.size(); ++i) outs.push_back(slot[i] == (size_t)-1 ? clone(a) : member(*r, (int)slot[i]));
+        return outs;
+    }
     for (u64 g : gs) {
         if (g == 1) {
             outs.push_back(clone(a));
@@ -1073,6 +1134,42 @@ std::vector<CtPtr> Engine::apply_galois_hoisted(const Ciphertext &a, const std::
     return outs;
 }
 CtPtr Engine::rotate(const Ciphertext &a, long k) { return rotate_hoisted(a, {k})[0]; }
+
+// member m of `a` rotated by ks[m] (every ks[m] keyed, i.e. not 0 mod n/2): one
+// ModUp of all members, then the key switches in the same launches
+CtPtr Engine::rotate_members(const Ciphertext &a, const std::vector<long> &ks) {
+    auto &I = *impl;
+    if ((int)ks.size() != a.batch) throw std::invalid_argument("rotate_members: one rotation per member");
+    const size_t nn = n(), ell = a.limbs, ln = ell * nn;
+    const int B = a.batch;
+    std::vector<u64> gs;
+    for (long k : ks) {
+        const u64 g = host::galois_for_rotation(I.P.logN, k);
+        if (g == 1) throw std::invalid_argument("rotate_members: identity rotation");
+        if (!I.ks->rotkeys.count(g)) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
+        gs.push_back(g);
+    }
+    auto extm = I.modup(a.data + ln, ell, B, 2 * ln);
+    const size_t es = (size_t)I.P.digits_at(ell) * (ell + I.P.K) * nn;
+    auto r = new_ct(a.level, a.slots, a.scale, ell, B);
+    auto c0m = I.alloc((size_t)B * ln * 8);
+    u64 *c0p = static_cast<u64 *>(c0m->p);
+    for (int c0 = 0; c0 < B; c0 += dev::KS_MAXKEYS) {
+        const int cnt = std::min(dev::KS_MAXKEYS, B - c0);
+        dev::KsKeys KK{};
+        for (int i = 0; i < cnt; ++i) {
+            KK.key[i] = static_cast<const u64 *>(I.ks->rotkeys.at(gs[c0 + i])->p);
+            KK.perm[i] = I.perm(gs[c0 + i]);
+        }
+        dev::ew_permute_multi(c0p + c0 * ln, a.data + c0 * 2 * ln, KK, (int)ell, cnt, seg3(ln, 2 * ln, 0), LOGN, ST);
+        I.ks_apply_multi(static_cast<u64 *>(extm->p) + c0 * es, es, a.data + c0 * 2 * ln + ln, 2 * ln, ell, cnt, KK,
+                         r->data + c0 * 2 * ln, c0p + c0 * ln, ln);
+    }
+    ctr.keyswitch += B;
+    ctr.rotations += B;
+    count_bytes(4.0 * ell + ks_units(ell), B);
+    return r;
+}
 
 CtPtr Engine::mod_raise(const Ciphertext &a) {
     auto &I = *impl;

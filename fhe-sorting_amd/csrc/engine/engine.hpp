@@ -147,6 +147,9 @@ class Engine {
     CtPtr square(const Ciphertext &a);
     CtPtr rotate(const Ciphertext &a, long k);
     std::vector<CtPtr> rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks);
+    // member m of a batch rotated by ks[m] (all keyed): the giant steps of a
+    // BSGS linear transform as one pipeline
+    CtPtr rotate_members(const Ciphertext &a, const std::vector<long> &ks);
     // keyed automorphisms sharing one ModUp; conjugate = g 2n - 1
     std::vector<CtPtr> apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs);
     CtPtr conjugate(const Ciphertext &a);
