@@ -34,7 +34,7 @@ struct BootstrapConfig {
     int K = 512;                         // EvalMod range |t / q0| <= K (uniform ternary secret)
     int r = 6;                           // double-angle iterations
     int degree = 88;                     // Chebyshev degree of the cosine
-    int correctionBits = 11;             // message scaled to q0 2^-bits before ModRaise
+    int correctionBits = 10;             // message scaled to q0 2^-bits before ModRaise
 };
 
 class Bootstrapper {

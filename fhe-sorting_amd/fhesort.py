@@ -250,7 +250,7 @@ class Bootstrapper:
     """EvalBootstrapSetup(levelBudget, {0, 0}, slots) / EvalBootstrapKeyGen /
     EvalBootstrap on the GPU (fhe_boot_*; tests/k-way/KWaySort235Test.cpp:46-48)."""
 
-    def __init__(self, ctx, slots, budget=(4, 4), K=512, r=6, degree=88, correction_bits=11, keygen=True):
+    def __init__(self, ctx, slots, budget=(4, 4), K=512, r=6, degree=88, correction_bits=10, keygen=True):
         p = BootParams(slots, budget[0], budget[1], K, r, degree, correction_bits)
         out = C.c_void_p()
         _chk(lib().fhe_boot_create(ctx.h, C.byref(p), C.byref(out)))

@@ -285,7 +285,7 @@ int fhe_kway_rotation_indices(int N, int32_t *rots, int max_rots);
  * uniform ternary secret), r double angles, cosine degree (EvalMod coefficients
  * evalmod_k<K>r<r>_<degree>.f64 in the coefficient directory), correction_bits:
  * the message is scaled to q0 2^-bits before ModRaise.  Zero fields take the
- * defaults {budget 4/4, K 512, r 6, degree 88, bits 11}.  The bootstrapper
+ * defaults {budget 4/4, K 512, r 6, degree 88, bits 10}.  The bootstrapper
  * refers to ctx: destroy it first. */
 typedef struct {
     int slots;

@@ -395,7 +395,7 @@ struct BootConfig {
     int K = 512;                          // EvalMod input range |t / q0| <= K
     int r = 6;                            // double-angle iterations
     int degree = 88;                      // Chebyshev degree of the cosine
-    int correction_bits = 11;             // message scaled to q0 2^-bits before ModRaise
+    int correction_bits = 10;             // message scaled to q0 2^-bits before ModRaise
 };
 class Bootstrapper {
   public:

@@ -459,7 +459,7 @@ class Bootstrapper:
     """EvalBootstrapSetup(levelBudget={budget_enc, budget_dec}, slots) +
     EvalBootstrapKeyGen + EvalBootstrap (oracle_boot.cpp)."""
 
-    def __init__(self, ctx, slots, budget=(4, 4), K=512, r=6, degree=88, correction_bits=11, keygen=True):
+    def __init__(self, ctx, slots, budget=(4, 4), K=512, r=6, degree=88, correction_bits=10, keygen=True):
         self.ctx = ctx
         self.cfg = dict(slots=slots, budget=tuple(budget), K=K, r=r, degree=degree, correction_bits=correction_bits)
         self.h = _check(lib().orc_boot_new(ctx.h, slots, budget[0], budget[1], K, r, degree, correction_bits))

@@ -149,3 +149,39 @@ def test_config4_kway_k5_n3125_ring16():
         assert np.max(err) < 0.01 and np.sum(err >= 0.01) == 0  # KWaySort235Test.cpp:291-292
     finally:
         gpu.close()
+
+
+# KWaySort235Test's size table (tests/k-way/KWaySort235Test.cpp:68-222): N, k, M,
+# d_f, d_g; run at ring 2^16 (config 4's ring) with the test's context otherwise
+# (depth 40, scale 2^59, levelBudget {4,4} for N <= 128, else {5,5}) and its
+# assertions (max error < 0.01, no slot >= 0.01).  N = 3125 is
+# test_config4_kway_k5_n3125_ring16.
+KWAY235 = [(4, 2, 2, 2, 2), (8, 2, 3, 2, 2), (9, 3, 2, 2, 2), (16, 2, 4, 2, 2), (25, 5, 2, 2, 3),
+           (27, 3, 3, 2, 3), (32, 2, 5, 2, 3), (64, 2, 6, 2, 3), (81, 3, 4, 2, 3), (125, 5, 3, 2, 3),
+           (128, 2, 7, 2, 4), (243, 3, 5, 2, 4), (256, 2, 8, 2, 4), (512, 2, 9, 2, 4), (625, 5, 4, 2, 5),
+           (729, 3, 6, 2, 5), (1024, 2, 10, 2, 5), (2048, 2, 11, 2, 5), (2187, 3, 7, 2, 5)]
+
+
+@pytest.fixture(scope='module')
+def kway_ctx():
+    gpu = F.Context(16, 40, 59, 60, 3, seed=235)
+    gpu.gen_rotation_keys(F.kway_rotation_indices(2187))  # +-2^i < 2187 covers every N here
+    boots = {}
+    yield gpu, boots
+    for b in boots.values():
+        b.close()
+    gpu.close()
+
+
+@pytest.mark.parametrize('N,k,M,d_f,d_g', KWAY235)
+def test_kway235_sizes(kway_ctx, N, k, M, d_f, d_g):
+    gpu, boots = kway_ctx
+    assert k ** M == N
+    s = _slots(N)
+    budget = (4, 4) if N <= 128 else (5, 5)
+    if (s, budget) not in boots:
+        boots[(s, budget)] = F.Bootstrapper(gpu, s, budget)
+    x = np.random.default_rng(N).permutation(N) * (1 - 1e-8) / N  # getVectorWithMinDiff(N, 0, 1, (1-1e-8)/N)
+    out = gpu.kway_sort(gpu.encrypt(x, s), k, M, (3, d_f, d_g), boot=boots[(s, budget)])
+    err = np.abs(gpu.decrypt(out)[:N] - np.sort(x))
+    assert np.max(err) < 0.01 and np.sum(err >= 0.01) == 0  # KWaySort235Test.cpp:291-292
