@@ -153,7 +153,7 @@ def device_sync(ctx):
 
 def pmc_lookup(table, name):
     """PMC entry for a clocked kernel name: the clock tags launches with their
-    caller phase ('k_ntt_fwd<8, 4, false, 2>@rescale') and omits template
+    caller phase ('k_ntt_fwd<8, 4, false, 2, 0, false>@rescale') and omits template
     arguments of the conversion kernels ('k_modup_convert'); rocprofv3 names
     the instantiation."""
     base = name.split('@')[0]
@@ -186,7 +186,7 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json'):
             json.dump(stats, f, indent=1)
     total_ms = sum(v['ms'] for v in stats.values())
     # the dominant kernel by rocprof symbol: the clock tags NTT launches with
-    # their caller ('k_ntt_inv<8, 4, false>@mul_tail'); aggregate the tags the
+    # their caller ('k_ntt_inv_row<0>@mul_tail'); aggregate the tags the
     # way rocprofv3 --stats does before choosing
     by_sym = {}
     for k, v in stats.items():

@@ -13,11 +13,13 @@
 #include "../algo/fhesort.hpp"
 #include "../algo/kway.hpp"
 #include "../engine/engine.hpp"
+#include "../wire/wire.hpp"
 
 using namespace fhe;
 
 struct fhe_ctx {
     std::unique_ptr<Engine> eng;
+    wire::CtxParams params;  // what the context was built from (wire format)
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1;
     // one rank sorter per (N, rotation set): its encoded public masks persist
@@ -50,6 +52,9 @@ int guard(F &&f) {
     } catch (const NoKeyError &e) {
         g_err = e.what();
         return FHE_ENOKEY;
+    } catch (const wire::IoError &e) {
+        g_err = e.what();
+        return FHE_EIO;
     } catch (const std::invalid_argument &e) {
         g_err = e.what();
         return FHE_EINVAL;
@@ -89,6 +94,7 @@ int fhe_ctx_create(const fhe_params *p, int device, fhe_ctx **out) {
         auto c = std::make_unique<fhe_ctx>();
         c->eng = std::make_unique<Engine>(p->log_n, p->mult_depth, p->scale_bits, p->first_bits, p->dnum, device,
                                           p->seed);
+        c->params = wire::CtxParams{p->log_n, p->mult_depth, p->scale_bits, p->first_bits, p->dnum, p->seed};
         *out = c.release();
     });
 }
@@ -844,6 +850,81 @@ int fhe_kernel_clock_stop(fhe_ctx *ctx, char *json, size_t cap, size_t *needed) 
             std::memcpy(json, s.data(), m);
             json[m] = 0;
         }
+    });
+}
+
+/* ------------------------------------------------------------ wire format */
+int fhe_wire_inspect(const char *path, fhe_wire_info *info) {
+    return guard([&] {
+        NEED(path);
+        NEED(info);
+        const auto i = wire::inspect(path);
+        info->kind = i.kind;
+        info->version = i.version;
+        info->params_id = i.params_id;
+        info->log_n = i.log_n;
+        info->nq = i.nq;
+        info->K = i.K;
+        info->body_words = i.body_words;
+    });
+}
+int fhe_serialize_context(fhe_ctx *ctx, const char *path) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(path);
+        wire::save_context(*ctx->eng, ctx->params, path);
+    });
+}
+int fhe_deserialize_context(const char *path, int device, fhe_ctx **out) {
+    return guard([&] {
+        NEED(path);
+        NEED(out);
+        const auto p = wire::read_context(path);
+        auto c = std::make_unique<fhe_ctx>();
+        c->eng = std::make_unique<Engine>(p.log_n, p.mult_depth, p.scale_bits, p.first_bits, p.dnum, device, p.seed);
+        c->params = p;
+        wire::check_context(*c->eng, p, path);
+        *out = c.release();
+    });
+}
+#define WIRE_KEY(name, call)                     \
+    int name(fhe_ctx *ctx, const char *path) {   \
+        return guard([&] {                       \
+            NEED(ctx);                           \
+            NEED(path);                          \
+            call(*ctx->eng, ctx->params, path);  \
+        });                                      \
+    }
+WIRE_KEY(fhe_serialize_public_key, wire::save_public_key)
+WIRE_KEY(fhe_deserialize_public_key, wire::load_public_key)
+WIRE_KEY(fhe_serialize_secret_key, wire::save_secret_key)
+WIRE_KEY(fhe_deserialize_secret_key, wire::load_secret_key)
+WIRE_KEY(fhe_serialize_eval_mult_key, wire::save_eval_mult_key)
+WIRE_KEY(fhe_deserialize_eval_mult_key, wire::load_eval_mult_key)
+WIRE_KEY(fhe_serialize_eval_automorphism_key, wire::save_automorphism_keys)
+#undef WIRE_KEY
+int fhe_deserialize_eval_automorphism_key(fhe_ctx *ctx, const char *path, int *count) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(path);
+        const int c = wire::load_automorphism_keys(*ctx->eng, ctx->params, path);
+        if (count) *count = c;
+    });
+}
+int fhe_serialize_ciphertext(fhe_ctx *ctx, const fhe_ct *ct, const char *path) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(ct);
+        NEED(path);
+        wire::save_ciphertext(*ctx->eng, ctx->params, *ct->p, path);
+    });
+}
+int fhe_deserialize_ciphertext(fhe_ctx *ctx, const char *path, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(path);
+        NEED(out);
+        *out = wrap(wire::load_ciphertext(*ctx->eng, ctx->params, path));
     });
 }
 

@@ -701,10 +701,19 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
                               T.logN, T, F);
     if (clk) {
         // same spelling as the demangled symbol rocprofv3 prints, plus the caller tag
-        static const std::string base = std::string(FWD ? "k_ntt_fwd<" : "k_ntt_inv<") + std::to_string(PB) + ", " +
-                                        std::to_string(EB) + (COLS ? ", true" : ", false") +
-                                        (FWD ? ", " + std::to_string(MODE) : std::string()) +
-                                        (sh ? ", true>" : ">");
+        // (the instantiation the branches above launched; the switches are per process)
+        static const std::string base = [&]() {
+            const std::string pe = std::to_string(PB) + ", " + std::to_string(EB) + (COLS ? ", true" : ", false");
+            const bool lean = FWD && !COLS && PB == 8 &&
+                              ((MODE == NTT_MULTAIL && (ntt_lean() & 1)) || (MODE == NTT_RESCALE && (ntt_lean() & 2)));
+            const int o = (ntt_occ() == 4 && PB == 8 && !lean) ? 4 : 0;
+            if (FWD && sh) return "k_ntt_fwd_row<" + std::to_string(MODE) + ", " + std::to_string(occ == 2 ? FWD_OCC : 0) + ">";
+            if (FWD)
+                return "k_ntt_fwd<" + pe + ", " + std::to_string(MODE) + ", " + std::to_string(o) +
+                       (lean ? ", true>" : ", false>");
+            if (sh) return std::string(occ == 2 ? "k_ntt_inv_row<5>" : "k_ntt_inv_row<0>");
+            return "k_ntt_inv<" + pe + ", " + std::to_string(o) + ">";
+        }();
         static std::map<const char *, std::string> names;
         static std::mutex mu;
         const char *ph = launch_phase();

@@ -645,6 +645,31 @@ bool Engine::has_galois_key(u64 g) const { return impl->ks->rotkeys.count(g) > 0
 bool Engine::has_rotation_key(long k) const {
     return impl->ks->rotkeys.count(host::galois_for_rotation(impl->P.logN, k)) > 0;
 }
+int Engine::key_digits() const { return impl->key_digits; }
+size_t Engine::switch_key_words() const { return (size_t)impl->key_digits * 2 * impl->P.nall() * impl->P.n; }
+bool Engine::has_secret() const { return (bool)impl->ks->s_ntt; }
+bool Engine::has_public() const { return (bool)impl->ks->pk; }
+bool Engine::has_relin() const { return (bool)impl->ks->relin; }
+namespace {
+void export_key(Engine::Impl &I, const std::shared_ptr<DevMem> &m, size_t words, u64 *out, const char *what) {
+    if (!m) throw std::invalid_argument(std::string("export: no ") + what);
+    HIP_OK(hipStreamSynchronize(I.st));
+    HIP_OK(hipMemcpy(out, m->p, words * 8, hipMemcpyDeviceToHost));
+}
+}  // namespace
+void Engine::export_secret(u64 *out) { export_key(*impl, impl->ks->s_ntt, impl->P.nall() * n(), out, "secret key"); }
+void Engine::export_public(u64 *out) { export_key(*impl, impl->ks->pk, 2 * impl->P.nq() * n(), out, "public key"); }
+void Engine::export_relin(u64 *out) { export_key(*impl, impl->ks->relin, switch_key_words(), out, "relinearisation key"); }
+std::vector<u64> Engine::galois_elements() const {
+    std::vector<u64> gs;
+    for (auto &kv : impl->ks->rotkeys) gs.push_back(kv.first);
+    return gs;
+}
+void Engine::export_galois(u64 g, u64 *out) {
+    auto it = impl->ks->rotkeys.find(g);
+    if (it == impl->ks->rotkeys.end()) throw std::invalid_argument("export: no key for galois element " + std::to_string(g));
+    export_key(*impl, it->second, switch_key_words(), out, "galois key");
+}
 size_t Engine::key_bytes() const {
     size_t b = impl->ks->relin ? impl->ks->relin->bytes : 0;
     for (auto &kv : impl->ks->rotkeys) b += kv.second->bytes;

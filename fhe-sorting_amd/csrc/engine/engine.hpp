@@ -103,6 +103,18 @@ class Engine {
     void load_galois(u64 g, const u64 *key);      // [digits][2][nall][n]
     bool has_galois_key(u64 g) const;
     size_t key_bytes() const;
+    // key export (wire format, csrc/wire): same layouts as the loads above;
+    // a missing key throws std::invalid_argument
+    int key_digits() const;
+    size_t switch_key_words() const;              // digits * 2 * nall * n
+    bool has_secret() const;
+    bool has_public() const;
+    bool has_relin() const;
+    void export_secret(u64 *out);
+    void export_public(u64 *out);
+    void export_relin(u64 *out);
+    std::vector<u64> galois_elements() const;     // ascending
+    void export_galois(u64 g, u64 *out);
 
     // ------------------------------------------------- encode / encrypt ---
     PtPtr encode(const std::vector<double> &v, int slots, int level);

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, 'lib', 'libfhesort.so')
 COEFF_DIR = os.path.join(HERE, 'data')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'fhe_gpu.h')
 
-FHE_OK, FHE_EINVAL, FHE_ENOKEY, FHE_EDEPTH, FHE_EHIP, FHE_ENOMEM, FHE_EINTERNAL, FHE_ENOCOMM = range(8)
+FHE_OK, FHE_EINVAL, FHE_ENOKEY, FHE_EDEPTH, FHE_EHIP, FHE_ENOMEM, FHE_EINTERNAL, FHE_ENOCOMM, FHE_EIO = range(9)
 NAF, BNAF, BINARY = 0, 1, 2
 
 
@@ -173,7 +173,34 @@ _SIGS = {
     'fhe_ct_member': (C.c_int, [vp, vp, C.c_int, C.POINTER(C.c_void_p)]),
     'fhe_ct_sum_members': (C.c_int, [vp, vp, C.POINTER(C.c_void_p)]),
     'fhe_kernel_clock_stop': (C.c_int, [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    'fhe_wire_inspect': (C.c_int, [C.c_char_p, vp]),
+    'fhe_serialize_context': (C.c_int, [vp, C.c_char_p]),
+    'fhe_deserialize_context': (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),
+    'fhe_serialize_ciphertext': (C.c_int, [vp, vp, C.c_char_p]),
+    'fhe_deserialize_ciphertext': (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_void_p)]),
+    'fhe_deserialize_eval_automorphism_key': (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_int)]),
+    **{f'fhe_{d}serialize_{k}': (C.c_int, [vp, C.c_char_p])
+       for d in ('', 'de') for k in ('public_key', 'secret_key', 'eval_mult_key')},
+    'fhe_serialize_eval_automorphism_key': (C.c_int, [vp, C.c_char_p]),
 }
+
+
+class WireInfo(C.Structure):
+    _fields_ = [('kind', C.c_uint32), ('version', C.c_uint32), ('params_id', C.c_uint64), ('log_n', C.c_uint64),
+                ('nq', C.c_uint64), ('K', C.c_uint64), ('body_words', C.c_uint64)]
+
+
+WIRE_KINDS = {1: 'context', 2: 'public_key', 3: 'eval_mult_key', 4: 'eval_automorphism_key', 5: 'ciphertext',
+              6: 'secret_key'}
+
+
+def wire_inspect(path):
+    """Header of a wire file (csrc/wire/wire.hpp) after its checksum is verified;
+    host only, no GPU needed."""
+    i = WireInfo()
+    _chk(lib().fhe_wire_inspect(os.fsencode(path), C.byref(i)))
+    return {'kind': WIRE_KINDS.get(i.kind, i.kind), 'version': i.version, 'params_id': i.params_id,
+            'log_n': i.log_n, 'nq': i.nq, 'K': i.K, 'body_words': i.body_words}
 
 
 def lib():
@@ -347,13 +374,15 @@ class Pt:
 class Context:
     """One engine on one GPU (`device`)."""
 
-    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, device=0, keygen=True):
+    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, device=0, keygen=True, _handle=None):
         self.logN, self.n, self.L = logN, 1 << logN, L
         self._boots = []
-        p = Params(logN, L, scale_bits, first_bits, dnum, seed)
-        h = C.c_void_p()
-        _chk(lib().fhe_ctx_create(C.byref(p), device, C.byref(h)))
-        self.h = h
+        if _handle is None:
+            p = Params(logN, L, scale_bits, first_bits, dnum, seed)
+            h = C.c_void_p()
+            _chk(lib().fhe_ctx_create(C.byref(p), device, C.byref(h)))
+            _handle = h
+        self.h = _handle
         nq, K, alpha = C.c_int(), C.c_int(), C.c_int()
         _chk(lib().fhe_ctx_info(self.h, C.byref(nq), C.byref(K), C.byref(alpha), None, None))
         self.nq, self.K, self.alpha = nq.value, K.value, alpha.value
@@ -362,6 +391,41 @@ class Context:
         _chk(lib().fhe_ctx_info(self.h, None, None, None, _u64(self.primes), _dbl(self.delta)))
         if keygen:
             self.keygen()
+
+    # ---- wire format (src/sort.h:31-74, 97-102: Serial::*ToFile, Serialize/DeserializeEval*Key)
+    @classmethod
+    def deserialize(cls, path, device=0):
+        """Serial::DeserializeFromFile(path, cc): a context with no keys."""
+        info = wire_inspect(path)
+        h = C.c_void_p()
+        _chk(lib().fhe_deserialize_context(os.fsencode(path), device, C.byref(h)))
+        return cls(int(info['log_n']), int(info['nq']) - 1, keygen=False, _handle=h)
+
+    def serialize(self, path):
+        _chk(lib().fhe_serialize_context(self.h, os.fsencode(path)))
+
+    def serialize_public_key(self, path): _chk(lib().fhe_serialize_public_key(self.h, os.fsencode(path)))
+    def deserialize_public_key(self, path): _chk(lib().fhe_deserialize_public_key(self.h, os.fsencode(path)))
+    def serialize_secret_key(self, path): _chk(lib().fhe_serialize_secret_key(self.h, os.fsencode(path)))
+    def deserialize_secret_key(self, path): _chk(lib().fhe_deserialize_secret_key(self.h, os.fsencode(path)))
+    def serialize_eval_mult_key(self, path): _chk(lib().fhe_serialize_eval_mult_key(self.h, os.fsencode(path)))
+    def deserialize_eval_mult_key(self, path): _chk(lib().fhe_deserialize_eval_mult_key(self.h, os.fsencode(path)))
+
+    def serialize_eval_automorphism_key(self, path):
+        _chk(lib().fhe_serialize_eval_automorphism_key(self.h, os.fsencode(path)))
+
+    def deserialize_eval_automorphism_key(self, path):
+        n = C.c_int()
+        _chk(lib().fhe_deserialize_eval_automorphism_key(self.h, os.fsencode(path), C.byref(n)))
+        return n.value
+
+    def serialize_ciphertext(self, ct, path):
+        _chk(lib().fhe_serialize_ciphertext(self.h, ct.h, os.fsencode(path)))
+
+    def deserialize_ciphertext(self, path):
+        h = C.c_void_p()
+        _chk(lib().fhe_deserialize_ciphertext(self.h, os.fsencode(path), C.byref(h)))
+        return Ct(self, h.value)
 
     def close(self):
         for b in getattr(self, '_boots', []):  # bootstrappers refer to the context

@@ -33,7 +33,8 @@ enum {
     FHE_EHIP = 4,      /* HIP runtime error */
     FHE_ENOMEM = 5,
     FHE_EINTERNAL = 6,
-    FHE_ENOCOMM = 7    /* collective requested without fhe_comm_init */
+    FHE_ENOCOMM = 7,   /* collective requested without fhe_comm_init */
+    FHE_EIO = 8        /* file cannot be read / written, or is not a valid wire file */
 };
 
 typedef struct fhe_ctx fhe_ctx;
@@ -350,6 +351,41 @@ int fhe_pool_stats(fhe_ctx *ctx, uint64_t *live, uint64_t *cached, uint64_t *pea
  * json (cap bytes, NUL-terminated, truncated if short; *needed = full size) */
 int fhe_kernel_clock_start(fhe_ctx *ctx);
 int fhe_kernel_clock_stop(fhe_ctx *ctx, char *json, size_t cap, size_t *needed);
+
+/* ------------------------------------------------------------ wire format
+ * The reference's CLI (src/sort.h:31-74, 97-102; src/main.cpp:9-44) reads the
+ * crypto context, public key, eval-mult key, eval-automorphism (rotation) keys
+ * and input ciphertext from files and writes the sorted ciphertext back, via
+ * OpenFHE's Serial API in SerType::BINARY.  These calls do the same in the
+ * engine's own format (fhe-sorting_amd/csrc/wire/wire.hpp):
+ * checksummed, tied to the context's modulus chain, validated before anything
+ * is loaded.  Errors: FHE_EIO (open / read / write / corrupt / not a wire file),
+ * FHE_EINVAL (wrong object kind, other context, out-of-range residues). */
+typedef struct {
+    uint32_t kind;     /* 1 context, 2 public key, 3 eval-mult key, 4 automorphism keys, 5 ciphertext, 6 secret key */
+    uint32_t version;
+    uint64_t params_id, log_n, nq, K, body_words;
+} fhe_wire_info;
+int fhe_wire_inspect(const char *path, fhe_wire_info *info);  /* host only: header + checksum */
+/* Serial::SerializeToFile / DeserializeFromFile(ccLocation, m_cc) (src/sort.h:34) */
+int fhe_serialize_context(fhe_ctx *ctx, const char *path);
+int fhe_deserialize_context(const char *path, int device, fhe_ctx **out);
+/* ... (pubKeyLocation, m_PublicKey) (src/sort.h:40) */
+int fhe_serialize_public_key(fhe_ctx *ctx, const char *path);
+int fhe_deserialize_public_key(fhe_ctx *ctx, const char *path);
+/* the client side's secret key (the reference's tests keep it in memory) */
+int fhe_serialize_secret_key(fhe_ctx *ctx, const char *path);
+int fhe_deserialize_secret_key(fhe_ctx *ctx, const char *path);
+/* SerializeEvalMultKey / DeserializeEvalMultKey (src/sort.h:46-55) */
+int fhe_serialize_eval_mult_key(fhe_ctx *ctx, const char *path);
+int fhe_deserialize_eval_mult_key(fhe_ctx *ctx, const char *path);
+/* SerializeEvalAutomorphismKey / DeserializeEvalAutomorphismKey (src/sort.h:57-67):
+ * every galois key of the context (rotations, conjugation); count: keys loaded */
+int fhe_serialize_eval_automorphism_key(fhe_ctx *ctx, const char *path);
+int fhe_deserialize_eval_automorphism_key(fhe_ctx *ctx, const char *path, int *count);
+/* Serial::{Deserialize,Serialize}ToFile of a ciphertext (src/sort.h:69-73, 97-102) */
+int fhe_serialize_ciphertext(fhe_ctx *ctx, const fhe_ct *ct, const char *path);
+int fhe_deserialize_ciphertext(fhe_ctx *ctx, const char *path, fhe_ct **out);
 
 #ifdef __cplusplus
 }

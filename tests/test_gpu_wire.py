@@ -1,0 +1,161 @@
+"""GPU: the wire format and the competition CLI (the reference's src/main.cpp +
+src/sort.h SortContext: deserialise context / keys / ciphertext, DirectSort<N>
+with CompositeSign(4, 3, 3), serialise the output).
+
+* every object round-trips: a context rebuilt from its file, with keys and
+  ciphertexts loaded from files, computes the same words as the original;
+  re-serialising gives byte-identical files;
+* damaged or mismatched files fail with FHE_EIO / FHE_EINVAL and leave the
+  loaded keys as they were;
+* end to end: client setup + encrypt -> bin/fhesort -> the output file, parsed
+  by the independent restatement (tests/wire_spec.py), equals the in-process
+  fhe_direct_sort words and the CPU oracle's DirectSort words on the same input
+  and keys, and decrypts sorted.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import fhesort as F
+import pyoracle as O
+import wire_spec as W
+
+pytestmark = pytest.mark.gpu
+
+PKG = os.path.dirname(os.path.abspath(F.__file__))
+CLI = os.path.join(PKG, 'bin', 'fhesort')
+CLIENT = os.path.join(PKG, 'client.py')
+ROTS = [1, 2, -1, 5]
+
+
+def _save_all(ctx, d, ct):
+    paths = {k: str(d / f'{k}.bin') for k in ('cc', 'pub', 'mult', 'rot', 'sec', 'ct')}
+    ctx.serialize(paths['cc'])
+    ctx.serialize_public_key(paths['pub'])
+    ctx.serialize_eval_mult_key(paths['mult'])
+    ctx.serialize_eval_automorphism_key(paths['rot'])
+    ctx.serialize_secret_key(paths['sec'])
+    ctx.serialize_ciphertext(ct, paths['ct'])
+    return paths
+
+
+def _load_all(paths):
+    c = F.Context.deserialize(paths['cc'])
+    c.deserialize_public_key(paths['pub'])
+    c.deserialize_eval_mult_key(paths['mult'])
+    nrot = c.deserialize_eval_automorphism_key(paths['rot'])
+    c.deserialize_secret_key(paths['sec'])
+    return c, nrot
+
+
+def test_objects_round_trip(tmp_path):
+    ctx = F.Context(12, 6, 40, 60, 3, seed=11)
+    ctx.gen_rotation_keys(ROTS)
+    v = np.linspace(-0.5, 0.5, 64)
+    x = ctx.encrypt(v, 64)
+    paths = _save_all(ctx, tmp_path, x)
+    c2, nrot = _load_all(paths)
+    assert nrot == len(ROTS)
+    assert np.array_equal(c2.primes, ctx.primes) and np.array_equal(c2.delta, ctx.delta)
+    x2 = c2.deserialize_ciphertext(paths['ct'])
+    assert x2.info() == x.info()
+    assert np.array_equal(x2.data(), x.data())
+    # the restated parser reads the engine's file
+    level, slots, limbs, scale, words = W.ciphertext(open(paths['ct'], 'rb').read(), ctx.n)
+    assert (level, slots, limbs, scale) == (x.level, 64, x.info()['limbs'], x.info()['scale'])
+    assert np.array_equal(words, x.data())
+    # loaded keys compute the same words
+    for k in ROTS:
+        assert np.array_equal(c2.rotate(x2, k).data(), ctx.rotate(x, k).data())
+    assert np.array_equal(c2.mul(x2, x2).data(), ctx.mul(x, x).data())
+    assert np.abs(c2.decrypt(x2)[:64] - v).max() < 1e-6
+    # re-serialised from the loaded context: byte-identical files
+    d2 = tmp_path / 'again'
+    d2.mkdir()
+    again = _save_all(c2, d2, x2)
+    for k in paths:
+        assert open(paths[k], 'rb').read() == open(again[k], 'rb').read(), k
+    assert F.wire_inspect(paths['rot'])['kind'] == 'eval_automorphism_key'
+
+
+def test_mismatches_and_damage_are_refused(tmp_path):
+    ctx = F.Context(12, 6, 40, 60, 3, seed=12)
+    ctx.gen_rotation_keys(ROTS)
+    x = ctx.encrypt(np.linspace(0, 1, 32), 32)
+    paths = _save_all(ctx, tmp_path, x)
+    other = F.Context(12, 7, 40, 60, 3, seed=12)  # one more level: another modulus chain
+    for fn, p in ((other.deserialize_ciphertext, paths['ct']), (other.deserialize_eval_mult_key, paths['mult']),
+                  (ctx.deserialize_eval_mult_key, paths['pub']), (ctx.deserialize_ciphertext, paths['rot'])):
+        with pytest.raises(F.FheError) as e:
+            fn(p)
+        assert e.value.code == F.FHE_EINVAL, (fn.__name__, p)
+    with pytest.raises(F.FheError) as e:
+        F.Context.deserialize(paths['ct'])
+    assert e.value.code == F.FHE_EINVAL
+    # a corrupted key set changes nothing: the context still rotates as before
+    before = ctx.rotate(x, 1).data()
+    raw = bytearray(open(paths['rot'], 'rb').read())
+    raw[len(raw) // 2] ^= 0x10
+    bad = tmp_path / 'rot_bad.bin'
+    bad.write_bytes(bytes(raw))
+    with pytest.raises(F.FheError) as e:
+        ctx.deserialize_eval_automorphism_key(str(bad))
+    assert e.value.code == F.FHE_EIO
+    assert np.array_equal(ctx.rotate(x, 1).data(), before)
+    # a residue >= q with a valid checksum: refused before upload
+    body = W.unpack(open(paths['ct'], 'rb').read())
+    b = body['body'].copy()
+    b[5] = np.uint64(ctx.primes[0])
+    forged = tmp_path / 'forged.bin'
+    forged.write_bytes(W.pack('ciphertext', body['params_id'], body['log_n'], body['nq'], body['K'], b))
+    with pytest.raises(F.FheError) as e:
+        ctx.deserialize_ciphertext(str(forged))
+    assert e.value.code == F.FHE_EINVAL and 'out of range' in str(e.value)
+
+
+def _run(cmd, **kw):
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, **kw)
+    assert r.returncode == 0, f'{cmd[:3]} failed ({r.returncode}):\n{r.stdout}\n{r.stderr}'
+    return r
+
+
+@pytest.mark.parametrize('N', [8])
+def test_cli_end_to_end_matches_oracle(tmp_path, N):
+    """N = 8 at ring 2^12, the CLI's CompositeSign(4, 3, 3) (depth 39)."""
+    d = tmp_path / 'art'
+    seed = 21
+    _run([sys.executable, CLIENT, 'setup', '--dir', str(d), '--n', str(N), '--log-n', '12', '--scale-bits', '50',
+          '--seed', str(seed)])
+    inp, out = str(tmp_path / 'x.bin'), str(tmp_path / 'y.bin')
+    _run([sys.executable, CLIENT, 'encrypt', '--dir', str(d), '--n', str(N), '--random', '5', '--output', inp])
+    r = _run([CLI, '--cc', str(d / 'cc.bin'), '--key_pub', str(d / 'key_pub.bin'), '--key_mult',
+              str(d / 'key_mult.bin'), '--key_rot', str(d / 'key_rot.bin'), '--input', inp, '--output', out,
+              '--n', str(N), '--timing'])
+    print(r.stderr.strip().splitlines()[-1])
+    level, slots, limbs, scale, y = W.ciphertext(open(out, 'rb').read(), 1 << 12)
+    assert level == 39 and slots == N
+    # in-process through the C-ABI on the same files
+    ctx = F.Context.deserialize(str(d / 'cc.bin'))
+    for load, f in ((ctx.deserialize_public_key, 'key_pub'), (ctx.deserialize_eval_mult_key, 'key_mult'),
+                    (ctx.deserialize_eval_automorphism_key, 'key_rot'), (ctx.deserialize_secret_key, 'key_sec')):
+        load(str(d / f'{f}.bin'))
+    x = ctx.deserialize_ciphertext(inp)
+    rots = F.size_parameters(N)[1]
+    g = ctx.direct_sort(x, N, rots, (4, 3, 3))
+    assert np.array_equal(g.data(), y)
+    # the CPU oracle with the same keys (same seed) on the same input words
+    orc = O.Context(12, 39, 50, 60, 3, seed=seed)
+    orc.gen_rotation_keys(rots)
+    xl, xs, _, xscale, xw = W.ciphertext(open(inp, 'rb').read(), 1 << 12)
+    ox = orc.ct_from(xw, xl, xs, xscale)
+    oy = orc.direct_sort(ox, N, rots, (4, 3, 3))
+    assert np.array_equal(oy.data(), y), 'CLI output differs from the oracle'
+    v = np.random.default_rng(5).permutation(N) / N
+    got = ctx.decrypt(ctx.deserialize_ciphertext(out))[:N]
+    assert np.abs(got - np.sort(v)).max() < 0.01
+    # the client's decrypt reads the same file
+    r = _run([sys.executable, CLIENT, 'decrypt', '--dir', str(d), '--n', str(N), '--input', out])
+    assert np.abs(np.array([float(t) for t in r.stdout.split()]) - np.sort(v)).max() < 0.01
