@@ -72,6 +72,9 @@ __device__ __forceinline__ u64 shoup_fold4(u64 a, u64 w, u64 wp, u64 nq) {  // [
     const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
     const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32), n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
     const u64 t = (u64)a0 * w0 + (u64)h0 * n0;
+    // (writing the + (cross << 32) as a 32-bit high-word add in inline asm cut
+    // 60 VALU slots per row pass but measured 9% slower: the asm blocks the
+    // scheduler's interleaving of independent butterflies)
     const uint32_t cross = a0 * w1 + a1 * w0 + h0 * n1 + h1 * n0;
     return t + ((u64)cross << 32);
 }
@@ -114,11 +117,11 @@ __device__ __forceinline__ u64 canon8(u64 x, u64 q, u64 q2) {  // [0, 8q) -> [0,
 // re-dealing the whole transform through LDS, a stage whose bit sits in a lane
 // bit swaps that lane bit with a register bit whose stage is done: lanes t and
 // t ^ 2^m exchange half of their registers with DPP moves (no LDS, no
-// barrier).  The schedules below need 5 such swaps per pass, all against
-// register bit 3 (slots j and j + 8), and start and end in the layout
+// barrier).  The forward schedule needs 5 such swaps per pass, all against
+// register bit 3 (slots j and j + 8), the inverse 4 (inv_swap); both end in
 //   idx = lane_index(t) + 16 * r      (lane bits = index bits 0..3),
 // so loads and stores are fully coalesced: the 16 lanes of a transform cover
-// one 128-B line per instruction.
+// one 128-B line per 8-B instruction.
 struct RowLayout {
     int lane[4];  // index bit held by lane bit m
     int reg[4];   // index bit held by register bit p
@@ -126,9 +129,13 @@ struct RowLayout {
 struct RowSwap {
     int m, p;  // swap lane bit m with register bit p before the stage (m < 0: none)
 };
-// GS inverse: stages take index bits 0, 1, ..., 7
+// GS inverse: stages take index bits 0, 1, ..., 7.  The inverse pass loads 16-B
+// pairs (register bit 0 = index bit 0, lanes = index bits 1..4, still one 256-B
+// run per transform and instruction), so stage 0 needs no swap and stages 1..4
+// each bring their lane bit in for the finished register bit 0: 4 swaps, ending
+// in lanes = index bits 0..3 for the coalesced 8-B stores
 __device__ constexpr RowSwap inv_swap(int s) {
-    return s <= 3 ? RowSwap{s, 3} : s == 7 ? RowSwap{0, 3} : RowSwap{-1, 0};
+    return s >= 1 && s <= 4 ? RowSwap{s - 1, 0} : RowSwap{-1, 0};
 }
 // CT forward: stages take index bits 7, 6, ..., 0; stage 8 is the final
 // fix-up swap (no butterfly) back to lane bits = index bits 0..3
@@ -137,7 +144,7 @@ __device__ constexpr RowSwap fwd_swap(int s) {
 }
 template <bool FWD>
 __device__ constexpr RowLayout row_layout(int s) {  // layout in effect during stage s (after its swap)
-    RowLayout L{{0, 1, 2, 3}, {4, 5, 6, 7}};
+    RowLayout L = FWD ? RowLayout{{0, 1, 2, 3}, {4, 5, 6, 7}} : RowLayout{{1, 2, 3, 4}, {0, 5, 6, 7}};
     for (int k = 0; k <= s; ++k) {
         const RowSwap w = FWD ? fwd_swap(k) : inv_swap(k);
         if (w.m >= 0) {
@@ -162,13 +169,16 @@ __device__ constexpr int reg_index(const RowLayout &L, int r) {
 // value of lane t ^ 2^m within the 16-lane row (DPP, VALU only)
 template <int M>
 __device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
+    // every source lane of these patterns lies inside the lane's own 16-lane row,
+    // so no lane keeps an "old" value: mov_dpp (old undefined, bound_ctrl) needs
+    // no zero-initialised destination and can fold into the consuming select
     int x = (int)v;
-    if (M == 0) x = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);        // quad_perm [1,0,3,2]
-    else if (M == 1) x = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    else if (M == 2) {                                                               // ^7 then ^3
-        x = __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);               // row_half_mirror
-        x = __builtin_amdgcn_update_dpp(0, x, 0x1B, 0xF, 0xF, false);                // quad_perm [3,2,1,0]
-    } else x = __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);            // row_ror:8
+    if (M == 0) x = __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);        // quad_perm [1,0,3,2]
+    else if (M == 1) x = __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    else if (M == 2) {                                                        // ^7 then ^3
+        x = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, true);               // row_half_mirror
+        x = __builtin_amdgcn_mov_dpp(x, 0x1B, 0xF, 0xF, true);                // quad_perm [3,2,1,0]
+    } else x = __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, true);            // row_ror:8
     return (uint32_t)x;
 }
 template <int M>
@@ -215,17 +225,18 @@ __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulong
     constexpr int b = FWD ? 7 - S : S;  // index bit of this stage
     constexpr int P = reg_of(L, b);
     const int li = lane_index(L, t);
+    // twiddle index = stage base + row part + (idx0 >> shift), idx0 = li | reg_index(j):
+    // lane and register bits are disjoint, so the shift splits into a per-lane
+    // offset and a compile-time one -> one address per stage, immediate offsets
+    constexpr int SH = FWD ? 8 - S : S + 1;
+    const ulonglong2 *tws = FWD ? tw + ((size_t)1 << (S0 + S)) + (row << S) + (uint32_t)(li >> SH)
+                                : tw + (n >> (S + 1)) + (row << (7 - S)) + (uint32_t)(li >> SH);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         if (j & (1 << P)) continue;
-        const int idx0 = li + reg_index(L, j);
-        if (FWD) {
-            const size_t i = (row << S) + (size_t)(idx0 >> (8 - S));
-            ct_bfly(x[j], x[j + (1 << P)], tw[((size_t)1 << (S0 + S)) + i], q4, nq);
-        } else {
-            const size_t i = (row * 256 + (size_t)idx0) >> (S + 1);
-            gs_bfly(x[j], x[j + (1 << P)], tw[(n >> (S + 1)) + i], q4, nq);
-        }
+        const ulonglong2 w = tws[reg_index(L, j) >> SH];
+        if (FWD) ct_bfly(x[j], x[j + (1 << P)], w, q4, nq);
+        else gs_bfly(x[j], x[j + (1 << P)], w, q4, nq);
     }
 }
 template <bool FWD>
@@ -514,9 +525,14 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
 
     const u64 *ain = F.src ? F.src + (size_t)zseg * F.seg_src + (size_t)limb * n : a;
     u64 x[E];
-    if constexpr (SH) {  // coalesced load (idx = t + 16 r), register-only stages, coalesced store
+    if constexpr (SH) {  // coalesced 16-B loads (idx = 2t + 32m + b -> x[2m + b]), register-only stages
 #pragma unroll
-        for (int r = 0; r < E; ++r) x[r] = valid ? ain[tid_global * LEN + t + T * r] : 0;
+        for (int m = 0; m < E / 2; ++m) {
+            const ulonglong2 v = valid ? *reinterpret_cast<const ulonglong2 *>(ain + tid_global * LEN + 2 * t + 32 * m)
+                                       : make_ulonglong2(0, 0);
+            x[2 * m] = v.x;
+            x[2 * m + 1] = v.y;
+        }
         row_pass_shfl<false>(x, t, tid_global, tw, n, 0, q4, nq);
         if (!valid) return;
 #pragma unroll

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'lib', 'libfhesort.so')
+LIB_PATH = os.environ.get('FHE_LIB') or os.path.join(HERE, 'lib', 'libfhesort.so')  # FHE_LIB: A/B builds
 COEFF_DIR = os.path.join(HERE, 'data')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'fhe_gpu.h')
 
