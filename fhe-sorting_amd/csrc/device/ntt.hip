@@ -78,13 +78,35 @@ __device__ __forceinline__ u64 shoup_fold4(u64 a, u64 w, u64 wp, u64 nq) {  // [
     const uint32_t cross = a0 * w1 + a1 * w0 + h0 * n1 + h1 * n0;
     return t + ((u64)cross << 32);
 }
-// lazy forward CT butterfly: x, y in [0, 8q) -> x, y in [0, 8q)   (q4 = 4q)
+// lazy forward CT butterfly (q4 = 4q): x, y < B q -> x, y < (B' + 4) q with
+// B' = B, or B' = 8 when R (x >= 8q loses 8q; needs B <= 16).  Every prime is
+// < 2^60, so values up to 16q fit in 64 bits and a pass reduces only on the
+// stages fwd_reduce picks (about every other one) instead of on every stage.
+template <bool R>
 __device__ __forceinline__ void ct_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q4, u64 nq) {
     u64 u = x;
-    u = u >= q4 ? u - q4 : u;                    // [0, 4q)
+    if (R) u = u >= 2 * q4 ? u - 2 * q4 : u;      // [0, 8q)
     const u64 v = shoup_fold4(y, w.x, w.y, nq);  // [0, 4q)
     x = u + v;
     y = u + q4 - v;
+}
+// Bound schedule of the forward passes (in units of q).  Column-pass inputs are
+// < 8q (canonical or lazy producers); the column pass leaves values < 16q; the
+// row pass starts from 16 and its last stage always reduces, so the fused
+// epilogues see v < 12q.  Stage s of a pass reduces iff the bound would pass 16
+// (or 12 at the row pass's last stage).
+__host__ __device__ constexpr bool fwd_reduce(bool cols, int pb, int s) {
+    int B = cols ? 8 : 16;
+    for (int k = 0;; ++k) {
+        const bool r = B + 4 > 16 || (!cols && k == pb - 1 && B + 4 > 12);
+        if (k == s) return r;
+        B = (r ? 8 : B) + 4;
+    }
+}
+template <int PB>
+__device__ __forceinline__ void ct_stage(bool cols, int s, u64 &x, u64 &y, ulonglong2 w, u64 q4, u64 nq) {
+    if (fwd_reduce(cols, PB, s)) ct_bfly<true>(x, y, w, q4, nq);
+    else ct_bfly<false>(x, y, w, q4, nq);
 }
 // lazy inverse GS butterfly: x, y in [0, 4q) -> x, y in [0, 4q)
 __device__ __forceinline__ void gs_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q4, u64 nq) {
@@ -102,6 +124,12 @@ __device__ __forceinline__ u64 smod64(int64_t v, int sh, const Mod &m) {  // v *
     u64 r = smod64(v, m);
     for (int i = 0; i < sh; ++i) r = r + r >= m.q ? r + r - m.q : r + r;
     return r;
+}
+__device__ __forceinline__ u64 canon12(u64 x, u64 q, u64 q2) {  // [0, 12q) -> [0, q)
+    x = x >= 4 * q2 ? x - 4 * q2 : x;
+    x = x >= 2 * q2 ? x - 2 * q2 : x;
+    x = x >= q2 ? x - q2 : x;
+    return x >= q ? x - q : x;
 }
 __device__ __forceinline__ u64 canon8(u64 x, u64 q, u64 q2) {  // [0, 8q) -> [0, q)
     x = x >= 2 * q2 ? x - 2 * q2 : x;
@@ -235,7 +263,7 @@ __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulong
     for (int j = 0; j < 16; ++j) {
         if (j & (1 << P)) continue;
         const ulonglong2 w = tws[reg_index(L, j) >> SH];
-        if (FWD) ct_bfly(x[j], x[j + (1 << P)], w, q4, nq);
+        if (FWD) ct_stage<8>(false, S, x[j], x[j + (1 << P)], w, q4, nq);
         else gs_bfly(x[j], x[j + (1 << P)], w, q4, nq);
     }
 }
@@ -367,10 +395,10 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     const u64 c2 = MODE == NTT_MULTAIL ? F.c2[limb] : 0, c2s = MODE == NTT_MULTAIL ? F.c2s[limb] : 0;
     // scaled rescale: out = (K x - v) q_last^-1 = x (K q_last^-1) - v q_last^-1
     const u64 kq = (MODE == NTT_RESCALE && F.scalar) ? mul_shoup(smod64(F.scalar, F.scalar_sh, mp), c1, c1s, q) : 0;
-    // row-pass store of transform value v (lazy, [0, 8q)) for element r at in-row index idx
+    // row-pass store of transform value v (lazy, [0, 12q)) for element r at in-row index idx
     auto store_row = [&](int r, int idx, u64 v) {
         const size_t z = (size_t)zseg, lo = (size_t)limb * n + tid_global * LEN;
-        // lazy epilogues: v in [0, 8q), every intermediate < 2^64 (q < 2^60), one
+        // lazy epilogues: v in [0, 12q), every intermediate < 2^64 (q < 2^60), one
         // final conditional subtraction (the exact Shoup products are in [0, 2q))
         if (MODE == NTT_RESCALE) {
             const u64 xin = EPI_X ? ex[EPI_X ? r : 0] : F.x[z * F.seg_x + lo + idx];
@@ -378,18 +406,18 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
             if (F.scalar) {  // (K x - v) q_last^-1 = x kq - v c1: [0, q) + 2q - [0, 2q)
                 o = mul_barrett(xin, kq, mp) + q2 - shoup_fold(v, c1, c1s, nq);
                 o = o >= q2 ? o - q2 : o;
-            } else {  // (x - v) q_last^-1, x + 8q - v < 9q
-                o = shoup_fold(xin + 2 * q4 - v, c1, c1s, nq);
+            } else {  // (x - v) q_last^-1, x + 12q - v < 13q
+                o = shoup_fold(xin + 3 * q4 - v, c1, c1s, nq);
             }
             F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
-        } else if (MODE == NTT_MULTAIL) {  // (acc + d c2 - v) c1, acc + d c2 + 8q - v < 11q
+        } else if (MODE == NTT_MULTAIL) {  // (acc + d c2 - v) c1, acc + d c2 + 12q - v < 15q
             const u64 acc = EPI_X ? ex[EPI_X ? r : 0] : F.x[z * F.seg_x + lo + idx];
             const u64 dd = EPI_D ? ed[EPI_D ? r : 0] : F.d[z * F.seg_d + lo + idx];
-            const u64 tt = acc + shoup_fold(dd, c2, c2s, nq) + 2 * q4 - v;
+            const u64 tt = acc + shoup_fold(dd, c2, c2s, nq) + 3 * q4 - v;
             const u64 o = shoup_fold(tt, c1, c1s, nq);
             F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
         } else {
-            a[tid_global * LEN + idx] = canon8(v, q, q2);
+            a[tid_global * LEN + idx] = canon12(v, q, q2);
         }
     };
     if constexpr (SH) {
@@ -409,7 +437,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
             const int idx0 = t + T * r0;
             const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
             const size_t wi = ((size_t)1 << (S0 + s)) + i;
-            ct_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q4, nq);
+            ct_stage<PB>(COLS, s, x[r0], x[r0 + (1 << hb)], tw[wi], q4, nq);
         }
     }
     // round-2 twiddles (G == 1: stage s needs 2^(s-EB) of them per lane, index
@@ -450,7 +478,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
                 const size_t wi = ((size_t)1 << (S0 + s)) + i;
                 const ulonglong2 w =
                     PRE ? tw2[PRE ? ((1 << (s - EB)) - 1) + (r0 >> (PB - s)) : 0] : tw[wi];
-                ct_bfly(x[g * T + r0], x[g * T + r0 + (1 << hb)], w, q4, nq);
+                ct_stage<PB>(COLS, s, x[g * T + r0], x[g * T + r0 + (1 << hb)], w, q4, nq);
             }
     }
     // ---- store.  COLS: layout L2 is already lane-contiguous in memory
