@@ -287,8 +287,7 @@ __device__ __forceinline__ int row_final_index(int t, int r) {
     return lane_index(L, t) + reg_index(L, r);
 }
 // FHE_NTT_ROW_SHFL bit mask (A/B timing): 1 inverse row pass, 2 forward row
-// pass use the register-only DPP passes; 4 adds a waves-per-EU hint.  0 keeps
-// both on the LDS-exchange passes.
+// pass use the register-only DPP passes.  0 keeps both on the LDS-exchange passes.
 int &row_shfl_enabled() {
     static int v = [] {
         const char *e = std::getenv("FHE_NTT_ROW_SHFL");
@@ -309,7 +308,7 @@ enum { NTT_PLAIN = 0, NTT_LIFT = 1, NTT_RESCALE = 2, NTT_MULTAIL = 3 };
 // ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
 // SH (row passes with PB = 8 only): register-only stages with DPP lane swaps
 // (row_pass_shfl) instead of the two LDS exchanges.
-template <int PB, int EB, bool COLS, int MODE, bool SH, bool LEAN = false>
+template <int PB, int EB, bool COLS, int MODE, bool SH, bool FULL>
 __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
                                              const NttTables &Tb, const NttFuse &F) {
     static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
@@ -341,7 +340,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     const int zseg = SH ? (int)blockIdx.x * (1 << F.lsegb) + (tr & ((1 << F.lsegb) - 1)) : (int)blockIdx.x;
     const size_t tid_global = SH ? (size_t)blockIdx.y * (NB >> F.lsegb) + (tr >> F.lsegb)
                                  : (size_t)blockIdx.y * NB + tr;  // column or row index
-    const bool valid = tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs);
+    const bool valid = FULL || (tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs));
     u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
     const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
@@ -375,9 +374,8 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // accumulators and d) are loaded now, so the loads overlap the butterflies
     // instead of stalling the store loop (the tile's LDS bounds occupancy, the
     // extra VGPRs do not)
-    // LEAN: the operands are loaded in the store loop instead (fewer VGPRs)
-    constexpr bool EPI_X = !LEAN && !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL);
-    constexpr bool EPI_D = !LEAN && !COLS && MODE == NTT_MULTAIL;
+    constexpr bool EPI_X = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL);
+    constexpr bool EPI_D = !COLS && MODE == NTT_MULTAIL;
     u64 ex[EPI_X ? E : 1], ed[EPI_D ? E : 1];
     if (EPI_X) {
         const size_t lo = (size_t)limb * n + tid_global * LEN;
@@ -444,7 +442,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // t 2^(s-EB) + (r0 >> (PB-s))), loaded before the exchange so their latency
     // overlaps the LDS round trip and barrier instead of stalling round 2
     // (row passes only: in the column pass the extra VGPRs cost a wave of occupancy)
-    constexpr bool PRE = G == 1 && !COLS && !LEAN;
+    constexpr bool PRE = G == 1 && !COLS;
     constexpr int NT2 = (1 << RB) - 1;
     ulonglong2 tw2[PRE ? NT2 : 1];
     if (PRE) {
@@ -515,7 +513,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
 // COLS covers sg in [logN - PB, logN) and multiplies by n^-1 on the way out.
 // F.src (optional): read the input from there instead (out-of-place first
 // pass; segment z, limb l at F.src + z * F.seg_src + l * n)
-template <int PB, int EB, bool COLS, bool SH>
+template <int PB, int EB, bool COLS, bool SH, bool FULL>
 __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
                                              const NttTables &Tb, const NttFuse &F) {
     static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
@@ -545,7 +543,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     // SH: one row of 2^F.lsegb segments per block (shared per-row twiddles)
     const int zseg = SH ? (int)blockIdx.x * (1 << F.lsegb) + (tr & ((1 << F.lsegb) - 1)) : (int)blockIdx.x;
     const size_t tid_global = SH ? (size_t)blockIdx.y * (NB >> F.lsegb) + (tr >> F.lsegb) : (size_t)blockIdx.y * NB + tr;
-    const bool valid = tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs);
+    const bool valid = FULL || (tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs));
     u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
     const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
@@ -646,48 +644,46 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     }
 }
 
-// OCC: requested waves per SIMD (0: the compiler's choice).  The LDS tile of a
-// 256-point pass (34 KiB per block) already caps a CU at 4 blocks = 4 waves per
-// SIMD; asking for 4 keeps the compiler from hoisting every twiddle load into
-// registers (the inverse column pass otherwise takes 232 VGPRs = 2 waves).
-template <int PB, int EB, bool COLS, int MODE, int OCC, bool LEAN = false>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, 8))) void k_ntt_fwd(
+// FULL: the grid covers the transforms exactly (every launch on rings >= 2^11),
+// so no lane needs the bounds check and the loads / stores carry no exec-mask
+// branches.  (Waves-per-EU hints and "lean" epilogue variants were measured
+// slower in round 2 and removed)
+template <int PB, int EB, bool COLS, int MODE, bool FULL>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_ntt_fwd(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_fwd_body<PB, EB, COLS, MODE, false, LEAN>(data, seg, pmap, smap, logN, Tb, F);
+    ntt_fwd_body<PB, EB, COLS, MODE, false, FULL>(data, seg, pmap, smap, logN, Tb, F);
 }
-// FHE_NTT_LEAN (A/B timing) bit mask: 1 = the HMult-tail row pass (mode 3),
-// 2 = the rescale row pass (mode 2) load their epilogue operands in the store
-// loop and skip the round-2 twiddle prefetch
-int &ntt_lean() {
+template <int PB, int EB, bool COLS, bool FULL>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_ntt_inv(
+    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
+    ntt_inv_body<PB, EB, COLS, false, FULL>(data, seg, pmap, smap, logN, Tb, F);
+}
+// register-only row passes (PB = 8)
+template <int MODE, bool FULL>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_ntt_fwd_row(
+    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
+    ntt_fwd_body<8, 4, false, MODE, true, FULL>(data, seg, pmap, smap, logN, Tb, F);
+}
+template <bool FULL>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_ntt_inv_row(
+    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
+    ntt_inv_body<8, 4, false, true, FULL>(data, seg, pmap, smap, logN, Tb, F);
+}
+
+// FHE_NTT_FULL (A/B timing): which passes take the exact-grid variant (bit mask:
+// 1 forward column, 2 forward column + lift, 4 forward row, 8 rescale row,
+// 16 HMult-tail row, 32 inverse column, 64 inverse row)
+int &ntt_full_mask() {
     static int v = [] {
-        const char *e = std::getenv("FHE_NTT_LEAN");
-        return e ? std::atoi(e) : 0;
+        const char *e = std::getenv("FHE_NTT_FULL");
+        return e ? std::atoi(e) : 53;  // measured: the rescale row, inverse row and lift column passes keep the checks (more VGPRs without them)
     }();
     return v;
 }
-template <int PB, int EB, bool COLS, int OCC>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, 8))) void k_ntt_inv(
-    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_inv_body<PB, EB, COLS, false>(data, seg, pmap, smap, logN, Tb, F);
-}
-// FHE_NTT_OCC (A/B timing): waves-per-SIMD hint of the LDS-exchange passes (0 = none)
-int &ntt_occ() {
-    static int v = [] {
-        const char *e = std::getenv("FHE_NTT_OCC");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-// register-only row passes (PB = 8): OCC = requested waves per SIMD (0: compiler's choice)
-template <int MODE, int OCC>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, 8))) void k_ntt_fwd_row(
-    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_fwd_body<8, 4, false, MODE, true>(data, seg, pmap, smap, logN, Tb, F);
-}
-template <int OCC>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 1, 8))) void k_ntt_inv_row(
-    u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_inv_body<8, 4, false, true>(data, seg, pmap, smap, logN, Tb, F);
+template <bool COLS, bool FWD, int MODE>
+constexpr int full_bit() {
+    return FWD ? (COLS ? (MODE == NTT_LIFT ? 2 : 1) : MODE == NTT_RESCALE ? 8 : MODE == NTT_MULTAIL ? 16 : 4)
+               : (COLS ? 32 : 64);
 }
 
 template <int PB, int EB, bool COLS, bool FWD, int MODE>
@@ -699,6 +695,8 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     const bool sh = CAN_SH && (mode & (FWD ? 2 : 1)) != 0;
     const int count = 1 << (T.logN - PB);  // columns (COLS) or rows (ROWS)
     dim3 grid((unsigned)segs, (unsigned)((count + NB - 1) / NB), (unsigned)limbs);
+    const bool want_full = (ntt_full_mask() & full_bit<COLS, FWD, MODE>()) != 0;
+    bool full = want_full && count % NB == 0;
     NttFuse Fs = F;
     if (sh) {  // 2^lsegb segments of one row per block (lsegb <= 4: 16 transforms per block)
         Fs.lsegb = 0;
@@ -707,63 +705,43 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
         const int rows_pb = NB >> Fs.lsegb;
         grid = dim3((unsigned)((segs + (1 << Fs.lsegb) - 1) >> Fs.lsegb), (unsigned)((count + rows_pb - 1) / rows_pb),
                     (unsigned)limbs);
+        full = want_full && count % rows_pb == 0 && segs % (1 << Fs.lsegb) == 0;
     }
     LaunchClock *clk = launch_clock();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const int slot = clk ? clk->events(e0, e1) : -1;
-    const int occ = (mode & 4) ? 2 : 1;
-    constexpr int FWD_OCC = MODE == NTT_MULTAIL ? 4 : MODE == NTT_RESCALE ? 5 : 6;
-    if (FWD && sh && occ == 2)
-        hipExtLaunchKernelGGL((k_ntt_fwd_row<MODE, FWD_OCC>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
-                              T, Fs);
-    else if (FWD && sh)
-        hipExtLaunchKernelGGL((k_ntt_fwd_row<MODE, 0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN,
-                              T, Fs);
-    else if (FWD && !COLS && PB == 8 && MODE == NTT_MULTAIL && (ntt_lean() & 1))
-        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE, 0, true>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg,
-                              pmap, smap, T.logN, T, F);
-    else if (FWD && !COLS && PB == 8 && MODE == NTT_RESCALE && (ntt_lean() & 2))
-        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE, 0, true>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg,
-                              pmap, smap, T.logN, T, F);
-    else if (FWD && ntt_occ() == 4 && PB == 8)
-        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE, 4>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap,
-                              smap, T.logN, T, F);
-    else if (FWD)
-        hipExtLaunchKernelGGL((k_ntt_fwd<PB, EB, COLS, MODE, 0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
-                              T.logN, T, F);
-    else if (sh && occ == 2)
-        hipExtLaunchKernelGGL((k_ntt_inv_row<5>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T,
-                              Fs);
-    else if (sh)
-        hipExtLaunchKernelGGL((k_ntt_inv_row<0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T,
-                              Fs);
-    else if (ntt_occ() == 4 && PB == 8)
-        hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS, 4>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
-                              T.logN, T, F);
-    else
-        hipExtLaunchKernelGGL((k_ntt_inv<PB, EB, COLS, 0>), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap,
-                              T.logN, T, F);
+#define FHE_NTT_LAUNCH(K, FF) \
+    hipExtLaunchKernelGGL((K), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
+    if (FWD && sh) {
+        if (full) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true>), Fs);
+        else FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false>), Fs);
+    } else if (FWD) {
+        if (full) FHE_NTT_LAUNCH((k_ntt_fwd<PB, EB, COLS, MODE, true>), F);
+        else FHE_NTT_LAUNCH((k_ntt_fwd<PB, EB, COLS, MODE, false>), F);
+    } else if (sh) {
+        if (full) FHE_NTT_LAUNCH((k_ntt_inv_row<true>), Fs);
+        else FHE_NTT_LAUNCH((k_ntt_inv_row<false>), Fs);
+    } else {
+        if (full) FHE_NTT_LAUNCH((k_ntt_inv<PB, EB, COLS, true>), F);
+        else FHE_NTT_LAUNCH((k_ntt_inv<PB, EB, COLS, false>), F);
+    }
+#undef FHE_NTT_LAUNCH
     if (clk) {
         // same spelling as the demangled symbol rocprofv3 prints, plus the caller tag
-        // (the instantiation the branches above launched; the switches are per process)
-        static const std::string base = [&]() {
-            const std::string pe = std::to_string(PB) + ", " + std::to_string(EB) + (COLS ? ", true" : ", false");
-            const bool lean = FWD && !COLS && PB == 8 &&
-                              ((MODE == NTT_MULTAIL && (ntt_lean() & 1)) || (MODE == NTT_RESCALE && (ntt_lean() & 2)));
-            const int o = (ntt_occ() == 4 && PB == 8 && !lean) ? 4 : 0;
-            if (FWD && sh) return "k_ntt_fwd_row<" + std::to_string(MODE) + ", " + std::to_string(occ == 2 ? FWD_OCC : 0) + ">";
-            if (FWD)
-                return "k_ntt_fwd<" + pe + ", " + std::to_string(MODE) + ", " + std::to_string(o) +
-                       (lean ? ", true>" : ", false>");
-            if (sh) return std::string(occ == 2 ? "k_ntt_inv_row<5>" : "k_ntt_inv_row<0>");
-            return "k_ntt_inv<" + pe + ", " + std::to_string(o) + ">";
-        }();
-        static std::map<const char *, std::string> names;
+        // (the instantiation the branches above launched)
+        const std::string pe = std::to_string(PB) + ", " + std::to_string(EB) + (COLS ? ", true" : ", false");
+        const std::string fl = full ? "true>" : "false>";
+        const std::string base = FWD && sh ? "k_ntt_fwd_row<" + std::to_string(MODE) + ", " + fl
+                                 : FWD     ? "k_ntt_fwd<" + pe + ", " + std::to_string(MODE) + ", " + fl
+                                 : sh      ? "k_ntt_inv_row<" + fl
+                                           : "k_ntt_inv<" + pe + ", " + fl;
+        static std::map<std::string, std::string> names;  // stable c_str() per (kernel, caller)
         static std::mutex mu;
         const char *ph = launch_phase();
+        const std::string key = ph ? base + "@" + ph : base;
         std::lock_guard<std::mutex> lk(mu);
-        auto it = names.find(ph);
-        if (it == names.end()) it = names.emplace(ph, ph ? base + "@" + ph : base).first;
+        auto it = names.find(key);
+        if (it == names.end()) it = names.emplace(key, key).first;
         // one read + one write of every limb touched (fused epilogues: + the extra operands)
         const double extra = MODE == NTT_RESCALE ? 1.0 : MODE == NTT_MULTAIL ? 2.0 : 0.0;
         clk->record(slot, it->second.c_str(), (2.0 + extra) * 8.0 * (double)limbs * segs * ((size_t)1 << T.logN));
