@@ -422,6 +422,8 @@ def run_kway(a, d):
     ct = ctx.encrypt(x, s)
     setup_s = time.time() - t0
 
+    ctx.set_sort_lanes(a.lanes)  # >= 2: a stage's two comparisons run on two streams
+
     def run():
         return ctx.kway_sort(ct, k, M, cfg, boot=B)
 
@@ -468,7 +470,7 @@ def run_kway(a, d):
             'config': {'workload': f'k-way network k={k}, M={M} (N={N}, {s} slots), ringDim 2^{logN}, depth {depth}, '
                                    f'scale 2^59, levelBudget {budget}, CompositeSign{cfg}, bootstrapping',
                        'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'slots': s,
-                       'parallelism': f'replicas x{d.world}', 'collective': 'none'},
+                       'lanes_per_gpu': min(a.lanes, 2), 'parallelism': f'replicas x{d.world}', 'collective': 'none'},
             'max_abs_err': err,
             'output_level': out.level,
             'hmult_per_sort': int(hm_total / a.steps / d.world),
@@ -480,8 +482,10 @@ def run_kway(a, d):
         }
         if not a.no_roofline:
             try:
+                ctx.set_sort_lanes(1)  # the live clock needs one stream
                 res['roofline'] = with_run(roofline(ctx, run, a.clock_json, 'pmc_traffic_kway.json'),
                                            res['ms_per_step'], 1, op_total / a.steps / d.world)
+                ctx.set_sort_lanes(a.lanes)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
         if d.world == 1 and not a.no_cpu_baseline:

@@ -4,6 +4,9 @@
 // meet (FLEXIBLEAUTO re-encodes a plaintext at its operand's level).
 #include "kway.hpp"
 
+#include <exception>
+#include <thread>
+
 #include <cstdio>
 #include <cstdlib>
 
@@ -145,6 +148,52 @@ void Sorter::checkLevel(CtPtr &c, int need, const SignConfig &cfg) {
         }
         std::fprintf(stderr, "  boot %d at level %d: max|in| %.6g, max|out - in| %.3g\n", bootstraps, in->level, mx, e);
     }
+}
+
+namespace {
+// run `lane` on a second host thread while `main` runs on this one; both
+// finish (and the lane's stream drains) before any exception is rethrown
+template <class A, class B>
+void concurrently(A &&main, B &&lane) {
+    std::exception_ptr err;
+    std::thread t([&] {
+        try {
+            lane();
+        } catch (...) {
+            err = std::current_exception();
+        }
+    });
+    try {
+        main();
+    } catch (...) {
+        t.join();
+        throw;
+    }
+    t.join();
+    if (err) std::rethrow_exception(err);
+}
+}  // namespace
+
+void Sorter::checkLevel2(CtPtr &c1, CtPtr &c2, int need, const SignConfig &cfg) {
+    const int L = cc.params().L;
+    if (!laneEng || L - c1->level >= need + 1 || L - c2->level >= need + 1) {
+        checkLevel(c1, need, cfg);  // at most one bootstrap: on this engine
+        checkLevel(c2, need, cfg);
+        return;
+    }
+    // both need a bootstrap: c2's runs on the lane (its own bootstrapper)
+    if (!cfg.boot || !laneCfg.boot) throw std::runtime_error("k-way: no levels left (set up bootstrapping for this depth)");
+    cc.sync();
+    CtPtr b2;
+    concurrently([&] { c1 = cfg.boot(*c1); },
+                 [&] {
+                     b2 = laneCfg.boot(*c2);
+                     laneEng->sync();
+                 });
+    c2 = b2;
+    bootstraps += 2;
+    cc.ctr += laneEng->ctr;
+    laneEng->ctr = Counters();
 }
 
 // EvalUtils.cpp:113-146: binary decomposition, ascending powers of two
@@ -395,8 +444,21 @@ void Sorter::comparisonForSort2(const CtPtr &x, const std::vector<std::vector<in
     CtPtr r1, r2;
     rightRotateForSort(x, ind, logDist, slope, r1, &fix);
     rightRotateForSort(r1, ind, logDist, slope, r2, nullptr);
-    c1 = comp.compare(cc, *x, *r1, SignFunc::CompositeSign, cfg);
-    c2 = comp.compare(cc, *x, *r2, SignFunc::CompositeSign, cfg);
+    if (!laneEng) {
+        c1 = comp.compare(cc, *x, *r1, SignFunc::CompositeSign, cfg);
+        c2 = comp.compare(cc, *x, *r2, SignFunc::CompositeSign, cfg);
+        return;
+    }
+    cc.sync();  // x, r2 complete before the lane's stream reads them
+    CtPtr d2;
+    concurrently([&] { c1 = comp.compare(cc, *x, *r1, SignFunc::CompositeSign, cfg); },
+                 [&] {
+                     d2 = comp.compare(*laneEng, *x, *r2, SignFunc::CompositeSign, laneCfg);
+                     laneEng->sync();
+                 });
+    c2 = d2;
+    cc.ctr += laneEng->ctr;
+    laneEng->ctr = Counters();
 }
 
 // Sorter.cpp:289-404
@@ -414,8 +476,7 @@ CtPtr Sorter::sorter(const Ciphertext &input, const SignConfig &cfg) {
             checkLevel(ct, level[(size_t)k], cfg);
             if (k == 5) {
                 comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
-                checkLevel(c1, level[5], cfg);
-                checkLevel(c2, level[5], cfg);
+                checkLevel2(c1, c2, level[5], cfg);
                 ct = runFiveSorter(ct, ind, shift, c1, c2);
             } else {
                 c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
@@ -430,16 +491,14 @@ CtPtr Sorter::sorter(const Ciphertext &input, const SignConfig &cfg) {
                 ct = runTwoSorter(ct, ind, shift, c1);
             } else {
                 comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
-                checkLevel(c1, level[4], cfg);
-                checkLevel(c2, level[4], cfg);
+                checkLevel2(c1, c2, level[4], cfg);
                 ct = runFourSorter(ct, ind, shift, c1, c2);
             }
             ct = cc.add(*ct, *fix);
         } else if (k == 5 && slope == 1) {
             checkLevel(ct, level[5], cfg);
             comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
-            checkLevel(c1, level[5], cfg);
-            checkLevel(c2, level[5], cfg);
+            checkLevel2(c1, c2, level[5], cfg);
             ct = cc.add(*run2345Sorter(ct, ind, shift, c1, c2), *fix);
         } else if ((k == 5 && slope == 2) || (k == 3 && slope == 1)) {
             checkLevel(ct, level[3], cfg);

@@ -42,6 +42,12 @@ class Sorter {
     CtPtr sorter(const Ciphertext &x, const SignConfig &cfg);
     int stagesRun = 0;   // stages completed by the last sorter() call
     int bootstraps = 0;  // checkLevelAndBoot bootstraps of the last sorter() call
+    // optional second lane: a forked engine (own stream and pool, shared keys)
+    // and the sign configuration to use on it (its own bootstrapper).  The two
+    // comparisons of a k = 5 stage and their level checks then run on two host
+    // threads at once; every operation is the same, so the words are too.
+    Engine *laneEng = nullptr;
+    SignConfig laneCfg;
     // SortUtils::fcnL (kk = 1: returns {fcnL(x0, x1, c0)}) or the kk-sorter,
     // kk = 2..5 (SortUtils.cpp:5-208), on their own: SortUtilsTest's cases
     std::vector<CtPtr> kSorter(int kk, const std::vector<CtPtr> &x, const std::vector<CtPtr> &cmp);
@@ -55,6 +61,8 @@ class Sorter {
 
     const Plaintext &mask(const std::vector<double> &v, const Ciphertext &like);
     void checkLevel(CtPtr &c, int need, const SignConfig &cfg);
+    // checkLevel of c1 (this engine) and c2 (the lane, when set) at once
+    void checkLevel2(CtPtr &c1, CtPtr &c2, int need, const SignConfig &cfg);
     CtPtr leftRotate(const CtPtr &c, long r);
     CtPtr rightRotate(const CtPtr &c, long r);
     CtPtr flip(const CtPtr &c, const std::vector<double> &m);

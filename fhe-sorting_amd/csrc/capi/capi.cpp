@@ -27,6 +27,7 @@ struct fhe_ctx {
     std::map<std::pair<int, std::vector<int>>, std::unique_ptr<DirectSortN>> sorters;
     int sort_stack = 32;
     int sort_lanes = 2;
+    std::unique_ptr<Engine> kway_lane;  // the k-way sorter's second lane (forked on first use)
 };
 struct fhe_ct {
     CtPtr p;
@@ -36,6 +37,7 @@ struct fhe_pt {
 };
 struct fhe_boot {
     std::unique_ptr<Bootstrapper> b;
+    std::unique_ptr<Bootstrapper> lane_b;  // the same setup on the context's k-way lane
 };
 struct fhe_rot_tree {
     std::unique_ptr<RotationTreeN> t;
@@ -550,6 +552,16 @@ int fhe_kway_sort_boot(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int 
         if (boot) {
             Bootstrapper *B = boot->b.get();
             cfg.boot = [B](const Ciphertext &c) { return B->evalBootstrap(c); };
+        }
+        if (ctx->sort_lanes >= 2) {  // the two comparisons of a stage on two streams
+            if (!ctx->kway_lane) ctx->kway_lane = ctx->eng->fork();
+            s.laneEng = ctx->kway_lane.get();
+            s.laneCfg = cfg;
+            if (boot) {
+                if (!boot->lane_b) boot->lane_b = std::make_unique<Bootstrapper>(*ctx->kway_lane, boot->b->cfg);
+                Bootstrapper *LB = boot->lane_b.get();
+                s.laneCfg.boot = [LB](const Ciphertext &c) { return LB->evalBootstrap(c); };
+            }
         }
         *out = wrap(s.sorter(*x->p, cfg));
         if (bootstraps) *bootstraps = s.bootstraps;

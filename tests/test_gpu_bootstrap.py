@@ -115,6 +115,33 @@ def test_kway_with_bootstrap_matches_oracle():
         gpu.close()
 
 
+def test_kway5_two_lanes_match_oracle():
+    """k = 5: a stage's two comparisons (and their level-check bootstraps) run on
+    two engine lanes at once (fhe_set_sort_lanes >= 2, the default); the words
+    equal the oracle's sequential sorter and the one-lane run."""
+    k, M = 5, 2
+    N = k ** M
+    rots = F.kway_rotation_indices(N)
+    orc, gpu, ob, gb = _pair(11, 26, 54, _slots(N), (2, 2))
+    try:
+        orc.gen_rotation_keys(rots)
+        gpu.gen_rotation_keys(rots)
+        x = np.random.default_rng(5).permutation(N) * (1 - 1e-8) / N
+        ox = orc.encrypt(x, _slots(N))
+        gpu.set_sort_lanes(2)
+        g2 = gpu.kway_sort(gpu.from_oracle(ox), k, M, (3, 2, 2), boot=gb)
+        b2 = gpu.kway_bootstraps
+        gpu.set_sort_lanes(1)
+        g1 = gpu.kway_sort(gpu.from_oracle(ox), k, M, (3, 2, 2), boot=gb)
+        assert b2 >= 1 and gpu.kway_bootstraps == b2
+        same(g2, g1)
+        o = orc.kway_sort(ox, k, M, (3, 2, 2), boot=ob)
+        same(g2, o)
+        assert np.max(np.abs(gpu.decrypt(g2)[:N] - np.sort(x))) < 0.01
+    finally:
+        gpu.close()
+
+
 @pytest.mark.parametrize('k,M,cfg', [(2, 4, (3, 2, 2)), (3, 2, (3, 2, 2)), (5, 2, (3, 2, 3))])
 def test_kway_with_bootstrap_sorts(k, M, cfg):
     N = k ** M
