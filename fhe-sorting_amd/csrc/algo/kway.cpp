@@ -8,6 +8,7 @@
 #include <thread>
 
 #include <cstdio>
+#include <map>
 #include <cstdlib>
 
 #include <cmath>
@@ -209,6 +210,50 @@ CtPtr Sorter::rightRotate(const CtPtr &c, long r) {
         if (r & 1) o = cc.rotate(*o, -p);
     return o;
 }
+// Several leftRotate (amt > 0) / rightRotate (amt < 0) chains at once: the j-th
+// power-of-two rotation of every chain at one level runs as one batch with a
+// rotation per member (Engine::rotate_members), so a stage's 4-12 rotation
+// chains cost one key-switch pipeline per step instead of one per rotation.
+// Each chain applies the same rotations in the same order as above.
+std::vector<CtPtr> Sorter::rotateMany(const std::vector<CtPtr> &src, const std::vector<long> &amt) {
+    const size_t m = src.size();
+    std::vector<CtPtr> cur = src;
+    std::vector<long> rem(m), pw(m, 1);
+    for (size_t i = 0; i < m; ++i) rem[i] = amt[i] < 0 ? -amt[i] : amt[i];
+    for (;;) {
+        std::map<int, std::vector<size_t>> at;  // level -> chains with a rotation this step
+        std::vector<long> step(m, 0);
+        for (size_t i = 0; i < m; ++i) {
+            while (rem[i] > 0 && !(rem[i] & 1)) {
+                rem[i] >>= 1;
+                pw[i] <<= 1;
+            }
+            if (rem[i] == 0) continue;
+            step[i] = amt[i] > 0 ? pw[i] : -pw[i];
+            rem[i] >>= 1;
+            pw[i] <<= 1;
+            at[cur[i]->level].push_back(i);
+        }
+        if (at.empty()) break;
+        for (auto &kv : at) {
+            const auto &idx = kv.second;
+            if (idx.size() == 1) {
+                cur[idx[0]] = cc.rotate(*cur[idx[0]], step[idx[0]]);
+                continue;
+            }
+            std::vector<const Ciphertext *> ptrs;
+            std::vector<long> ks;
+            for (size_t i : idx) {
+                ptrs.push_back(cur[i].get());
+                ks.push_back(step[i]);
+            }
+            const CtPtr r = cc.rotate_members(*cc.stack(ptrs), ks);
+            for (size_t j = 0; j < idx.size(); ++j) cur[idx[j]] = cc.member(*r, (int)j);
+        }
+    }
+    return cur;
+}
+
 // EvalUtils::flipCtxt(ctxt, mask) = mask - ctxt (EvalUtils.cpp:102-105)
 CtPtr Sorter::flip(const CtPtr &c, const std::vector<double> &m) { return cc.plain_sub(mask(m, *c), *c); }
 CtPtr Sorter::maskMul(const CtPtr &c, const std::vector<double> &m) { return cc.mul_plain(*c, mask(m, *c)); }
@@ -291,8 +336,15 @@ std::vector<CtPtr> Sorter::kSorter(int kk, const std::vector<CtPtr> &x, const st
 }
 // SortUtils.cpp:424-433
 CtPtr Sorter::slotAssemble(const CtPtr *s, long num, long shift) {
+    std::vector<CtPtr> src;
+    std::vector<long> amt;
+    for (long i = 1; i < num; ++i) {
+        src.push_back(s[i]);
+        amt.push_back(-i * shift);
+    }
+    const auto r = rotateMany(src, amt);
     CtPtr o = s[0];
-    for (long i = 1; i < num; ++i) o = cc.add(*o, *rightRotate(s[i], i * shift));
+    for (auto &c : r) o = cc.add(*o, *c);
     return o;
 }
 
@@ -310,17 +362,18 @@ CtPtr Sorter::runTwoSorter(const CtPtr &x, const std::vector<std::vector<int>> &
     CtPtr s[2];
     twoSorter(x, leftRotate(x, shift), c, s);
     for (auto &v : s) v = maskMul(v, m2);
-    return cc.add(*s[0], *rightRotate(s[1], shift));
+    return slotAssemble(s, 2, shift);
 }
 // Sorter.cpp:38-68 (+ slotMatching3, SortUtils.cpp:219-241)
 CtPtr Sorter::runThreeSorter(const CtPtr &x, const std::vector<std::vector<int>> &ind, long shift, const CtPtr &c) {
     const auto m3 = groupMask(ind, 3);
-    const CtPtr xs[3] = {x, leftRotate(x, shift), leftRotate(x, 2 * shift)};
-    const CtPtr cs[3] = {flip(leftRotate(c, shift), m3), c, flip(leftRotate(c, 2 * shift), m3)};
+    const auto r = rotateMany({x, x, c, c}, {shift, 2 * shift, shift, 2 * shift});
+    const CtPtr xs[3] = {x, r[0], r[1]};
+    const CtPtr cs[3] = {flip(r[2], m3), c, flip(r[3], m3)};
     CtPtr s[3];
     threeSorter(xs, cs, s);
     for (auto &v : s) v = maskMul(v, m3);
-    return cc.add(*cc.add(*s[0], *rightRotate(s[1], shift)), *rightRotate(s[2], 2 * shift));
+    return slotAssemble(s, 3, shift);
 }
 // Sorter.cpp:70-85 (+ slotMatching4, SortUtils.cpp:243-287; the reference's
 // masked products at :262-267 are overwritten before use and are skipped)
@@ -328,15 +381,18 @@ CtPtr Sorter::runFourSorter(const CtPtr &x, const std::vector<std::vector<int>> 
                             const CtPtr &c2) {
     std::vector<double> m41;
     genMask(ind, 4, 1, m41);
+    const auto r = rotateMany({c1, c1, c1, c2, x, x, x},
+                              {shift, 2 * shift, 3 * shift, shift, shift, 2 * shift, 3 * shift});
     CtPtr cs[6];
     cs[2] = c1;
-    cs[0] = flip(leftRotate(c1, shift), m41);
-    cs[3] = flip(leftRotate(c1, 2 * shift), m41);
-    cs[5] = flip(leftRotate(c1, 3 * shift), m41);
+    cs[0] = flip(r[0], m41);
+    cs[3] = flip(r[1], m41);
+    cs[5] = flip(r[2], m41);
     cs[1] = c2;
-    cs[4] = leftRotate(c2, shift);
+    cs[4] = r[3];
     CtPtr xs[4];
-    for (int i = 0; i < 4; ++i) xs[i] = maskMul(leftRotate(x, i * shift), m41);
+    xs[0] = maskMul(x, m41);
+    for (int i = 1; i < 4; ++i) xs[i] = maskMul(r[3 + (size_t)i], m41);
     CtPtr s[4];
     fourSorter(xs, cs, s);
     return slotAssemble(s, 4, shift);
@@ -346,17 +402,21 @@ CtPtr Sorter::runFiveSorter(const CtPtr &x, const std::vector<std::vector<int>> 
                             const CtPtr &c2) {
     const auto m5 = groupMask(ind, 5);
     CtPtr xs[5], cs[10];
-    for (int i = 0; i < 5; ++i) xs[i] = leftRotate(x, i * shift);
+    const auto r = rotateMany({x, x, x, x, c1, c1, c1, c1, c2, c2, c2, c2},
+                              {shift, 2 * shift, 3 * shift, 4 * shift, shift, 2 * shift, 3 * shift, 4 * shift,
+                               shift, 2 * shift, 3 * shift, 4 * shift});
+    xs[0] = x;
+    for (int i = 1; i < 5; ++i) xs[i] = r[(size_t)i - 1];
     cs[3] = c1;
-    cs[0] = leftRotate(c1, shift);
-    cs[4] = leftRotate(c1, 2 * shift);
-    cs[7] = leftRotate(c1, 3 * shift);
-    cs[9] = leftRotate(c1, 4 * shift);
+    cs[0] = r[4];
+    cs[4] = r[5];
+    cs[7] = r[6];
+    cs[9] = r[7];
     cs[2] = c2;
-    cs[6] = leftRotate(c2, shift);
-    cs[1] = leftRotate(c2, 2 * shift);
-    cs[5] = leftRotate(c2, 3 * shift);
-    cs[8] = leftRotate(c2, 4 * shift);
+    cs[6] = r[8];
+    cs[1] = r[9];
+    cs[5] = r[10];
+    cs[8] = r[11];
     for (int i : {0, 1, 4, 5, 7, 8, 9}) cs[i] = flip(cs[i], m5);
     CtPtr s[5];
     fiveSorter(xs, cs, s);
@@ -379,17 +439,22 @@ CtPtr Sorter::run2345Sorter(const CtPtr &x, const std::vector<std::vector<int>> 
         if (g == 5) m5[i] = 1.0;
     }
     CtPtr xs[5], cs[10];
-    for (int i = 0; i < 5; ++i) xs[i] = leftRotate(x, i * shift);
-    cs[0] = flip(leftRotate(c1, shift), m2345);
-    cs[1] = cc.add(*maskMul(c1, m3), *flip(maskMul(leftRotate(c2, 2 * shift), m45), m45));
+    const auto r = rotateMany({x, x, x, x, c1, c1, c1, c1, c2, c2, c2, c2},
+                              {shift, 2 * shift, 3 * shift, 4 * shift, shift, 2 * shift, 3 * shift, 4 * shift,
+                               shift, 2 * shift, 3 * shift, 4 * shift});
+    xs[0] = x;
+    for (int i = 1; i < 5; ++i) xs[i] = r[(size_t)i - 1];
+    const CtPtr *c1r = &r[4] - 1, *c2r = &r[8] - 1;  // c1r[i] = leftRotate(c1, i shift), i >= 1
+    cs[0] = flip(c1r[1], m2345);
+    cs[1] = cc.add(*maskMul(c1, m3), *flip(maskMul(c2r[2], m45), m45));
     cs[2] = cc.add(*maskMul(c1, m4), *maskMul(c2, m5));
     cs[3] = maskMul(c1, m5);
-    cs[4] = flip(maskMul(leftRotate(c1, 2 * shift), m345), m345);
-    cs[5] = flip(maskMul(leftRotate(c2, 3 * shift), m45), m45);
-    cs[6] = maskMul(leftRotate(c2, shift), m5);
-    cs[7] = flip(maskMul(leftRotate(c1, 3 * shift), m45), m45);
-    cs[8] = flip(maskMul(leftRotate(c2, 4 * shift), m5), m5);
-    cs[9] = flip(maskMul(leftRotate(c1, 4 * shift), m5), m5);
+    cs[4] = flip(maskMul(c1r[2], m345), m345);
+    cs[5] = flip(maskMul(c2r[3], m45), m45);
+    cs[6] = maskMul(c2r[1], m5);
+    cs[7] = flip(maskMul(c1r[3], m45), m45);
+    cs[8] = flip(maskMul(c2r[4], m5), m5);
+    cs[9] = flip(maskMul(c1r[4], m5), m5);
     CtPtr s[5];
     fiveSorter(xs, cs, s);
     s[0] = maskMul(s[0], m2345);
@@ -417,7 +482,8 @@ void Sorter::rightRotateForSort(const CtPtr &x, const std::vector<std::vector<in
         const long g = slope == 0 ? k - 1 : k - 2;  // the one group size present
         const CtPtr xr = maskMul(x, right[(size_t)g]);
         if (slope != 0 && fix) *fix = cc.sub(*cc.sub(*x, *xl), *xr);
-        rot = cc.add(*rightRotate(xl, r), *leftRotate(xr, g * r));
+        const auto rr = rotateMany({xl, xr}, {-r, g * r});
+        rot = cc.add(*rr[0], *rr[1]);
         return;
     }
     std::vector<CtPtr> xr((size_t)k);
@@ -427,8 +493,15 @@ void Sorter::rightRotateForSort(const CtPtr &x, const std::vector<std::vector<in
         for (long i = 0; i < k; ++i) f = cc.sub(*f, *xr[(size_t)i]);
         *fix = f;
     }
-    rot = rightRotate(xl, r);
-    for (long i = 1; i < k; ++i) rot = cc.add(*rot, *leftRotate(xr[(size_t)i], i * r));
+    std::vector<CtPtr> src{xl};
+    std::vector<long> amt{-r};
+    for (long i = 1; i < k; ++i) {
+        src.push_back(xr[(size_t)i]);
+        amt.push_back(i * r);
+    }
+    const auto rr = rotateMany(src, amt);
+    rot = rr[0];
+    for (size_t i = 1; i < rr.size(); ++i) rot = cc.add(*rot, *rr[i]);
 }
 
 // Sorter.cpp:258-268: comp = [x > rot(x)]

@@ -65,6 +65,7 @@ class Sorter {
     void checkLevel2(CtPtr &c1, CtPtr &c2, int need, const SignConfig &cfg);
     CtPtr leftRotate(const CtPtr &c, long r);
     CtPtr rightRotate(const CtPtr &c, long r);
+    std::vector<CtPtr> rotateMany(const std::vector<CtPtr> &src, const std::vector<long> &amt);
     CtPtr flip(const CtPtr &c, const std::vector<double> &m);
     CtPtr maskMul(const CtPtr &c, const std::vector<double> &m);
     CtPtr fcnL(const CtPtr &a, const CtPtr &b, const CtPtr &cmp);
