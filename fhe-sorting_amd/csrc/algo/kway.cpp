@@ -4,11 +4,13 @@
 // meet (FLEXIBLEAUTO re-encodes a plaintext at its operand's level).
 #include "kway.hpp"
 
+#include <chrono>
 #include <exception>
 #include <thread>
 
 #include <cstdio>
 #include <map>
+#include <string>
 #include <cstdlib>
 
 #include <cmath>
@@ -152,6 +154,23 @@ void Sorter::checkLevel(CtPtr &c, int need, const SignConfig &cfg) {
 }
 
 namespace {
+// FHE_KWAY_TIMES (diagnostics): wall time per phase of sorter(), the engine
+// synchronised at every phase boundary; printed to stderr after the sort
+struct PhaseTimes {
+    bool on = std::getenv("FHE_KWAY_TIMES") != nullptr;
+    std::map<std::string, double> s;
+    std::chrono::steady_clock::time_point t0;
+    void start(Engine &cc) {
+        if (!on) return;
+        cc.sync();
+        t0 = std::chrono::steady_clock::now();
+    }
+    void stop(Engine &cc, const char *what) {
+        if (!on) return;
+        cc.sync();
+        s[what] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
 // run `lane` on a second host thread while `main` runs on this one; both
 // finish (and the lane's stream drains) before any exception is rethrown
 template <class A, class B>
@@ -539,6 +558,7 @@ CtPtr Sorter::sorter(const Ciphertext &input, const SignConfig &cfg) {
     CtPtr ct = cc.clone(input), fix, c1, c2;
     const int stages = stageCount((int)k, (int)M);
     stagesRun = 0;
+    PhaseTimes T;
     bootstraps = 0;
     for (int stage = 0; stage < stages; ++stage) {
         int m, logDist, slope;
@@ -546,46 +566,100 @@ CtPtr Sorter::sorter(const Ciphertext &input, const SignConfig &cfg) {
         const long shift = getRotateDistance(k, logDist, slope);
         const auto ind = genIndices(numSlots, k, M, m, logDist, slope);
         if (slope == 0) {
+            T.start(cc);
             checkLevel(ct, level[(size_t)k], cfg);
+            T.stop(cc, "level checks / bootstraps");
             if (k == 5) {
+                T.start(cc);
                 comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
+                T.stop(cc, "comparisons");
+                T.start(cc);
                 checkLevel2(c1, c2, level[5], cfg);
+                T.stop(cc, "level checks / bootstraps");
+                T.start(cc);
                 ct = runFiveSorter(ct, ind, shift, c1, c2);
+                T.stop(cc, "sorting networks");
             } else {
+                T.start(cc);
                 c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
+                T.stop(cc, "comparisons");
+                T.start(cc);
                 checkLevel(c1, level[(size_t)k], cfg);
+                T.stop(cc, "level checks / bootstraps");
                 ct = k == 2 ? runTwoSorter(ct, ind, shift, c1) : runThreeSorter(ct, ind, shift, c1);
             }
         } else if (slope == k / 2 + 1) {  // k = 3 or 5 (k = 2 has slopes 0, 1 only)
+            T.start(cc);
             checkLevel(ct, level[(size_t)k - 1], cfg);
+            T.stop(cc, "level checks / bootstraps");
             if (k == 3) {
+                T.start(cc);
                 c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
+                T.stop(cc, "comparisons");
+                T.start(cc);
                 checkLevel(c1, level[2], cfg);
+                T.stop(cc, "level checks / bootstraps");
+                T.start(cc);
                 ct = runTwoSorter(ct, ind, shift, c1);
+                T.stop(cc, "sorting networks");
             } else {
+                T.start(cc);
                 comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
+                T.stop(cc, "comparisons");
+                T.start(cc);
                 checkLevel2(c1, c2, level[4], cfg);
+                T.stop(cc, "level checks / bootstraps");
+                T.start(cc);
                 ct = runFourSorter(ct, ind, shift, c1, c2);
+                T.stop(cc, "sorting networks");
             }
             ct = cc.add(*ct, *fix);
         } else if (k == 5 && slope == 1) {
+            T.start(cc);
             checkLevel(ct, level[5], cfg);
+            T.stop(cc, "level checks / bootstraps");
+            T.start(cc);
             comparisonForSort2(ct, ind, logDist, slope, c1, c2, fix, cfg);
+            T.stop(cc, "comparisons");
+            T.start(cc);
             checkLevel2(c1, c2, level[5], cfg);
+            T.stop(cc, "level checks / bootstraps");
+            T.start(cc);
             ct = cc.add(*run2345Sorter(ct, ind, shift, c1, c2), *fix);
+            T.stop(cc, "sorting networks");
         } else if ((k == 5 && slope == 2) || (k == 3 && slope == 1)) {
+            T.start(cc);
             checkLevel(ct, level[3], cfg);
+            T.stop(cc, "level checks / bootstraps");
+            T.start(cc);
             c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
+            T.stop(cc, "comparisons");
+            T.start(cc);
             checkLevel(c1, level[2], cfg);  // Sorter.cpp:373-376: checked for 2, then for 3
+            T.stop(cc, "level checks / bootstraps");
+            T.start(cc);
             const CtPtr two = runTwoSorter(ct, ind, shift, c1);
+            T.stop(cc, "sorting networks");
+            T.start(cc);
             checkLevel(c1, level[3], cfg);
+            T.stop(cc, "level checks / bootstraps");
+            T.start(cc);
             const CtPtr three = runThreeSorter(ct, ind, shift, c1);
+            T.stop(cc, "sorting networks");
             ct = cc.add(*cc.add(*two, *fix), *three);
         } else if (k == 2 && slope == 1) {
+            T.start(cc);
             checkLevel(ct, level[2], cfg);
+            T.stop(cc, "level checks / bootstraps");
+            T.start(cc);
             c1 = comparisonForSort(ct, ind, logDist, slope, fix, cfg);
+            T.stop(cc, "comparisons");
+            T.start(cc);
             checkLevel(c1, level[2], cfg);
+            T.stop(cc, "level checks / bootstraps");
+            T.start(cc);
             ct = cc.add(*runTwoSorter(ct, ind, shift, c1), *fix);
+            T.stop(cc, "sorting networks");
         } else {
             throw std::invalid_argument("k-way: no matching k and slope");
         }
@@ -601,6 +675,8 @@ CtPtr Sorter::sorter(const Ciphertext &input, const SignConfig &cfg) {
                          stage, m, logDist, slope, ct->level, lo, hi, bootstraps);
         }
     }
+    if (T.on)
+        for (auto &kv : T.s) std::fprintf(stderr, "k-way %-26s %8.3f s\n", kv.first.c_str(), kv.second);
     return ct;
 }
 
