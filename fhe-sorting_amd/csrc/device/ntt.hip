@@ -96,6 +96,10 @@ __device__ __forceinline__ void ct_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q4, u6
 // epilogues see v < 12q.  Stage s of a pass reduces iff the bound would pass 16
 // (or 12 at the row pass's last stage).
 __host__ __device__ constexpr bool fwd_reduce(bool cols, int pb, int s) {
+    // 512-point passes (ring 2^17 columns) reduce on every stage: with the lazy
+    // schedule the compiler spilled their 32 coefficients per lane to scratch
+    // (132 VGPRs + 272 B, 3x slower); 2^16-point and smaller passes do not
+    if (pb >= 9) return true;
     int B = cols ? 8 : 16;
     for (int k = 0;; ++k) {
         const bool r = B + 4 > 16 || (!cols && k == pb - 1 && B + 4 > 12);
