@@ -136,11 +136,19 @@ const Plaintext &Sorter::mask(const std::vector<double> &v, const Ciphertext &li
 
 // EvalUtils::checkLevelAndBoot (EvalUtils.cpp:59-86): bootstrap when fewer
 // than need + 1 levels remain (cfg.boot); without a bootstrapper that is an error
-void Sorter::checkLevel(CtPtr &c, int need, const SignConfig &cfg) {
-    if (cc.params().L - c->level >= need + 1) return;
+CtPtr checkLevelAndBoot(Engine &cc, const CtPtr &c, int need, const SignConfig &cfg, bool *booted) {
+    if (booted) *booted = false;
+    if (cc.params().L - c->level >= need + 1) return c;
     if (!cfg.boot) throw std::runtime_error("k-way: no levels left (set up bootstrapping for this depth)");
+    if (booted) *booted = true;
+    return cfg.boot(*c);
+}
+
+void Sorter::checkLevel(CtPtr &c, int need, const SignConfig &cfg) {
+    bool booted = false;
     CtPtr in = c;
-    c = cfg.boot(*c);
+    c = checkLevelAndBoot(cc, c, need, cfg, &booted);
+    if (!booted) return;
     ++bootstraps;
     if (std::getenv("FHE_KWAY_TRACE")) {
         const auto a = cc.decrypt(*in), b = cc.decrypt(*c);

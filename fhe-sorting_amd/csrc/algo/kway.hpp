@@ -35,6 +35,10 @@ int stageCount(int k, int M);  // M + M(M-1)/2 * ceil(k/2)  (Sorter.cpp:290)
 // KWayAdapter<N>::getSizeParameters: rotations +-2^i for 2^i < N
 std::vector<int> rotationIndices(int N);
 
+// EvalUtils::checkLevelAndBoot (EvalUtils.cpp:57-86): c bootstrapped (cfg.boot)
+// when fewer than need + 1 levels remain, else c itself; *booted says which
+CtPtr checkLevelAndBoot(Engine &cc, const CtPtr &c, int need, const SignConfig &cfg, bool *booted = nullptr);
+
 class Sorter {
   public:
     // numSlots = k^M values; the ciphertext holds next_pow2(numSlots) slots

@@ -568,6 +568,23 @@ int fhe_kway_sort_boot(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int 
     });
 }
 
+int fhe_check_level_and_boot(fhe_ctx *ctx, const fhe_ct *x, int need, fhe_boot *boot, int *booted, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(x);
+        NEED(out);
+        if (boot && &boot->b->cc != ctx->eng.get()) throw std::invalid_argument("bootstrapper of another context");
+        SignConfig cfg(CompositeSignConfig(3, 2, 2), ctx->eng->params().L);
+        if (boot) {
+            Bootstrapper *B = boot->b.get();
+            cfg.boot = [B](const Ciphertext &c) { return B->evalBootstrap(c); };
+        }
+        bool b = false;
+        *out = wrap(kwaySort::checkLevelAndBoot(*ctx->eng, x->p, need, cfg, &b));
+        if (booted) *booted = b ? 1 : 0;
+    });
+}
+
 int fhe_kway_sorter(fhe_ctx *ctx, int kk, const fhe_ct *const *x, int nx, const fhe_ct *const *cmp, int ncmp,
                     fhe_ct **out) {
     return guard([&] {

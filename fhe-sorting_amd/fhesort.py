@@ -137,6 +137,7 @@ _SIGS = {
     'fhe_boot_rotation_indices': (C.c_int, [vp, C.POINTER(C.c_int32), C.c_int]),
     'fhe_boot_depth': (C.c_int, [vp]),
     'fhe_bootstrap': (C.c_int, [vp, vp, PP]),
+    'fhe_check_level_and_boot': (C.c_int, [vp, vp, C.c_int, vp, C.POINTER(C.c_int), PP]),
     'fhe_bootstrap_stage': (C.c_int, [vp, vp, C.c_int, PP]),
     'fhe_conjugate': (C.c_int, [vp, vp, PP]),
     'fhe_gen_galois_keys': (C.c_int, [vp, u64p, C.c_int]),
@@ -640,6 +641,12 @@ class Context:
         out = self._new(lib().fhe_kway_sort_boot, x.h, k, M, cfg[1], cfg[2], boot.h, C.byref(nb))
         self.kway_bootstraps = nb.value
         return out
+
+    def check_level_and_boot(self, x, need, boot=None):
+        """EvalUtils::checkLevelAndBoot: (ciphertext, booted)."""
+        b = C.c_int()
+        out = self._new(lib().fhe_check_level_and_boot, x.h, need, boot.h if boot is not None else None, C.byref(b))
+        return out, bool(b.value)
 
     def kway_sorter(self, kk, xs, cmps):
         """SortUtils::fcnL (kk = 1) or the kk-sorter (kk = 2..5): ascending outputs."""

@@ -262,6 +262,11 @@ int fhe_kway_sort_boot(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int 
  * (SortUtils.cpp:32-208): nx = kk inputs, ncmp = kk(kk-1)/2 comparison
  * ciphertexts in SortUtilsTest's order (a>b, a>c, ..., tests/k-way/
  * SortUtilsTest.cpp:68-260); out receives kk ciphertexts in ascending order. */
+/* EvalUtils::checkLevelAndBoot(ctxt, level, multDepth) (src/k-way/EvalUtils.cpp:57-86), the
+ * k-way sorter's own level check: *out = x bootstrapped with `boot` when fewer than need + 1
+ * levels remain (FHE_EDEPTH without a bootstrapper), else x; *booted = 1 / 0.
+ * checkLevelAndBoot2 (:88-94) is this call on each of its two ciphertexts. */
+int fhe_check_level_and_boot(fhe_ctx *ctx, const fhe_ct *x, int need, fhe_boot *boot, int *booted, fhe_ct **out);
 int fhe_kway_sorter(fhe_ctx *ctx, int kk, const fhe_ct *const *x, int nx, const fhe_ct *const *cmp, int ncmp,
                     fhe_ct **out);
 /* kwaySort::sortType(k, M, stage) -> (m, logDist, slope) (src/k-way/Masking.cpp:25-48) */

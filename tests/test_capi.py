@@ -66,3 +66,11 @@ def test_errors_cross_as_status_codes():
     with pytest.raises(F.FheError) as e:
         F.size_parameters(3)
     assert e.value.code == F.FHE_EINVAL
+
+
+def test_binding_declares_every_entry_point():
+    """Every C-ABI function has a ctypes signature in fhesort.py: without one ctypes
+    passes Python ints as 32-bit C ints and truncates handle pointers (a missing
+    entry once segfaulted a GPU test)."""
+    missing = [f for f in declared_symbols() if f not in F._SIGS]
+    assert not missing, missing

@@ -130,3 +130,79 @@ def test_direct_sort_n2048_ring16():
         assert np.max(np.abs(ctx.decrypt(out)[:N] - np.sort(x))) < 0.01
     finally:
         ctx.close()
+
+
+# ---- EvalUtilsTest (tests/k-way/EvalUtilsTest.cpp): ring 2^12, depth 50, scale
+# 2^59, 16 slots, rotations +-1,2,4,8, bootstrapping {3,3}.  dnum 4 instead of
+# OpenFHE's 3: the engine's digits hold <= 16 primes (51 Q primes / 3 = 17).
+@pytest.fixture(scope='module')
+def ectx():
+    ctx = F.Context(12, 50, 59, 60, 4, seed=77)
+    ctx.gen_rotation_keys([1, 2, 4, 8, -1, -2, -4, -8])
+    boot = F.Bootstrapper(ctx, 16, (3, 3))
+    yield ctx, boot
+    ctx.close()
+
+
+def _near(ctx, ct, expected, tol=0.1):
+    got = ctx.decrypt(ct)[:len(expected)]
+    assert np.max(np.abs(got - np.asarray(expected, dtype=float))) < tol, got
+
+
+@pytest.mark.parametrize('coeff,expected', [(3, [3.0, 6.0, 9.0, 12.0]), (-2, [-2.0, -4.0, -6.0, -8.0])])
+def test_evalutils_mult_by_int(ectx, coeff, expected):
+    """MultByIntPositive / MultByIntNegative: EvalUtils::multByInt's double-and-add
+    chain is exact mod q, i.e. the integer product fhe_mul_int computes."""
+    ctx, _ = ectx
+    _near(ctx, ctx.mul_int(ctx.encrypt([1.0, 2.0, 3.0, 4.0], 16), coeff), expected)
+
+
+def test_evalutils_mult_and_square(ectx):
+    ctx, _ = ectx
+    a, b = ctx.encrypt([1.0, 2.0, 3.0, 4.0], 16), ctx.encrypt([2.0, 3.0, 4.0, 5.0], 16)
+    _near(ctx, ctx.mul(a, b), [2.0, 6.0, 12.0, 20.0])
+    _near(ctx, ctx.square(a), [1.0, 4.0, 9.0, 16.0])
+
+
+def test_evalutils_rotation(ectx):
+    """leftRotate(3) = rotations by 1 then 2, rightRotate(2) = rotation by -2
+    (EvalUtils.cpp:113-146, ascending powers of two)."""
+    ctx, _ = ectx
+    x = ctx.encrypt(np.arange(1.0, 17.0), 16)
+    _near(ctx, ctx.rotate(ctx.rotate(x, 1), 2), [4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 1, 2, 3])
+    _near(ctx, ctx.rotate(x, -2), [15, 16, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+
+
+def test_evalutils_bootstrapping(ectx):
+    """Bootstrapping: at level 40 of 50, a level budget of 2 needs no bootstrap;
+    11 does (50 - 40 < 11 + 1), and the level drops; values within 0.2."""
+    ctx, boot = ectx
+    x = ctx.encrypt([0.1, 0.2, 0.3, 0.4], 16, level=40)
+    y, booted = ctx.check_level_and_boot(x, 2, boot)
+    assert not booted and y.level == x.level == 40
+    z, booted = ctx.check_level_and_boot(y, 11, boot)
+    assert booted and z.level < 40
+    _near(ctx, z, [0.1, 0.2, 0.3, 0.4], 0.2)
+
+
+def test_evalutils_bootstrapping_two_ciphertexts(ectx):
+    """BootstrappingTwoCiphertexts: checkLevelAndBoot2 at budget 12 boots the
+    level-40 ciphertext and leaves the level-35 one, whose level is then higher."""
+    ctx, boot = ectx
+    a = ctx.encrypt([0.1, 0.2, 0.3, 0.4], 16, level=40)
+    b = ctx.encrypt([0.5, 0.6, 0.7, 0.8], 16, level=35)
+    assert a.level != b.level
+    a2, ba = ctx.check_level_and_boot(a, 12, boot)
+    b2, bb = ctx.check_level_and_boot(b, 12, boot)
+    assert ba and not bb
+    assert a2.level < b2.level
+    _near(ctx, a2, [0.1, 0.2, 0.3, 0.4], 0.2)
+    _near(ctx, b2, [0.5, 0.6, 0.7, 0.8], 0.2)
+
+
+def test_check_level_without_bootstrapper_is_edepth(ectx):
+    ctx, _ = ectx
+    x = ctx.encrypt([0.1], 16, level=45)
+    with pytest.raises(F.FheError) as e:
+        ctx.check_level_and_boot(x, 11)
+    assert e.value.code == F.FHE_EDEPTH
