@@ -81,3 +81,29 @@ def test_sortutils_sorters_bit_exact(kk):
     for g, o, e in zip(go, oo, expected):
         assert np.array_equal(g.data(), o.data())
         assert np.max(np.abs(gpu.decrypt(g)[:len(e)] - e)) < 0.1
+
+
+@pytest.fixture(scope='module')
+def sorter_ctx():
+    """SorterTest's context (tests/k-way/SorterTest.cpp:14-45): ring 2^12, depth
+    59, scale 2^59, 16 slots, rotations +-1..15, bootstrapping {4,4}; dnum 4
+    (60 Q primes in 3 digits would exceed the engine's 16 primes per digit)."""
+    gpu = F.Context(12, 59, 59, 60, 4, seed=59)
+    gpu.gen_rotation_keys([r for i in range(1, 16) for r in (i, -i)])
+    boot = F.Bootstrapper(gpu, 16, (4, 4))
+    yield gpu, boot
+    gpu.close()
+
+
+@pytest.mark.parametrize('k,M,x', [
+    (2, 3, [0.5, 0.2, 0.8, 0.1, 0.3, 0.6, 0.4, 0.7]),  # TwoWaySorting
+    (3, 1, [0.5, 0.2, 0.8]),                          # ThreeWaySorting
+    (5, 1, [0.5, 0.3, 0.4, 0.1, 0.2]),                # FiveWaySorting
+])
+def test_sortertest_whole_sorters(sorter_ctx, k, M, x):
+    """SorterTest's TwoWay/ThreeWay/FiveWaySorting (SorterTest.cpp:313-383):
+    Sorter::sorter with CompositeSign(3, d_g = 5, d_f = 2) sorts within 0.1."""
+    gpu, boot = sorter_ctx
+    out = gpu.kway_sort(gpu.encrypt(x, 16), k, M, (3, 5, 2), boot=boot)
+    got = gpu.decrypt(out)[:len(x)]
+    assert np.max(np.abs(got - np.sort(x))) < 0.1, got
