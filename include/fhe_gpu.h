@@ -264,7 +264,8 @@ int fhe_kway_sort_boot(fhe_ctx *ctx, const fhe_ct *x, int k, int M, int dg, int 
  * SortUtilsTest.cpp:68-260); out receives kk ciphertexts in ascending order. */
 /* EvalUtils::checkLevelAndBoot(ctxt, level, multDepth) (src/k-way/EvalUtils.cpp:57-86), the
  * k-way sorter's own level check: *out = x bootstrapped with `boot` when fewer than need + 1
- * levels remain (FHE_EDEPTH without a bootstrapper), else x; *booted = 1 / 0.
+ * levels remain (FHE_EDEPTH without a bootstrapper), else a new handle sharing x's
+ * storage (free both; fhe_ct_set_slots on one shows on the other); *booted = 1 / 0.
  * checkLevelAndBoot2 (:88-94) is this call on each of its two ciphertexts. */
 int fhe_check_level_and_boot(fhe_ctx *ctx, const fhe_ct *x, int need, fhe_boot *boot, int *booted, fhe_ct **out);
 int fhe_kway_sorter(fhe_ctx *ctx, int kk, const fhe_ct *const *x, int nx, const fhe_ct *const *cmp, int ncmp,
