@@ -83,6 +83,16 @@ __global__ __launch_bounds__(NT) void k_mul_scalar(u64 *out, const u64 *a, int64
     const ulonglong2 x = ld2(a + oa);
     st2(out + oo, make_ulonglong2(mul_barrett(x.x, w, m), mul_barrett(x.y, w, m)));
 }
+// out[l] += a[l] * W.w[l] (per-limb constants < q_l): key generation's P * s'
+// term over the primes of one digit in one launch
+__global__ __launch_bounds__(NT) void k_add_scaled(u64 *out, const u64 *a, LimbConsts W, Seg S, const Mod *mods,
+                                                   int logN) {
+    EW_PROLOGUE
+    const Mod m = mods[l];
+    const u64 w = W.w[l];
+    const ulonglong2 x = ld2(a + oa), o = ld2(out + oo);
+    st2(out + oo, make_ulonglong2(add_mod(o.x, mul_barrett(x.x, w, m), q), add_mod(o.y, mul_barrett(x.y, w, m), q)));
+}
 __global__ __launch_bounds__(NT) void k_add_scalar(u64 *out, const u64 *a, int64_t K, int sh, Seg S,
                                                    const Mod *mods, int logN) {
     EW_PROLOGUE
@@ -667,6 +677,13 @@ void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S
     const double B = 8.0 * 2 * limbs * segs * ((size_t)1 << logN);
     launch_clocked("k_mul_scalar", B, k_mul_scalar, ew_grid(logN, limbs, segs), dim3(NT), st, out, a, K, sh, S, mods,
                    logN);
+}
+void ew_add_scaled(u64 *out, const u64 *a, const LimbConsts &W, int limbs, Seg S, const Mod *mods, int logN,
+                   hipStream_t st) {
+    if (limbs <= 0) return;
+    if (limbs > LIMB_CONSTS_MAX) throw std::invalid_argument("ew_add_scaled: too many limbs");
+    const double B = 8.0 * 3 * limbs * ((size_t)1 << logN);
+    launch_clocked("k_add_scaled", B, k_add_scaled, ew_grid(logN, limbs, 1), dim3(NT), st, out, a, W, S, mods, logN);
 }
 void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
                    hipStream_t st, int sh) {

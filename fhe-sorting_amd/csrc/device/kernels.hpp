@@ -115,6 +115,13 @@ void ew_neg(u64 *out, const u64 *a, int limbs, int segs, Seg S, const Mod *mods,
 // out = a * (K 2^sh mod q_l)   (K: signed integer constant, reduced in-kernel)
 void ew_mul_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
                    hipStream_t st, int sh = 0);
+// out[l] += a[l] * W.w[l] for l < limbs (constants already reduced mod q_l)
+constexpr int LIMB_CONSTS_MAX = 32;
+struct LimbConsts {
+    u64 w[LIMB_CONSTS_MAX];
+};
+void ew_add_scaled(u64 *out, const u64 *a, const LimbConsts &W, int limbs, Seg S, const Mod *mods, int logN,
+                   hipStream_t st);
 // out = a + (K 2^sh mod q_l)
 void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S, const Mod *mods, int logN,
                    hipStream_t st, int sh = 0);

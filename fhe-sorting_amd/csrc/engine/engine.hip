@@ -578,10 +578,9 @@ void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out) {
         dev::ew_mul_plain(tmp, aj, S, (int)nall, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
         dev::ew_sub(bj, bj, tmp, (int)nall, 1, dev::Seg{0, 0, 0}, I.mods, I.P.logN, I.st);
         const size_t lo = (size_t)j * I.P.alpha, hi = std::min(nq, (size_t)(j + 1) * I.P.alpha);
-        for (size_t i = lo; i < hi; ++i) {
-            dev::ew_mul_scalar(tmp, sp + i * n, Pmod[i], 1, 1, dev::Seg{0, 0, 0}, I.mods + i, I.P.logN, I.st);
-            dev::ew_add(bj + i * n, bj + i * n, tmp, 1, 1, dev::Seg{0, 0, 0}, I.mods + i, I.P.logN, I.st);
-        }
+        dev::LimbConsts W{};  // + P s' over the digit's primes, one launch
+        for (size_t i = lo; i < hi; ++i) W.w[i - lo] = (u64)Pmod[i];
+        dev::ew_add_scaled(bj + lo * n, sp + lo * n, W, (int)(hi - lo), dev::Seg{0, 0, 0}, I.mods + lo, I.P.logN, I.st);
         HIP_OK(hipStreamSynchronize(I.st));  // host buffers A[j], E[j] go out of scope after the loop
     }
 }
