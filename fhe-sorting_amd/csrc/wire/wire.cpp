@@ -245,6 +245,11 @@ CtxParams read_context(const std::string &path) {
     p.seed = r.word();
     if (p.log_n != (int)r.info.log_n || (uint64_t)p.mult_depth + 1 != r.info.nq)
         throw IoError(path + ": context header and body disagree");
+    // a context file drives allocations: refuse parameters no engine build uses
+    if (p.log_n < 10 || p.log_n > 17 || p.mult_depth < 1 || p.mult_depth > 200 || p.scale_bits < 20 ||
+        p.scale_bits > 60 || p.first_bits < 20 || p.first_bits > 60 || p.dnum < 1 || p.dnum > 64)
+        throw std::invalid_argument(path + ": context parameters out of range (ring 2^" + std::to_string(p.log_n) +
+                                    ", depth " + std::to_string(p.mult_depth) + ")");
     return p;
 }
 void check_context(const Engine &e, const CtxParams &p, const std::string &path) {

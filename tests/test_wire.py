@@ -119,3 +119,16 @@ def test_cli_binary_fails_like_the_reference(tmp_path):
     r = subprocess.run([exe, '--cc', str(tmp_path / 'none.bin')], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1
     assert 'Could not deserialize cryptocontext file' in r.stderr
+
+
+def test_context_with_absurd_parameters_is_refused(tmp_path):
+    """A context file drives allocations: ring 2^40 or depth 10^6 are refused
+    before any engine is built (FHE_EINVAL), no GPU needed."""
+    for log_n, depth in ((40, 10), (12, 1000000)):
+        body = np.array([log_n, depth, 50, 60, 3, 1, 2, 3, 5], dtype=np.uint64)
+        p = tmp_path / f'cc_{log_n}_{depth}.bin'
+        p.write_bytes(W.pack('context', 1, log_n, depth + 1, 1, body))
+        h = F.C.c_void_p()
+        rc = F.lib().fhe_deserialize_context(str(p).encode(), 0, F.C.byref(h))
+        assert rc == F.FHE_EINVAL and not h.value
+        assert 'out of range' in F.lib().fhe_last_error().decode()
