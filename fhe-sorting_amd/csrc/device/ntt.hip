@@ -596,17 +596,18 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     // ---- round A: local stages 0..RB-1 (pair bit s)
 #pragma unroll
     for (int s = 0; s < RB; ++s) {
+        // twiddle index (row offset + idx0) >> (s + 1) with idx0 = t E + c, c < E:
+        // E is a multiple of 2^(s+1), so it splits into a per-lane base and the
+        // compile-time c >> (s + 1) (COLS: the column bits of idx0 << k2 vanish)
+        const int sg = SG0 + s;
+        const size_t lane_base = ((COLS ? 0 : tid_global * LEN) + (size_t)t * E) >> (s + 1);
+        const ulonglong2 *tws = tw + (n >> (sg + 1)) + lane_base;
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int r0 = 0; r0 < T; ++r0) {
                 if (r0 & (1 << s)) continue;
-                const int idx0 = (t * G + g) * T + r0;
-                const int sg = SG0 + s;
-                const size_t j = COLS ? 0 : tid_global * LEN;  // row offset (COLS: column bits vanish)
-                const size_t i = (j + (size_t)idx0 * (COLS ? ((size_t)1 << k2) : 1)) >> (sg + 1);
-                const size_t wi = (n >> (sg + 1)) + i;
-                gs_bfly(x[g * T + r0], x[g * T + r0 + (1 << s)], tw[wi], q4, nq);
+                gs_bfly(x[g * T + r0], x[g * T + r0 + (1 << s)], tws[(g * T + r0) >> (s + 1)], q4, nq);
             }
     }
     // ---- exchange L2 -> L1 (idx = t + T * r)
