@@ -69,7 +69,8 @@ def _context(kind):
 def _worker(rank, world, port, outdir, kind):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
-    os.environ['OMP_NUM_THREADS'] = '2'
+    # the oracle is OpenMP: split the host's cores between the ranks
+    os.environ['OMP_NUM_THREADS'] = str(max(1, (os.cpu_count() or 2) // world))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     c = _context(kind)
     x, ct = _input(c, kind)
