@@ -164,8 +164,15 @@ struct PSEval {
     void evaluate_chunk(size_t first) {
         const int target = leaves[first].target;
         const bool raw = leaves[first].raw;
+        // up to 10 leaves per linear-sum pass (one read of the baby steps for all
+        // of them; FHE_PS_CHUNK for A/B timing)
+        static const size_t max_chunk = [] {
+            const char *e = std::getenv("FHE_PS_CHUNK");
+            const int v = e ? std::atoi(e) : 10;
+            return (size_t)std::min(10, std::max(1, v));
+        }();
         std::vector<size_t> chunk;
-        for (size_t i = first; i < leaves.size() && chunk.size() < 8; ++i)
+        for (size_t i = first; i < leaves.size() && chunk.size() < max_chunk; ++i)
             if (leaves[i].target == target && leaves[i].raw == raw && !ready.count(i) && has_terms(leaves[i].a))
                 chunk.push_back(i);
         std::vector<int> idx;  // union of the baby steps the chunk uses

@@ -188,7 +188,7 @@ __global__ __launch_bounds__(NT) void k_linear_sum(u64 *out, LinArgs A, size_t s
 // outputs (the Paterson-Stockmeyer leaves all combine the same baby steps).
 // Inputs may have different limb counts (segment stride xseg[i]); constants
 // are reduced once per block into LDS; lazy 128-bit accumulation.
-constexpr int MLS_G = 8, MLS_M = 32;
+constexpr int MLS_G = 10, MLS_M = 32;  // arguments: 3.5 KB of the 4 KB kernel-argument limit
 struct MultiLinArgs {
     u64 *out[MLS_G];
     const u64 *x[MLS_M];
@@ -731,7 +731,7 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
                          int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st,
                          const uint8_t *sh) {
     if (limbs <= 0 || segs <= 0 || G <= 0 || m <= 0) return;
-    if (G > MLS_G) throw std::invalid_argument("ew_linear_sum_multi: at most 8 outputs per pass");
+    if (G > MLS_G) throw std::invalid_argument("ew_linear_sum_multi: at most 10 outputs per pass");
     for (int base = 0; base < m; base += MLS_M) {
         MultiLinArgs A{};
         A.m = std::min(MLS_M, m - base);
@@ -753,7 +753,8 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
     case g:                                                                                                  \
         launch_clocked("k_linear_sum_multi", B, k_linear_sum_multi<g>, grid, dim3(NT), st, A, seg, mods, logN); \
         break;
-            MLS_CASE(1) MLS_CASE(2) MLS_CASE(3) MLS_CASE(4) MLS_CASE(5) MLS_CASE(6) MLS_CASE(7) MLS_CASE(8)
+            MLS_CASE(1) MLS_CASE(2) MLS_CASE(3) MLS_CASE(4) MLS_CASE(5) MLS_CASE(6) MLS_CASE(7) MLS_CASE(8) MLS_CASE(9)
+                MLS_CASE(10)
 #undef MLS_CASE
         }
     }

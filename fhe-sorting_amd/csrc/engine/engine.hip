@@ -1261,7 +1261,8 @@ CtPtr Engine::linear_sum_to(const std::vector<const Ciphertext *> &xs, const std
 
 // Several linear sums of the same inputs to one target level: row g of `c`
 // gives the coefficients of output g.  Equal, word for word, to one
-// linear_sum_to per row, but each input is streamed once per 8 outputs.
+// linear_sum_to per row, but each input is streamed once per pass of up to
+// 10 outputs.
 std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> &xs,
                                           const std::vector<std::vector<double>> &c, int target, bool rescale) {
     auto &I = *impl;
@@ -1280,8 +1281,10 @@ std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> 
         xseg[i] = xs[i]->limbs * nn;
     }
     std::vector<CtPtr> outs;
-    for (size_t g0 = 0; g0 < c.size(); g0 += 8) {
-        const int G = (int)std::min<size_t>(8, c.size() - g0);
+    // passes of at most 10 outputs (the kernel's limit), balanced: 18 -> 9 + 9
+    const size_t passes = (c.size() + 9) / 10, per = (c.size() + passes - 1) / passes;
+    for (size_t g0 = 0; g0 < c.size(); g0 += per) {
+        const int G = (int)std::min<size_t>(per, c.size() - g0);
         std::vector<int64_t> K((size_t)G * m);
         std::vector<uint8_t> sh((size_t)G * m);
         for (int g = 0; g < G; ++g) {
