@@ -11,6 +11,7 @@
 //     companion.
 #include "kernels.hpp"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <utility>
 #include <type_traits>
@@ -200,9 +201,10 @@ struct MultiLinArgs {
 // One coefficient per lane, G outputs.  Every residue and constant is < 2^60,
 // so both split into 30-bit halves and a term costs four v_mad_u64_u32 with
 // accumulate (mac4, no carries); 16 terms fit the four 64-bit partial sums, so
-// each chunk of 16 baby steps is folded and reduced once into a running
-// residue.  The constants are split once per block into LDS (wave-uniform
-// broadcast reads).
+// each chunk of 16 baby steps folds into a 128-bit running sum per output,
+// reduced once at the end (a reduction per chunk measured 3.7% slower,
+// profiles/r2_l).  The constants are split once per block into LDS
+// (wave-uniform broadcast reads).
 template <int G>
 __global__ __launch_bounds__(NT) void k_linear_sum_multi(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
     __shared__ Split30 w[G * MLS_M];
@@ -214,9 +216,9 @@ __global__ __launch_bounds__(NT) void k_linear_sum_multi(MultiLinArgs A, size_t 
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
     const size_t ln = (size_t)l * n + k, oo = (size_t)blockIdx.z * seg + ln;
-    u64 run[G];
+    Acc128 run[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) run[g] = A.accumulate ? A.out[g][oo] : 0;
+    for (int g = 0; g < G; ++g) run[g].lo = A.accumulate ? A.out[g][oo] : 0;
     for (int base = 0; base < A.m; base += 16) {
         const int end = min(A.m, base + 16);
         Acc4 s[G];
@@ -236,10 +238,10 @@ __global__ __launch_bounds__(NT) void k_linear_sum_multi(MultiLinArgs A, size_t 
             }
         }
 #pragma unroll
-        for (int g = 0; g < G; ++g) run[g] = add_mod(run[g], reduce4(s[g], md), md.q);
+        for (int g = 0; g < G; ++g) fold4(run[g], s[g]);
     }
 #pragma unroll
-    for (int g = 0; g < G; ++g) A.out[g][oo] = run[g];
+    for (int g = 0; g < G; ++g) A.out[g][oo] = reduce128(run[g], md);
 }
 
 // out[m][c] = sum_i ct_i[m][c] * pt_i  (accumulate: + out), lazy 128-bit.
