@@ -789,6 +789,10 @@ int fhe_comm_get_unique_id(uint8_t id[128]) {
 }
 int fhe_comm_init(fhe_ctx *ctx, const uint8_t id[128], int rank, int world) {
     return guard([&] {
+        NEED(ctx);
+        NEED(id);
+        if (rank < 0 || rank >= world) throw std::invalid_argument("fhe_comm_init: rank outside [0, world)");
+        checkShardWorld(ctx->eng->params(), world);  // before RCCL is touched
         ncclUniqueId u;
         std::memcpy(&u, id, 128);
         if (hipSetDevice(ctx->eng->device()) != hipSuccess) throw std::runtime_error("HIP error: hipSetDevice");
@@ -811,6 +815,8 @@ int fhe_ct_allreduce(fhe_ctx *ctx, fhe_ct *ct) {
     }
     return guard([&] {
         NEED(ct);
+        // the u64 sum of residues is exact only while world * q_max < 2^64
+        checkShardWorld(ctx->eng->params(), ctx->world);
         hipStream_t st = static_cast<hipStream_t>(ctx->eng->stream_handle());
         const size_t cnt = 2 * (size_t)ct->p->batch * ct->p->limbs * ctx->eng->n();
         if (ncclAllReduce(ct->p->data, ct->p->data, cnt, ncclUint64, ncclSum, ctx->comm, st) != ncclSuccess)

@@ -325,6 +325,8 @@ int fhe_pt_encode_complex(fhe_ctx *ctx, const double *re, const double *im, int 
 
 /* ------------------------------------------------------ multi-GPU (RCCL) */
 int fhe_comm_get_unique_id(uint8_t id[128]);
+/* FHE_EINVAL, before RCCL is touched, unless 0 <= rank < world and world * q_max < 2^64
+ * (the all-reduce sums u64 residues; world <= 16 at a 60-bit q0) */
 int fhe_comm_init(fhe_ctx *ctx, const uint8_t id[128], int rank, int world);
 int fhe_comm_destroy(fhe_ctx *ctx);
 /* sum the ciphertext over all ranks (RCCL all-reduce u64 + per-limb mod q) */

@@ -59,6 +59,19 @@ def test_world_beyond_u64_bound_is_refused():
     assert e.value.code == F.FHE_EINVAL
 
 
+def test_comm_init_refuses_worlds_beyond_u64_bound():
+    """fhe_comm_init checks world * q_max < 2^64 (and the rank) before RCCL is
+    touched, so fhe_ct_allreduce never runs a wrapping u64 sum."""
+    ctx, _ = _ctx()
+    uid = F.Context.comm_unique_id()
+    with pytest.raises(F.FheError, match='overflow') as e:
+        ctx.comm_init(uid, 0, 17)
+    assert e.value.code == F.FHE_EINVAL
+    with pytest.raises(F.FheError) as e:
+        ctx.comm_init(uid, 1, 1)
+    assert e.value.code == F.FHE_EINVAL
+
+
 def test_mismatched_partial_levels_fail_before_data_allreduce():
     ctx, rots = _ctx()
     ct = ctx.encrypt(np.random.default_rng(2).permutation(N) / N, N)
