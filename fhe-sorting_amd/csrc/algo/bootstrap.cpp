@@ -226,7 +226,9 @@ void Bootstrapper::keyGen() {
     cc.gen_galois_keys({2 * (uint64_t)cc.params().n - 1});
 }
 
-int Bootstrapper::depth() const { return (int)(enc.size() + dec.size()) + chebPSDepth((int)cheb.size() - 1) + cfg.r; }
+int Bootstrapper::depth() const {
+    return (int)(enc.size() + dec.size()) + chebPSDepthSplit((int)cheb.size() - 1, cc.ps_split) + cfg.r;
+}
 
 CtPtr Bootstrapper::transform(const Ciphertext &x, const Level &lv, int tag) {
     const int m = 2 * cfg.slots;

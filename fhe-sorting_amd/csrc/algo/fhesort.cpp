@@ -233,9 +233,341 @@ struct PSEval {
     }
 };
 
+// ------------------------------------------------ OpenFHE's split (spec 1) --
+// OpenFHE's EvalChebyshevSeriesPS / InnerEvalChebyshevPS (ckksrns-advancedshe.cpp)
+// with ComputeDegreesPS and LongDivisionChebyshev (ckksrns-utils.cpp): baby
+// steps T_1..T_k, giant steps T_{k 2^i}, the series padded to degree
+// k(2^m - 1) by a monic T term that is subtracted again at the end, and at
+// every node  f = (T_{k 2^(mm-1)} + c) q + s  from two long divisions.  The
+// quotients stay monic (leading coefficient a power of two), so |q(x)| is
+// bounded by ~2^(mm-1) at every node: fresh noise in a giant step is never
+// multiplied by the tail of the series.  DESIGN.md §3 measures the effect
+// (scripts/ps_noise_model.py).  oracle: oracle_algo.cpp PSOpenFHE.
+
+// last index with a nonzero coefficient (OpenFHE Degree: exact zero test)
+int degree_of(const std::vector<double> &c) {
+    for (int i = (int)c.size() - 1; i >= 0; --i)
+        if (c[i] != 0.0) return i;
+    return 0;
+}
+
+// OpenFHE ComputeDegreesPS(n): the (k, m) minimising k + 2m + 2^(m-1) - 4 over
+// k (2^m - 1) > n with |floor(log2 k) - floor(log2 sqrt(n/2))| <= 1 (integer
+// n/2 and n/k as the unsigned original); ties: the first (smallest k).  Up to
+// degree 2204 OpenFHE's depth is its published band (openfhe_ps_depth, the
+// budget of the reference's multDepth tables); the heuristic exceeds the band by
+// one level at 46 degrees (12-13, 56-59, 240-247, 992-1007, 2016-2031, none of
+// them a degree the reference evaluates), so candidates deeper than the band
+// are excluded there (and the window dropped if that leaves none).
+void openfhe_degrees_ps(int n, int &k_out, int &m_out) {
+    const double sqn2 = std::floor(std::log2(std::sqrt((double)(unsigned)(n / 2))));
+    const int band = n <= 2204 ? openfhe_ps_depth(n) : 1 << 30;
+    for (int window = 1; window >= 0; --window) {
+        long best = -1;
+        for (long k = 1; k <= n; ++k) {
+            const long q = n / k;
+            if (q == 0) break;
+            const double mmax = std::ceil(std::log2((double)q) + 1) + 1;
+            for (long m = 1; (double)m <= mmax; ++m) {
+                if ((long)n - k * ((1L << m) - 1) >= 0) continue;
+                if (window && std::fabs(std::floor(std::log2((double)k)) - sqn2) > 1) continue;
+                if (ceil_log2(k) + m > band) continue;
+                const long mult = k + 2 * m + (1L << (m - 1)) - 4;
+                if (best < 0 || mult < best) {
+                    best = mult;
+                    k_out = (int)k;
+                    m_out = (int)m;
+                }
+            }
+        }
+        if (best >= 0) return;
+    }
+    throw std::invalid_argument("openfhe_degrees_ps: no (k, m) for this degree");
+}
+
+// OpenFHE LongDivisionChebyshev: f = q g + r for series in the c_0/2 convention
+// (q returned in the same convention).  The divisors used here are monic or
+// have a power-of-two leading coefficient, so every step is exact in its
+// leading term.
+void long_division_chebyshev(const std::vector<double> &f, const std::vector<double> &g, std::vector<double> &q,
+                             std::vector<double> &r) {
+    int n = degree_of(f);
+    const int k = degree_of(g);
+    if (n != (int)f.size() - 1 || k != (int)g.size() - 1)
+        throw std::invalid_argument("long_division_chebyshev: zero leading coefficient");
+    r = f;
+    if (n - k < 0) {
+        q.assign(1, 0.0);
+        return;
+    }
+    q.assign(n - k + 1, 0.0);
+    const double gk = g[k];
+    while (n - k > 0) {
+        q[n - k] = 2 * r.back();
+        if (gk != 1.0) q[n - k] /= gk;
+        std::vector<double> d(n + 1, 0.0);
+        if (k == n - k) {
+            d[0] = 2 * g[n - k];
+            for (int i = 1; i < 2 * k + 1; ++i) d[i] = g[std::abs(n - k - i)];
+        } else if (k > n - k) {
+            d[0] = 2 * g[n - k];
+            for (int i = 1; i < k - (n - k) + 1; ++i) d[i] = g[std::abs(n - k - i)] + g[n - k + i];
+            for (int i = k - (n - k) + 1; i < n + 1; ++i) d[i] = g[std::abs(i - n + k)];
+        } else {
+            d[n - k] = g[0];
+            for (int i = n - 2 * k; i < n + 1; ++i)
+                if (i != n - k) d[i] = g[std::abs(i - n + k)];
+        }
+        const double rn = r.back();
+        if (rn != 1.0)
+            for (double &v : d) v *= rn;
+        if (gk != 1.0)
+            for (double &v : d) v /= gk;
+        for (size_t i = 0; i < r.size(); ++i) r[i] -= d[i];
+        if (r.size() > 1) {
+            const int n_old = n;
+            n = degree_of(r);
+            r.resize(n + 1);
+            // a non-finite or non-cancelling leading term would loop forever
+            if (n >= n_old) throw std::invalid_argument("evalChebyshevSeriesPS: long division does not converge");
+        }
+    }
+    if (n == k) {
+        q[0] = r.back();
+        if (gk != 1.0) q[0] /= gk;
+        std::vector<double> d(g);
+        const double rn = r.back();
+        if (rn != 1.0)
+            for (double &v : d) v *= rn;
+        if (gk != 1.0)
+            for (double &v : d) v /= gk;
+        for (size_t i = 0; i < r.size(); ++i) r[i] -= d[i];
+        if (r.size() > 1) {
+            n = degree_of(r);
+            r.resize(n + 1);
+        }
+    }
+    q[0] *= 2;
+}
+
+// The division tree of one series, computed once per coefficient table.
+// Leaves are linear sums over T_1..T_k: `a` holds sum a_i T_i (a[0] the
+// constant added afterwards, already halved).
+struct OFNode {
+    int mm = 0;
+    int cu = -1;          // leaf index of c(u), or -1 (then c0 is the constant)
+    double c0 = 0.0;      // c's constant when cu < 0
+    int qleaf = -1, sleaf = -1;  // leaf indices, or -1 (child nodes)
+    std::unique_ptr<OFNode> qn, sn;
+};
+struct OFLeaf {
+    std::vector<double> a;  // size k+1
+    int mm;                 // node depth: target level = lk + mm - 1
+    bool raw;               // s-leaf: folded into the node's product before its rescale
+};
+struct OFPlan {
+    int k = 0, m = 0;
+    std::unique_ptr<OFNode> root;
+    std::vector<OFLeaf> leaves;
+    double cmax = 0.0;  // largest |c| quotient coefficient of the tree
+};
+// OpenFHE's padding keeps every quotient bounded (|c| <= 2m for the series the
+// reference evaluates: sinc tables, g_4, EvalMod) only while the monic T term
+// dominates the series.  A series with O(1) coefficients that do not decay
+// makes the second division ill-conditioned (|c| ~ 1e7 at degree 60, 1e46 at
+// 126: the evaluation then cancels to garbage), so such a series, or one whose
+// division does not converge, is evaluated with the power-of-two split.
+constexpr double OF_CMAX = 1024.0;
+
+int of_leaf(OFPlan &P, const std::vector<double> &c, int upto, int mm, bool raw) {
+    OFLeaf L;
+    L.a.assign(P.k + 1, 0.0);
+    for (int i = 1; i <= upto && i < (int)c.size(); ++i) L.a[i] = c[i];
+    L.a[0] = c[0] / 2;
+    L.mm = mm;
+    L.raw = raw;
+    P.leaves.push_back(std::move(L));
+    return (int)P.leaves.size() - 1;
+}
+
+std::unique_ptr<OFNode> of_build(OFPlan &P, const std::vector<double> &f, int mm) {
+    const int k = P.k;
+    auto node = std::make_unique<OFNode>();
+    node->mm = mm;
+    const int k2m2k = k * (1 << (mm - 1)) - k;
+    std::vector<double> Tkm(k2m2k + k + 1, 0.0), q, r, cq, cr;
+    Tkm.back() = 1.0;
+    long_division_chebyshev(f, Tkm, q, r);
+    std::vector<double> r2 = r;
+    if (k2m2k - degree_of(r) <= 0) {
+        r2[k2m2k] -= 1;
+        r2.resize(degree_of(r2) + 1);
+    } else {
+        r2.resize(k2m2k + 1, 0.0);
+        r2.back() = -1;
+    }
+    long_division_chebyshev(r2, q, cq, cr);
+    std::vector<double> s2 = cr;
+    s2.resize(k2m2k + 1, 0.0);
+    s2.back() = 1;
+    const int dc = degree_of(cq);
+    for (double v : cq) P.cmax = std::max(P.cmax, std::fabs(v));
+    if (dc >= 1)
+        node->cu = of_leaf(P, cq, dc, mm, false);
+    else
+        node->c0 = cq[0] / 2;
+    if (degree_of(q) > k)
+        node->qn = of_build(P, q, mm - 1);
+    else
+        node->qleaf = of_leaf(P, q, k, mm, false);  // q[k] is the power-of-two leading term
+    if (degree_of(s2) > k)
+        node->sn = of_build(P, s2, mm - 1);
+    else
+        node->sleaf = of_leaf(P, s2, k, mm, true);  // s2[k] = 1 (monic)
+    return node;
+}
+
+std::shared_ptr<const OFPlan> of_plan(const std::vector<double> &c) {
+    static std::mutex mu;
+    static std::map<std::vector<double>, std::shared_ptr<const OFPlan>> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(c);
+    if (it != cache.end()) return it->second;
+    auto P = std::make_shared<OFPlan>();
+    const int n = degree_of(c);
+    openfhe_degrees_ps(n, P->k, P->m);
+    if (P->m < 2) {
+        cache[c] = nullptr;
+        return nullptr;
+    }
+    const int k2m2k = P->k * (1 << (P->m - 1)) - P->k;
+    std::vector<double> f2(c.begin(), c.begin() + n + 1);
+    f2.resize(2 * k2m2k + P->k + 1, 0.0);
+    f2.back() = 1;  // + T_{k(2^m - 1)}, subtracted after the evaluation
+    try {
+        P->root = of_build(*P, f2, P->m);
+    } catch (const std::invalid_argument &) {
+        P->cmax = INFINITY;
+    }
+    std::shared_ptr<const OFPlan> out = P;
+    if (!(P->cmax <= OF_CMAX)) out = nullptr;  // ill-conditioned: power-of-two split
+    cache[c] = out;
+    return out;
+}
+
+struct PSOpenFHE {
+    Engine &cc;
+    std::shared_ptr<const OFPlan> P;
+    int k, m, lk;
+    std::vector<CtPtr> T;   // T[i] = T_i, 1 <= i <= k
+    std::vector<CtPtr> T2;  // T2[j] = T_{k 2^j}
+    std::map<size_t, CtPtr> ready;
+
+    PSOpenFHE(Engine &c, const Ciphertext &x, std::shared_ptr<const OFPlan> plan)
+        : cc(c), P(std::move(plan)), k(P->k), m(P->m), lk(x.level + ceil_log2(P->k)) {
+        T.resize(k + 1);
+        T[1] = cc.clone(x);
+    }
+    // 2 a b (+ c x): the doubling is applied to an operand, before the product's
+    // single rescale (OpenFHE doubles before its deferred rescale as well); an
+    // operand below the other's level is doubled by the level-adjusting
+    // constant product itself
+    CtPtr twice_prod(const Ciphertext &a, const Ciphertext &b, const Ciphertext *x, double cx) {
+        const Ciphertext *lo = &a, *hi = &b;
+        if (lo->level > hi->level) std::swap(lo, hi);
+        CtPtr a2 = lo->level < hi->level ? cc.mul_const_to(*lo, 2.0, hi->level) : cc.add(*lo, *lo);
+        if (!x) return cc.mul(*a2, *hi);
+        return cc.mul_add(*a2, *hi, {x}, {cx});
+    }
+    // T_i: powers of two and even i by 2 T_{i/2}^2 - 1, odd i by 2 T_{i/2} T_{i/2+1} - T_1
+    void build() {
+        for (int i = 2; i <= k; ++i) {
+            if (i % 2 == 0)
+                T[i] = cc.add_const(*twice_prod(*T[i / 2], *T[i / 2], nullptr, 0.0), -1.0);
+            else
+                T[i] = twice_prod(*T[i / 2], *T[i / 2 + 1], T[1].get(), -1.0);
+        }
+        T2.push_back(T[k]);
+        for (int j = 1; j < m; ++j) T2.push_back(cc.add_const(*twice_prod(*T2[j - 1], *T2[j - 1], nullptr, 0.0), -1.0));
+    }
+    // T_{k(2^m - 1)} = 2 T_{k(2^(j) - 1)} T_{k 2^j} - T_k, j = 1..m-1
+    CtPtr t2km1() {
+        CtPtr t = T2[0];
+        for (int j = 1; j < m; ++j) t = twice_prod(*t, *T2[j], T2[0].get(), -1.0);
+        return t;
+    }
+    // leaves sharing (target, raw) are evaluated up to 10 per linear-sum pass
+    void evaluate_chunk(size_t first) {
+        const OFLeaf &L0 = P->leaves[first];
+        std::vector<size_t> chunk;
+        for (size_t i = first; i < P->leaves.size() && chunk.size() < 10; ++i)
+            if (P->leaves[i].mm == L0.mm && P->leaves[i].raw == L0.raw && !ready.count(i)) chunk.push_back(i);
+        std::vector<int> idx;
+        for (size_t c : chunk)
+            for (int i = 1; i <= k; ++i)
+                if (P->leaves[c].a[i] != 0.0) idx.push_back(i);
+        std::sort(idx.begin(), idx.end());
+        idx.erase(std::unique(idx.begin(), idx.end()), idx.end());
+        const int target = lk + L0.mm - 1 + (L0.raw ? 1 : 0);
+        // every leaf has a T term: c(u) only exists with degree >= 1, q and s2
+        // end in their (power-of-two / monic) T_k term
+        if (idx.empty()) throw std::logic_error("openfhe split: leaf without T terms");
+        std::vector<const Ciphertext *> xs;
+        for (int i : idx) xs.push_back(T[i].get());
+        std::vector<std::vector<double>> rows;
+        for (size_t c : chunk) {
+            std::vector<double> row;
+            for (int i : idx) row.push_back(P->leaves[c].a[i]);
+            rows.push_back(row);
+        }
+        auto outs = cc.linear_sums_to(xs, rows, target, !L0.raw);
+        for (size_t g = 0; g < chunk.size(); ++g) {
+            CtPtr r = outs[g];
+            if (!L0.raw && P->leaves[chunk[g]].a[0] != 0.0) r = cc.add_const(*r, P->leaves[chunk[g]].a[0]);
+            ready[chunk[g]] = r;
+        }
+    }
+    CtPtr leaf(int i) {
+        if (!ready.count(i)) evaluate_chunk(i);
+        CtPtr r = ready.at(i);
+        ready.erase(i);
+        return r;
+    }
+    // node at depth mm: (T2[mm-1] + c) q + s, output level lk + mm
+    CtPtr node(const OFNode &N) {
+        CtPtr a = N.cu >= 0 ? cc.add(*T2[N.mm - 1], *leaf(N.cu))
+                            : (N.c0 != 0.0 ? cc.add_const(*T2[N.mm - 1], N.c0) : T2[N.mm - 1]);
+        CtPtr qu = N.qn ? node(*N.qn) : leaf(N.qleaf);
+        if (N.sn) {
+            CtPtr su = node(*N.sn);  // level lk + mm - 1: added before the product's rescale
+            return cc.mul_add(*a, *qu, {su.get()}, {1.0});
+        }
+        const double s0 = P->leaves[N.sleaf].a[0];
+        CtPtr raw = leaf(N.sleaf);
+        CtPtr out = cc.mul_add_raw(*a, *qu, *raw);
+        return s0 != 0.0 ? cc.add_const(*out, s0) : out;
+    }
+    CtPtr run() {
+        build();
+        CtPtr top = node(*P->root);
+        return cc.sub(*top, *t2km1());
+    }
+};
+
 }  // namespace
 
-int chebPSDepth(int d) { return std::max(std::max(1, ceil_log2((long)d + 1)), openfhe_ps_depth(d)); }
+// (the conditioning fallback never changes the depth: for every degree >= 5
+// OpenFHE's ceil(log2 k) + m equals the power-of-two split's max(D, OpenFHE's
+// published band), tests/test_oracle.py::test_ps_depth_tables)
+int chebPSDepthSplit(int d, int split) {
+    if (split == PS_SPLIT_OPENFHE && d >= 5) {
+        int k = 0, m = 0;
+        openfhe_degrees_ps(d, k, m);
+        if (m >= 2) return ceil_log2(k) + m;
+    }
+    return std::max(std::max(1, ceil_log2((long)d + 1)), openfhe_ps_depth(d));
+}
+int chebPSDepth(int d) { return chebPSDepthSplit(d, PS_SPLIT_OPENFHE); }
 
 CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<double> &coeffs, double a,
                             double b) {
@@ -247,9 +579,15 @@ CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<
         x = cc.mul_const(*x, 2.0 / (b - a));
         x = cc.add_const(*x, -(a + b) / (b - a));
     }
+    const int d = (int)c.size() - 1;
+    if (cc.ps_split == PS_SPLIT_OPENFHE && d >= 5) {
+        if (auto plan = of_plan(c)) {
+            PSOpenFHE ev(cc, *x, plan);
+            return ev.run();
+        }
+    }
     std::vector<double> s(c);
     s[0] = c[0] / 2.0;
-    const int d = (int)s.size() - 1;
     if (d == 0) return cc.add_const(*cc.trivial_const(0.0, x->level, x->slots, x->batch), s[0]);
     PSEval ev(cc, *x, d);
     ev.build_baby();

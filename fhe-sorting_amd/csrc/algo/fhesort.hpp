@@ -41,12 +41,15 @@ struct SignConfig {
     SignConfig(CompositeSignConfig c, int depth) : compos(c), multDepth(depth) {}
 };
 
-// Chebyshev series sum c_0/2 + sum_{i>=1} c_i T_i((2x-a-b)/(b-a)), depth-optimal
-// Paterson-Stockmeyer; replaces OpenFHE EvalChebyshevSeriesPS.
+// Chebyshev series sum c_0/2 + sum_{i>=1} c_i T_i((2x-a-b)/(b-a)) by
+// Paterson-Stockmeyer; replaces OpenFHE EvalChebyshevSeriesPS.  The split is
+// cc.ps_split: OpenFHE's (default) or the engine's power-of-two one.
 CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x, const std::vector<double> &coeffs, double a,
                             double b);
-// levels evalChebyshevSeriesPS consumes for a degree-d series
+// levels evalChebyshevSeriesPS consumes for a degree-d series (OpenFHE split /
+// given split)
 int chebPSDepth(int degree);
+int chebPSDepthSplit(int degree, int split);
 
 CtPtr compositeSignN(Engine &cc, const Ciphertext &x, int n, const SignConfig &cfg);
 template <int n>

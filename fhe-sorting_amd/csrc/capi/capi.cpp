@@ -779,6 +779,27 @@ int fhe_set_sort_lanes(fhe_ctx *ctx, int lanes) {
     });
 }
 
+int fhe_set_ps_split(fhe_ctx *ctx, int split) {
+    return guard([&] {
+        NEED(ctx);
+        if (split != FHE_PS_SPLIT_ENGINE && split != FHE_PS_SPLIT_OPENFHE)
+            throw std::invalid_argument("ps split must be FHE_PS_SPLIT_ENGINE or FHE_PS_SPLIT_OPENFHE");
+        ctx->eng->ps_split = split;
+    });
+}
+
+int fhe_get_ps_split(const fhe_ctx *ctx) { return ctx ? ctx->eng->ps_split : -FHE_EINVAL; }
+
+int fhe_cheb_ps_depth(int degree, int split) {
+    int d = -1;
+    const int rc = guard([&] {
+        if (degree < 0 || (split != FHE_PS_SPLIT_ENGINE && split != FHE_PS_SPLIT_OPENFHE))
+            throw std::invalid_argument("fhe_cheb_ps_depth: bad degree or split");
+        d = chebPSDepthSplit(degree, split);
+    });
+    return rc ? -rc : d;
+}
+
 int fhe_comm_get_unique_id(uint8_t id[128]) {
     return guard([&] {
         ncclUniqueId u;

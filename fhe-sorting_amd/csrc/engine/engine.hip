@@ -423,6 +423,7 @@ Engine::Engine(ForkTag) {}
 
 std::unique_ptr<Engine> Engine::fork() const {
     std::unique_ptr<Engine> e(new Engine(ForkTag{}));
+    e->ps_split = ps_split;
     e->impl.reset(new Impl(*impl));  // shares tables and keys (shared_ptr / raw device pointers)
     auto &I = *e->impl;
     HIP_OK(hipSetDevice(I.device));

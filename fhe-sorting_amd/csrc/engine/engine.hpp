@@ -73,9 +73,15 @@ struct Counters {
     }
 };
 
+// Paterson-Stockmeyer split used by evalChebyshevSeriesPS (csrc/algo): OpenFHE's
+// (k, m) long-division split (the default, as the reference), or the
+// power-of-two split of rounds 1-2
+enum : int { PS_SPLIT_ENGINE = 0, PS_SPLIT_OPENFHE = 1 };
+
 class Engine {
   public:
     Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int device, u64 seed);
+    int ps_split = PS_SPLIT_OPENFHE;  // copied by fork()
     ~Engine();
     // A second engine on its own HIP stream and memory pool sharing this one's
     // keys and tables: independent work issued to both (from two host threads)

@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('FHE_LIB') or os.path.join(HERE, 'lib', 'libfhesort.so')  # FHE_LIB: A/B builds
 COEFF_DIR = os.path.join(HERE, 'data')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'fhe_gpu.h')
+PS_SPLIT_ENGINE, PS_SPLIT_OPENFHE = 0, 1  # fhe_set_ps_split (include/fhe_gpu.h)
 
 FHE_OK, FHE_EINVAL, FHE_ENOKEY, FHE_EDEPTH, FHE_EHIP, FHE_ENOMEM, FHE_EINTERNAL, FHE_ENOCOMM, FHE_EIO = range(9)
 NAF, BNAF, BINARY = 0, 1, 2
@@ -166,6 +167,9 @@ _SIGS = {
     'fhe_kernel_clock_start': (C.c_int, [vp]),
     'fhe_set_sort_stack': (C.c_int, [vp, C.c_int]),
     'fhe_set_sort_lanes': (C.c_int, [vp, C.c_int]),
+    'fhe_set_ps_split': (C.c_int, [vp, C.c_int]),
+    'fhe_get_ps_split': (C.c_int, [vp]),
+    'fhe_cheb_ps_depth': (C.c_int, [C.c_int, C.c_int]),
     'fhe_pool_trim': (C.c_int, [vp]),
     'fhe_pool_stats': (C.c_int, [vp, u64p, u64p, u64p]),
     'fhe_ct_stack': (C.c_int, [vp, C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_void_p)]),
@@ -375,7 +379,8 @@ class Pt:
 class Context:
     """One engine on one GPU (`device`)."""
 
-    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, device=0, keygen=True, _handle=None):
+    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, device=0, keygen=True, _handle=None,
+                 ps_split=None):
         self.logN, self.n, self.L = logN, 1 << logN, L
         self._boots = []
         if _handle is None:
@@ -390,6 +395,8 @@ class Context:
         self.primes = np.empty(self.nq + self.K, dtype=np.uint64)
         self.delta = np.empty(L + 1)
         _chk(lib().fhe_ctx_info(self.h, None, None, None, _u64(self.primes), _dbl(self.delta)))
+        if ps_split is not None:
+            self.set_ps_split(ps_split)
         if keygen:
             self.keygen()
 
@@ -679,6 +686,14 @@ class Context:
     def set_sort_lanes(self, m):
         _chk(lib().fhe_set_sort_lanes(self.h, m))
 
+    def set_ps_split(self, split):
+        """PS_SPLIT_OPENFHE (default) or PS_SPLIT_ENGINE (fhe_set_ps_split)"""
+        _chk(lib().fhe_set_ps_split(self.h, int(split)))
+
+    @property
+    def ps_split(self):
+        return int(lib().fhe_get_ps_split(self.h))
+
     def set_sort_stack(self, m):
         _chk(lib().fhe_set_sort_stack(self.h, m))
 
@@ -755,6 +770,14 @@ class KernelClock:
             raise FheError(FHE_EINTERNAL, 'kernel clock report truncated')
         self.stats = json.loads(buf.value.decode())
         return False
+
+
+def cheb_ps_depth(degree, split=PS_SPLIT_OPENFHE):
+    """levels a degree-d Chebyshev series consumes under `split` (fhe_cheb_ps_depth)"""
+    r = lib().fhe_cheb_ps_depth(int(degree), int(split))
+    if r < 0:
+        raise FheError(-r, lib().fhe_last_error().decode())
+    return r
 
 
 def size_parameters(N):

@@ -195,6 +195,23 @@ int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack);
  * so independent batch stacks overlap on the GPU.  Results do not depend on it. */
 int fhe_set_sort_lanes(fhe_ctx *ctx, int lanes);
 
+/* Paterson-Stockmeyer split of every Chebyshev series the context evaluates
+ * (fhe_cheb_ps, the doubled-sinc index check, g_4, the hybrid sort's sinc,
+ * EvalMod).  FHE_PS_SPLIT_OPENFHE (the default) is OpenFHE's
+ * EvalChebyshevSeriesPS, which the reference calls (src/sort_algo.h:629,727,
+ * src/sign.cpp:76): ComputeDegreesPS's (k, m), long division by T_{k 2^(m-1)},
+ * the series padded by a monic T_{k(2^m-1)}.  FHE_PS_SPLIT_ENGINE is rounds 1-2's
+ * power-of-two split.  Same polynomial, same depth for the reference's degrees;
+ * the OpenFHE split keeps a degree-6510 series within the reference's 0.01 at
+ * 40-bit scaling where the other does not. */
+#define FHE_PS_SPLIT_ENGINE 0
+#define FHE_PS_SPLIT_OPENFHE 1
+int fhe_set_ps_split(fhe_ctx *ctx, int split);
+int fhe_get_ps_split(const fhe_ctx *ctx);
+/* levels a degree-`degree` series consumes under `split` (the output level of
+ * fhe_cheb_ps is the input level plus this); < 0 on bad arguments */
+int fhe_cheb_ps_depth(int degree, int split);
+
 /* ------------------------------------------------------------ hybrid sort */
 /* DirectSort<N>::sort_hybrid (src/sort_algo.h:1050-1064; mode 0) or
  * rotationIndexCheckHybrid(rank, x) (:893-1047; mode 1): constructRank, then the

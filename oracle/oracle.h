@@ -181,6 +181,9 @@ class Context {
     std::map<u64, SwitchKey> rotkeys;  // galois element -> key
     u64 enc_counter = 0;
     OpCounters ctr;
+    // Paterson-Stockmeyer split of cheb_series_ps: 1 = OpenFHE's (default),
+    // 0 = the power-of-two split
+    int ps_split = 1;
 
     void keygen();
     void gen_rotation_keys(const std::vector<int> &rot);
@@ -266,6 +269,7 @@ struct SignConfig {
 
 CtPtr cheb_series_ps(Context &cc, const Ciphertext &x, const std::vector<double> &coeffs,
                      double a, double b);
+int cheb_ps_depth_split(int degree, int split);
 CtPtr composite_sign(Context &cc, const Ciphertext &x, const SignConfig &cfg);
 CtPtr sign(Context &cc, const Ciphertext &x, SignFunc f, const SignConfig &cfg);
 CtPtr compare(Context &cc, const Ciphertext &a, const Ciphertext &b, SignFunc f,

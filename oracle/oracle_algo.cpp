@@ -169,9 +169,251 @@ struct PSEval {
     }
 };
 
+// ---------------------------------------------- OpenFHE's split (spec 1) ---
+// Restates OpenFHE's EvalChebyshevSeriesPS + InnerEvalChebyshevPS
+// (pke/lib/scheme/ckksrns/ckksrns-advancedshe.cpp) with ComputeDegreesPS and
+// LongDivisionChebyshev (ckksrns-utils.cpp), the function the reference calls at
+// src/sort_algo.h:629,727 and src/sign.cpp:76.  OpenFHE is not vendored in the
+// reference (CMakeLists.txt:35), so this follows its published algorithm; the
+// CKKS op mapping (one rescale per product / linear sum, doubling before the
+// rescale, leaves at the level of their node) is this build's spec, which
+// fhe-sorting_amd/csrc/algo/fhesort.cpp PSOpenFHE evaluates word for word.
+
+// highest index with c_i != 0 (OpenFHE Degree)
+int cdeg(const std::vector<double> &c) {
+    int i = (int)c.size() - 1;
+    while (i > 0 && c[i] == 0.0) --i;
+    return i;
+}
+
+// ComputeDegreesPS(n) -> (k, m), held to OpenFHE's published depth band up to
+// degree 2204 (openfhe_ps_depth; only 46 degrees, none used by the reference,
+// are affected)
+void degrees_ps(int n, int &k_out, int &m_out) {
+    const unsigned un = (unsigned)n;
+    const double sqn2 = std::floor(std::log2(std::sqrt((double)(un / 2))));
+    const int band = n <= 2204 ? openfhe_ps_depth(n) : 1 << 30;
+    for (int pass = 0; pass < 2; ++pass) {
+        long best = -1;
+        for (unsigned k = 1; k <= un; ++k) {
+            if (un / k == 0) break;
+            for (unsigned m = 1; (double)m <= std::ceil(std::log2((double)(un / k)) + 1) + 1; ++m) {
+                if ((long)un - (long)k * ((1L << m) - 1) >= 0) continue;
+                if (pass == 0 && std::fabs(std::floor(std::log2((double)k)) - sqn2) > 1) continue;
+                if (ceil_log2((long)k) + (int)m > band) continue;
+                const long mult = (long)k + 2L * m + (1L << (m - 1)) - 4;
+                if (best < 0 || mult < best) {
+                    best = mult;
+                    k_out = (int)k;
+                    m_out = (int)m;
+                }
+            }
+        }
+        if (best >= 0) return;
+    }
+    throw std::invalid_argument("ComputeDegreesPS: no (k, m)");
+}
+
+// LongDivisionChebyshev(f, g) = (q, r), c_0/2 convention for f, g, q
+void cheb_divide(const std::vector<double> &f, const std::vector<double> &g, std::vector<double> &q,
+                 std::vector<double> &r) {
+    int n = cdeg(f);
+    const int k = cdeg(g);
+    if (n + 1 != (int)f.size() || k + 1 != (int)g.size()) throw std::invalid_argument("cheb_divide: leading zero");
+    r = f;
+    if (n < k) {
+        q = {0.0};
+        return;
+    }
+    q.assign(n - k + 1, 0.0);
+    // subtract (r_n / g_k) * (2 T_{n-k} g) (or g itself when n == k), whose
+    // T_n coefficient is r_n: 2 T_j T_i = T_{i+j} + T_{|i-j|}
+    auto step = [&](int j) {
+        std::vector<double> d(n + 1, 0.0);
+        if (j == 0) {
+            d = g;
+        } else if (k == j) {
+            d[0] = 2 * g[j];
+            for (int i = 1; i <= 2 * k; ++i) d[i] = g[std::abs(j - i)];
+        } else if (k > j) {
+            d[0] = 2 * g[j];
+            for (int i = 1; i <= k - j; ++i) d[i] = g[std::abs(j - i)] + g[j + i];
+            for (int i = k - j + 1; i <= n; ++i) d[i] = g[std::abs(i - j)];
+        } else {
+            d[j] = g[0];
+            for (int i = n - 2 * k; i <= n; ++i)
+                if (i != j) d[i] = g[std::abs(i - j)];
+        }
+        const double lead = r[n];
+        if (lead != 1.0)
+            for (double &v : d) v *= lead;
+        if (g[k] != 1.0)
+            for (double &v : d) v /= g[k];
+        for (int i = 0; i < (int)r.size(); ++i) r[i] -= d[i];
+        if (r.size() > 1) {
+            const int before = n;
+            n = cdeg(r);
+            r.resize(n + 1);
+            if (j > 0 && n >= before) throw std::invalid_argument("cheb_divide: leading term did not cancel");
+        }
+    };
+    while (n > k) {
+        q[n - k] = 2 * r[n];
+        if (g[k] != 1.0) q[n - k] /= g[k];
+        step(n - k);
+    }
+    if (n == k) {
+        q[0] = r[n];
+        if (g[k] != 1.0) q[0] /= g[k];
+        step(0);
+    }
+    q[0] *= 2;
+}
+
+struct PSOpenFHE {
+    Context &cc;
+    int k = 0, m = 0, lk = 0;
+    std::vector<CtPtr> T, T2;
+
+    // 2 a b (+ cx x) with one rescale; the lower operand is doubled while it is
+    // brought to the other's level
+    CtPtr dbl_mul(const Ciphertext &a, const Ciphertext &b, const Ciphertext *x, double cx) {
+        const Ciphertext *lo = &a, *hi = &b;
+        if (lo->level > hi->level) std::swap(lo, hi);
+        CtPtr two = lo->level < hi->level ? cc.mul_const_to(*lo, 2.0, hi->level) : cc.add(*lo, *lo);
+        return x ? cc.mul_add(*two, *hi, {x}, {cx}) : cc.mul(*two, *hi);
+    }
+    // sum_{i=1..upto} c_i T_i + c_0/2 at `target` (rescaled), or the raw sum
+    // folded into a product (raw: returns the pieces for mul_add)
+    CtPtr lsum(const std::vector<double> &c, int upto, int target) {
+        std::vector<const Ciphertext *> xs;
+        std::vector<double> cs;
+        for (int i = 1; i <= upto && i < (int)c.size(); ++i)
+            if (c[i] != 0.0) {
+                xs.push_back(T[i].get());
+                cs.push_back(c[i]);
+            }
+        CtPtr r = cc.linear_sum_to(xs, cs, target);
+        return c[0] != 0.0 ? cc.add_const(*r, c[0] / 2) : r;
+    }
+    CtPtr inner(const std::vector<double> &f, int mm) {
+        const int k2m2k = k * (1 << (mm - 1)) - k;
+        const int lvl = lk + mm - 1;  // level of T2[mm-1], of c(u) and of q(u)
+        std::vector<double> Tkm(k2m2k + k + 1, 0.0), q, r, cq, cr;
+        Tkm[k2m2k + k] = 1.0;
+        cheb_divide(f, Tkm, q, r);
+        std::vector<double> r2(r);
+        if (k2m2k <= cdeg(r)) {
+            r2[k2m2k] -= 1;
+            r2.resize(cdeg(r2) + 1);
+        } else {
+            r2.resize(k2m2k + 1, 0.0);
+            r2[k2m2k] = -1;
+        }
+        cheb_divide(r2, q, cq, cr);
+        std::vector<double> s2(cr);
+        s2.resize(k2m2k + 1, 0.0);
+        s2[k2m2k] = 1;
+        // (T_{k 2^(mm-1)} + c(u))
+        CtPtr a;
+        if (cdeg(cq) >= 1)
+            a = cc.add(*T2[mm - 1], *lsum(cq, cdeg(cq), lvl));
+        else
+            a = cq[0] != 0.0 ? cc.add_const(*T2[mm - 1], cq[0] / 2) : T2[mm - 1];
+        CtPtr qu = cdeg(q) > k ? inner(q, mm - 1) : lsum(q, k, lvl);
+        if (cdeg(s2) > k) {
+            CtPtr su = inner(s2, mm - 1);
+            return cc.mul_add(*a, *qu, {su.get()}, {1.0});
+        }
+        // s(u) is summed into the product before its rescale
+        std::vector<const Ciphertext *> xs;
+        std::vector<double> cs;
+        for (int i = 1; i <= k; ++i)
+            if (s2[i] != 0.0) {
+                xs.push_back(T[i].get());
+                cs.push_back(s2[i]);
+            }
+        CtPtr out = cc.mul_add(*a, *qu, xs, cs);
+        return s2[0] != 0.0 ? cc.add_const(*out, s2[0] / 2) : out;
+    }
+    CtPtr run(const Ciphertext &x, const std::vector<double> &c) {
+        const int n = cdeg(c);
+        degrees_ps(n, k, m);
+        lk = x.level + ceil_log2(k);
+        T.assign(k + 1, nullptr);
+        T[1] = cc.clone(x);
+        for (int i = 2; i <= k; ++i)
+            T[i] = (i & 1) ? dbl_mul(*T[i / 2], *T[i / 2 + 1], T[1].get(), -1.0)
+                           : cc.add_const(*dbl_mul(*T[i / 2], *T[i / 2], nullptr, 0.0), -1.0);
+        T2 = {T[k]};
+        for (int j = 1; j < m; ++j) T2.push_back(cc.add_const(*dbl_mul(*T2[j - 1], *T2[j - 1], nullptr, 0.0), -1.0));
+        // f + T_{k(2^m - 1)}, evaluated, minus T_{k(2^m - 1)}
+        const int k2m2k = k * (1 << (m - 1)) - k;
+        std::vector<double> f2(c.begin(), c.begin() + n + 1);
+        f2.resize(2 * k2m2k + k + 1, 0.0);
+        f2.back() = 1.0;
+        CtPtr res = inner(f2, m);
+        CtPtr t = T2[0];
+        for (int j = 1; j < m; ++j) t = dbl_mul(*t, *T2[j], T2[0].get(), -1.0);
+        return cc.sub(*res, *t);
+    }
+};
+
+// The node split of PSOpenFHE::inner without the ciphertexts: the largest |c|
+// quotient coefficient of the division tree
+double tree_cmax(const std::vector<double> &f, int k, int mm) {
+    const int k2m2k = k * (1 << (mm - 1)) - k;
+    std::vector<double> Tkm(k2m2k + k + 1, 0.0), q, r, cq, cr;
+    Tkm[k2m2k + k] = 1.0;
+    cheb_divide(f, Tkm, q, r);
+    std::vector<double> r2(r);
+    if (k2m2k <= cdeg(r)) {
+        r2[k2m2k] -= 1;
+        r2.resize(cdeg(r2) + 1);
+    } else {
+        r2.resize(k2m2k + 1, 0.0);
+        r2[k2m2k] = -1;
+    }
+    cheb_divide(r2, q, cq, cr);
+    double mx = 0.0;
+    for (double v : cq) mx = std::max(mx, std::fabs(v));
+    std::vector<double> s2(cr);
+    s2.resize(k2m2k + 1, 0.0);
+    s2[k2m2k] = 1;
+    if (cdeg(q) > k) mx = std::max(mx, tree_cmax(q, k, mm - 1));
+    if (cdeg(s2) > k) mx = std::max(mx, tree_cmax(s2, k, mm - 1));
+    return mx;
+}
+
+// OpenFHE's split is used when it applies (degree >= 5, m >= 2) and its division
+// tree is well-conditioned (every |c| <= 1024; the reference's series stay
+// below 2m): a non-decaying O(1) series makes OpenFHE's second division blow up
+// (|c| ~ 1e7 at degree 60) and is evaluated with the power-of-two split instead
+bool openfhe_split_applies(const std::vector<double> &c) {
+    const int d = cdeg(c);
+    if (d < 5) return false;
+    int k = 0, m = 0;
+    degrees_ps(d, k, m);
+    if (m < 2) return false;
+    const int k2m2k = k * (1 << (m - 1)) - k;
+    std::vector<double> f2(c.begin(), c.begin() + d + 1);
+    f2.resize(2 * k2m2k + k + 1, 0.0);
+    f2.back() = 1.0;
+    try {
+        return tree_cmax(f2, k, m) <= 1024.0;
+    } catch (const std::invalid_argument &) {
+        return false;
+    }
+}
+
 }  // namespace
 
-int cheb_ps_depth(int d) { return std::max(std::max(1, ceil_log2((long)d + 1)), openfhe_ps_depth(d)); }
+int cheb_ps_depth_split(int d, int split) {
+    int k = 0, m = 0;
+    if (split == 1 && d >= 5 && (degrees_ps(d, k, m), m >= 2)) return ceil_log2(k) + m;
+    return std::max(std::max(1, ceil_log2((long)d + 1)), openfhe_ps_depth(d));
+}
+int cheb_ps_depth(int d) { return cheb_ps_depth_split(d, 1); }
 
 CtPtr cheb_series_ps(Context &cc, const Ciphertext &x0, const std::vector<double> &coeffs, double a,
                      double b) {
@@ -182,6 +424,10 @@ CtPtr cheb_series_ps(Context &cc, const Ciphertext &x0, const std::vector<double
     if (!(a == -1.0 && b == 1.0)) {
         x = cc.mul_const(*x, 2.0 / (b - a));
         x = cc.add_const(*x, -(a + b) / (b - a));
+    }
+    if (cc.ps_split == 1 && openfhe_split_applies(c)) {
+        PSOpenFHE ev{cc};
+        return ev.run(*x, c);
     }
     std::vector<double> std_c(c);
     std_c[0] = c[0] / 2.0;  // OpenFHE convention: p = c0/2 + sum c_i T_i

@@ -39,7 +39,7 @@
 
 namespace oracle {
 
-int cheb_ps_depth(int degree);  // oracle_algo.cpp
+int cheb_ps_depth_split(int degree, int split);  // oracle_algo.cpp
 
 namespace {
 
@@ -264,7 +264,7 @@ void Bootstrapper::keygen() {
 }
 
 int Bootstrapper::depth() const {
-    return (int)(cts.size() + stc.size()) + cheb_ps_depth((int)cheb.size() - 1) + cfg.r;
+    return (int)(cts.size() + stc.size()) + cheb_ps_depth_split((int)cheb.size() - 1, cc.ps_split) + cfg.r;
 }
 
 CtPtr Bootstrapper::linear(const Ciphertext &x, const LinLevel &lv, int tag) {

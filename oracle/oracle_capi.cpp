@@ -54,6 +54,15 @@ void *orc_ctx_new(int logN, int L, int scale_bits, int first_bits, int dnum, uin
                  (void *)nullptr);
 }
 void orc_ctx_free(void *c) { delete static_cast<Context *>(c); }
+int orc_cheb_ps_depth(int degree, int split) {
+    return guard([&]() { return cheb_ps_depth_split(degree, split); }, -1);
+}
+// Paterson-Stockmeyer split (1 = OpenFHE's, 0 = power-of-two), as fhe_set_ps_split
+int orc_set_ps_split(void *c, int split) {
+    if (split != 0 && split != 1) return -1;
+    static_cast<Context *>(c)->ps_split = split;
+    return 0;
+}
 
 int orc_params(void *c, uint64_t *primes, int *nq, int *K, int *alpha, double *delta) {
     auto *cc = static_cast<Context *>(c);

@@ -33,6 +33,8 @@ def lib():
             'orc_last_error': (C.c_char_p, []),
             'orc_ctx_new': (vp, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]),
             'orc_ctx_free': (None, [vp]),
+            'orc_set_ps_split': (C.c_int, [vp, C.c_int]),
+            'orc_cheb_ps_depth': (C.c_int, [C.c_int, C.c_int]),
             'orc_params': (C.c_int, [vp, u64p, ip, ip, ip, dp]),
             'orc_keygen': (C.c_int, [vp]),
             'orc_gen_rotation_keys': (C.c_int, [vp, ip, C.c_int]),
@@ -224,8 +226,13 @@ class Pt:
         return out
 
 
+def cheb_ps_depth(degree, split=1):
+    """levels a degree-d Chebyshev series consumes under the given PS split"""
+    return int(lib().orc_cheb_ps_depth(int(degree), int(split)))
+
+
 class Context:
-    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, keygen=True):
+    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, keygen=True, ps_split=1):
         self.logN, self.n, self.L = logN, 1 << logN, L
         self.h = _check(lib().orc_ctx_new(logN, L, scale_bits, first_bits, dnum, seed))
         nq, K, alpha = C.c_int(), C.c_int(), C.c_int()
@@ -235,6 +242,7 @@ class Context:
         self.delta = np.empty(L + 1)
         lib().orc_params(self.h, _u64(self.primes), None, None, None, _dbl(self.delta))
         self.params = dict(logN=logN, L=L, scale_bits=scale_bits, first_bits=first_bits, dnum=dnum, seed=seed)
+        self.set_ps_split(ps_split)
         if keygen:
             self.keygen()
 
@@ -243,6 +251,12 @@ class Context:
             lib().orc_ctx_free(self.h)
         except Exception:
             pass
+
+    def set_ps_split(self, split):
+        """1: OpenFHE's EvalChebyshevSeriesPS split (default); 0: power-of-two split"""
+        if lib().orc_set_ps_split(self.h, int(split)) != 0:
+            raise ValueError('ps split must be 0 or 1')
+        self.ps_split = int(split)
 
     # keys -------------------------------------------------------------
     def keygen(self):

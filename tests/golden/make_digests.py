@@ -17,7 +17,10 @@ Cases:
             (tests/DirectSortTest.cpp:24-31,105-106,175; src/sort_algo.h:99-102)
   config2   N=128,  ring 2^16, depth 30, scale 40, CompositeSign(3,3,2)
   config3   N=1024, ring 2^16, depth 39, scale 50, CompositeSign(3,5,2) -- the
-            bench workload (bench.py; DESIGN.md §3 for the scale)
+            round-2 bench workload
+  *_of      the same with OpenFHE's Paterson-Stockmeyer split (round 3's
+            default) and 40-bit scaling throughout; config3_of is the bench
+            workload
 Each case pins the sorted output (level multDepth, one limb) and the
 constructRank output (mode 1: the rank ciphertext, many limbs).
 
@@ -41,9 +44,14 @@ sys.path.insert(0, os.path.join(REPO, 'oracle'))
 
 SEED = 20250704
 CASES = {
-    'config1': dict(N=8, logN=17, depth=24, scale_bits=40, dnum=3, cfg=(3, 2, 2)),
-    'config2': dict(N=128, logN=16, depth=30, scale_bits=40, dnum=3, cfg=(3, 3, 2)),
-    'config3': dict(N=1024, logN=16, depth=39, scale_bits=50, dnum=3, cfg=(3, 5, 2)),
+    # rounds 1-2: the power-of-two Paterson-Stockmeyer split (ps_split 0)
+    'config1': dict(N=8, logN=17, depth=24, scale_bits=40, dnum=3, cfg=(3, 2, 2), ps_split=0),
+    'config2': dict(N=128, logN=16, depth=30, scale_bits=40, dnum=3, cfg=(3, 3, 2), ps_split=0),
+    'config3': dict(N=1024, logN=16, depth=39, scale_bits=50, dnum=3, cfg=(3, 5, 2), ps_split=0),
+    # round 3: OpenFHE's split (the default), the reference's 40-bit scaling for every N
+    'config1_of': dict(N=8, logN=17, depth=24, scale_bits=40, dnum=3, cfg=(3, 2, 2), ps_split=1),
+    'config2_of': dict(N=128, logN=16, depth=30, scale_bits=40, dnum=3, cfg=(3, 3, 2), ps_split=1),
+    'config3_of': dict(N=1024, logN=16, depth=39, scale_bits=40, dnum=3, cfg=(3, 5, 2), ps_split=1),
 }
 OUT = os.path.join(HERE, 'sort_digests.json')
 
@@ -59,7 +67,7 @@ def run(name):
     depth, rots = O.size_parameters(N)
     assert depth == c['depth'], (depth, c['depth'])
     t0 = time.time()
-    orc = O.Context(c['logN'], depth, c['scale_bits'], 60, c['dnum'], seed=SEED)
+    orc = O.Context(c['logN'], depth, c['scale_bits'], 60, c['dnum'], seed=SEED, ps_split=c['ps_split'])
     orc.gen_rotation_keys(rots)
     x = np.random.default_rng(SEED).permutation(N) / N
     ct = orc.encrypt(x, N)

@@ -34,7 +34,9 @@ def test_direct_sort_matches_oracle_digest(name):
     N = c['N']
     depth, rots = F.size_parameters(N)
     assert depth == c['depth'] and [int(r) for r in rots] == c['rotations']
-    ctx = F.Context(c['logN'], depth, c['scale_bits'], 60, c['dnum'], seed=c['seed'])
+    # records made before the OpenFHE split became the default carry ps_split 0
+    ctx = F.Context(c['logN'], depth, c['scale_bits'], 60, c['dnum'], seed=c['seed'],
+                    ps_split=c.get('ps_split', F.PS_SPLIT_ENGINE))
     try:
         ctx.gen_rotation_keys(rots)
         x = np.random.default_rng(c['seed']).permutation(N) / N

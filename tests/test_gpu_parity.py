@@ -3,6 +3,8 @@ keys and inputs, and decrypts within the reference tests' tolerances.
 
 All calls go through the C ABI (include/fhe_gpu.h) via fhesort.py.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -194,10 +196,16 @@ def test_linear_sum_mixed_levels(pair):
     same(gpu.linear_sum_to(gx, cs, 3), orc.linear_sum_to(xs, cs, 3))
 
 
-@pytest.mark.parametrize('deg', [1, 3, 7, 27, 70])
-def test_chebyshev_ps(deg):
-    orc = O.Context(12, 10, 40, 60, 3, seed=9)
-    gpu = F.Context(12, 10, 40, 60, 3, seed=9, keygen=False)
+@pytest.mark.parametrize('split', [F.PS_SPLIT_OPENFHE, F.PS_SPLIT_ENGINE])
+@pytest.mark.parametrize('deg', [1, 3, 7, 27, 70, 119, 200])
+def test_chebyshev_ps(deg, split):
+    """evalChebyshevSeriesPS under both Paterson-Stockmeyer splits (OpenFHE's
+    (k, m) long division -- the default -- and the power-of-two one): word for
+    word equal to the oracle, same output level (the depth OpenFHE consumes),
+    within 1e-5 of the plain series."""
+    L = 10 if deg <= 119 else 11
+    orc = O.Context(12, L, 40, 60, 3, seed=9, ps_split=split)
+    gpu = F.Context(12, L, 40, 60, 3, seed=9, keygen=False, ps_split=split)
     gpu.load_keys_from(orc)
     x = np.linspace(-1, 1, 16)
     ox = orc.encrypt(x, 16)
@@ -205,8 +213,29 @@ def test_chebyshev_ps(deg):
     oy = orc.cheb(ox, c)
     gy = gpu.cheb(gpu.from_oracle(ox), c)
     same(gy, oy)
+    assert gy.level == O.cheb_ps_depth(deg, split)
     ref = np.polynomial.chebyshev.chebval(x, np.concatenate([[c[0] / 2], c[1:]]))
     assert np.max(np.abs(gpu.decrypt(gy) - ref)) < 1e-5
+
+
+@pytest.mark.parametrize('split', [F.PS_SPLIT_OPENFHE, F.PS_SPLIT_ENGINE])
+def test_doubled_sinc_ps_bit_exact(split):
+    """The N=128 doubled-sinc series (degree 848, src/sort_algo.h:725-728) on the
+    index-check grid x = j/(2N): both splits word-identical to the oracle at ring
+    2^12, and the OpenFHE split at least as precise as the power-of-two one."""
+    N = 128
+    c = np.fromfile(os.path.join(F.COEFF_DIR, f'doubled_sinc_{N}.f64'))
+    orc = O.Context(12, 12, 40, 60, 3, seed=21, ps_split=split)
+    gpu = F.Context(12, 12, 40, 60, 3, seed=21, keygen=False, ps_split=split)
+    gpu.load_keys_from(orc)
+    x = np.resize(np.arange(-(2 * N - 2), N) / (2 * N), 1024)
+    ox = orc.encrypt(x, 1024)
+    gy = gpu.cheb(gpu.from_oracle(ox), c)
+    same(gy, orc.cheb(ox, c))
+    assert gy.level == 10  # OpenFHE's depth for degree 848 (ComputeDegreesPS: k = 28, m = 5)
+    ref = np.polynomial.chebyshev.chebval(x, np.concatenate([[c[0] / 2], c[1:]]))
+    err = np.max(np.abs(gpu.decrypt(gy) - ref))
+    assert err < (2e-5 if split == F.PS_SPLIT_OPENFHE else 1e-3)
 
 
 def test_composite_sign_and_compare():
@@ -448,22 +477,27 @@ def test_config3_direct_sort_full_size():
     assert np.array_equal(a.data(), b.data())
 
 
-@pytest.mark.parametrize('N,scale_bits', [(1024, 50), (128, 40)])
+@pytest.mark.parametrize('N,scale_bits', [(128, 40), (256, 40), (512, 40), (1024, 40), (1024, 50)])
 def test_reference_shipped_context_ring17(N, scale_bits):
     """DirectSortTest's own context (tests/DirectSortTest.cpp:24-51): ring 2^17,
-    the getSizeParameters depth/rotations (src/sort_algo.h:87-201).  The
-    reference's 40-bit scaling holds the 0.01 bound up to N = 128 here; at
-    N >= 256 the doubled-sinc index check is noise-limited at 40 bits (measured
-    N = 256: 0.012, N = 1024: 0.63, profiles/r2_c/diag_ring17.jsonl; the error
-    falls 870x for 10 more bits), so N = 1024 runs at 2^50 as the
-    bench does.  Bound and level assertion as DirectSortTest.cpp:128,169."""
+    the reference's 40-bit scaling primes, the getSizeParameters depth/rotations
+    (src/sort_algo.h:87-201), N up to 1024 (DirectSortTest.cpp:174-179).  With
+    OpenFHE's Paterson-Stockmeyer split (the default) the degree-6510 doubled-sinc
+    index check holds the reference's 0.01 at 40 bits; the power-of-two split of
+    rounds 1-2 missed it for N >= 256 (0.012 / 0.63 at N = 256 / 1024,
+    profiles/r2_c/diag_ring17.jsonl).  Bound and level assertion as
+    DirectSortTest.cpp:128,169."""
     depth, rots = F.size_parameters(N)
     gpu = F.Context(17, depth, scale_bits, 60, 3, seed=1234)
     try:
+        assert gpu.ps_split == F.PS_SPLIT_OPENFHE
         gpu.gen_rotation_keys(rots)
         x = np.random.default_rng(N).permutation(N) / N
-        out = gpu.direct_sort(gpu.encrypt(x, N), N, rots, (3, 5, 2) if N == 1024 else (3, 3, 2))
+        cfg = (3, 2, 2) if N <= 16 else (3, 3, 2) if N <= 128 else (3, 4, 2) if N <= 512 else (3, 5, 2)
+        out = gpu.direct_sort(gpu.encrypt(x, N), N, rots, cfg)
         assert out.level == depth
-        assert np.max(np.abs(gpu.decrypt(out) - np.sort(x))) < 0.01
+        err = float(np.max(np.abs(gpu.decrypt(out) - np.sort(x))))
+        print(f'N={N} scale 2^{scale_bits} ring 2^17: max err {err:.3e}')
+        assert err < 0.01
     finally:
         gpu.close()

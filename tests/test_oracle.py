@@ -16,11 +16,14 @@ reference is "parity unpinned" (DESIGN.md §6).
 """
 import json
 import os
+import sys
 
 import numpy as np
 import pytest
 
 import pyoracle as O
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
@@ -240,6 +243,66 @@ def test_chebyshev_ps_depth_and_value(deg):
     ref = np.polynomial.chebyshev.chebval(x, np.concatenate([[co[0] / 2], co[1:]]))
     assert np.max(np.abs(c.decrypt(y) - ref)) < 2e-6 * np.sum(np.abs(co))
     assert y.level == OPENFHE_PS_DEPTH[deg]  # levels OpenFHE's EvalChebyshevSeriesPS consumes
+
+
+def test_ps_depth_tables():
+    """Both Paterson-Stockmeyer splits consume the same levels for every degree
+    (OpenFHE's (k, m) held to its published band up to 2204), so the
+    conditioning fallback of the OpenFHE split never changes an output level."""
+    for d in range(1, 4097):
+        assert O.cheb_ps_depth(d, 1) == O.cheb_ps_depth(d, 0), d
+    # the reference's series (doubled sinc N = 4..2048, g_4, scaled sinc, EvalMod)
+    for d, depth in [(42, 6), (70, 7), (126, 8), (232, 8), (438, 9), (848, 10), (1662, 11), (3280, 12),
+                     (6510, 13), (13020, 14), (27, 5), (88, 7)]:
+        assert O.cheb_ps_depth(d, 1) == depth
+
+
+@pytest.mark.parametrize('N', [16, 64])
+def test_openfhe_split_doubled_sinc(N):
+    """OpenFHE's split (the default) evaluates the doubled-sinc index-check series
+    (src/sort_algo.h:725-728) on its grid x = j/(2N) at the depth the reference
+    budgets, more precisely than the power-of-two split at the same 40-bit scale
+    (the power-of-two split amplifies baby-step noise 4^11-fold at x = 0)."""
+    c = np.fromfile(os.path.join(REPO, 'fhe-sorting_amd', 'data', f'doubled_sinc_{N}.f64'))
+    x = np.resize(np.arange(-(2 * N - 2), N) / (2 * N), 256)
+    ref = np.polynomial.chebyshev.chebval(x, np.concatenate([[c[0] / 2], c[1:]]))
+    errs = {}
+    for split in (1, 0):
+        ctx = O.Context(11, 10, 40, 60, 3, seed=4, ps_split=split)
+        y = ctx.cheb(ctx.encrypt(x, 256), c)
+        assert y.level == O.cheb_ps_depth(len(c) - 1)
+        errs[split] = float(np.max(np.abs(ctx.decrypt(y)[:256] - ref)))
+    assert errs[1] < 1e-5 and errs[1] <= errs[0]
+
+
+def test_openfhe_split_ill_conditioned_falls_back():
+    """A series with O(1) coefficients that do not decay makes OpenFHE's second
+    division blow up (|c| ~ 1e7 at degree 60): such a series is evaluated with the
+    power-of-two split, word for word, instead of returning garbage."""
+    co = np.random.default_rng(60).normal(size=61)
+    x = np.linspace(-1, 1, 32)
+    words = []
+    for split in (1, 0):
+        ctx = O.Context(11, 8, 40, 60, 3, seed=6, ps_split=split)
+        y = ctx.cheb(ctx.encrypt(x, 32), co)
+        words.append(y.data())
+        ref = np.polynomial.chebyshev.chebval(x, np.concatenate([[co[0] / 2], co[1:]]))
+        assert np.max(np.abs(ctx.decrypt(y)[:32] - ref)) < 1e-4
+    assert np.array_equal(words[0], words[1])
+
+
+def test_ps_noise_model_restatement():
+    """scripts/ps_noise_model.py's restatements of both splits reproduce the plain
+    series without noise (the model behind DESIGN.md §3's table)."""
+    sys.path.insert(0, os.path.join(REPO, 'scripts'))
+    import ps_noise_model as M
+    c = M.coeffs(64)
+    x = np.arange(-126, 64) / 128.0
+    ref = np.polynomial.chebyshev.chebval(x, np.concatenate([[c[0] / 2], c[1:]]))
+    for ev in (M.engine_eval, M.openfhe_eval):
+        out = ev(c, x, M.Noisy(0.0, None, None), {})
+        assert np.max(np.abs(out - ref)) < 1e-12
+    assert M.compute_degrees_ps(6510) == (52, 7)
 
 
 # ------------------------------------------------------------ DirectSort ---
