@@ -2,14 +2,16 @@
 """Benchmark: encrypted rank sort (DirectSort) on MI355X.
 
 Workload (BASELINE.json metric): DirectSort of N=1024 reals at ring dimension
-2^16, multiplicative depth 39 (40 Q primes + 10 special primes, dnum=3),
+2^16, multiplicative depth 39 (40 Q primes: 60-bit q0 + the reference's 40-bit
+scaling primes, K special primes, dnum=3; OpenFHE's Paterson-Stockmeyer split),
 161 rotation keys, CompositeSign(3,5,2) -- the reference's DirectSortTest
 configuration for N=1024 (tests/DirectSortTest.cpp:104-112,
 src/sort_algo.h:147-165).  One step = one full sort() of an encrypted input
 already resident in HBM (constructRank + rotationIndexCheckN); keys, the
 input encryption and the public plaintext masks are produced before timing.
 
-Multi-GPU (torchrun, one process per GPU): the 32 comparator batches of
+Multi-GPU (one process per GPU: `python bench.py --gpus N` starts the N ranks
+itself, or run it under torchrun): the 32 comparator batches of
 constructRank and the 32 index-check batches of rotationIndexCheckN are
 sharded over ranks (batch b -> rank b % world); the partial ranks/outputs are
 summed by one RCCL all-reduce each (u64 sum + mod q) -- strong scaling.
@@ -56,15 +58,84 @@ def parse():
     ap.add_argument('--n-sort', type=int, default=None, help='values to sort (default 1024; mehp24: 4096)')
     ap.add_argument('--log-n', type=int, default=16)
     ap.add_argument('--seed', type=int, default=20250704)
-    ap.add_argument('--scale-bits', type=int, default=50,
-                    help='scaling-prime size; 40 (the reference) leaves the N>=128 sort noise-limited, DESIGN.md §3')
+    ap.add_argument('--scale-bits', type=int, default=40,
+                    help="scaling-prime size (the reference's 40, src/sort_algo.h:92,199)")
+    ap.add_argument('--ps-split', choices=('openfhe', 'engine'), default='openfhe',
+                    help="Paterson-Stockmeyer split: OpenFHE's (the reference's EvalChebyshevSeriesPS; holds the "
+                         "0.01 bound at 40 bits) or rounds 1-2's power-of-two split (needs 50 bits at N=1024), "
+                         "DESIGN.md §3")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true', help='skip the instrumented roofline sort (PMC passes)')
     ap.add_argument('--cpu-sample-mults', type=int, default=0, help='override CPU sample size')
     ap.add_argument('--clock-json', default=None, help='write the full per-kernel clock of the roofline sort here')
     ap.add_argument('--lanes', type=int, default=3, help='concurrent batch lanes (forked engines) per GPU (3: 885 vs 898 ms for 2)')
     ap.add_argument('--stack', type=int, default=32, help='max batches stacked into one ciphertext batch')
+    ap.add_argument('--rendezvous-check', action='store_true',
+                    help='launch/rendezvous only: ranks meet over gloo, exchange a max and a sum, rank 0 prints '
+                         'one JSON line (no GPU work; the multi-rank launcher test)')
     return ap.parse_args()
+
+
+def launched_by_torchrun():
+    return 'RANK' in os.environ and 'WORLD_SIZE' in os.environ
+
+
+def self_launch(a):
+    """`python bench.py --gpus N` without a launcher: start N fresh interpreters
+    running this script as ranks 0..N-1 (the env torchrun would set: RANK,
+    LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free
+    MASTER_PORT), before this process touches HIP or torch.cuda.  Rank 0 prints
+    the JSON line on the inherited stdout; if any rank fails the others are
+    stopped and the exit code is the first failure's."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(('127.0.0.1', 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:  # a rank that failed leaves the others waiting in a collective
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+    return rc if rc >= 0 else 128 - rc
+
+
+def rendezvous_check(a, d):
+    t = time.perf_counter()
+    d.barrier()
+    mx = d.max(float(d.rank))
+    sm = d.sum(1.0)
+    d.barrier()
+    if d.rank == 0:
+        print(json.dumps({'rendezvous': 'ok', 'world': d.world, 'max_rank': mx, 'ranks_counted': sm,
+                          'launcher': 'torchrun' if os.environ.get('TORCHELASTIC_RUN_ID') else 'bench.py self-launch'
+                          if d.world > 1 else 'none', 'seconds': round(time.perf_counter() - t, 3)}), flush=True)
 
 
 def sign_cfg(N):  # tests/DirectSortTest.cpp:104-112
@@ -78,15 +149,17 @@ def sign_cfg(N):  # tests/DirectSortTest.cpp:104-112
 
 
 class Dist:
-    def __init__(self, world):
+    def __init__(self, world, probe_devices=True):
         self.world = world
         self.rank = int(os.environ.get('RANK', '0'))
         self.local = int(os.environ.get('LOCAL_RANK', '0'))
-        try:  # one rank per GPU; ranks beyond the visible devices share them (rehearsals only)
-            import torch
-            ndev = torch.cuda.device_count()
-        except Exception:
-            ndev = 0
+        ndev = 0
+        if probe_devices:  # one rank per GPU; ranks beyond the visible devices share them (rehearsals only)
+            try:
+                import torch
+                ndev = torch.cuda.device_count()
+            except Exception:
+                ndev = 0
         self.device = self.local % ndev if ndev > 0 else self.local
         # RCCL needs distinct devices; a rehearsal with more ranks than GPUs
         # exchanges the partial sums through host memory and gloo instead
@@ -499,7 +572,13 @@ def run_kway(a, d):
 
 def main():
     a = parse()
-    d = Dist(a.gpus)
+    if a.gpus > 1 and not launched_by_torchrun():
+        sys.exit(self_launch(a))
+    if launched_by_torchrun() and int(os.environ['WORLD_SIZE']) != a.gpus:
+        raise SystemExit(f'--gpus {a.gpus} but WORLD_SIZE={os.environ["WORLD_SIZE"]}')
+    d = Dist(a.gpus, probe_devices=not a.rendezvous_check)
+    if a.rendezvous_check:
+        return rendezvous_check(a, d)
     if a.workload == 'mehp24':
         return run_mehp24(a, d)
     if a.workload == 'kway':
@@ -508,7 +587,8 @@ def main():
     depth, rots = F.size_parameters(N)
     cfg = sign_cfg(N)
     t0 = time.time()
-    ctx = F.Context(logN, depth, a.scale_bits, 60, 3, seed=a.seed, device=d.device)
+    ctx = F.Context(logN, depth, a.scale_bits, 60, 3, seed=a.seed, device=d.device,
+                    ps_split=F.PS_SPLIT_OPENFHE if a.ps_split == 'openfhe' else F.PS_SPLIT_ENGINE)
     ctx.gen_rotation_keys(rots)
     ctx.set_sort_lanes(a.lanes)
     ctx.set_sort_stack(a.stack)
@@ -571,8 +651,10 @@ def main():
             'dtype': 'u64',
             'data': 'synthetic: seeded permutation of {k/N}, keys and encryption from a seeded PRNG',
             'config': {'workload': f'DirectSort N={N}, ringDim 2^{logN}, depth {depth}, scale 2^{a.scale_bits}, '
-                                   f'{len(rots)} rotation keys, CompositeSign{cfg}, dnum 3',
-                       'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'lanes_per_gpu': a.lanes,
+                                   f'{len(rots)} rotation keys, CompositeSign{cfg}, dnum 3, '
+                                   f'{"OpenFHE" if a.ps_split == "openfhe" else "power-of-two"} PS split',
+                       'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'scale_bits': a.scale_bits,
+                       'ps_split': a.ps_split, 'special_primes': ctx.K, 'lanes_per_gpu': a.lanes,
                        'max_stack': a.stack, 'parallelism': f'batch-shard x{d.world}',
                        'collective': 'none' if d.world == 1 else ('rccl' if d.rccl else 'host+gloo (more ranks than GPUs)')},
             'max_abs_err': max_err,

@@ -149,3 +149,60 @@ def test_exception_in_hook_propagates():
         raise Boom('transport down')
     with pytest.raises(Boom):
         _run(c, 'direct', ct, shard=(0, 2), allreduce=failing)
+
+
+# ------------------------------------------------- bench.py multi-rank launch
+BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'bench.py')
+
+
+def _bench(args, timeout=180, env=None):
+    import subprocess
+    import sys
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout,
+                          env=env)
+
+
+def _json_line(out):
+    import json
+    lines = [ln for ln in out.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_bench_self_launch_rendezvous(world):
+    """`python bench.py --gpus N` with no launcher starts its N ranks itself
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set per child, 127.0.0.1 and a
+    free port), the ranks meet over gloo, and rank 0 alone prints one JSON line:
+    the driver's 1-GPU command shape, run with --gpus N."""
+    r = _bench(['--gpus', str(world), '--rendezvous-check'])
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = _json_line(r.stdout)
+    assert j['world'] == world and j['max_rank'] == world - 1 and j['ranks_counted'] == world
+    assert j['launcher'] == 'bench.py self-launch'
+
+
+def test_bench_torchrun_launch_still_works():
+    import subprocess
+    import sys
+    with socket.socket() as so:
+        so.bind(('127.0.0.1', 0))
+        port = so.getsockname()[1]
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+                        '--master-addr', '127.0.0.1', '--master-port', str(port), BENCH, '--gpus', '2',
+                        '--rendezvous-check'], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = _json_line(r.stdout)
+    assert j['world'] == 2 and j['launcher'] == 'torchrun'
+
+
+def test_bench_self_launch_failing_rank_ends_the_job():
+    """A rank that fails (here: no GPU in this container) must not leave the
+    other ranks waiting in a collective: the launcher stops them and returns
+    the failure's exit code, quickly."""
+    import time
+    t = time.time()
+    r = _bench(['--gpus', '2', '--steps', '1', '--warmup', '0', '--no-cpu-baseline', '--no-roofline'], timeout=170)
+    assert r.returncode != 0
+    assert time.time() - t < 160
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
