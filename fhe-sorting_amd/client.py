@@ -118,7 +118,8 @@ def main(argv=None):
             s.add_argument('--scale-bits', type=int, default=50)
             s.add_argument('--sign', default='4,3,3')
             s.add_argument('--depth', type=int, default=0)
-            s.add_argument('--seed', type=int, default=1)
+            s.add_argument('--seed', type=int, default=0,
+                           help='0 (default): keys from the OS CSPRNG; nonzero: reproducible keys, for tests only')
         elif name == 'encrypt':
             g = s.add_mutually_exclusive_group(required=True)
             g.add_argument('--values')

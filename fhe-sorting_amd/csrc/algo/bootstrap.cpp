@@ -160,6 +160,11 @@ Bootstrapper::Bootstrapper(Engine &c, const BootstrapConfig &cf) : cc(c), cfg(cf
         throw std::invalid_argument("bootstrap: slots must be a power of two in [2, n/4]");
     if (cfg.budgetEnc < 1 || cfg.budgetDec < 1 || cfg.r < 0 || cfg.K < 1 || cfg.degree < 1)
         throw std::invalid_argument("bootstrap: bad configuration");
+    // the message is scaled to q0 2^-bits before ModRaise; 2^bits / (4 pi) is
+    // folded into SlotsToCoeffs (decInt doubles up to it): bounded so that
+    // stays finite and the integer factor fits a long
+    if (cfg.correctionBits < 1 || cfg.correctionBits > 40)
+        throw std::invalid_argument("bootstrap: correction bits must be in 1..40");
     int logs = 0;
     while ((1L << logs) < s) ++logs;
     const uint64_t M = 2 * (uint64_t)n;
@@ -191,7 +196,7 @@ Bootstrapper::Bootstrapper(Engine &c, const BootstrapConfig &cf) : cc(c), cfg(cf
     }
     // per-level factor <= 2 keeps merged diagonals below 4 (63-bit coefficients
     // at 60-bit scales); the power-of-two rest is one integer product
-    while (std::pow(c_dec / (double)decInt, 1.0 / (double)ld.size()) > 2.0) decInt *= 2;
+    while (std::pow(c_dec / (double)decInt, 1.0 / (double)ld.size()) > 2.0 && decInt < (1L << 50)) decInt *= 2;
     t = 0;
     for (size_t li = 0; li < ld.size(); ++li) {
         DiagMap cur = li == 0 ? join_halves(m) : DiagMap();

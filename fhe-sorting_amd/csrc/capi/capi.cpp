@@ -89,6 +89,15 @@ extern "C" {
 
 const char *fhe_last_error(void) { return g_err.c_str(); }
 
+int fhe_prng_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]) {
+    return guard([&] {
+        NEED(key);
+        NEED(nonce);
+        NEED(out);
+        host::chacha20_block(key, counter, nonce, out);
+    });
+}
+
 int fhe_ctx_create(const fhe_params *p, int device, fhe_ctx **out) {
     return guard([&] {
         NEED(p);
@@ -362,7 +371,17 @@ int fhe_size_parameters(int N, int *depth, int32_t *rots, int max_rots) {
 
 // The reduction a sharded sort uses: the caller's hook if given, else RCCL on
 // the context's communicator (fhe_comm_init), on the engine stream.
-static CtAllReduce make_allreduce(fhe_ctx *ctx, int shard_world, fhe_allreduce_fn fn, void *user) {
+// The reduction of a sharded sort (fhe_gpu.h, fhe_direct_sort):
+//  * 1 <= shard_world and 0 <= shard_rank < shard_world, always;
+//  * a caller hook, when given, is used (any shard world);
+//  * else the RCCL communicator of fhe_comm_init is used iff shard_world equals
+//    its world (then shard_rank must be this context's rank): an unsharded sort
+//    (0, 1) on a context of a world-8 communicator runs locally, a world-1
+//    communicator runs the reduction through RCCL;
+//  * else shard_world must be 1 (local).
+static CtAllReduce make_allreduce(fhe_ctx *ctx, int shard_rank, int shard_world, fhe_allreduce_fn fn, void *user) {
+    if (shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world)
+        throw std::invalid_argument("sharded sort: need 1 <= shard_world and 0 <= shard_rank < shard_world");
     if (shard_world > 1) checkShardWorld(ctx->eng->params(), shard_world);  // before any work
     if (fn) {
         // the partial sums are produced asynchronously on the context stream:
@@ -375,12 +394,14 @@ static CtAllReduce make_allreduce(fhe_ctx *ctx, int shard_world, fhe_allreduce_f
             if (rc != 0) throw std::runtime_error("HIP error: allreduce hook returned " + std::to_string(rc));
         };
     }
-    if (!ctx->comm) {
-        if (shard_world > 1) throw std::runtime_error("sharded sort needs fhe_comm_init or an allreduce hook");
+    if (!ctx->comm || shard_world != ctx->world) {
+        if (shard_world > 1)
+            throw std::invalid_argument(ctx->comm ? "sharded sort: shard world differs from the communicator's world"
+                                                  : "sharded sort needs fhe_comm_init or an allreduce hook");
         return nullptr;
     }
-    if (shard_world != ctx->world)
-        throw std::invalid_argument("sharded sort: shard world differs from the communicator's world");
+    if (shard_rank != ctx->rank)
+        throw std::invalid_argument("sharded sort: shard_rank must equal the communicator rank of this context");
     ncclComm_t comm = ctx->comm;
     hipStream_t st = static_cast<hipStream_t>(ctx->eng->stream_handle());
     return [comm, st](u64 *d, size_t c) {
@@ -394,6 +415,7 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
     return guard([&] {
         NEED(ctx);
         NEED(x);
+        CtAllReduce reduce = make_allreduce(ctx, shard_rank, shard_world, fn, user);  // validates the shard first
         auto key = std::make_pair(N, std::vector<int>(rots, rots + nrot));
         auto &slot = ctx->sorters[key];
         if (!slot) slot = std::make_unique<DirectSortN>(*ctx->eng, N, key.second);
@@ -402,7 +424,7 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
         ds.lanes = ctx->sort_lanes;
         ds.shard_rank = shard_rank;
         ds.shard_world = shard_world;
-        ds.allreduce = make_allreduce(ctx, shard_world, fn, user);
+        ds.allreduce = std::move(reduce);
         const SignConfig cfg = cfgof(n, dg, df);
         if (mode == 1)
             *out = wrap(ds.constructRank(*x->p, SignFunc::CompositeSign, cfg));
@@ -432,7 +454,7 @@ int fhe_sort_hybrid(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
         ds.lanes = ctx->sort_lanes;
         ds.shard_rank = shard_rank;
         ds.shard_world = shard_world;
-        ds.allreduce = make_allreduce(ctx, shard_world, fn, user);
+        ds.allreduce = make_allreduce(ctx, shard_rank, shard_world, fn, user);
         ds.hybrid_max_array = max_array;
         ds.hybrid_mask = mask_mode;
         if (mode == 1) {
@@ -499,7 +521,7 @@ int fhe_mehp24_sort_sharded(fhe_ctx *ctx, const fhe_ct *x, int N, int sub, int n
         Shard sh;
         sh.rank = shard_rank;
         sh.world = shard_world;
-        sh.allreduce = make_allreduce(ctx, shard_world, fn, user);
+        sh.allreduce = make_allreduce(ctx, shard_rank, shard_world, fn, user);
         const SignConfig cfg = cfgof(n, dg, df);
         if (sub == 0) {
             if ((long)N * N != (long)x->p->slots) throw std::invalid_argument("mehp24 sortFG: needs N*N slots");

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -141,7 +142,10 @@ struct Engine::Impl {
     hipStream_t st = nullptr;
     std::shared_ptr<Pool> pool;
     u64 seed = 0;
-    u64 enc_counter = 0;
+    host::Entropy ent;  // sampling keys: deterministic streams for seed != 0, else getrandom
+    // encryption-randomness stream index, shared with forked engines so no
+    // two encryptions under one context ever reuse (v, e0, e1)
+    std::shared_ptr<std::atomic<u64>> enc_counter = std::make_shared<std::atomic<u64>>(0);
 
     // static device tables
     std::vector<std::shared_ptr<DevMem>> keep;
@@ -346,6 +350,7 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     auto &I = *impl;
     I.device = device;
     I.seed = seed;
+    I.ent = host::Entropy::from_seed(seed);
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&I.st, hipStreamNonBlocking));
     I.pool = std::make_shared<Pool>();
@@ -488,8 +493,8 @@ CtPtr Engine::new_ct(int level, int slots, double scale, size_t limbs, int batch
 
 // ================================================================ keys ====
 namespace {
-std::vector<int64_t> sample_coeffs(u64 seed, u64 tag, size_t n, bool ternary) {
-    host::SplitMix64 g(seed, tag);
+std::vector<int64_t> sample_coeffs(const host::Entropy &ent, u64 tag, size_t n, bool ternary) {
+    host::Prng g(ent, tag);
     std::vector<int64_t> v(n);
     for (size_t k = 0; k < n; ++k) v[k] = ternary ? host::sample_ternary(g) : host::sample_cbd(g);
     return v;
@@ -500,7 +505,7 @@ void Engine::keygen() {
     auto &I = *impl;
     const size_t n = I.n(), nall = I.P.nall(), nq = I.P.nq();
     // secret over every prime
-    auto s = sample_coeffs(I.seed, host::tags::secret, n, true);
+    auto s = sample_coeffs(I.ent, host::tags::secret, n, true);
     auto coef = I.alloc(n * 8);
     HIP_OK(hipMemcpyAsync(coef->p, s.data(), n * 8, hipMemcpyHostToDevice, I.st));
     I.ks->s_ntt = I.alloc(nall * n * 8);
@@ -510,11 +515,11 @@ void Engine::keygen() {
     // public key
     std::vector<u64> a(nq * n);
     {
-        host::SplitMix64 g(I.seed, host::tags::pk_a);
+        host::Prng g(I.ent, host::tags::pk_a, true);
         for (size_t l = 0; l < nq; ++l)
             for (size_t k = 0; k < n; ++k) a[l * n + k] = host::sample_uniform_mod(g, I.P.primes[l]);
     }
-    auto e = sample_coeffs(I.seed, host::tags::pk_e, n, false);
+    auto e = sample_coeffs(I.ent, host::tags::pk_e, n, false);
     I.ks->pk = I.alloc(2 * nq * n * 8);
     u64 *pk = static_cast<u64 *>(I.ks->pk->p);
     HIP_OK(hipMemcpyAsync(pk + nq * n, a.data(), nq * n * 8, hipMemcpyHostToDevice, I.st));
@@ -556,11 +561,11 @@ void gen_switch_key_impl(Engine::Impl &I, const u64 *sp, u64 kid, u64 *out) {
         std::vector<std::thread> th;
         for (int j = 0; j < digits; ++j)
             th.emplace_back([&, j]() {
-                host::SplitMix64 ga(I.seed, host::tags::swk_a(kid, j));
+                host::Prng ga(I.ent, host::tags::swk_a(kid, j), true);
                 A[j].resize(nall * n);
                 for (size_t l = 0; l < nall; ++l)
                     for (size_t k = 0; k < n; ++k) A[j][l * n + k] = host::sample_uniform_mod(ga, I.P.primes[l]);
-                host::SplitMix64 ge(I.seed, host::tags::swk_e(kid, j));
+                host::Prng ge(I.ent, host::tags::swk_e(kid, j));
                 E[j].resize(n);
                 for (size_t k = 0; k < n; ++k) E[j][k] = host::sample_cbd(ge);
             });
@@ -608,26 +613,38 @@ void Engine::gen_galois_keys(const std::vector<u64> &gs) {
     HIP_OK(hipStreamSynchronize(I.st));
 }
 
+// Keys are replaced in the KeySet shared with forked engines, from pooled
+// blocks: drain every stream of the device first (this engine's, its forks',
+// anyone's), so no kernel still reads the key being replaced and no pending
+// work still owns the block the pool hands out for the new one.
+namespace {
+void drain_before_key_load() { HIP_OK(hipDeviceSynchronize()); }
+}  // namespace
+
 void Engine::load_secret(const u64 *s) {
     auto &I = *impl;
+    drain_before_key_load();
     const size_t bytes = I.P.nall() * I.n() * 8;
     I.ks->s_ntt = I.alloc(bytes);
     HIP_OK(hipMemcpy(I.ks->s_ntt->p, s, bytes, hipMemcpyHostToDevice));
 }
 void Engine::load_public(const u64 *pk) {
     auto &I = *impl;
+    drain_before_key_load();
     const size_t bytes = 2 * I.P.nq() * I.n() * 8;
     I.ks->pk = I.alloc(bytes);
     HIP_OK(hipMemcpy(I.ks->pk->p, pk, bytes, hipMemcpyHostToDevice));
 }
 void Engine::load_relin(const u64 *key) {
     auto &I = *impl;
+    drain_before_key_load();
     const size_t bytes = (size_t)I.key_digits * 2 * I.P.nall() * I.n() * 8;
     I.ks->relin = I.alloc(bytes);
     HIP_OK(hipMemcpy(I.ks->relin->p, key, bytes, hipMemcpyHostToDevice));
 }
 void Engine::load_rotation(long k, const u64 *key) {
     auto &I = *impl;
+    drain_before_key_load();
     const size_t bytes = (size_t)I.key_digits * 2 * I.P.nall() * I.n() * 8;
     const u64 g = host::galois_for_rotation(I.P.logN, k);
     auto m = I.alloc(bytes);
@@ -636,6 +653,7 @@ void Engine::load_rotation(long k, const u64 *key) {
 }
 void Engine::load_galois(u64 g, const u64 *key) {
     auto &I = *impl;
+    drain_before_key_load();
     const size_t bytes = (size_t)I.key_digits * 2 * I.P.nall() * I.n() * 8;
     auto m = I.alloc(bytes);
     HIP_OK(hipMemcpy(m->p, key, bytes, hipMemcpyHostToDevice));
@@ -722,12 +740,12 @@ CtPtr Engine::encrypt_pt(const Plaintext &pt) {
     auto &I = *impl;
     if (!I.ks->pk) throw std::runtime_error("encrypt: no public key");
     const size_t n = I.n(), nq = I.P.nq(), ell = pt.limbs;
-    const u64 c = I.enc_counter++;
+    const u64 c = (*I.enc_counter)++;
     std::vector<int64_t> smp(3 * n);
     {
-        auto v = sample_coeffs(I.seed, host::tags::enc_v(c), n, true);
-        auto e0 = sample_coeffs(I.seed, host::tags::enc_e0(c), n, false);
-        auto e1 = sample_coeffs(I.seed, host::tags::enc_e1(c), n, false);
+        auto v = sample_coeffs(I.ent, host::tags::enc_v(c), n, true);
+        auto e0 = sample_coeffs(I.ent, host::tags::enc_e0(c), n, false);
+        auto e1 = sample_coeffs(I.ent, host::tags::enc_e1(c), n, false);
         std::copy(v.begin(), v.end(), smp.begin());
         std::copy(e0.begin(), e0.end(), smp.begin() + n);
         std::copy(e1.begin(), e1.end(), smp.begin() + 2 * n);

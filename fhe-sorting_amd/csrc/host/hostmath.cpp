@@ -1,6 +1,11 @@
 // Host-side precomputation for the MI355X RNS-CKKS engine (see hostmath.hpp).
 #include "hostmath.hpp"
 
+#include <sys/random.h>
+
+#include <cerrno>
+#include <cstring>
+
 #include <algorithm>
 #include <cmath>
 #include <complex>
@@ -349,22 +354,73 @@ u64 SplitMix64::next() {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
-u64 sample_uniform_mod(SplitMix64 &g, u64 q) {
-    const int bits = 64 - __builtin_clzll(q);
-    for (;;) {
-        const u64 r = g.next() >> (64 - bits);
-        if (r < q) return r;
+namespace {
+inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+inline void quarter(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+    a += b, d ^= a, d = rotl32(d, 16);
+    c += d, b ^= c, b = rotl32(b, 12);
+    a += b, d ^= a, d = rotl32(d, 8);
+    c += d, b ^= c, b = rotl32(b, 7);
+}
+}  // namespace
+
+void chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]) {
+    uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    for (int i = 0; i < 8; ++i) s[4 + i] = key[i];
+    s[12] = counter;
+    s[13] = nonce[0], s[14] = nonce[1], s[15] = nonce[2];
+    uint32_t x[16];
+    std::memcpy(x, s, sizeof x);
+    for (int r = 0; r < 10; ++r) {
+        quarter(x[0], x[4], x[8], x[12]);
+        quarter(x[1], x[5], x[9], x[13]);
+        quarter(x[2], x[6], x[10], x[14]);
+        quarter(x[3], x[7], x[11], x[15]);
+        quarter(x[0], x[5], x[10], x[15]);
+        quarter(x[1], x[6], x[11], x[12]);
+        quarter(x[2], x[7], x[8], x[13]);
+        quarter(x[3], x[4], x[9], x[14]);
     }
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + s[i];
 }
-int sample_ternary(SplitMix64 &g) {
-    const u64 r = g.next() % 3;
-    return r == 0 ? 0 : (r == 1 ? 1 : -1);
+ChaCha20::ChaCha20(const uint32_t k[8], u64 tag) {
+    std::memcpy(key, k, sizeof key);
+    nonce[0] = (uint32_t)tag, nonce[1] = (uint32_t)(tag >> 32), nonce[2] = 0x53454846u;  // "FHES"
 }
-int sample_cbd(SplitMix64 &g) {
-    const u64 m = (1ULL << 21) - 1;
-    const u64 a = g.next(), b = g.next();
-    return __builtin_popcountll(a & m) - __builtin_popcountll(b & m);
+u64 ChaCha20::next() {
+    if (pos >= 16) {
+        if (counter == 0xffffffffu) throw std::runtime_error("ChaCha20: stream exhausted");
+        chacha20_block(key, counter++, nonce, buf);
+        pos = 0;
+    }
+    const u64 r = (u64)buf[pos] | ((u64)buf[pos + 1] << 32);
+    pos += 2;
+    return r;
 }
+Entropy Entropy::from_seed(u64 seed) {
+    Entropy e;
+    if (seed) {
+        e.seed = seed;
+        return e;
+    }
+    e.secure = true;
+    uint32_t w[10];
+    size_t got = 0;
+    while (got < sizeof w) {
+        const ssize_t r = getrandom(reinterpret_cast<char *>(w) + got, sizeof w - got, 0);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            throw std::runtime_error("getrandom failed: cannot seed the key / encryption sampler");
+        }
+        got += (size_t)r;
+    }
+    std::memcpy(e.key, w, sizeof e.key);
+    e.seed_a = (u64)w[8] | ((u64)w[9] << 32);
+    std::memset(w, 0, sizeof w);
+    return e;
+}
+Prng::Prng(const Entropy &e, u64 tag, bool pub)
+    : use_cc(e.secure && !pub), sm(e.secure ? e.seed_a : e.seed, tag), cc(e.key, tag) {}
 
 // ---------------------------------------------------------- level tables --
 LevelTables make_level_tables(const Params &P) {

@@ -74,15 +74,62 @@ SConst scaled_const(double x);
 SConst const_to_target(double c, double delta_target, u64 q_dropped, double scale_in);
 SConst const_at_scale(double c, double scale);
 
-// seeded sampling
+// Sampling ("Sampling").  Two modes:
+//  * deterministic (a nonzero context seed; tests and the CPU oracle, which
+//    restates exactly these streams): SplitMix64 streams keyed by (seed, tag);
+//  * secure (seed 0, the default of the client and every deserialised
+//    context): the secret, every error and the encryption randomness come from
+//    ChaCha20 (RFC 8439 block function) under a 256-bit key drawn from the OS
+//    CSPRNG (getrandom), the stream's tag as nonce; the public uniform parts
+//    (pk a, switching-key a) from SplitMix64 under an independent random seed.
 struct SplitMix64 {
     u64 s;
     SplitMix64(u64 seed, u64 tag);
     u64 next();
 };
-u64 sample_uniform_mod(SplitMix64 &g, u64 q);
-int sample_ternary(SplitMix64 &g);
-int sample_cbd(SplitMix64 &g);
+// RFC 8439 §2.3 ChaCha20 block: 16 output words for (key, counter, nonce)
+void chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]);
+struct ChaCha20 {
+    uint32_t key[8], nonce[3], counter = 0, buf[16];
+    int pos = 16;
+    ChaCha20(const uint32_t k[8], u64 tag);
+    u64 next();
+};
+struct Entropy {
+    bool secure = false;
+    u64 seed = 0;    // deterministic streams
+    u64 seed_a = 0;  // secure mode: public uniform streams
+    uint32_t key[8] = {};
+    static Entropy from_seed(u64 seed);  // seed 0 -> secure (getrandom), else deterministic
+};
+// one sampling stream: `pub` marks the public uniform parts
+struct Prng {
+    Prng(const Entropy &e, u64 tag, bool pub = false);
+    u64 next() { return use_cc ? cc.next() : sm.next(); }
+    bool use_cc;
+    SplitMix64 sm;
+    ChaCha20 cc;
+};
+template <class G>
+u64 sample_uniform_mod(G &g, u64 q) {
+    const int bits = 64 - __builtin_clzll(q);
+    for (;;) {
+        const u64 r = g.next() >> (64 - bits);
+        if (r < q) return r;
+    }
+}
+template <class G>
+int sample_ternary(G &g) {
+    const u64 r = g.next() % 3;
+    return r == 0 ? 0 : (r == 1 ? 1 : -1);
+}
+// centred binomial, eta = 21
+template <class G>
+int sample_cbd(G &g) {
+    const u64 m = (1ULL << 21) - 1;
+    const u64 a = g.next(), b = g.next();
+    return __builtin_popcountll(a & m) - __builtin_popcountll(b & m);
+}
 namespace tags {
 constexpr u64 secret = 1, pk_a = 2, pk_e = 3;
 inline u64 swk_a(u64 kid, int j) { return 0x100000ULL + kid * 16 + 2 * (u64)j; }

@@ -3,6 +3,9 @@
 // ciphertext download / upload, one key (≤ a few hundred MB) at a time.
 #include "wire.hpp"
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -21,6 +24,7 @@ constexpr uint64_t P1 = 0x9e3779b185ebca87ull, P2 = 0xc2b2ae3d27d4eb4full;
 struct File {
     FILE *f = nullptr;
     std::string path;
+    File() = default;
     File(const std::string &p, const char *mode) : path(p) {
         f = std::fopen(p.c_str(), mode);
         if (!f) throw IoError("cannot open " + p + (mode[0] == 'w' ? " for writing" : " for reading"));
@@ -37,15 +41,36 @@ struct File {
     }
 };
 
+// Writes go to a temporary file beside the target (created with mode 0600 for
+// a secret key, 0644 otherwise, before the umask) that replaces the target by
+// rename() only once the whole object is written: a failed write never leaves
+// a truncated file in place of a good one.
 class Writer {
   public:
     Writer(const std::string &path, Kind kind, uint64_t pid, const host::Params &P, uint64_t body_words)
-        : file_(path, "wb") {
+        : target_(path) {
+        tmp_ = path + ".tmp." + std::to_string((long)getpid());
+        const int fd = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, kind == SecretKey ? 0600 : 0644);
+        if (fd < 0) throw IoError("cannot open " + path + " for writing");
+        file_.path = path;
+        file_.f = ::fdopen(fd, "wb");
+        if (!file_.f) {
+            ::close(fd);
+            ::unlink(tmp_.c_str());
+            throw IoError("cannot open " + path + " for writing");
+        }
         const uint64_t h[kHeaderWords] = {kMagic, (uint64_t)kVersion | ((uint64_t)kind << 32), pid, (uint64_t)P.logN,
                                           P.nq(), (uint64_t)P.K, body_words, 0};
         raw(h, 1);
         put(h + 1, kHeaderWords - 1);
         left_ = body_words;
+    }
+    ~Writer() {
+        if (!done_) {
+            if (file_.f) std::fclose(file_.f);
+            file_.f = nullptr;
+            ::unlink(tmp_.c_str());
+        }
     }
     void put(const uint64_t *w, size_t count) {
         sum_.update(w, count);
@@ -61,16 +86,21 @@ class Writer {
         if (left_) throw std::logic_error("wire: body shorter than declared");
         const uint64_t d = sum_.digest();
         raw(&d, 1);
+        if (std::fflush(file_.f) != 0 || ::fsync(::fileno(file_.f)) != 0) throw IoError("write error on " + target_);
         file_.close();
+        if (::rename(tmp_.c_str(), target_.c_str()) != 0) throw IoError("cannot replace " + target_);
+        done_ = true;
     }
 
   private:
     void raw(const uint64_t *w, size_t count) {
         if (std::fwrite(w, 8, count, file_.f) != count) throw IoError("write error on " + file_.path);
     }
+    std::string target_, tmp_;
     File file_;
     Checksum sum_;
     uint64_t left_ = 0;
+    bool done_ = false;
 };
 
 // opens a file, validates header and checksum (one streaming pass), then
@@ -226,8 +256,10 @@ Info inspect(const std::string &path) { return Reader(path).info; }
 void save_context(const Engine &e, const CtxParams &p, const std::string &path) {
     const auto &P = e.params();
     Writer w(path, Context, pid_of(e, p), P, 7 + P.nall());
+    // the seed word stays 0: a context file goes to the untrusted evaluator, and
+    // a deterministic seed would let it regenerate the secret key
     const uint64_t h[7] = {(uint64_t)p.log_n, (uint64_t)p.mult_depth, (uint64_t)p.scale_bits, (uint64_t)p.first_bits,
-                           (uint64_t)p.dnum, p.seed, (uint64_t)P.nall()};
+                           (uint64_t)p.dnum, 0, (uint64_t)P.nall()};
     w.body(h, 7);
     w.body(P.primes.data(), P.nall());
     w.finish();
@@ -242,7 +274,8 @@ CtxParams read_context(const std::string &path) {
     p.scale_bits = (int)r.word();
     p.first_bits = (int)r.word();
     p.dnum = (int)r.word();
-    p.seed = r.word();
+    (void)r.word();  // seed word: never taken from a file (a deserialised context samples from getrandom)
+    p.seed = 0;
     if (p.log_n != (int)r.info.log_n || (uint64_t)p.mult_depth + 1 != r.info.nq)
         throw IoError(path + ": context header and body disagree");
     // a context file drives allocations: refuse parameters no engine build uses

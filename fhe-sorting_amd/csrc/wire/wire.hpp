@@ -13,7 +13,9 @@
 //   body     body_words x u64 (layout per kind below)
 //   trailer  u64 checksum (wire::checksum over header words 1..7 and the body)
 //
-//   kind 1 context        log_n, mult_depth, scale_bits, first_bits, dnum, seed,
+//   kind 1 context        log_n, mult_depth, scale_bits, first_bits, dnum, 0 (the
+//                         seed word: always written 0 and ignored on read, a
+//                         context file never carries key-generation entropy),
 //                         nall, primes[nall]
 //   kind 2 public key     [2][nq][n]
 //   kind 3 eval-mult key  digits, [digits][2][nall][n]
@@ -48,7 +50,7 @@ struct IoError : std::runtime_error {
 
 struct CtxParams {
     int log_n = 0, mult_depth = 0, scale_bits = 0, first_bits = 0, dnum = 0;
-    uint64_t seed = 0;
+    uint64_t seed = 0;  // in memory only: never serialised (save_context writes 0)
 };
 
 struct Info {

@@ -168,6 +168,7 @@ _SIGS = {
     'fhe_set_sort_stack': (C.c_int, [vp, C.c_int]),
     'fhe_set_sort_lanes': (C.c_int, [vp, C.c_int]),
     'fhe_set_ps_split': (C.c_int, [vp, C.c_int]),
+    'fhe_prng_block': (C.c_int, [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     'fhe_get_ps_split': (C.c_int, [vp]),
     'fhe_cheb_ps_depth': (C.c_int, [C.c_int, C.c_int]),
     'fhe_pool_trim': (C.c_int, [vp]),
@@ -377,9 +378,12 @@ class Pt:
 
 
 class Context:
-    """One engine on one GPU (`device`)."""
+    """One engine on one GPU (`device`).  seed 0 (the default): the secret, the
+    errors and the encryption randomness come from the OS CSPRNG; a nonzero seed
+    makes keys and encryptions reproducible (tests, oracle parity) and must not
+    be used to protect data."""
 
-    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=1, device=0, keygen=True, _handle=None,
+    def __init__(self, logN, L, scale_bits=40, first_bits=60, dnum=3, seed=0, device=0, keygen=True, _handle=None,
                  ps_split=None):
         self.logN, self.n, self.L = logN, 1 << logN, L
         self._boots = []
@@ -770,6 +774,16 @@ class KernelClock:
             raise FheError(FHE_EINTERNAL, 'kernel clock report truncated')
         self.stats = json.loads(buf.value.decode())
         return False
+
+
+def prng_block(key, counter, nonce):
+    """ChaCha20 block of the secure sampler (fhe_prng_block), 16 u32 words"""
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    nn = np.ascontiguousarray(nonce, dtype=np.uint32)
+    out = np.zeros(16, dtype=np.uint32)
+    P32 = C.POINTER(C.c_uint32)
+    _chk(lib().fhe_prng_block(k.ctypes.data_as(P32), int(counter), nn.ctypes.data_as(P32), out.ctypes.data_as(P32)))
+    return out
 
 
 def cheb_ps_depth(degree, split=PS_SPLIT_OPENFHE):

@@ -50,10 +50,18 @@ typedef struct {
     int scale_bits;  /* SetScalingModSize */
     int first_bits;  /* first modulus size (OpenFHE default 60) */
     int dnum;        /* hybrid key-switching digits (OpenFHE default 3) */
-    uint64_t seed;   /* seeds key generation and encryption randomness */
+    uint64_t seed;   /* 0: the secret, every error and the encryption randomness are
+                        drawn from ChaCha20 keyed by the OS CSPRNG (getrandom) -- use
+                        this to protect data.  Nonzero: reproducible SplitMix64 streams
+                        keyed by the seed (tests, parity with the CPU oracle); anyone
+                        who knows the seed can regenerate the secret key.  The seed is
+                        never written to a file (fhe_serialize_context writes 0). */
 } fhe_params;
 
 const char *fhe_last_error(void);
+/* the secure sampler's block function (ChaCha20, RFC 8439 §2.3): 16 output
+ * words for (key, counter, nonce).  Host-only, for known-answer tests. */
+int fhe_prng_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]);
 
 /* ---------------------------------------------------------------- context */
 /* replaces GenCryptoContext(parameters) (tests/DirectSortTest.cpp:33) */
@@ -180,8 +188,13 @@ typedef int (*fhe_allreduce_fn)(uint64_t *dev_data, uint64_t count, void *user);
 /* DirectSort<N>(cc, pk, rots, enc).{sort | constructRank | rotationIndexCheckN}
  * (src/sort_algo.h:752-774 / 368-506 / 658-750); mode 0 sort, 1 rank, 2 index
  * check (then `rank` is the rank ciphertext).  Batches b with b % world == rank
- * run locally; partial ranks/outputs are summed with `allreduce` (or with the
- * RCCL communicator of fhe_comm_init when allreduce == NULL and world > 1). */
+ * run locally (1 <= shard_world, 0 <= shard_rank < shard_world, else
+ * FHE_EINVAL); partial ranks/outputs are summed with `allreduce` when given;
+ * else with the RCCL communicator of fhe_comm_init when shard_world equals its
+ * world (shard_rank must then be the communicator rank; a world-1 communicator
+ * runs its one-rank reduction through RCCL); else shard_world must be 1 and the
+ * sort is local -- so an unsharded sort (0, 1) still runs on a context that
+ * joined a larger communicator. */
 int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, const int32_t *rots, int nrot,
                     int n, int dg, int df, int mode, int shard_rank, int shard_world, fhe_allreduce_fn allreduce,
                     void *user, fhe_ct **out);

@@ -74,3 +74,14 @@ def test_binding_declares_every_entry_point():
     entry once segfaulted a GPU test)."""
     missing = [f for f in declared_symbols() if f not in F._SIGS]
     assert not missing, missing
+
+
+def test_secure_sampler_block_matches_rfc8439():
+    """The secure sampler (seed 0: secret, errors and encryption randomness) is
+    ChaCha20; its block function reproduces RFC 8439 §2.3.2's test vector."""
+    key = np.frombuffer(bytes(range(32)), dtype='<u4')
+    nonce = np.frombuffer(bytes.fromhex('000000090000004a00000000'), dtype='<u4')
+    want = bytes.fromhex('10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e'
+                         'd2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e')
+    assert F.prng_block(key, 1, nonce).astype('<u4').tobytes() == want
+

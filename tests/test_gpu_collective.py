@@ -121,3 +121,28 @@ def test_keys_loaded_after_a_sort_reach_every_lane():
         gout = gpu.direct_sort(gpu.from_oracle(ox), N, rots, (3, 3, 2))
         oout = orc.direct_sort(ox, N, rots, (3, 3, 2))
         assert np.array_equal(gout.data(), oout.data()), f'keys of seed {seed}: GPU differs from the oracle'
+
+
+@pytest.mark.parametrize('shard', [(0, 0), (2, 2), (-1, 2), (3, 2)])
+def test_bad_shard_arguments_are_refused(shard):
+    """1 <= shard_world and 0 <= shard_rank < shard_world are
+    checked before any work (shard_world 0 used to divide by zero in the batch
+    assignment), for the rank sort, the hybrid sort and MEHP24."""
+    ctx, rots = _ctx()
+    ct = ctx.encrypt(np.random.default_rng(4).permutation(N) / N, N)
+    hook = lambda p, n, u: None
+    with pytest.raises(F.FheError) as e:
+        ctx.direct_sort(ct, N, rots, (3, 3, 2), shard=shard, allreduce=hook)
+    assert e.value.code == F.FHE_EINVAL
+    ok = ctx.direct_sort(ct, N, rots, (3, 3, 2))  # the cached sorter is unharmed
+    assert np.max(np.abs(ctx.decrypt(ok)[:N] - np.sort(ctx.decrypt(ct)[:N]))) < 0.01
+
+
+def test_bootstrap_correction_bits_bounded():
+    """correction bits outside 1..40 are refused (70 used to
+    overflow the SlotsToCoeffs factor and hang setup); 0 selects the default 10."""
+    ctx = F.Context(11, 30, 59, 60, 3, seed=8)
+    for bits in (41, 70, -3):
+        with pytest.raises(F.FheError) as e:
+            F.Bootstrapper(ctx, 8, (2, 2), correction_bits=bits, keygen=False)
+        assert e.value.code == F.FHE_EINVAL

@@ -159,3 +159,47 @@ def test_cli_end_to_end_matches_oracle(tmp_path, N):
     # the client's decrypt reads the same file
     r = _run([sys.executable, CLIENT, 'decrypt', '--dir', str(d), '--n', str(N), '--input', out])
     assert np.abs(np.array([float(t) for t in r.stdout.split()]) - np.sort(v)).max() < 0.01
+
+
+def test_context_file_carries_no_key_entropy(tmp_path):
+    """the context file is handed to the untrusted evaluator.
+    It carries no seed, so a context deserialised from it and key-generated gets
+    unrelated keys and cannot decrypt the client's ciphertext; two encryptions of
+    one message under a deserialised (CSPRNG-seeded) context differ; a context
+    with seed 0 draws a fresh secret each time."""
+    ctx = F.Context(12, 6, 40, 60, 3)  # seed 0: getrandom-keyed ChaCha20 sampling
+    cc, pub = str(tmp_path / 'cc.bin'), str(tmp_path / 'pub.bin')
+    ctx.serialize(cc)
+    ctx.serialize_public_key(pub)
+    body = open(cc, 'rb').read()[64:]
+    assert int.from_bytes(body[40:48], 'little') == 0  # the seed word
+    v = np.linspace(-0.5, 0.5, 64)
+    client = F.Context.deserialize(cc)
+    client.deserialize_public_key(pub)
+    x1, x2 = client.encrypt(v, 64), client.encrypt(v, 64)
+    assert not np.array_equal(x1.data(), x2.data())
+    assert np.abs(ctx.decrypt(x1)[:64] - v).max() < 1e-5  # the owner decrypts
+    attacker = F.Context.deserialize(cc)  # the evaluator's view, then fresh key generation
+    attacker.keygen()
+    path = str(tmp_path / 'x.bin')
+    client.serialize_ciphertext(x1, path)
+    got = attacker.decrypt(attacker.deserialize_ciphertext(path))
+    assert np.abs(got[:64] - v).max() > 1.0
+    other = F.Context(12, 6, 40, 60, 3)
+    pk1, pk2 = str(tmp_path / 'pk1.bin'), str(tmp_path / 'pk2.bin')
+    ctx.serialize_public_key(pk1)
+    other.serialize_public_key(pk2)
+    assert open(pk1, 'rb').read()[64:] != open(pk2, 'rb').read()[64:]
+    for c in (ctx, client, attacker, other):
+        c.close()
+
+
+def test_secret_key_file_mode_and_atomic_replace(tmp_path):
+    """a secret key is written 0600 (before the umask) through a
+    temporary file renamed over the target, so no partial file replaces a good one."""
+    ctx = F.Context(12, 6, 40, 60, 3, seed=3)
+    sk = str(tmp_path / 'sk.bin')
+    ctx.serialize_secret_key(sk)
+    assert os.stat(sk).st_mode & 0o077 == 0
+    assert sorted(os.listdir(tmp_path)) == ['sk.bin']
+    ctx.close()
