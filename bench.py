@@ -600,14 +600,17 @@ def main():
 
     out = None
     cold_s = None
+    cold_parts = None
     for i in range(a.warmup):
         if i == 0:  # the first sort encodes every mask (the reference re-encodes them per sort)
             device_sync(ctx)
             d.barrier()
+            F.host_stats(reset=True)
             tc = time.perf_counter()
         out = ctx.direct_sort(ct, N, rots, cfg, shard=shard, allreduce=allreduce)
         if i == 0:
             device_sync(ctx)
+            cold_parts = F.host_stats(reset=True)
             d.barrier()
             cold_s = d.max(time.perf_counter() - tc)
     device_sync(ctx)
@@ -615,6 +618,7 @@ def main():
     ctx.reset_counters()
     device_sync(ctx)
     d.barrier()
+    F.host_stats(reset=True)
     t = time.perf_counter()
     for _ in range(a.steps):
         out = ctx.direct_sort(ct, N, rots, cfg, shard=shard, allreduce=allreduce)
@@ -622,6 +626,7 @@ def main():
     d.barrier()
     dt = time.perf_counter() - t
     dt = d.max(dt)
+    warm_parts = F.host_stats(reset=True)
     cnt = ctx.counters()
     peak_gb = ctx.pool_stats()['peak'] / 1e9
     ctx.pool_trim()  # ranks idle at the final barrier hold no cache while rank 0 measures
@@ -665,6 +670,10 @@ def main():
             # (src/sort_algo.h:341-342, 714-716 pay these on every sort) and the
             # allocation pool's first growth; null without a warmup step
             'cold_sort_s': round(cold_s, 4) if cold_s is not None else None,
+            # rank 0's host costs inside the cold sort (mask / checking-vector
+            # encodes, pool-miss hipMallocs) and inside the timed sorts (none)
+            'cold_breakdown': cold_parts,
+            'timed_host_costs': warm_parts,
             'hbm_peak_gb_rank0': round(peak_gb, 1),
         }
         res['roofline'] = None

@@ -1052,16 +1052,22 @@ std::vector<CtPtr> DirectSortN::run_lanes(const std::vector<int> &batches, F &&w
 }
 
 // kind 0: mask_vector(k) rotated by `r` (vector_rotate); kind 1: checking vector(k)
+// Encoded outside the lock, so concurrent lanes encode their masks in parallel;
+// a mask two lanes race for is encoded twice (identical words) and the first
+// published copy is kept.
 const Plaintext &DirectSortN::mask(Engine &E, int kind, int num_slots, int k, int r, int level) {
     auto key = std::make_tuple(kind, num_slots, k, r, level);
-    std::lock_guard<std::mutex> lk(mask_mu);
-    auto it = mask_cache.find(key);
-    if (it != mask_cache.end()) return *it->second;
+    {
+        std::lock_guard<std::mutex> lk(mask_mu);
+        auto it = mask_cache.find(key);
+        if (it != mask_cache.end()) return *it->second;
+    }
     std::vector<double> v = kind == 0 ? vector_rotate(mask_vector(num_slots, N, k), r) : checking_vector(num_slots, N, k);
     PtPtr p = E.encode(v, num_slots, level);
     E.sync();  // complete before another lane's stream reads it
-    mask_cache[key] = p;
-    return *p;
+    std::lock_guard<std::mutex> lk(mask_mu);
+    auto ins = mask_cache.emplace(key, p);
+    return *ins.first->second;
 }
 
 void checkShardWorld(const host::Params &P, int world) {

@@ -871,6 +871,23 @@ int fhe_ct_allreduce(fhe_ctx *ctx, fhe_ct *ct) {
 int fhe_ntt(fhe_ctx *ctx, uint64_t *h, int prime_index, int limbs, int inverse) {
     return guard([&] { ctx->eng->ntt_host(h, prime_index, limbs, inverse != 0); });
 }
+int fhe_ntt_dev(fhe_ctx *ctx, uint64_t *dev_limbs, int first_prime, int nlimbs, int segments, uint64_t seg_stride,
+                int inverse, void *stream) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(dev_limbs);
+        ctx->eng->ntt_dev(dev_limbs, first_prime, nlimbs, segments, (size_t)seg_stride, inverse != 0, stream);
+    });
+}
+int fhe_automorph_dev(fhe_ctx *ctx, const uint64_t *dev_in, int limbs, uint64_t galois, uint64_t *dev_out,
+                      void *stream) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(dev_in);
+        NEED(dev_out);
+        ctx->eng->automorph_dev(dev_in, dev_out, (size_t)limbs, galois, stream);
+    });
+}
 int fhe_modup(fhe_ctx *ctx, const uint64_t *d, int ell, uint64_t *ext) {
     return guard([&] { ctx->eng->modup_host(d, (size_t)ell, ext); });
 }
@@ -904,6 +921,15 @@ int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double
     });
 }
 
+int fhe_host_stats(double out[4]) {
+    return guard([&] {
+        NEED(out);
+        Engine::host_stats_get(out);
+    });
+}
+int fhe_host_stats_reset(void) {
+    return guard([&] { Engine::host_stats_reset(); });
+}
 int fhe_pool_trim(fhe_ctx *ctx) {
     return guard([&] { ctx->eng->pool_trim(); });
 }

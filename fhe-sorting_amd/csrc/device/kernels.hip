@@ -9,6 +9,15 @@
 //     coefficient in registers and emit a chunk of target limbs per thread;
 //     every constant multiply is a Shoup multiply with a precomputed
 //     companion.
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <ucontext.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
 #include "kernels.hpp"
 
 #include <cstdlib>
@@ -784,6 +793,7 @@ void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, in
 void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,
                 hipStream_t st) {
     if (limbs <= 0 || segs <= 0) return;
+    note_launch("k_permute", pt_grid(logN, limbs, segs), dim3(NT));
     hipLaunchKernelGGL(k_permute, pt_grid(logN, limbs, segs), dim3(NT), 0, st, out, in, perm, S, logN);
 }
 void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap, const Mod *mods, int logN,
@@ -942,5 +952,135 @@ void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, i
     launch_clocked("k_moddown_finish", B, k_moddown_finish, ew_grid(logN, ell, segs), dim3(NT), st, out, acc, conv, add,
                    seg_out, seg_acc, seg_add, pinv, pinv_s, mods, logN);
 }
+
+// ------------------------------------------------------- fault diagnostics --
+namespace {
+struct LaunchNote {
+    std::atomic<unsigned long long> count{0};
+    const char *volatile name = nullptr;
+    volatile unsigned g[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+};
+LaunchNote g_note;
+struct sigaction g_prev_segv, g_prev_bus;
+
+// async-signal-safe output helpers
+void out_str(const char *s) {
+    size_t n = 0;
+    while (s[n]) ++n;
+    ssize_t r = ::write(2, s, n);
+    (void)r;
+}
+void out_hex(unsigned long long v) {
+    char b[19] = "0x";
+    for (int i = 0; i < 16; ++i) b[2 + i] = "0123456789abcdef"[(v >> (60 - 4 * i)) & 15];
+    b[18] = 0;
+    out_str(b);
+}
+void out_dec(unsigned long long v) {
+    char b[24];
+    int i = 23;
+    b[i] = 0;
+    do {
+        b[--i] = (char)('0' + v % 10);
+        v /= 10;
+    } while (v && i > 0);
+    out_str(b + i);
+}
+unsigned long long parse_hex(const char *&p) {
+    unsigned long long v = 0;
+    for (;; ++p) {
+        const char c = *p;
+        if (c >= '0' && c <= '9') v = v * 16 + (unsigned)(c - '0');
+        else if (c >= 'a' && c <= 'f') v = v * 16 + (unsigned)(c - 'a' + 10);
+        else break;
+    }
+    return v;
+}
+// print the /proc/self/maps lines whose range holds one of the addresses
+void out_maps(unsigned long long a, unsigned long long b) {
+    const int fd = ::open("/proc/self/maps", O_RDONLY);
+    if (fd < 0) return;
+    static char buf[1 << 16];
+    static char line[1024];
+    size_t ll = 0;
+    for (;;) {
+        const ssize_t r = ::read(fd, buf, sizeof buf);
+        if (r <= 0) break;
+        for (ssize_t i = 0; i < r; ++i) {
+            const char c = buf[i];
+            if (ll + 1 < sizeof line) line[ll++] = c;
+            if (c != '\n') continue;
+            line[ll] = 0;
+            const char *p = line;
+            const unsigned long long lo = parse_hex(p);
+            if (*p == '-') ++p;
+            const unsigned long long hi = parse_hex(p);
+            if ((a >= lo && a < hi) || (b >= lo && b < hi) || (b >= hi && b - hi < (1ull << 21)) ||
+                (b < lo && lo - b < (1ull << 21))) {
+                out_str("  maps: ");
+                out_str(line);
+            }
+            ll = 0;
+        }
+    }
+    ::close(fd);
+}
+void on_fault(int sig, siginfo_t *si, void *ucv) {
+    const auto *uc = static_cast<ucontext_t *>(ucv);
+    const unsigned long long pc = uc ? (unsigned long long)uc->uc_mcontext.gregs[REG_RIP] : 0;
+    const unsigned long long addr = (unsigned long long)si->si_addr;
+    out_str(sig == SIGBUS ? "\n[fhe fault report] SIGBUS" : "\n[fhe fault report] SIGSEGV");
+    out_str(" si_code ");
+    out_dec((unsigned long long)(si->si_code < 0 ? -si->si_code : si->si_code));
+    out_str(si->si_code <= 0 ? " (sent by a process)" : "");
+    out_str(" pc ");
+    out_hex(pc);
+    out_str(" addr ");
+    out_hex(addr);
+    out_str(" tid ");
+    out_dec((unsigned long long)::syscall(SYS_gettid));
+    out_str(" pid ");
+    out_dec((unsigned long long)::getpid());
+    out_str("\n  launches noted: ");
+    out_dec(g_note.count.load());
+    out_str(", last: ");
+    out_str(g_note.name ? g_note.name : "(none)");
+    out_str(" grid ");
+    out_dec(g_note.g[0]), out_str("x"), out_dec(g_note.g[1]), out_str("x"), out_dec(g_note.g[2]);
+    out_str(" block ");
+    out_dec(g_note.b[0]);
+    out_str("\n");
+    out_maps(pc, addr);
+    // chain: the previous handler runs when the faulting instruction re-executes
+    // (or now, for a signal another thread or process sent)
+    sigaction(sig, sig == SIGBUS ? &g_prev_bus : &g_prev_segv, nullptr);
+    if (si->si_code <= 0) raise(sig);
+}
+}  // namespace
+
+bool fault_report_enabled() {
+    static const bool on = std::getenv("FHE_FAULT_REPORT") != nullptr;
+    return on;
+}
+void note_launch_slow(const char *name, dim3 grid, dim3 block) {
+    g_note.count++;
+    g_note.name = name;
+    g_note.g[0] = grid.x, g_note.g[1] = grid.y, g_note.g[2] = grid.z;
+    g_note.b[0] = block.x, g_note.b[1] = block.y, g_note.b[2] = block.z;
+}
+void install_fault_report() {
+    if (!fault_report_enabled()) return;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        struct sigaction sa {};
+        sa.sa_sigaction = on_fault;
+        sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+        sigemptyset(&sa.sa_mask);
+        sigaction(SIGSEGV, &sa, &g_prev_segv);
+        sigaction(SIGBUS, &sa, &g_prev_bus);
+        out_str("[fhe fault report] handler installed\n");
+    });
+}
+
 }  // namespace dev
 }  // namespace fhe

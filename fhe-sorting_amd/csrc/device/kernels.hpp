@@ -39,6 +39,19 @@ LaunchClock *&launch_clock();
 // caller tag appended to clocked NTT names ("k_ntt_fwd<8, 4, true>@modup"); per thread
 const char *&launch_phase();
 
+// Fault diagnostics (environment FHE_FAULT_REPORT=1): every launch notes its
+// kernel and grid in a process-global record, and install_fault_report() (the
+// engine calls it once) adds a SIGSEGV / SIGBUS handler that prints the faulting
+// PC and address, the thread, the launch count, the last launch and the
+// /proc/self/maps lines holding the PC and the address, then chains to the
+// previous handler (a profiler's, or the default).  Off: one predictable branch.
+bool fault_report_enabled();
+void note_launch_slow(const char *name, dim3 grid, dim3 block);
+inline void note_launch(const char *name, dim3 grid, dim3 block) {
+    if (fault_report_enabled()) note_launch_slow(name, grid, block);
+}
+void install_fault_report();
+
 // Launch through hipExtLaunchKernelGGL; when a clock is installed the launch is
 // timed by events recorded at the kernel's own start/end and booked under
 // `name` with its algorithmic HBM bytes.
@@ -48,6 +61,7 @@ inline void launch_clocked(const char *name, double bytes, Kern kernel, dim3 gri
     LaunchClock *clk = launch_clock();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const int slot = clk ? clk->events(e0, e1) : -1;
+    note_launch(name, grid, block);
     hipExtLaunchKernelGGL(kernel, grid, block, 0, st, e0, e1, 0, args...);
     if (clk) clk->record(slot, name, bytes);
 }

@@ -715,6 +715,8 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     LaunchClock *clk = launch_clock();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const int slot = clk ? clk->events(e0, e1) : -1;
+    note_launch(FWD ? (COLS ? "k_ntt_fwd(col)" : "k_ntt_fwd(row)") : (COLS ? "k_ntt_inv(col)" : "k_ntt_inv(row)"), grid,
+                dim3(NTB));
 #define FHE_NTT_LAUNCH(K, FF) \
     hipExtLaunchKernelGGL((K), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
     if (FWD && sh) {

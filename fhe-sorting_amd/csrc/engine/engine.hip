@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -31,6 +32,22 @@ using dev::Mod;
 // Every engine (and every fork: concurrent sort lanes) owns a pool; an
 // allocation that fails first releases the cached blocks of all pools of the
 // process, so one lane's cache never starves another lane or a later phase.
+// process-wide host-side cost counters (cold-start breakdown, fhe_host_stats):
+// host encodes (special FFT + rounding + upload + NTT, until the plaintext is
+// complete) and device allocations that missed the pool's cache
+struct HostStats {
+    std::atomic<u64> encode_ns{0}, encodes{0}, malloc_ns{0}, mallocs{0};
+};
+HostStats &host_stats() {
+    static HostStats h;
+    return h;
+}
+u64 now_ns() {
+    return (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
 struct Pool;
 std::mutex &pool_registry_mu() {
     static std::mutex m;
@@ -82,11 +99,14 @@ struct Pool {
             }
         }
         void *p = nullptr;
+        const u64 t0 = now_ns();
         hipError_t e = hipMalloc(&p, bytes);
         if (e != hipSuccess) {
             trim_all_pools();
             HIP_OK(hipMalloc(&p, bytes));
         }
+        host_stats().malloc_ns += now_ns() - t0;
+        host_stats().mallocs++;
         std::lock_guard<std::mutex> lk(mu);
         live += bytes;
         peak = std::max(peak, live);
@@ -152,6 +172,7 @@ struct Engine::Impl {
     Mod *mods = nullptr;
     dev::NttTables T{};
     int *extmap = nullptr;   // [nq+1][nq+K]
+    int *iota = nullptr;     // [nall]: 0, 1, 2, ... (prime maps of consecutive primes)
     u64 *modup_tab = nullptr;  // packed ModUp tables
     u64 *phinv = nullptr, *phinv_s = nullptr, *phat = nullptr, *pinv = nullptr, *pinv_s = nullptr;
     u64 *qlinv = nullptr, *qlinv_s = nullptr;
@@ -351,6 +372,7 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.device = device;
     I.seed = seed;
     I.ent = host::Entropy::from_seed(seed);
+    dev::install_fault_report();  // FHE_FAULT_REPORT=1 only
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&I.st, hipStreamNonBlocking));
     I.pool = std::make_shared<Pool>();
@@ -406,6 +428,11 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.T.mods = I.mods;
     I.T.logN = logN;
     I.extmap = I.upload_static(I.LT.extmap);
+    {
+        std::vector<int> io(I.P.nall());
+        for (size_t i = 0; i < io.size(); ++i) io[i] = (int)i;
+        I.iota = I.upload_static(io);
+    }
     I.modup_tab = I.upload_static(I.LT.modup);
     I.phinv = I.upload_static(I.LT.phinv);
     I.phinv_s = I.upload_static(I.LT.phinv_s);
@@ -700,6 +727,7 @@ PtPtr Engine::encode(const std::vector<double> &v, int slots, int level) {
 }
 PtPtr Engine::encode_scaled(const std::vector<double> &v, int slots, int level, double scale) {
     auto &I = *impl;
+    const u64 t0 = now_ns();
     const size_t n = I.n(), ell = I.P.limbs_at(level);
     auto coef = host::encode_coeffs(v, n, slots, scale);
     auto cm = I.alloc(n * 8);
@@ -714,7 +742,22 @@ PtPtr Engine::encode_scaled(const std::vector<double> &v, int slots, int level, 
     dev::ew_signed_to_rns(pt->data, static_cast<int64_t *>(cm->p), (int)ell, nullptr, I.mods, I.P.logN, I.st);
     dev::ntt_forward(pt->data, (int)ell, 1, 0, nullptr, I.T, I.st);
     HIP_OK(hipStreamSynchronize(I.st));  // `coef` (pageable host) must outlive the copy
+    host_stats().encode_ns += now_ns() - t0;
+    host_stats().encodes++;
     return pt;
+}
+
+void Engine::host_stats_get(double out[4]) {
+    out[0] = (double)host_stats().encodes.load();
+    out[1] = (double)host_stats().encode_ns.load() * 1e-9;
+    out[2] = (double)host_stats().mallocs.load();
+    out[3] = (double)host_stats().malloc_ns.load() * 1e-9;
+}
+void Engine::host_stats_reset() {
+    host_stats().encodes = 0;
+    host_stats().encode_ns = 0;
+    host_stats().mallocs = 0;
+    host_stats().malloc_ns = 0;
 }
 
 PtPtr Engine::encode_complex(const std::vector<std::complex<double>> &v, int slots, int level, double scale) {
@@ -1453,6 +1496,28 @@ void Engine::moddown_host(const u64 *in, size_t ell, u64 *out) {
                         I.pinv_s, MODS, LOGN, ST);
     HIP_OK(hipMemcpyAsync(out, om->p, ell * nn * 8, hipMemcpyDeviceToHost, ST));
     HIP_OK(hipStreamSynchronize(ST));
+}
+void Engine::ntt_dev(u64 *data, int prime_index, int limbs, int segments, size_t seg_stride, bool inverse,
+                     void *stream) {
+    auto &I = *impl;
+    if (prime_index < 0 || limbs < 1 || segments < 1 || (size_t)(prime_index + limbs) > I.P.nall())
+        throw std::invalid_argument("ntt_dev: primes [prime_index, prime_index + limbs) outside the context");
+    if (segments > 1 && seg_stride < (size_t)limbs * n())
+        throw std::invalid_argument("ntt_dev: segment stride shorter than a segment");
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ST;
+    const int *pm = prime_index == 0 ? nullptr : I.iota + prime_index;
+    if (inverse)
+        dev::ntt_inverse(data, limbs, segments, seg_stride, pm, I.T, st);
+    else
+        dev::ntt_forward(data, limbs, segments, seg_stride, pm, I.T, st);
+}
+void Engine::automorph_dev(const u64 *in, u64 *out, size_t limbs, u64 g, void *stream) {
+    auto &I = *impl;
+    if (g % 2 == 0 || g >= 2 * (u64)n()) throw std::invalid_argument("automorph_dev: galois element must be odd and < 2n");
+    if (limbs < 1 || limbs > I.P.nall()) throw std::invalid_argument("automorph_dev: bad limb count");
+    const uint32_t *pm = I.perm(g);  // built and uploaded on the engine stream, which perm() drains
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ST;
+    dev::ew_permute(out, in, pm, (int)limbs, 1, dev::Seg{0, 0, 0}, LOGN, st);
 }
 void Engine::automorph_host(const u64 *in, size_t limbs, u64 g, u64 *out) {
     auto &I = *impl;

@@ -196,6 +196,12 @@ class Engine {
     void modup_host(const u64 *d, size_t ell, u64 *ext);          // ext [digits][ell+K][n] NTT
     void moddown_host(const u64 *in, size_t ell, u64 *out);        // in [ell+K][n] -> [ell][n]
     void automorph_host(const u64 *in, size_t limbs, u64 g, u64 *out);
+    // device-resident variants: enqueued on `stream` (nullptr:
+    // the engine stream), no host synchronisation.  ntt_dev transforms `limbs`
+    // consecutive-prime limbs of `segments` polynomials in place (segment s at
+    // data + s * seg_stride); automorph_dev writes in[...] o X -> X^g (NTT form).
+    void ntt_dev(u64 *data, int prime_index, int limbs, int segments, size_t seg_stride, bool inverse, void *stream);
+    void automorph_dev(const u64 *in, u64 *out, size_t limbs, u64 g, void *stream);
     // time `iters` back-to-back launches of one kernel on the engine stream
     // (HIP events), shaped like a key switch at `limbs` Q limbs; returns the
     // average ms per launch and the algorithmic HBM bytes per launch.
@@ -204,6 +210,10 @@ class Engine {
     // pass is bracketed by HIP events on the engine stream; stop() returns JSON
     // {"kernel": {"launches": c, "ms": total, "bytes": total_algorithmic}, ...}
     // device pool: release cached blocks; bytes live / cached / peak live
+    // process-wide host costs: {encodes, encode seconds, pool-miss hipMallocs,
+    // hipMalloc seconds} (the cold-sort breakdown)
+    static void host_stats_get(double out[4]);
+    static void host_stats_reset();
     void pool_trim();
     void pool_stats(size_t &live, size_t &cached, size_t &peak) const;
     void kernel_clock_start();

@@ -242,16 +242,21 @@ void bit_reverse(std::vector<cd> &v) {
     }
 }
 // inverse special FFT: slot values -> (real, imag) coefficient halves
+// (lq is a power of two: rot % lq is rot & (lq - 1); the twiddle of butterfly j
+// of a stage is the same for every block i, so it is looked up once per stage.
+// The floating-point operations and their order are unchanged, so the encoder
+// stays bit-identical to the oracle's.)
 void special_ifft(std::vector<cd> &v, const Emb &E, size_t n) {
     const size_t S = v.size(), M = 2 * n;
+    std::vector<cd> tw(S / 2 + 1);
     for (size_t len = S; len >= 1; len >>= 1) {
+        const size_t h = len >> 1, lq = len << 2, gap = M / lq;
+        for (size_t j = 0; j < h; ++j) tw[j] = E.ksi[(lq - (E.rot[j] & (lq - 1))) * gap];
         for (size_t i = 0; i < S; i += len) {
-            const size_t h = len >> 1, lq = len << 2, gap = M / lq;
             for (size_t j = 0; j < h; ++j) {
-                const size_t idx = (lq - (E.rot[j] % lq)) * gap;
                 cd u = v[i + j] + v[i + j + h];
                 cd w = v[i + j] - v[i + j + h];
-                w *= E.ksi[idx];
+                w *= tw[j];
                 v[i + j] = u;
                 v[i + j + h] = w;
             }
@@ -263,14 +268,15 @@ void special_ifft(std::vector<cd> &v, const Emb &E, size_t n) {
 void special_fft(std::vector<cd> &v, const Emb &E, size_t n) {
     const size_t S = v.size(), M = 2 * n;
     bit_reverse(v);
+    std::vector<cd> tw(S / 2 + 1);
     for (size_t len = 2; len <= S; len <<= 1) {
+        const size_t h = len >> 1, lq = len << 2, gap = M / lq;
+        for (size_t j = 0; j < h; ++j) tw[j] = E.ksi[(E.rot[j] & (lq - 1)) * gap];
         for (size_t i = 0; i < S; i += len) {
-            const size_t h = len >> 1, lq = len << 2, gap = M / lq;
             for (size_t j = 0; j < h; ++j) {
-                const size_t idx = (E.rot[j] % lq) * gap;
                 cd u = v[i + j];
                 cd w = v[i + j + h];
-                w *= E.ksi[idx];
+                w *= tw[j];
                 v[i + j] = u + w;
                 v[i + j + h] = u - w;
             }

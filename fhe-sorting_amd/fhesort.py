@@ -168,6 +168,10 @@ _SIGS = {
     'fhe_set_sort_stack': (C.c_int, [vp, C.c_int]),
     'fhe_set_sort_lanes': (C.c_int, [vp, C.c_int]),
     'fhe_set_ps_split': (C.c_int, [vp, C.c_int]),
+    'fhe_ntt_dev': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]),
+    'fhe_automorph_dev': (C.c_int, [vp, vp, C.c_int, C.c_uint64, vp, vp]),
+    'fhe_host_stats': (C.c_int, [dp]),
+    'fhe_host_stats_reset': (C.c_int, []),
     'fhe_prng_block': (C.c_int, [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     'fhe_get_ps_split': (C.c_int, [vp]),
     'fhe_cheb_ps_depth': (C.c_int, [C.c_int, C.c_int]),
@@ -711,6 +715,16 @@ class Context:
         _chk(lib().fhe_ntt(self.h, _u64(d), prime_index, limbs, 1 if inverse else 0))
         return d
 
+    def ntt_dev(self, dev_ptr, first_prime, limbs, inverse=False, segments=1, seg_stride=0, stream=None):
+        """fhe_ntt_dev: in place on device memory, enqueued on `stream` (hipStream_t
+        as an int, None = the context stream); returns without synchronising"""
+        _chk(lib().fhe_ntt_dev(self.h, C.c_void_p(dev_ptr), first_prime, limbs, segments, seg_stride,
+                               1 if inverse else 0, C.c_void_p(stream) if stream else None))
+
+    def automorph_dev(self, dev_in, limbs, galois, dev_out, stream=None):
+        _chk(lib().fhe_automorph_dev(self.h, C.c_void_p(dev_in), limbs, galois, C.c_void_p(dev_out),
+                                     C.c_void_p(stream) if stream else None))
+
     def modup(self, d):
         d = np.ascontiguousarray(d, dtype=np.uint64)
         ell = d.shape[0]
@@ -774,6 +788,16 @@ class KernelClock:
             raise FheError(FHE_EINTERNAL, 'kernel clock report truncated')
         self.stats = json.loads(buf.value.decode())
         return False
+
+
+def host_stats(reset=False):
+    """process-wide host costs (fhe_host_stats): encodes, encode s, pool-miss mallocs, malloc s"""
+    out = np.zeros(4)
+    _chk(lib().fhe_host_stats(_dbl(out)))
+    if reset:
+        _chk(lib().fhe_host_stats_reset())
+    return {'encodes': int(out[0]), 'encode_s': round(float(out[1]), 4), 'mallocs': int(out[2]),
+            'malloc_s': round(float(out[3]), 4)}
 
 
 def prng_block(key, counter, nonce):

@@ -367,6 +367,18 @@ int fhe_ntt(fhe_ctx *ctx, uint64_t *host, int prime_index, int limbs, int invers
 int fhe_modup(fhe_ctx *ctx, const uint64_t *d, int ell, uint64_t *ext);
 int fhe_moddown(fhe_ctx *ctx, const uint64_t *in, int ell, uint64_t *out);
 int fhe_automorph(fhe_ctx *ctx, const uint64_t *in, int limbs, uint64_t galois, uint64_t *out);
+/* Device-memory variants (SURVEY §8(b) fhe_ntt_fwd/inv, fhe_automorph): the
+ * limbs are device pointers, the work is enqueued on `stream` (a hipStream_t;
+ * NULL = the context stream) and the call returns without synchronising.
+ * fhe_ntt_dev transforms, in place, `nlimbs` limbs over the consecutive primes
+ * first_prime.. of `segments` polynomials (polynomial s at dev_limbs + s *
+ * seg_stride words; layout [limb][n], NTT order as fhe_ntt).  The ring's
+ * twiddle tables are the context's; the caller keeps the buffers alive until
+ * the stream has run the work. */
+int fhe_ntt_dev(fhe_ctx *ctx, uint64_t *dev_limbs, int first_prime, int nlimbs, int segments, uint64_t seg_stride,
+                int inverse, void *stream);
+int fhe_automorph_dev(fhe_ctx *ctx, const uint64_t *dev_in, int limbs, uint64_t galois, uint64_t *dev_out,
+                      void *stream);
 /* op counters: hmult, keyswitch, rotations, rescale, ptmult, constmult, and
  * the op-level algorithmic HBM bytes of SURVEY §8(d) (HMult, rotation, ct x pt,
  * ct x const, add, linear sum formulas, each op at its own level) */
@@ -382,6 +394,11 @@ int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double
 /* device memory pool of the context: release cached blocks to HIP; bytes in
  * use, cached, and the peak in use since creation */
 int fhe_pool_trim(fhe_ctx *ctx);
+/* process-wide host costs since the last reset: out = {plaintext encodes, seconds
+ * in them (host special FFT, rounding, upload, NTT), device allocations that
+ * missed the pools' caches, seconds in hipMalloc} -- the cold-sort breakdown */
+int fhe_host_stats(double out[4]);
+int fhe_host_stats_reset(void);
 int fhe_pool_stats(fhe_ctx *ctx, uint64_t *live, uint64_t *cached, uint64_t *peak);
 /* live kernel clock over real work: after start, every NTT pass launched by
  * this process is bracketed by HIP events on its stream; stop writes JSON

@@ -66,6 +66,73 @@ def test_ntt_batched_limbs():
         assert np.array_equal(g[i], orc.ntt(i, x[i]))
 
 
+class _Hip:
+    """device buffers and a stream through the HIP runtime the engine loaded
+    (libamdhip64; torch's own HIP runtime cannot share this process)"""
+
+    def __init__(self):
+        import ctypes as C
+        self.C = C
+        self.h = C.CDLL('libamdhip64.so')
+        self.h.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+        self.h.hipFree.argtypes = [C.c_void_p]
+        self.h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        self.h.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+        self.h.hipStreamSynchronize.argtypes = [C.c_void_p]
+        self.h.hipStreamDestroy.argtypes = [C.c_void_p]
+
+    def upload(self, a):
+        p = self.C.c_void_p()
+        assert self.h.hipMalloc(self.C.byref(p), a.nbytes) == 0
+        assert self.h.hipMemcpy(p, a.ctypes.data, a.nbytes, 1) == 0
+        return p.value
+
+    def download(self, p, like):
+        out = np.empty_like(like)
+        assert self.h.hipMemcpy(out.ctypes.data, self.C.c_void_p(p), out.nbytes, 2) == 0
+        return out
+
+    def stream(self):
+        s = self.C.c_void_p()
+        assert self.h.hipStreamCreate(self.C.byref(s)) == 0
+        return s.value
+
+
+@pytest.mark.parametrize('logN', [12, 16])
+def test_ntt_and_automorph_on_device_memory(logN):
+    """fhe_ntt_dev / fhe_automorph_dev: limbs in device memory,
+    primes 1..4 of 2 segments, on a caller's stream and on the context stream,
+    no host round trip -- the same words as the oracle's NTT; the inverse
+    restores the input; an automorphism equals the index permutation."""
+    orc = O.Context(logN, 5, 40, 60, 3, seed=1, keygen=False)
+    gpu = F.Context(logN, 5, 40, 60, 3, seed=1, keygen=False)
+    hip = _Hip()
+    n, first, limbs, segs = gpu.n, 1, 4, 2
+    rng = np.random.default_rng(logN)
+    x = np.stack([np.stack([rng.integers(0, int(gpu.primes[first + i]), size=n, dtype=np.uint64)
+                            for i in range(limbs)]) for _ in range(segs)])  # [seg][limb][n]
+    want = np.stack([np.stack([orc.ntt(first + i, x[s_, i]) for i in range(limbs)]) for s_ in range(segs)])
+    dev = hip.upload(x)
+    st = hip.stream()
+    gpu.ntt_dev(dev, first, limbs, segments=segs, seg_stride=limbs * n, stream=st)
+    assert hip.h.hipStreamSynchronize(hip.C.c_void_p(st)) == 0
+    assert np.array_equal(hip.download(dev, x), want)
+    gpu.ntt_dev(dev, first, limbs, inverse=True, segments=segs, seg_stride=limbs * n)  # context stream
+    gpu.sync()
+    assert np.array_equal(hip.download(dev, x), x)
+    g = O.galois(logN, 3)
+    src = hip.upload(np.ascontiguousarray(want[0]))
+    dst = hip.upload(np.zeros_like(want[0]))
+    gpu.automorph_dev(src, limbs, g, dst, stream=st)
+    assert hip.h.hipStreamSynchronize(hip.C.c_void_p(st)) == 0
+    assert np.array_equal(hip.download(dst, want[0]), want[0][:, O.automorph_perm(logN, g)])
+    with pytest.raises(F.FheError):
+        gpu.ntt_dev(dev, gpu.nq + gpu.K - 1, 2)  # one prime beyond the context's
+    for p in (dev, src, dst):
+        hip.h.hipFree(hip.C.c_void_p(p))
+    hip.h.hipStreamDestroy(hip.C.c_void_p(st))
+
+
 def test_encrypt_decrypt_and_upload(pair):
     orc, gpu = pair
     x = np.linspace(-1, 1, 16)
