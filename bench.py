@@ -43,6 +43,8 @@ sys.path.insert(0, os.path.join(REPO, 'fhe-sorting_amd'))
 import fhesort as F  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+N_SIMD = 256 * 4        # 256 CUs x 4 SIMDs
+F_CLK = 2.4e9           # peak engine clock (the effective clock under load is lower: valu_frac is a lower bound)
 
 
 def parse():
@@ -241,7 +243,56 @@ def pmc_lookup(table, name):
     return {'launches': n, 'hbm_bytes_per_launch': sum(v['hbm_bytes_per_launch'] * v['launches'] for v in hits) / n}
 
 
-def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json'):
+def valu_fraction(name, avg_s, sq_file, mix_file='valu_mix.json'):
+    """The compute roof of the dominant kernel: the share of the chip's measured
+    VALU throughput its launches use.  valu_frac = SQ_INSTS_VALU per launch (the
+    committed SQ pass of the same workload, profiles/pmc_sq*.json,
+    scripts/pmc_sq_summary.py) x 64 lanes x the seconds one lane-instruction of
+    the kernel's instruction mix costs at the measured MI355X rates
+    (profiles/valu_mix.json, scripts/valu_mix.py: full-rate 67.5 T, half-rate
+    36 T, v_mad_u64_u32 23 T, carry/compare pairs 39 T lane-instructions/s) /
+    the live average launch duration.  Near 1: VALU-bound (the HBM fraction
+    cannot rise without fewer instructions).  Instantiations booked under one
+    clock name are launch-weighted."""
+    sq_path = os.path.join(REPO, 'profiles', sq_file)
+    mix_path = os.path.join(REPO, 'profiles', mix_file)
+    if not (os.path.exists(sq_path) and os.path.exists(mix_path)):
+        return {}
+    with open(sq_path) as f:
+        sq = json.load(f)
+    with open(mix_path) as f:
+        mix = json.load(f)
+    base = name.split('@')[0]
+    keys = [k for k in sq if k == base or k.split('<')[0] == base]
+    keys = [k for k in keys if k in mix and 'SQ_INSTS_VALU' in sq[k]]
+    if not keys:
+        return {}
+    n = sum(sq[k]['launches'] for k in keys)
+    valu_s = sum(sq[k]['launches'] * sq[k]['SQ_INSTS_VALU'] * 64 * mix[k]['ps_per_lane_instr'] * 1e-12
+                 for k in keys) / n
+    insts = sum(sq[k]['launches'] * sq[k]['SQ_INSTS_VALU'] for k in keys) / n
+    wc = sum(sq[k]['launches'] * sq[k].get('SQ_WAVE_CYCLES', 0) for k in keys) / n or 1
+    wait = sum(sq[k]['launches'] * sq[k].get('SQ_WAIT_ANY', 0) for k in keys) / n
+    stall = sum(sq[k]['launches'] * sq[k].get('SQ_WAIT_INST_ANY', 0) for k in keys) / n
+    return {'valu_frac': round(valu_s / avg_s, 4), 'valu_insts_per_launch': round(insts),
+            'valu_seconds_per_launch': valu_s, 'valu_source': f'profiles/{sq_file} + profiles/{mix_file}',
+            'wave_cycle_split': {'waitcnt': round(wait / wc, 3), 'issue_stall': round(stall / wc, 3)}}
+
+
+def pmc_lookup_all(table, name):
+    """like pmc_lookup, averaging every field over instantiations (launch-weighted)"""
+    base = name.split('@')[0]
+    if base in table:
+        return table[base]
+    hits = [v for k, v in table.items() if k.split('<')[0] == base]
+    if not hits:
+        return None
+    n = sum(v['launches'] for v in hits)
+    keys = set().union(*[v.keys() for v in hits]) - {'launches'}
+    return {'launches': n, **{k: sum(v.get(k, 0) * v['launches'] for v in hits) / n for k in keys}}
+
+
+def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc_sq.json'):
     """Roofline of the dominant kernel, measured live: one more (untimed) sort
     runs with every hot kernel launched through hipExtLaunchKernelGGL with
     start/stop events on the engine stream (the stream it runs on), one lane so
@@ -291,6 +342,7 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json'):
     return {'kernel': name, 'bound': 'hbm', 'limiter': limiter, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_source': src,
+            **valu_fraction(name, avg_s, sq_file),
             'avg_us': round(avg_s * 1e6, 2), 'launches': st['launches'],
             'algorithmic_bytes_per_launch': per_launch, 'clocked_ms_per_sort': round(total_ms, 1),
             'kernels': table(by_sym.items()), 'kernels_by_caller': table(stats.items()),
@@ -435,7 +487,7 @@ def run_mehp24(a, d):
         if not a.no_roofline and d.world == 1:
             try:
                 ctx.pool_trim()
-                res['roofline'] = with_run(roofline(ctx, run, a.clock_json, 'pmc_traffic_mehp24.json'),
+                res['roofline'] = with_run(roofline(ctx, run, a.clock_json, 'pmc_traffic_mehp24.json', 'pmc_sq_mehp24.json'),
                                            res['ms_per_step'], 1, op_total / a.steps)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
@@ -556,7 +608,7 @@ def run_kway(a, d):
         if not a.no_roofline:
             try:
                 ctx.set_sort_lanes(1)  # the live clock needs one stream
-                res['roofline'] = with_run(roofline(ctx, run, a.clock_json, 'pmc_traffic_kway.json'),
+                res['roofline'] = with_run(roofline(ctx, run, a.clock_json, 'pmc_traffic_kway.json', 'pmc_sq_kway.json'),
                                            res['ms_per_step'], 1, op_total / a.steps / d.world)
                 ctx.set_sort_lanes(a.lanes)
             except Exception as e:  # never hide the main number
