@@ -32,8 +32,25 @@ namespace dev {
 namespace {
 
 constexpr int NT = 256;     // threads per block
-constexpr int TCH = 64;     // target limbs per thread in basis conversions (all of them: the
-                            // per-coefficient prologue then runs once)
+// Basis conversions give each thread one coefficient and a chunk of target
+// limbs: all of them (the per-coefficient prologue -- loading and scaling the
+// source residues -- then runs once) unless the launch is too narrow to fill the
+// chip (a single ciphertext at ring 2^16: n / NT x digits = 768 blocks, 3 waves
+// per SIMD, each looping over ~40 targets), then the targets are chunked so the
+// grid has >= 3072 blocks (12 per CU), >= 4 targets per chunk.  The outputs are
+// independent, so the words do not depend on the chunking.
+inline int conv_chunk(int logN, int targets, int zdim) {
+    static const int force = [] {
+        const char *e = std::getenv("FHE_CONV_CHUNK");  // A/B: a fixed chunk (0 = adaptive)
+        return e ? std::atoi(e) : 0;
+    }();
+    if (targets < 1) return 1;
+    if (force > 0) return force;
+    const size_t base = (((size_t)1 << logN) + NT - 1) / NT * (size_t)std::max(zdim, 1);
+    if (targets <= 4 || base >= 3072) return targets;
+    const int chunks = (int)((3072 + base - 1) / base);
+    return std::max(4, (targets + chunks - 1) / chunks);
+}
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
@@ -351,14 +368,14 @@ struct ModUpArgs {
     size_t coef_stride, ext_stride;
 };
 
-// grid: x = n / NT, y = target chunks of TCH, z = member * digits + digit.
+// grid: x = n / NT, y = target chunks of tch (conv_chunk), z = member * digits + digit.
 // coef: member m at m * A.coef_stride ([ell][n], coefficient form);
 // ext: member m at m * A.ext_stride ([digits][W][n]).  AT = alpha (digit
 // size): the source loop is straight-line; a shorter last digit reads a
 // clamped limb times a zero constant.
 template <int AT>
 __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, const u64 *__restrict__ coef, int W, int ell, ModUpArgs A,
-                                                      const int *pmap_ext, const Mod *mods, int logN) {
+                                                      const int *pmap_ext, const Mod *mods, int logN, int tch) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
@@ -367,7 +384,7 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
     coef += mb * A.coef_stride;
     ext += mb * A.ext_stride;
     const int lo = A.lo[j], hi = A.hi[j];
-    const int t0 = blockIdx.y * TCH;
+    const int t0 = blockIdx.y * tch;
     Split30 y[AT];
 #pragma unroll
     for (int i = 0; i < AT; ++i) {
@@ -375,7 +392,7 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
         y[i] = split30(mul_shoup(coef[(size_t)src * n + k], A.qhinv[j][i], A.qhinv_s[j][i], mods[src].q));
     }
     const u64 *qh = A.qhat[j];
-    for (int t = t0; t < t0 + TCH && t < W; ++t) {
+    for (int t = t0; t < t0 + tch && t < W; ++t) {
         if (t >= lo && t < hi) continue;
         const Mod mt = mods[pmap_ext[t]];
         Acc4 acc;  // lazy: one reduction per output
@@ -534,7 +551,7 @@ __global__ __launch_bounds__(NT) void k_permute_mk(u64 *out, const u64 *in, KsKe
     out[(size_t)blockIdx.z * S.o + ln + k] = in[(size_t)blockIdx.z * S.a + ln + perm[k]];
 }
 
-// grid: x = n / NT, y = ceil(ell / TCH), z = segment.  KT = K special primes;
+// grid: x = n / NT, y = ceil(ell / tch), z = segment.  KT = K special primes;
 // phat [nq][KT] (the constants of one target contiguous: one scalar burst)
 // Exact centred conversion: y_k = [x P_k^-1]_{p_k}, x mod P = sum_k y_k P_k -
 // v P with v = round(sum_k y_k / p_k) (fp64, fixed order; oracle: moddown), so
@@ -552,7 +569,7 @@ template <int KT>
 __global__ __launch_bounds__(NT) void k_moddown_convert(u64 *__restrict__ conv, const u64 *__restrict__ pc, int ell, int nq, size_t seg_in,
                                                         size_t seg_out, const u64 *phinv, const u64 *phinv_s,
                                                         const u64 *phat, const u64 *pmod, const double *pinvd,
-                                                        const Mod *mods, int logN) {
+                                                        const Mod *mods, int logN, int tch) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
@@ -566,8 +583,8 @@ __global__ __launch_bounds__(NT) void k_moddown_convert(u64 *__restrict__ conv, 
         v[i] = split30(y[i]);
     }
     const Split30 cnt = split30(centre_count<KT>(y, pinvd));
-    const int i0 = blockIdx.y * TCH;
-    for (int i = i0; i < i0 + TCH && i < ell; ++i) {
+    const int i0 = blockIdx.y * tch;
+    for (int i = i0; i < i0 + tch && i < ell; ++i) {
         Acc4 acc;
 #pragma unroll
         for (int kk = 0; kk < KT; ++kk) mac4(acc, v[kk], split30(phat[(size_t)i * KT + kk]));
@@ -607,14 +624,14 @@ __global__ __launch_bounds__(NT) void k_moddown_finish(u64 *out, const u64 *acc,
 // d_last P + acc_last) and the K special limbs already inverse-transformed.
 // corr_i = Conv_{P->q_i}(acc_P) + P * [y_last]_centred  for i < ell-1, where
 // y_last = (x_last - Conv_{P->q_last}(acc_P)) * P^-1 mod q_last is the last
-// limb of the ModDown output.  grid: x = n / NT, y = ceil((ell-1) / TCH), z = seg
+// limb of the ModDown output.  grid: x = n / NT, y = ceil((ell-1) / tch), z = seg
 template <int KT>
 __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict__ corr, const u64 *__restrict__ acc, int ell, int nq,
                                                                 size_t seg_acc, size_t seg_corr, const u64 *phinv,
                                                                 const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                                                                 const u64 *pinv_s, const u64 *pmod, const double *pinvd,
                                                                 const u64 *ninv, const u64 *ninv_s, const Mod *mods,
-                                                                int logN) {
+                                                                int logN, int tch) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
@@ -642,8 +659,8 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict_
     const u64 xl = mul_shoup(src[k], ninv[last], ninv_s[last], ql);
     const u64 y = mul_shoup(sub_mod(xl, cl, ql), pinv[last], pinv_s[last], ql);
     const bool neg = y > (ql >> 1);
-    const int i0 = blockIdx.y * TCH;
-    for (int i = i0; i < i0 + TCH && i < last; ++i) {
+    const int i0 = blockIdx.y * tch;
+    for (int i = i0; i < i0 + tch && i < last; ++i) {
         const Mod mi = mods[i];
         // centred lift of y: q_last / 2 < q_i (checked at context creation)
         const u64 lift = neg ? mi.q - (ql - y) : y;
@@ -853,8 +870,9 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
         const double B = 8.0 * members * (double)((size_t)nd * W) * (double)n;  // sources in + targets out
         dispatch_int<1, 16>(at, [&](auto c) {
             constexpr int AT = decltype(c)::value;
-            launch_clocked("k_modup_convert", B, k_modup_convert<AT>, pt_grid(logN, (W + TCH - 1) / TCH, nd * members),
-                           dim3(NT), st, ext0, coef, W, ell, Ar, pmap_ext, mods, logN);
+            const int tch = conv_chunk(logN, W, nd * members);
+            launch_clocked("k_modup_convert", B, k_modup_convert<AT>, pt_grid(logN, (W + tch - 1) / tch, nd * members),
+                           dim3(NT), st, ext0, coef, W, ell, Ar, pmap_ext, mods, logN, tch);
         });
     };
     if (full > 0) {
@@ -929,9 +947,10 @@ void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, 
     const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
     dispatch_int<1, 15>(K, [&](auto c) {
         constexpr int KT = decltype(c)::value;
+        const int tch = conv_chunk(logN, ell - 1, segs);
         launch_clocked("k_moddown_rescale_convert", B, k_moddown_rescale_convert<KT>,
-                       pt_grid(logN, (ell - 1 + TCH - 1) / TCH, segs), dim3(NT), st, corr, acc, ell, nq, seg_acc,
-                       seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, pinvd, ninv, ninv_s, mods, logN);
+                       pt_grid(logN, (ell - 1 + tch - 1) / tch, segs), dim3(NT), st, corr, acc, ell, nq, seg_acc,
+                       seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, pinvd, ninv, ninv_s, mods, logN, tch);
     });
 }
 void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t seg_in, size_t seg_out, int segs,
@@ -940,9 +959,10 @@ void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t se
     const double B = 8.0 * segs * (double)(K + ell) * ((size_t)1 << logN);
     dispatch_int<1, 15>(K, [&](auto c) {
         constexpr int KT = decltype(c)::value;
-        launch_clocked("k_moddown_convert", B, k_moddown_convert<KT>, pt_grid(logN, (ell + TCH - 1) / TCH, segs),
+        const int tch = conv_chunk(logN, ell, segs);
+        launch_clocked("k_moddown_convert", B, k_moddown_convert<KT>, pt_grid(logN, (ell + tch - 1) / tch, segs),
                        dim3(NT), st, conv, pc, ell, nq, seg_in, seg_out, phinv, phinv_s, phat, pmod, pinvd, mods,
-                       logN);
+                       logN, tch);
     });
 }
 void moddown_finish(u64 *out, const u64 *acc, const u64 *conv, const u64 *add, int ell, int segs, size_t seg_out,
