@@ -70,6 +70,7 @@ def parse():
     ap.add_argument('--no-roofline', action='store_true', help='skip the instrumented roofline sort (PMC passes)')
     ap.add_argument('--cpu-sample-mults', type=int, default=0, help='override CPU sample size')
     ap.add_argument('--clock-json', default=None, help='write the full per-kernel clock of the roofline sort here')
+    ap.add_argument('--dnum', type=int, default=0, help='MEHP24: key-switch digits (0: the parameter table, OpenFHE default 3)')
     ap.add_argument('--lanes', type=int, default=3, help='concurrent batch lanes (forked engines) per GPU (3: 885 vs 898 ms for 2)')
     ap.add_argument('--stack', type=int, default=32, help='max batches stacked into one ciphertext batch')
     ap.add_argument('--rendezvous-check', action='store_true',
@@ -417,6 +418,8 @@ def run_mehp24(a, d):
     compares and P^2 indicators are sharded over ranks (strong scaling)."""
     N = a.n_sort or 4096
     p = F.mehp24_parameters(N)
+    if a.dnum:
+        p['dnum'] = a.dnum
     t0 = time.time()
     ctx = F.Context(p['log_ring'], p['depth'] + 1, p['scale_bits'], 60, p['dnum'], seed=a.seed, device=d.device)
     ctx.gen_rotation_keys(p['rots'])

@@ -1744,7 +1744,9 @@ Parameters parameters(size_t N) {
     Parameters p;
     p.multDepth = it->second;
     p.levels = p.multDepth + 1;  // + the FLEXIBLEAUTOEXT encryption level (Engine::encrypt_ext)
-    p.dnum = std::max(3, (p.levels + 1 + 14) / 15);  // digits of <= 15 primes (engine limit: alpha <= 16)
+    // OpenFHE's default for depth > 3 (the reference sets no digit count): 3 digits of
+    // <= 22 primes, within the engine's alpha <= 24 / K <= 16 (the 4096 table: K = 16)
+    p.dnum = std::max(3, (p.levels + 1 + 22) / 23);
     p.logRingDim = 17;
     p.scaleModSize = 40;
     p.cfg = SignConfig(CompositeSignConfig(3, N <= 16 ? 2 : N <= 128 ? 3 : N <= 512 ? 4 : 5, 2));

@@ -396,9 +396,14 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
         if (t >= lo && t < hi) continue;
         const Mod mt = mods[pmap_ext[t]];
         Acc4 acc;  // lazy: one reduction per output
+        Acc128 r;
 #pragma unroll
-        for (int i = 0; i < AT; ++i) mac4(acc, y[i], split30(qh[(size_t)t * A.qstride + i]));
-        ext[((size_t)j * W + t) * n + k] = reduce4(acc, mt);
+        for (int i = 0; i < AT; ++i) {
+            mac4(acc, y[i], split30(qh[(size_t)t * A.qstride + i]));
+            spill4<AT>(r, acc, i);
+        }
+        fold4(r, acc);
+        ext[((size_t)j * W + t) * n + k] = reduce128(r, mt);
     }
 }
 
@@ -586,10 +591,15 @@ __global__ __launch_bounds__(NT) void k_moddown_convert(u64 *__restrict__ conv, 
     const int i0 = blockIdx.y * tch;
     for (int i = i0; i < i0 + tch && i < ell; ++i) {
         Acc4 acc;
+        Acc128 r;
 #pragma unroll
-        for (int kk = 0; kk < KT; ++kk) mac4(acc, v[kk], split30(phat[(size_t)i * KT + kk]));
+        for (int kk = 0; kk < KT; ++kk) {
+            mac4(acc, v[kk], split30(phat[(size_t)i * KT + kk]));
+            spill4<KT + 1>(r, acc, kk);
+        }
         mac4(acc, cnt, split30(mods[i].q - pmod[i]));  // - v P
-        dst[(size_t)i * n + k] = reduce4(acc, mods[i]);
+        fold4(r, acc);
+        dst[(size_t)i * n + k] = reduce128(r, mods[i]);
     }
 }
 
@@ -650,10 +660,15 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict_
     const Mod ml = mods[last];
     const u64 ql = ml.q;
     Acc4 cacc;
+    Acc128 cr;
 #pragma unroll
-    for (int kk = 0; kk < KT; ++kk) mac4(cacc, v[kk], split30(phat[(size_t)last * KT + kk]));
+    for (int kk = 0; kk < KT; ++kk) {
+        mac4(cacc, v[kk], split30(phat[(size_t)last * KT + kk]));
+        spill4<KT + 1>(cr, cacc, kk);
+    }
     mac4(cacc, cnt, split30(ql - pmod[last]));
-    const u64 cl = reduce4(cacc, ml);
+    fold4(cr, cacc);
+    const u64 cl = reduce128(cr, ml);
     // the limbs arrive from an unscaled inverse NTT (n x, in [0, 2q)): phinv
     // carries n^-1 for the special limbs, x_last takes it here
     const u64 xl = mul_shoup(src[k], ninv[last], ninv_s[last], ql);
@@ -664,13 +679,18 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict_
         const Mod mi = mods[i];
         // centred lift of y: q_last / 2 < q_i (checked at context creation)
         const u64 lift = neg ? mi.q - (ql - y) : y;
-        // P (lift - v): one term, so K + 1 terms stay within Acc4's 16
+        // P (lift - v): one term, K + 1 in all
         const u64 lv = lift >= cntv ? lift - cntv : lift + mi.q - cntv;
         Acc4 a4;
+        Acc128 r;
         mac4(a4, split30(lv), split30(pmod[i]));
 #pragma unroll
-        for (int kk = 0; kk < KT; ++kk) mac4(a4, v[kk], split30(phat[(size_t)i * KT + kk]));
-        dst[(size_t)i * n + k] = reduce4(a4, mi);
+        for (int kk = 0; kk < KT; ++kk) {
+            mac4(a4, v[kk], split30(phat[(size_t)i * KT + kk]));
+            spill4<KT + 1>(r, a4, kk + 1);
+        }
+        fold4(r, a4);
+        dst[(size_t)i * n + k] = reduce128(r, mi);
     }
 }
 inline dim3 ew_grid(int logN, int limbs, int segs) {
@@ -868,7 +888,7 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
     const size_t n = (size_t)1 << logN;
     auto launch = [&](int nd, int at, const ModUpArgs &Ar, u64 *ext0) {
         const double B = 8.0 * members * (double)((size_t)nd * W) * (double)n;  // sources in + targets out
-        dispatch_int<1, 16>(at, [&](auto c) {
+        dispatch_int<1, 24>(at, [&](auto c) {
             constexpr int AT = decltype(c)::value;
             const int tch = conv_chunk(logN, W, nd * members);
             launch_clocked("k_modup_convert", B, k_modup_convert<AT>, pt_grid(logN, (W + tch - 1) / tch, nd * members),
@@ -945,7 +965,7 @@ void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, 
                              const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st) {
     if (ell <= 1) return;
     const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
-    dispatch_int<1, 15>(K, [&](auto c) {
+    dispatch_int<1, 16>(K, [&](auto c) {
         constexpr int KT = decltype(c)::value;
         const int tch = conv_chunk(logN, ell - 1, segs);
         launch_clocked("k_moddown_rescale_convert", B, k_moddown_rescale_convert<KT>,
@@ -957,7 +977,7 @@ void moddown_convert(u64 *conv, const u64 *pc, int ell, int K, int nq, size_t se
                      const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pmod, const double *pinvd,
                      const Mod *mods, int logN, hipStream_t st) {
     const double B = 8.0 * segs * (double)(K + ell) * ((size_t)1 << logN);
-    dispatch_int<1, 15>(K, [&](auto c) {
+    dispatch_int<1, 16>(K, [&](auto c) {
         constexpr int KT = decltype(c)::value;
         const int tch = conv_chunk(logN, ell, segs);
         launch_clocked("k_moddown_convert", B, k_moddown_convert<KT>, pt_grid(logN, (ell + tch - 1) / tch, segs),

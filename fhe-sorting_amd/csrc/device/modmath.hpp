@@ -119,6 +119,15 @@ __device__ __forceinline__ void fold4(Acc128 &r, const Acc4 &s) {
     r.lo += tl;
     r.hi += (s.s11 >> 4) + (r.lo < tl);
 }
+// a sum longer than Acc4's 16 terms: after term i (0-based) of T, fold every
+// full group of 16 into the exact 128-bit total (compiled out for T <= 16)
+template <int T>
+__device__ __forceinline__ void spill4(Acc128 &r, Acc4 &s, int i) {
+    if (T > 16 && i % 16 == 15 && i + 1 < T) {
+        fold4(r, s);
+        s = Acc4{};
+    }
+}
 // s00 + (s01 + s10) 2^30 + s11 2^60 mod q
 __device__ __forceinline__ u64 reduce4(const Acc4 &s, const Mod &m) {
     Acc128 r;

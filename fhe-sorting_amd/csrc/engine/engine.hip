@@ -383,8 +383,8 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     // registers and accumulate 30-bit-split products of residues < 2^60
     for (u64 q : I.P.primes)
         if (q >> 60) throw std::invalid_argument("engine: every prime must be < 2^60 (first_bits <= 60)");
-    if (I.P.alpha > 16 || I.P.K > 15)
-        throw std::invalid_argument("engine: digit size <= 16 and special primes <= 15 required (raise dnum)");
+    if (I.P.alpha > 24 || I.P.K > 16)
+        throw std::invalid_argument("engine: digit size <= 24 and special primes <= 16 required (raise dnum)");
     // rescales lift the last limb with a compare-select: every prime that can be
     // rescaled away (q_1..q_L) must satisfy q_l / 2 < q_i for all Q primes
     {

@@ -244,7 +244,7 @@ int fhe_hybrid_parameters(int N, int *mult_depth, int32_t *rots, int max_rots);
 /* ------------------------------------------------------------ MEHP24 sort */
 /* the reference's MEHP24 test parameters for N (tests/mehp24/Mehp24SortTest.cpp:26-128)
  * and mehp24::utils::getRotationIndices(N) (src/mehp24/mehp24_utils.cpp:197-225):
- * depth, ring log, scale bits, key-switch digits (dnum: digits of <= 15 primes),
+ * depth, ring log, scale bits, key-switch digits (dnum: 3, OpenFHE's default),
  * CompositeSign (n, dg, df), indicator (dg_i, df_i), part length (0: one-ciphertext
  * sortFG).  The context gets mult_depth + 1 levels and the input is encrypted with
  * fhe_encrypt_ext (OpenFHE's default FLEXIBLEAUTOEXT).  Returns #rotations. */

@@ -17,7 +17,7 @@ else:  # beyond the reference table: same Cfg / dg_i rule, depth from argv
 if len(sys.argv) > 2:
     p['depth'] = int(sys.argv[2])
 levels = p['depth'] + 1
-dnum = max(3, (levels + 1 + 14) // 15)
+dnum = p['dnum']
 t0 = time.time()
 ctx = F.Context(p['log_ring'], levels, p['scale_bits'], 60, dnum, seed=N)
 ctx.gen_rotation_keys(p['rots'])

@@ -491,6 +491,42 @@ def test_ring_2_17_ops_match_oracle():
     assert np.max(np.abs(gpu.decrypt(r) - np.roll(x, 32768))) < 1e-5
 
 
+@pytest.mark.parametrize('L,alpha,K', [(65, 22, 16), (61, 21, 15), (50, 17, 12)])
+def test_wide_digits_match_oracle(L, alpha, K):
+    """OpenFHE's default 3 digits at the MEHP24 depths (src/mehp24 leaves the digit
+    count unset): digits of 17-22 primes and up to 16 special primes, past Acc4's
+    16-term sums (ModUp alpha terms, ModDown K + 1) -- ModUp / ModDown at full and
+    partial digits, relinearised products down the chain, rotations, hoisted
+    rotations, all word-identical to the oracle."""
+    rots = [1, -3, 7]
+    orc = O.Context(12, L, 40, 60, 3, seed=L)
+    orc.gen_rotation_keys(rots)
+    gpu = F.Context(12, L, 40, 60, 3, seed=L, keygen=False)
+    gpu.load_keys_from(orc, rots)
+    assert (orc.alpha, orc.K) == (alpha, K) and np.array_equal(orc.primes, gpu.primes)
+    rng = np.random.default_rng(L)
+    for ell in (L + 1, 2 * alpha, 2 * alpha - 5, alpha + 1, alpha, 7):
+        d = np.stack([rng.integers(0, int(q), size=orc.n, dtype=np.uint64) for q in orc.primes[:ell]])
+        assert np.array_equal(orc.modup(d), gpu.modup(d)), f'modup differs at ell={ell}'
+        x = np.stack([rng.integers(0, int(q), size=orc.n, dtype=np.uint64)
+                      for q in list(orc.primes[:ell]) + list(orc.primes[orc.nq:])])
+        assert np.array_equal(orc.moddown(x), gpu.moddown(x)), f'moddown differs at ell={ell}'
+    a, b = rng.uniform(-1, 1, 16), rng.uniform(-1, 1, 16)
+    oa, ob = orc.encrypt(a, 16), orc.encrypt(b, 16)
+    ga, gb = gpu.from_oracle(oa), gpu.from_oracle(ob)
+    oc, gc = oa, ga
+    for i in range(L - 2):  # every level: each digit count, full and partial last digits
+        oc, gc = orc.mul(oc, ob), gpu.mul(gc, gb)
+        if i % 9 == 0:
+            same(gc, oc)
+            for k in rots:
+                same(gpu.rotate(gc, k), orc.rotate(oc, k))
+    same(gc, oc)
+    for h, k in zip(gpu.rotate_hoisted(ga, rots), rots):
+        same(h, orc.rotate(oa, k))
+    assert np.max(np.abs(gpu.decrypt(gpu.mul(ga, gb)) - a * b)) < 1e-6
+
+
 def test_config2_direct_sort_full_size_bit_exact():
     """BASELINE config 2 at its full size: DirectSort N=128 at ring 2^16, depth 30,
     the reference's 40-bit scaling primes, 30 rotation keys, CompositeSign(3,3,2)
