@@ -103,6 +103,8 @@ void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int s
 void ntt_forward_rescale(u64 *tmp, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
 // HMult tail: out = (x + d * c2 - NTT(corr)) * c1 (corr is overwritten by the first pass only)
 void ntt_forward_multail(u64 *corr, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
+// key-switch ModDown finish: out = (x - NTT(conv)) * c1 + d (d on even segments, member z / 2)
+void ntt_forward_ksfinish(u64 *conv, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st);
 // one row pass (forward: the second pass; inverse: the first) alone, for kernel timing
 void ntt_row_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st,
                   bool forward);

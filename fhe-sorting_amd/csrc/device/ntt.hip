@@ -304,9 +304,12 @@ int &row_shfl_enabled() {
 // of one coefficient-form limb (`last`, prime lastp) instead of `data`
 // (rescale: the lifted limb is never materialised per prime); 2 row pass
 // stores out = (x - NTT) * c1 (rescale finish); 3 row pass stores
-// out = (x + d * c2 - NTT) * c1 (fused ModDown+rescale finish of an HMult).
-// Modes 2/3 do not write `data` back.
-enum { NTT_PLAIN = 0, NTT_LIFT = 1, NTT_RESCALE = 2, NTT_MULTAIL = 3 };
+// out = (x + d * c2 - NTT) * c1 (fused ModDown+rescale finish of an HMult);
+// 4 row pass stores out = (x - NTT) * c1 + d (the ModDown finish of a key
+// switch: x the accumulators, c1 = P^-1, d the permuted c0 added to the even
+// segments, member z / 2 at (z / 2) * seg_d, or none).
+// Modes 2-4 do not write `data` back.
+enum { NTT_PLAIN = 0, NTT_LIFT = 1, NTT_RESCALE = 2, NTT_MULTAIL = 3, NTT_KSFINISH = 4 };
 
 // COLS: the transform index is a column `col`, element idx sits at idx * 2^k2 + col.
 // ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
@@ -378,8 +381,11 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // accumulators and d) are loaded now, so the loads overlap the butterflies
     // instead of stalling the store loop (the tile's LDS bounds occupancy, the
     // extra VGPRs do not)
-    constexpr bool EPI_X = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL);
-    constexpr bool EPI_D = !COLS && MODE == NTT_MULTAIL;
+    constexpr bool EPI_X = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL || MODE == NTT_KSFINISH);
+    constexpr bool EPI_D = !COLS && (MODE == NTT_MULTAIL || MODE == NTT_KSFINISH);
+    // key-switch finish: only c0 segments (even z) take the added polynomial
+    const bool has_d = MODE == NTT_KSFINISH ? (F.d != nullptr && !(zseg & 1)) : true;
+    const size_t d_base = MODE == NTT_KSFINISH ? (size_t)(zseg >> 1) * F.seg_d : (size_t)zseg * F.seg_d;
     u64 ex[EPI_X ? E : 1], ed[EPI_D ? E : 1];
     if (EPI_X) {
         const size_t lo = (size_t)limb * n + tid_global * LEN;
@@ -387,11 +393,11 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
         for (int r = 0; r < E; ++r) {
             const int idx = SH ? row_final_index<true>(t, r) : t + T * r;  // where the pass leaves element r
             ex[r] = valid ? F.x[(size_t)zseg * F.seg_x + lo + idx] : 0;
-            if (EPI_D) ed[EPI_D ? r : 0] = valid ? F.d[(size_t)zseg * F.seg_d + lo + idx] : 0;
+            if (EPI_D) ed[EPI_D ? r : 0] = valid && has_d ? F.d[d_base + lo + idx] : 0;
         }
     }
     // per-limb epilogue constants (fused row-pass modes)
-    const bool EPI = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL);
+    const bool EPI = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL || MODE == NTT_KSFINISH);
     const Mod mp = Tb.mods[p];
     const u64 c1 = EPI ? F.c1[limb] : 0, c1s = EPI ? F.c1s[limb] : 0;
     const u64 c2 = MODE == NTT_MULTAIL ? F.c2[limb] : 0, c2s = MODE == NTT_MULTAIL ? F.c2s[limb] : 0;
@@ -417,6 +423,11 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
             const u64 dd = EPI_D ? ed[EPI_D ? r : 0] : F.d[z * F.seg_d + lo + idx];
             const u64 tt = acc + shoup_fold(dd, c2, c2s, nq) + 3 * q4 - v;
             const u64 o = shoup_fold(tt, c1, c1s, nq);
+            F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
+        } else if (MODE == NTT_KSFINISH) {  // (acc - v) P^-1 + d, acc + 12q - v < 13q
+            const u64 acc = ex[EPI_X ? r : 0];
+            u64 o = shoup_fold(acc + 3 * q4 - v, c1, c1s, nq);
+            o = (o >= q ? o - q : o) + ed[EPI_D ? r : 0];  // d = 0 on c1 segments
             F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
         } else {
             a[tid_global * LEN + idx] = canon12(v, q, q2);
@@ -677,17 +688,18 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) voi
 
 // FHE_NTT_FULL (A/B timing): which passes take the exact-grid variant (bit mask:
 // 1 forward column, 2 forward column + lift, 4 forward row, 8 rescale row,
-// 16 HMult-tail row, 32 inverse column, 64 inverse row)
+// 16 HMult-tail row, 32 inverse column, 64 inverse row, 128 key-switch-finish row)
 int &ntt_full_mask() {
     static int v = [] {
         const char *e = std::getenv("FHE_NTT_FULL");
-        return e ? std::atoi(e) : 53;  // measured: the rescale row, inverse row and lift column passes keep the checks (more VGPRs without them)
+        return e ? std::atoi(e) : 53 | 128;  // measured: the rescale row, inverse row and lift column passes keep the checks (more VGPRs without them)
     }();
     return v;
 }
 template <bool COLS, bool FWD, int MODE>
 constexpr int full_bit() {
-    return FWD ? (COLS ? (MODE == NTT_LIFT ? 2 : 1) : MODE == NTT_RESCALE ? 8 : MODE == NTT_MULTAIL ? 16 : 4)
+    return FWD ? (COLS ? (MODE == NTT_LIFT ? 2 : 1)
+                       : MODE == NTT_RESCALE ? 8 : MODE == NTT_MULTAIL ? 16 : MODE == NTT_KSFINISH ? 128 : 4)
                : (COLS ? 32 : 64);
 }
 
@@ -750,7 +762,7 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
         auto it = names.find(key);
         if (it == names.end()) it = names.emplace(key, key).first;
         // one read + one write of every limb touched (fused epilogues: + the extra operands)
-        const double extra = MODE == NTT_RESCALE ? 1.0 : MODE == NTT_MULTAIL ? 2.0 : 0.0;
+        const double extra = MODE == NTT_RESCALE ? 1.0 : MODE == NTT_MULTAIL ? 2.0 : MODE == NTT_KSFINISH ? 1.5 : 0.0;
         clk->record(slot, it->second.c_str(), (2.0 + extra) * 8.0 * (double)limbs * segs * ((size_t)1 << T.logN));
     }
 }
@@ -848,6 +860,14 @@ void ntt_forward_multail(u64 *corr, int limbs, int segs, const NttFuse &F, const
     const size_t seg = (size_t)limbs << T.logN;
     dispatch<true, true, NTT_PLAIN>(k1, corr, limbs, segs, seg, nullptr, nullptr, T, F, st);
     dispatch<false, true, NTT_MULTAIL>(k2, corr, limbs, segs, seg, nullptr, nullptr, T, F, st);
+}
+
+void ntt_forward_ksfinish(u64 *conv, int limbs, int segs, const NttFuse &F, const NttTables &T, hipStream_t st) {
+    if (limbs <= 0 || segs <= 0) return;
+    const int k1 = (T.logN + 1) / 2, k2 = T.logN - k1;
+    const size_t seg = (size_t)limbs << T.logN;
+    dispatch<true, true, NTT_PLAIN>(k1, conv, limbs, segs, seg, nullptr, nullptr, T, F, st);
+    dispatch<false, true, NTT_KSFINISH>(k2, conv, limbs, segs, seg, nullptr, nullptr, T, F, st);
 }
 
 }  // namespace dev

@@ -262,9 +262,7 @@ struct Engine::Impl {
         u64 *conv = static_cast<u64 *>(convm->p);
         dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, segs, phinv, phinv_s,
                              phat, pmod, pinvd, mods, P.logN, st);
-        dev::ntt_forward(conv, (int)ell, segs, ell * nn, nullptr, T, st);
-        dev::moddown_finish(out, acc, conv, add, (int)ell, segs, ell * nn, W * nn, add_stride, pinv, pinv_s, mods,
-                            P.logN, st);
+        ks_finish(conv, acc, ell, segs, out, add, add_stride);
     }
     // `count` key switches in the same launches: switch m uses keys.key[m] and
     // reads its ext (stride e_stride; 0 = one hoisted ModUp shared by all)
@@ -288,9 +286,22 @@ struct Engine::Impl {
         u64 *conv = static_cast<u64 *>(convm->p);
         dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, segs, phinv, phinv_s,
                              phat, pmod, pinvd, mods, P.logN, st);
-        dev::ntt_forward(conv, (int)ell, segs, ell * nn, nullptr, T, st);
-        dev::moddown_finish(out, acc, conv, add, (int)ell, segs, ell * nn, W * nn, add_stride, pinv, pinv_s, mods,
-                            P.logN, st);
+        ks_finish(conv, acc, ell, segs, out, add, add_stride);
+    }
+    // out[s] = (acc[s] - NTT(conv[s])) P^-1 (+ add[s / 2] on c0): the forward NTT of
+    // the converted special part whose row pass finishes the ModDown
+    void ks_finish(u64 *conv, const u64 *acc, size_t ell, int segs, u64 *out, const u64 *add, size_t add_stride) {
+        const size_t nn = n(), W = ell + (size_t)P.K;
+        dev::NttFuse F;
+        F.out = out;
+        F.seg_out = ell * nn;
+        F.x = acc;
+        F.seg_x = W * nn;
+        F.d = add;
+        F.seg_d = add_stride;
+        F.c1 = pinv;
+        F.c1s = pinv_s;
+        dev::ntt_forward_ksfinish(conv, (int)ell, segs, F, T, st);
     }
     // HMult tail, fused: out[m] ([2][ell-1][n]) = Rescale(d01[m] + ModDown(Sum_j ext_j * key_j)).
     // Bit-identical to a ModDown with d01 added followed by rescale(): both
