@@ -275,10 +275,12 @@ CtPtr Bootstrapper::transform(const Ciphertext &x, const Level &lv, int tag) {
             cc.add_inplace(acc, *r);
         else
             acc = r;
-    } else if (!shifted.empty()) {  // giant steps: one batch, one rotation per member, summed
+    } else if (!shifted.empty()) {
+        // giant steps: one batch, one rotation per member, the key products summed
+        // over QP and ONE ModDown (OpenFHE's outer sum in the extended basis)
         std::vector<const Ciphertext *> ptrs;
         for (auto &c : shifted) ptrs.push_back(c.get());
-        CtPtr r = cc.sum_members(*cc.rotate_members(*cc.stack(ptrs), shifts));
+        CtPtr r = cc.rotate_members_sum(*cc.stack(ptrs), shifts);
         if (acc)
             cc.add_inplace(acc, *r);
         else

@@ -546,6 +546,56 @@ __global__ __launch_bounds__(NT) void k_ks_inner_mk(u64 *acc, const u64 *ext, co
     acc[(size_t)t * n + k] = a0;
     acc[((size_t)W + t) * n + k] = a1;
 }
+// Summed multi-key variant (the giant steps of a bootstrap's linear transform):
+// acc (+)= sum_m <ext_m o perm_m, key_m> over the count members, one
+// accumulator pair.  grid: x = coefficient block, y = target.
+template <int D>
+__global__ __launch_bounds__(NT) void k_ks_inner_mk_sum(u64 *acc, const u64 *ext, const u64 *dntt, KsKeys KK,
+                                                        int count, int accumulate, int ell, int W, int nall,
+                                                        int alpha, const int *pmap_ext, const Mod *mods, int logN,
+                                                        KsStrides st) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const int t = blockIdx.y;
+    const int pt = pmap_ext[t];
+    const Mod m = mods[pt];
+    u64 a0 = accumulate ? acc[(size_t)t * n + k] : 0, a1 = accumulate ? acc[((size_t)W + t) * n + k] : 0;
+    for (int mb = 0; mb < count; ++mb) {
+        const u64 *key = KK.key[mb];
+        const uint32_t *perm = KK.perm[mb];
+        const size_t kk = perm ? perm[k] : k;
+        u64 x[D], kb[D], ka[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
+            x[j] = (t >= lo && t < hi) ? dntt[(size_t)mb * st.d + (size_t)t * n + kk]
+                                       : ext[(size_t)mb * st.ext + ((size_t)j * W + t) * n + kk];
+            kb[j] = key[(((size_t)j * 2 + 0) * nall + pt) * n + k];
+            ka[j] = key[(((size_t)j * 2 + 1) * nall + pt) * n + k];
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            a0 = add_mod(a0, mul_barrett(x[j], kb[j], m), m.q);
+            a1 = add_mod(a1, mul_barrett(x[j], ka[j], m), m.q);
+        }
+    }
+    acc[(size_t)t * n + k] = a0;
+    acc[((size_t)W + t) * n + k] = a1;
+}
+// out (+)= sum_m in_m o perm_m over `count` members (input m at m * S.a).
+// grid: x = n / NT, y = limb
+__global__ __launch_bounds__(NT) void k_permute_sum(u64 *out, const u64 *in, KsKeys KK, int count, int accumulate,
+                                                    Seg S, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t ln = (size_t)blockIdx.y * n;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const u64 q = mods[blockIdx.y].q;
+    u64 r = accumulate ? out[ln + k] : 0;
+    for (int mb = 0; mb < count; ++mb) r = add_mod(r, in[(size_t)mb * S.a + ln + KK.perm[mb][k]], q);
+    out[ln + k] = r;
+}
 // grid: x = n / NT, y = limb, z = member
 __global__ __launch_bounds__(NT) void k_permute_mk(u64 *out, const u64 *in, KsKeys KK, Seg S, int logN) {
     const size_t n = (size_t)1 << logN;
@@ -952,6 +1002,28 @@ void ks_inner_multikey(u64 *acc, const u64 *ext, const u64 *dntt, const KsKeys &
         launch_clocked("k_ks_inner", B, k_ks_inner_mk<D>, grid, dim3(NT), st, acc, ext, dntt, keys, ell, W, nall,
                        alpha, pmap_ext, mods, logN, str);
     });
+}
+void ks_inner_multikey_sum(u64 *acc, const u64 *ext, const u64 *dntt, const KsKeys &keys, int count, bool accumulate,
+                           int ell, int K, int nall, int alpha, int digits, const int *pmap_ext, const Mod *mods,
+                           int logN, hipStream_t st, KsStrides str) {
+    if (count <= 0) return;
+    if (count > KS_MAXKEYS) throw std::invalid_argument("ks_inner_multikey_sum: too many keys");
+    const int W = ell + K;
+    // every member's ext and key, one accumulator pair (read when accumulating)
+    const double B = 8.0 * (count * 3.0 * digits * W + 2.0 * W * (1 + accumulate)) * ((size_t)1 << logN);
+    const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
+    dispatch_int<1, 8>(digits, [&](auto c) {
+        constexpr int D = decltype(c)::value;
+        launch_clocked("k_ks_inner", B, k_ks_inner_mk_sum<D>, grid, dim3(NT), st, acc, ext, dntt, keys, count,
+                       (int)accumulate, ell, W, nall, alpha, pmap_ext, mods, logN, str);
+    });
+}
+void ew_permute_sum(u64 *out, const u64 *in, const KsKeys &keys, int limbs, int count, bool accumulate, size_t in_stride,
+                    const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0 || count <= 0) return;
+    if (count > KS_MAXKEYS) throw std::invalid_argument("ew_permute_sum: too many keys");
+    hipLaunchKernelGGL(k_permute_sum, pt_grid(logN, limbs, 1), dim3(NT), 0, st, out, in, keys, count, (int)accumulate,
+                       Seg{0, in_stride, 0}, mods, logN);
 }
 void ew_permute_multi(u64 *out, const u64 *in, const KsKeys &keys, int limbs, int count, Seg S, int logN,
                       hipStream_t st) {

@@ -199,6 +199,14 @@ struct KsKeys {
     const u64 *key[KS_MAXKEYS];
     const uint32_t *perm[KS_MAXKEYS];
 };
+// acc [2][ell+K][n] (+)= sum over the count members of their key products
+// (member m: ext at m * str.ext, own digit at m * str.d, keys.key/perm[m])
+void ks_inner_multikey_sum(u64 *acc, const u64 *ext, const u64 *dntt, const KsKeys &keys, int count, bool accumulate,
+                           int ell, int K, int nall, int alpha, int digits, const int *pmap_ext, const Mod *mods,
+                           int logN, hipStream_t st, KsStrides str);
+// out [limbs][n] (+)= sum_m in_m o keys.perm[m] (member m at m * in_stride)
+void ew_permute_sum(u64 *out, const u64 *in, const KsKeys &keys, int limbs, int count, bool accumulate, size_t in_stride,
+                    const Mod *mods, int logN, hipStream_t st);
 void ks_inner_multikey(u64 *acc, const u64 *ext, const u64 *dntt, const KsKeys &keys, int count, int ell, int K,
                        int nall, int alpha, int digits, const int *pmap_ext, const Mod *mods, int logN,
                        hipStream_t st, KsStrides str);

@@ -256,7 +256,12 @@ struct Engine::Impl {
         str.d = d_stride;
         dev::ks_inner(acc, e, d, key, (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha, digits, pm, ext(ell), mods,
                       P.logN, st, members, str);
-        // ModDown of both accumulators of every member
+        ks_moddown(acc, ell, segs, out, add, add_stride);
+    }
+    // ModDown of `segs` accumulators acc [segs][ell+K][n] (NTT form): out[s] =
+    // ModDown(acc[s]) (+ add[s / 2] on the c0 segments)
+    void ks_moddown(u64 *acc, size_t ell, int segs, u64 *out, const u64 *add, size_t add_stride) {
+        const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         dev::ntt_inverse(acc + ell * nn, (int)K, segs, W * nn, ext(ell) + ell, T, st, /*raw*/ true);
         auto convm = alloc((size_t)segs * ell * nn * 8);
         u64 *conv = static_cast<u64 *>(convm->p);
@@ -281,12 +286,7 @@ struct Engine::Impl {
         str.d = d_stride;
         dev::ks_inner_multikey(acc, e, d, keys, count, (int)ell, P.K, (int)P.nall(), P.alpha, digits, ext(ell), mods,
                                P.logN, st, str);
-        dev::ntt_inverse(acc + ell * nn, (int)K, segs, W * nn, ext(ell) + ell, T, st, /*raw*/ true);
-        auto convm = alloc((size_t)segs * ell * nn * 8);
-        u64 *conv = static_cast<u64 *>(convm->p);
-        dev::moddown_convert(conv, acc + ell * nn, (int)ell, P.K, (int)P.nq(), W * nn, ell * nn, segs, phinv, phinv_s,
-                             phat, pmod, pinvd, mods, P.logN, st);
-        ks_finish(conv, acc, ell, segs, out, add, add_stride);
+        ks_moddown(acc, ell, segs, out, add, add_stride);
     }
     // out[s] = (acc[s] - NTT(conv[s])) P^-1 (+ add[s / 2] on c0): the forward NTT of
     // the converted special part whose row pass finishes the ModDown
@@ -1262,6 +1262,52 @@ CtPtr Engine::rotate_members(const Ciphertext &a, const std::vector<long> &ks) {
         I.ks_apply_multi(static_cast<u64 *>(extm->p) + c0 * es, es, a.data + c0 * 2 * ln + ln, 2 * ln, ell, cnt, KK,
                          r->data + c0 * 2 * ln, c0p + c0 * ln, ln);
     }
+    ctr.keyswitch += B;
+    ctr.rotations += B;
+    count_bytes(4.0 * ell + ks_units(ell), B);
+    return r;
+}
+
+// sum_m rotate(member m, ks[m]) with one ModDown: the key products of all
+// members accumulate over QP, the permuted c0s are summed and added by the
+// ModDown finish (oracle: Context::rotate_sum)
+CtPtr Engine::rotate_members_sum(const Ciphertext &a, const std::vector<long> &ks) {
+    auto &I = *impl;
+    if ((int)ks.size() != a.batch) throw std::invalid_argument("rotate_members_sum: one rotation per member");
+    const size_t nn = n(), ell = a.limbs, ln = ell * nn, W = ell + (size_t)I.P.K;
+    const int B = a.batch;
+    std::vector<u64> gs;
+    for (long k : ks) {
+        const u64 g = host::galois_for_rotation(I.P.logN, k);
+        if (g == 1) throw std::invalid_argument("rotate_members_sum: identity rotation");
+        if (!I.ks->rotkeys.count(g)) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
+        gs.push_back(g);
+    }
+    auto extm = I.modup(a.data + ln, ell, B, 2 * ln);
+    const int digits = I.P.digits_at(ell);
+    const size_t es = (size_t)digits * W * nn;
+    auto accm = I.alloc(2 * W * nn * 8);
+    u64 *acc = static_cast<u64 *>(accm->p);
+    auto c0m = I.alloc(ln * 8);
+    u64 *c0 = static_cast<u64 *>(c0m->p);
+    dev::KsStrides str;
+    str.acc = 0;
+    str.ext = es;
+    str.d = 2 * ln;
+    for (int b0 = 0; b0 < B; b0 += dev::KS_MAXKEYS) {
+        const int cnt = std::min(dev::KS_MAXKEYS, B - b0);
+        dev::KsKeys KK{};
+        for (int i = 0; i < cnt; ++i) {
+            KK.key[i] = static_cast<const u64 *>(I.ks->rotkeys.at(gs[b0 + i])->p);
+            KK.perm[i] = I.perm(gs[b0 + i]);
+        }
+        dev::ew_permute_sum(c0, a.data + b0 * 2 * ln, KK, (int)ell, cnt, b0 > 0, 2 * ln, MODS, LOGN, ST);
+        dev::ks_inner_multikey_sum(acc, static_cast<u64 *>(extm->p) + b0 * es, a.data + b0 * 2 * ln + ln, KK, cnt,
+                                   b0 > 0, (int)ell, I.P.K, (int)I.P.nall(), I.P.alpha, digits, I.ext(ell), MODS, LOGN,
+                                   ST, str);
+    }
+    auto r = new_ct(a.level, a.slots, a.scale, ell, 1);
+    I.ks_moddown(acc, ell, 2, r->data, c0, 0);
     ctr.keyswitch += B;
     ctr.rotations += B;
     count_bytes(4.0 * ell + ks_units(ell), B);

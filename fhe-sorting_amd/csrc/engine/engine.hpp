@@ -168,6 +168,8 @@ class Engine {
     // member m of a batch rotated by ks[m] (all keyed): the giant steps of a
     // BSGS linear transform as one pipeline
     CtPtr rotate_members(const Ciphertext &a, const std::vector<long> &ks);
+    // sum over members of member m rotated by ks[m], one ModDown (bootstrap giant steps)
+    CtPtr rotate_members_sum(const Ciphertext &a, const std::vector<long> &ks);
     // keyed automorphisms sharing one ModUp; conjugate = g 2n - 1
     std::vector<CtPtr> apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs);
     CtPtr conjugate(const Ciphertext &a);

@@ -230,6 +230,10 @@ class Context {
     // keyed automorphisms X -> X^g sharing one ModUp (rotations are g = 5^k)
     std::vector<CtPtr> apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs);
     CtPtr conjugate(const Ciphertext &a);                            // g = 2n - 1
+    // sum_m rotate(xs[m], ks[m]) with ONE ModDown: the key products of every
+    // member accumulate over QP and the rotated c0s are added after the ModDown
+    // (the giant steps of a bootstrap's linear transform, OpenFHE's outer sum)
+    CtPtr rotate_sum(const std::vector<const Ciphertext *> &xs, const std::vector<long> &ks);
     void gen_galois_keys(const std::vector<u64> &gs);
     // ModRaise (bootstrapping): a ciphertext at the last level (one limb, q0)
     // re-read over every Q prime by the centred lift of its coefficients; the
@@ -250,6 +254,9 @@ class Context {
     void modup(const u64 *d_ntt, size_t ell, std::vector<u64> &ext) const;   // ext [digits][ell+K][n]
     void keyswitch_core(const std::vector<u64> &ext, size_t ell, const SwitchKey &key,
                         const std::vector<uint32_t> *perm, std::vector<u64> &out01) const;
+    // acc [2][ell+K][n] += <ext o perm, key> (the inner product of keyswitch_core)
+    void keyswitch_acc(const std::vector<u64> &ext, size_t ell, const SwitchKey &key,
+                       const std::vector<uint32_t> *perm, std::vector<u64> &acc) const;
     void moddown(const u64 *in_ext_poly, size_t ell, u64 *out_q) const; // in: [ell+K][n] NTT
 
     double delta(int level) const { return P.delta[level]; }

@@ -282,6 +282,8 @@ CtPtr Bootstrapper::linear(const Ciphertext &x, const LinLevel &lv, int tag) {
     }
     const auto babies = cc.rotate_hoisted(x, lv.baby);
     CtPtr acc;
+    std::vector<CtPtr> inner;
+    std::vector<long> shifts;
     for (size_t gi = 0; gi < lv.giants.size(); ++gi) {
         const Giant &g = lv.giants[gi];
         std::vector<const Ciphertext *> a;
@@ -291,8 +293,19 @@ CtPtr Bootstrapper::linear(const Ciphertext &x, const LinLevel &lv, int tag) {
             p.push_back(&it->second[gi][j]);
         }
         CtPtr t = cc.mul_plain_sum(a, p);
-        if (g.shift) t = cc.rotate(*t, g.shift);
-        acc = acc ? cc.add(*acc, *t) : t;
+        if (g.shift) {
+            inner.push_back(t);
+            shifts.push_back(g.shift);
+        } else {
+            acc = t;
+        }
+    }
+    // the giant steps: their key products summed over QP, one ModDown (rotate_sum)
+    if (!inner.empty()) {
+        std::vector<const Ciphertext *> ptrs;
+        for (auto &c : inner) ptrs.push_back(c.get());
+        CtPtr r = cc.rotate_sum(ptrs, shifts);
+        acc = acc ? cc.add(*acc, *r) : r;
     }
     return acc;
 }
