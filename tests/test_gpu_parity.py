@@ -527,6 +527,30 @@ def test_wide_digits_match_oracle(L, alpha, K):
     assert np.max(np.abs(gpu.decrypt(gpu.mul(ga, gb)) - a * b)) < 1e-6
 
 
+@pytest.mark.parametrize('logN,L', [(16, 10), (17, 6)])
+def test_relinearised_products_large_rings(logN, L):
+    """Rings 2^16 / 2^17 (256-point row passes: the ModUp row pass runs fused with
+    the relinearisation inner product, k_modup_row_ks): single and stacked
+    products, squares and mul_add down the chain, word-identical to the oracle."""
+    orc = O.Context(logN, L, 40, 60, 3, seed=logN)
+    gpu = F.Context(logN, L, 40, 60, 3, seed=logN, keygen=False)
+    gpu.load_keys_from(orc, [])
+    rng = np.random.default_rng(logN)
+    xs = [orc.encrypt(rng.uniform(-1, 1, 64), 64) for _ in range(3)]
+    gx = [gpu.from_oracle(x) for x in xs]
+    oc, gc = xs[0], gx[0]
+    for i in range(L - 1):
+        oc, gc = orc.mul(oc, xs[1]), gpu.mul(gc, gx[1])
+        if i % 2 == 0:
+            same(gc, oc)
+    same(gc, oc)
+    same(gpu.square(gx[2]), orc.square(xs[2]))
+    st = gpu.mul(gpu.stack(gx), gx[1])  # three members times one (broadcast)
+    for m in range(3):
+        same(gpu.member(st, m), orc.mul(xs[m], xs[1]))
+    assert np.max(np.abs(gpu.decrypt(gpu.mul(gx[0], gx[1])) - orc.decrypt(orc.mul(xs[0], xs[1])))) < 1e-9
+
+
 def test_config2_direct_sort_full_size_bit_exact():
     """BASELINE config 2 at its full size: DirectSort N=128 at ring 2^16, depth 30,
     the reference's 40-bit scaling primes, 30 rotation keys, CompositeSign(3,3,2)
