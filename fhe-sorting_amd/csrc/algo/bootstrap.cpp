@@ -102,8 +102,12 @@ std::vector<int> level_sizes(int stages, int budget) {
     return g;
 }
 
-// baby-step giant-step schedule: offset d = G + i * step with baby i < b,
-// b the power of two (<= 64) that needs the fewest keyed rotations
+// baby-step giant-step schedule: diagonal x step = G + (emin + i) step with
+// baby i < b (the babies centred on the diagonals, so a level that fits in one
+// giant needs no giant rotation).  A baby costs one key product inside
+// linear_transform_ext (it is never brought down to Q); a rotated giant a
+// ModDown, a ModUp and a key switch of its own, priced at kGiantCost babies.
+constexpr long kGiantCost = 8;
 Bootstrapper::Level schedule(const DiagMap &D, long m) {
     long step = m;
     for (const auto &kv : D)
@@ -111,15 +115,16 @@ Bootstrapper::Level schedule(const DiagMap &D, long m) {
     std::vector<long> e;
     for (const auto &kv : D) e.push_back((kv.first > m / 2 ? kv.first - m : kv.first) / step);
     const long emin = *std::min_element(e.begin(), e.end());
+    auto baby_rot = [&](long i) { return (((emin + i) * step) % m + m) % m; };
     long bsel = 1, best = LONG_MAX;
     for (long b = 1; b <= 64; b <<= 1) {
         std::set<long> bs, gs;
         for (long x : e) {
             const long i = (x - emin) % b;
-            bs.insert(i);
-            gs.insert((((x - i) * step) % m + m) % m);
+            bs.insert(baby_rot(i));
+            gs.insert((((x - emin - i) * step) % m + m) % m);
         }
-        const long cost = (long)bs.size() - (long)bs.count(0) + (long)gs.size() - (long)gs.count(0);
+        const long cost = (long)bs.size() - (long)bs.count(0) + kGiantCost * ((long)gs.size() - (long)gs.count(0));
         if (cost < best) {
             best = cost;
             bsel = b;
@@ -131,14 +136,14 @@ Bootstrapper::Level schedule(const DiagMap &D, long m) {
     std::map<long, int> slot;
     for (long i : used) {
         slot[i] = (int)lv.baby.size();
-        lv.baby.push_back((i * step) % m);
+        lv.baby.push_back(baby_rot(i));
     }
     std::map<long, Bootstrapper::GiantStep> giants;
     size_t j = 0;
     for (const auto &kv : D) {
         const long x = e[j++];
         const long i = (x - emin) % bsel;
-        const long G = (((x - i) * step) % m + m) % m;
+        const long G = (((x - emin - i) * step) % m + m) % m;
         auto &g = giants[G];
         g.shift = G;
         g.baby.push_back(slot[i]);
@@ -239,54 +244,23 @@ CtPtr Bootstrapper::transform(const Ciphertext &x, const Level &lv, int tag) {
     const int m = 2 * cfg.slots;
     auto key = std::make_pair(tag, x.level);
     auto it = pts.find(key);
-    if (it == pts.end()) {  // diagonals are encoded once per (level, ciphertext level), kept in HBM
+    if (it == pts.end()) {  // diagonals over Q_level u P, encoded once per (level, ciphertext level), kept in HBM
         std::vector<std::vector<PtPtr>> enc_pts;
         for (const GiantStep &g : lv.giants) {
             std::vector<PtPtr> row;
-            for (const auto &v : g.diag) row.push_back(cc.encode_complex(v, m, x.level, cc.delta(x.level)));
+            for (const auto &v : g.diag) row.push_back(cc.encode_complex_ext(v, m, x.level, cc.delta(x.level)));
             enc_pts.push_back(std::move(row));
         }
         it = pts.emplace(key, std::move(enc_pts)).first;
     }
-    // baby steps: one ModUp, all key switches in the same launches
-    const auto babies = cc.rotate_hoisted(x, lv.baby);
-    CtPtr acc;
-    std::vector<CtPtr> shifted;
-    std::vector<long> shifts;
+    // double hoisting: one ModUp, babies over Q u P, one ModDown per level
+    std::vector<Engine::LtGiant> G(lv.giants.size());
     for (size_t gi = 0; gi < lv.giants.size(); ++gi) {
-        const GiantStep &g = lv.giants[gi];
-        std::vector<const Ciphertext *> a;
-        std::vector<const Plaintext *> p;
-        for (size_t j = 0; j < g.baby.size(); ++j) {
-            a.push_back(babies[(size_t)g.baby[j]].get());
-            p.push_back(it->second[gi][j].get());
-        }
-        CtPtr inner = cc.mul_plain_sum(a, p);
-        if (g.shift) {
-            shifted.push_back(inner);
-            shifts.push_back(g.shift);
-        } else {
-            acc = inner;
-        }
+        G[gi].shift = lv.giants[gi].shift;
+        G[gi].baby = lv.giants[gi].baby;
+        for (const auto &p : it->second[gi]) G[gi].pts.push_back(p.get());
     }
-    if (shifted.size() == 1) {
-        CtPtr r = cc.rotate(*shifted[0], shifts[0]);
-        if (acc)
-            cc.add_inplace(acc, *r);
-        else
-            acc = r;
-    } else if (!shifted.empty()) {
-        // giant steps: one batch, one rotation per member, the key products summed
-        // over QP and ONE ModDown (OpenFHE's outer sum in the extended basis)
-        std::vector<const Ciphertext *> ptrs;
-        for (auto &c : shifted) ptrs.push_back(c.get());
-        CtPtr r = cc.rotate_members_sum(*cc.stack(ptrs), shifts);
-        if (acc)
-            cc.add_inplace(acc, *r);
-        else
-            acc = r;
-    }
-    return acc;
+    return cc.linear_transform_ext(x, lv.baby, G);
 }
 
 CtPtr Bootstrapper::coeffsToSlots(const Ciphertext &raised) {

@@ -583,6 +583,53 @@ __global__ __launch_bounds__(NT) void k_ks_inner_mk_sum(u64 *acc, const u64 *ext
     acc[(size_t)t * n + k] = a0;
     acc[((size_t)W + t) * n + k] = a1;
 }
+// grid: x = coefficient block, y = target t < W (the prime of t: pmap_ext[t])
+template <int D>
+__global__ __launch_bounds__(NT) void k_lt_inner(u64 *out, const u64 *ext, const u64 *c, LtArgs A, int accumulate,
+                                                 int ell, int W, int nall, int alpha, const int *pmap_ext,
+                                                 const u64 *pmodq, const u64 *pmodq_s, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
+    if (k >= n) return;
+    const int t = blockIdx.y;
+    const int pt = pmap_ext[t];
+    const Mod m = mods[pt];
+    const bool ql = t < ell;  // a Q limb: P sigma(c0) enters; on the P limbs P = 0
+    const u64 Pt = ql ? pmodq[t] : 0, Pts = ql ? pmodq_s[t] : 0;
+    const u64 *c0 = c + (size_t)t * n, *c1 = c + ((size_t)ell + t) * n;
+    u64 a0 = accumulate ? out[(size_t)t * n + k] : 0, a1 = accumulate ? out[((size_t)W + t) * n + k] : 0;
+    for (int b = 0; b < A.nb; ++b) {
+        const u64 w = A.pt[b][(size_t)t * n + k];
+        u64 b0 = 0, b1 = 0;
+        if (!A.key[b]) {
+            if (ql) {
+                b0 = mul_shoup(c0[k], Pt, Pts, m.q);
+                b1 = mul_shoup(c1[k], Pt, Pts, m.q);
+            }
+        } else {
+            const u64 *key = A.key[b];
+            const size_t kk = A.perm[b][k];
+            u64 x[D], kb[D], ka[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
+                x[j] = (t >= lo && t < hi) ? c1[kk] : ext[((size_t)j * W + t) * n + kk];
+                kb[j] = key[(((size_t)j * 2 + 0) * nall + pt) * n + k];
+                ka[j] = key[(((size_t)j * 2 + 1) * nall + pt) * n + k];
+            }
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                b0 = add_mod(b0, mul_barrett(x[j], kb[j], m), m.q);
+                b1 = add_mod(b1, mul_barrett(x[j], ka[j], m), m.q);
+            }
+            if (ql) b0 = add_mod(b0, mul_shoup(c0[kk], Pt, Pts, m.q), m.q);
+        }
+        a0 = add_mod(a0, mul_barrett(b0, w, m), m.q);
+        a1 = add_mod(a1, mul_barrett(b1, w, m), m.q);
+    }
+    out[(size_t)t * n + k] = a0;
+    out[((size_t)W + t) * n + k] = a1;
+}
 // out (+)= sum_m in_m o perm_m over `count` members (input m at m * S.a).
 // grid: x = n / NT, y = limb
 __global__ __launch_bounds__(NT) void k_permute_sum(u64 *out, const u64 *in, KsKeys KK, int count, int accumulate,
@@ -1016,6 +1063,25 @@ void ks_inner_multikey_sum(u64 *acc, const u64 *ext, const u64 *dntt, const KsKe
         constexpr int D = decltype(c)::value;
         launch_clocked("k_ks_inner", B, k_ks_inner_mk_sum<D>, grid, dim3(NT), st, acc, ext, dntt, keys, count,
                        (int)accumulate, ell, W, nall, alpha, pmap_ext, mods, logN, str);
+    });
+}
+void lt_inner(u64 *out, const u64 *ext, const u64 *c, const LtArgs &A, bool accumulate, int ell, int K, int nall,
+              int alpha, int digits, const int *pmap_ext, const u64 *pmodq, const u64 *pmodq_s, const Mod *mods,
+              int logN, hipStream_t st) {
+    if (A.nb <= 0) return;
+    if (A.nb > LT_MAXB) throw std::invalid_argument("lt_inner: too many babies per launch");
+    const int W = ell + K;
+    int keyed = 0;
+    for (int b = 0; b < A.nb; ++b) keyed += A.key[b] != nullptr;
+    // per keyed baby: its key and the gathered ext digits; per baby a plaintext;
+    // the ciphertext once, the accumulator pair out (and in)
+    const double B = 8.0 * ((double)keyed * 3.0 * digits * W + (double)A.nb * W + 2.0 * ell + 2.0 * W * (1 + accumulate)) *
+                     ((size_t)1 << logN);
+    const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
+    dispatch_int<1, 8>(digits, [&](auto dc) {
+        constexpr int D = decltype(dc)::value;
+        launch_clocked("k_lt_inner", B, k_lt_inner<D>, grid, dim3(NT), st, out, ext, c, A, (int)accumulate, ell, W,
+                       nall, alpha, pmap_ext, pmodq, pmodq_s, mods, logN);
     });
 }
 void ew_permute_sum(u64 *out, const u64 *in, const KsKeys &keys, int limbs, int count, bool accumulate, size_t in_stride,

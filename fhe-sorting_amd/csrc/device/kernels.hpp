@@ -204,6 +204,20 @@ struct KsKeys {
 void ks_inner_multikey_sum(u64 *acc, const u64 *ext, const u64 *dntt, const KsKeys &keys, int count, bool accumulate,
                            int ell, int K, int nall, int alpha, int digits, const int *pmap_ext, const Mod *mods,
                            int logN, hipStream_t st, KsStrides str);
+// Baby steps of a double-hoisted linear transform (bootstrap CoeffsToSlots /
+// SlotsToCoeffs): out [2][W][n] (+)= sum_b pt_b * baby_b over Q u P, where baby b
+// is (P sigma_b(c0), 0) + <sigma_b(ext), key_b> (key null: (P c0, P c1)), never
+// brought down to Q.  c: the ciphertext [2][ell][n]; ext its c1's ModUp.
+constexpr int LT_MAXB = 16;
+struct LtArgs {
+    const u64 *key[LT_MAXB];
+    const uint32_t *perm[LT_MAXB];
+    const u64 *pt[LT_MAXB];  // extended plaintexts [W][n]
+    int nb;
+};
+void lt_inner(u64 *out, const u64 *ext, const u64 *c, const LtArgs &A, bool accumulate, int ell, int K, int nall,
+              int alpha, int digits, const int *pmap_ext, const u64 *pmodq, const u64 *pmodq_s, const Mod *mods,
+              int logN, hipStream_t st);
 // out [limbs][n] (+)= sum_m in_m o keys.perm[m] (member m at m * in_stride)
 void ew_permute_sum(u64 *out, const u64 *in, const KsKeys &keys, int limbs, int count, bool accumulate, size_t in_stride,
                     const Mod *mods, int logN, hipStream_t st);

@@ -790,6 +790,25 @@ PtPtr Engine::encode_complex(const std::vector<std::complex<double>> &v, int slo
     return pt;
 }
 
+PtPtr Engine::encode_complex_ext(const std::vector<std::complex<double>> &v, int slots, int level, double scale) {
+    auto &I = *impl;
+    const size_t n = I.n(), ell = I.P.limbs_at(level), W = ell + (size_t)I.P.K;
+    auto coef = host::encode_coeffs_complex(v, n, slots, scale);
+    auto cm = I.alloc(n * 8);
+    HIP_OK(hipMemcpyAsync(cm->p, coef.data(), n * 8, hipMemcpyHostToDevice, I.st));
+    auto pt = std::make_shared<Plaintext>();
+    pt->mem = I.alloc(W * n * 8);
+    pt->data = static_cast<u64 *>(pt->mem->p);
+    pt->level = level;
+    pt->slots = slots;
+    pt->scale = scale;
+    pt->limbs = W;
+    dev::ew_signed_to_rns(pt->data, static_cast<int64_t *>(cm->p), (int)W, I.ext(ell), I.mods, I.P.logN, I.st);
+    dev::ntt_forward(pt->data, (int)W, 1, 0, I.ext(ell), I.T, I.st);
+    HIP_OK(hipStreamSynchronize(I.st));  // `coef` (pageable host) must outlive the copy
+    return pt;
+}
+
 CtPtr Engine::encrypt_pt(const Plaintext &pt) {
     auto &I = *impl;
     if (!I.ks->pk) throw std::runtime_error("encrypt: no public key");
@@ -1311,6 +1330,113 @@ CtPtr Engine::rotate_members_sum(const Ciphertext &a, const std::vector<long> &k
     ctr.keyswitch += B;
     ctr.rotations += B;
     count_bytes(4.0 * ell + ks_units(ell), B);
+    return r;
+}
+
+CtPtr Engine::linear_transform_ext(const Ciphertext &x, const std::vector<long> &baby,
+                                   const std::vector<LtGiant> &giants) {
+    auto &I = *impl;
+    if (x.batch != 1) throw std::invalid_argument("linear_transform_ext: one ciphertext at a time");
+    if (x.level >= I.P.L) throw std::runtime_error("linear_transform_ext: no levels left");
+    const size_t nn = n(), ell = x.limbs, ln = ell * nn, W = ell + (size_t)I.P.K;
+    const int digits = I.P.digits_at(ell);
+    std::vector<const u64 *> bkey(baby.size(), nullptr);
+    std::vector<const uint32_t *> bperm(baby.size(), nullptr);
+    size_t keyed = 0;
+    for (size_t b = 0; b < baby.size(); ++b) {
+        const u64 g = host::galois_for_rotation(I.P.logN, baby[b]);
+        if (g == 1) continue;
+        auto it = I.ks->rotkeys.find(g);
+        if (it == I.ks->rotkeys.end()) throw NoKeyError("rotate: no rotation key for index " + std::to_string(baby[b]));
+        bkey[b] = static_cast<const u64 *>(it->second->p);
+        bperm[b] = I.perm(g);
+        ++keyed;
+    }
+    auto extm = I.modup(x.data + ln, ell, 1, 2 * ln);
+    const u64 *ext = static_cast<const u64 *>(extm->p);
+    size_t npt = 0;
+    auto inner_of = [&](const LtGiant &G, u64 *out) {
+        if (G.baby.empty() || G.baby.size() != G.pts.size())
+            throw std::invalid_argument("linear_transform_ext: one plaintext per baby");
+        for (size_t b0 = 0; b0 < G.baby.size(); b0 += dev::LT_MAXB) {
+            dev::LtArgs A{};
+            A.nb = (int)std::min<size_t>(dev::LT_MAXB, G.baby.size() - b0);
+            for (int i = 0; i < A.nb; ++i) {
+                const int bi = G.baby[b0 + i];
+                const Plaintext *p = G.pts[b0 + i];
+                if (bi < 0 || (size_t)bi >= baby.size()) throw std::invalid_argument("linear_transform_ext: bad baby index");
+                if (p->limbs != W || p->level != x.level)
+                    throw std::invalid_argument("linear_transform_ext: plaintexts must be extended, at the input's level");
+                A.key[i] = bkey[(size_t)bi];
+                A.perm[i] = bperm[(size_t)bi];
+                A.pt[i] = p->data;
+            }
+            dev::lt_inner(out, ext, x.data, A, b0 > 0, (int)ell, I.P.K, (int)I.P.nall(), I.P.alpha, digits, I.ext(ell),
+                          I.pmod, I.pmod_s, MODS, LOGN, ST);
+        }
+        npt += G.baby.size();
+    };
+    auto accm = I.alloc(2 * W * nn * 8);
+    u64 *acc = static_cast<u64 *>(accm->p);
+    bool have_acc = false;
+    std::vector<const LtGiant *> shifted;
+    for (const LtGiant &G : giants) {
+        if (G.shift != 0) {
+            shifted.push_back(&G);
+            continue;
+        }
+        if (have_acc) throw std::invalid_argument("linear_transform_ext: two unrotated giants");
+        inner_of(G, acc);
+        have_acc = true;
+    }
+    std::shared_ptr<DevMem> c0m;
+    const int S = (int)shifted.size();
+    if (S > 0) {
+        // each rotated giant's inner sum brought down to Q, then all of them
+        // rotated with their key products summed into acc (rotate_members_sum)
+        auto qm = I.alloc((size_t)S * 2 * ln * 8), tm = I.alloc(2 * W * nn * 8);
+        u64 *q = static_cast<u64 *>(qm->p), *tmp = static_cast<u64 *>(tm->p);
+        std::vector<u64> gs;
+        for (int i = 0; i < S; ++i) {
+            inner_of(*shifted[(size_t)i], tmp);
+            I.ks_moddown(tmp, ell, 2, q + (size_t)i * 2 * ln, nullptr, 0);
+            const u64 g = host::galois_for_rotation(I.P.logN, shifted[(size_t)i]->shift);
+            if (g == 1 || !I.ks->rotkeys.count(g))
+                throw NoKeyError("rotate: no rotation key for index " + std::to_string(shifted[(size_t)i]->shift));
+            gs.push_back(g);
+        }
+        auto ext2 = I.modup(q + ln, ell, S, 2 * ln);
+        const size_t es = (size_t)digits * W * nn;
+        c0m = I.alloc(ln * 8);
+        u64 *c0 = static_cast<u64 *>(c0m->p);
+        dev::KsStrides str;
+        str.ext = es;
+        str.d = 2 * ln;
+        for (int b0 = 0; b0 < S; b0 += dev::KS_MAXKEYS) {
+            const int cnt = std::min(dev::KS_MAXKEYS, S - b0);
+            dev::KsKeys KK{};
+            for (int i = 0; i < cnt; ++i) {
+                KK.key[i] = static_cast<const u64 *>(I.ks->rotkeys.at(gs[(size_t)(b0 + i)])->p);
+                KK.perm[i] = I.perm(gs[(size_t)(b0 + i)]);
+            }
+            dev::ew_permute_sum(c0, q + (size_t)b0 * 2 * ln, KK, (int)ell, cnt, b0 > 0, 2 * ln, MODS, LOGN, ST);
+            dev::ks_inner_multikey_sum(acc, static_cast<u64 *>(ext2->p) + (size_t)b0 * es, q + (size_t)b0 * 2 * ln + ln,
+                                       KK, cnt, have_acc || b0 > 0, (int)ell, I.P.K, (int)I.P.nall(), I.P.alpha,
+                                       digits, I.ext(ell), MODS, LOGN, ST, str);
+        }
+        have_acc = true;
+    }
+    if (!have_acc) throw std::invalid_argument("linear_transform_ext: no giants");
+    auto tm2 = I.alloc(2 * ln * 8);
+    u64 *t = static_cast<u64 *>(tm2->p);
+    I.ks_moddown(acc, ell, 2, t, c0m ? static_cast<const u64 *>(c0m->p) : nullptr, 0);
+    auto r = new_ct(x.level + 1, x.slots, I.P.delta[x.level + 1], ell - 1, 1);
+    I.rescale(t, ell, ln, 2, r->data);
+    ctr.keyswitch += keyed + (size_t)S;
+    ctr.rotations += keyed + (size_t)S;
+    ctr.ptmult += npt;
+    ctr.rescale += 1;
+    count_bytes((4.0 * ell + ks_units(ell)) * (double)(keyed + (size_t)S) + 3.0 * ell * (double)npt, 1);
     return r;
 }
 

@@ -126,6 +126,8 @@ class Engine {
     PtPtr encode(const std::vector<double> &v, int slots, int level);
     PtPtr encode_scaled(const std::vector<double> &v, int slots, int level, double scale);
     PtPtr encode_complex(const std::vector<std::complex<double>> &v, int slots, int level, double scale);
+    // the same plaintext over Q_level u P (ell + K limbs, special primes last)
+    PtPtr encode_complex_ext(const std::vector<std::complex<double>> &v, int slots, int level, double scale);
     CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
     CtPtr encrypt_pt(const Plaintext &pt);
     // OpenFHE FLEXIBLEAUTOEXT-style encryption: one extra level absorbs the
@@ -170,6 +172,17 @@ class Engine {
     CtPtr rotate_members(const Ciphertext &a, const std::vector<long> &ks);
     // sum over members of member m rotated by ks[m], one ModDown (bootstrap giant steps)
     CtPtr rotate_members_sum(const Ciphertext &a, const std::vector<long> &ks);
+    // Double-hoisted baby-step giant-step linear transform (oracle:
+    // Context::linear_transform_ext): one ModUp of x, the baby rotations kept
+    // over Q u P and multiplied there by extended plaintexts (encode_complex_ext),
+    // the unrotated giant as the starting accumulator, every rotated giant brought
+    // down, rotated and summed over Q u P, one final ModDown, then the rescale.
+    struct LtGiant {
+        long shift = 0;
+        std::vector<int> baby;               // indices into `baby`
+        std::vector<const Plaintext *> pts;  // extended plaintexts at x's level
+    };
+    CtPtr linear_transform_ext(const Ciphertext &x, const std::vector<long> &baby, const std::vector<LtGiant> &giants);
     // keyed automorphisms sharing one ModUp; conjugate = g 2n - 1
     std::vector<CtPtr> apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs);
     CtPtr conjugate(const Ciphertext &a);

@@ -194,7 +194,10 @@ class Context {
     Plaintext encode(const std::vector<double> &v, int slots, int level) const;
     Plaintext encode_scaled(const std::vector<double> &v, int slots, int level, double scale) const;
     // complex slot values (bootstrapping's linear-transform diagonals)
-    Plaintext encode_complex(const std::vector<std::complex<double>> &v, int slots, int level, double scale) const;
+    // ext: the same integer polynomial over Q_level u P (ell + K limbs, special
+    // primes last) for products in the extended basis (linear_transform_ext)
+    Plaintext encode_complex(const std::vector<std::complex<double>> &v, int slots, int level, double scale,
+                             bool ext = false) const;
     std::vector<double> decode(const std::vector<u64> &m0_coeff_limb0, int slots, double scale) const;
     std::vector<double> decode_real(const std::vector<double> &m_coeff, int slots, double scale) const;
     CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
@@ -234,6 +237,18 @@ class Context {
     // member accumulate over QP and the rotated c0s are added after the ModDown
     // (the giant steps of a bootstrap's linear transform, OpenFHE's outer sum)
     CtPtr rotate_sum(const std::vector<const Ciphertext *> &xs, const std::vector<long> &ks);
+    // Baby-step giant-step linear transform with double hoisting: one ModUp of
+    // x; every baby rotation stays over Q u P (no ModDown); each giant's inner
+    // sum sum_j pt_j * baby_j is formed there with extended plaintexts; the
+    // unrotated giant is the starting accumulator, every other giant is brought
+    // down (ModDown), rotated and summed as in rotate_sum; one final ModDown,
+    // then the rescale.  Result: level + 1, canonical scale.
+    struct LtGiant {
+        long shift = 0;
+        std::vector<int> baby;                 // indices into the baby rotation list
+        std::vector<const Plaintext *> pts;    // extended plaintexts, one per baby
+    };
+    CtPtr linear_transform_ext(const Ciphertext &x, const std::vector<long> &baby, const std::vector<LtGiant> &giants);
     void gen_galois_keys(const std::vector<u64> &gs);
     // ModRaise (bootstrapping): a ciphertext at the last level (one limb, q0)
     // re-read over every Q prime by the centred lift of its coefficients; the
@@ -428,7 +443,7 @@ class Bootstrapper {
         std::vector<std::vector<std::complex<double>>> v;  // pre-rotated diagonals, 2s entries
     };
     struct LinLevel {
-        std::vector<long> baby;  // baby rotations (mod 2s), baby[0] == 0 when used
+        std::vector<long> baby;  // baby rotations (mod 2s): (emin + i) step, i ascending
         std::vector<Giant> giants;
     };
     std::vector<LinLevel> cts, stc;

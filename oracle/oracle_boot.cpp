@@ -139,7 +139,11 @@ std::vector<int> split_levels(int stages, int budget) {
     return g;
 }
 
-// baby-step giant-step plan of one level: offset d = G + i step, baby i < b
+// baby-step giant-step plan of one level: diagonal x step = G + (emin + i) step,
+// baby i < b.  A baby costs one key product inside linear_transform_ext (no
+// ModDown); a rotated giant a ModDown, a ModUp and a key switch of its own,
+// priced at kGiantCost babies.
+constexpr long kGiantCost = 8;
 Bootstrapper::LinLevel plan(const Diags &D, long m) {
     long step = m;
     for (const auto &kv : D)
@@ -147,15 +151,17 @@ Bootstrapper::LinLevel plan(const Diags &D, long m) {
     std::vector<long> e;
     for (const auto &kv : D) e.push_back((kv.first > m / 2 ? kv.first - m : kv.first) / step);
     const long emin = *std::min_element(e.begin(), e.end());
+    auto baby_rot = [&](long i) { return (((emin + i) * step) % m + m) % m; };
     long best_b = 1, best_cost = LONG_MAX;
     for (long b = 1; b <= 64; b <<= 1) {
         std::set<long> babies, giants;
         for (long x : e) {
             const long i = (x - emin) % b;
-            babies.insert(i);
-            giants.insert((((x - i) * step) % m + m) % m);
+            babies.insert(baby_rot(i));
+            giants.insert((((x - emin - i) * step) % m + m) % m);
         }
-        const long cost = (long)babies.size() - (long)babies.count(0) + (long)giants.size() - (long)giants.count(0);
+        const long cost = (long)babies.size() - (long)babies.count(0) +
+                          kGiantCost * ((long)giants.size() - (long)giants.count(0));
         if (cost < best_cost) {
             best_cost = cost;
             best_b = b;
@@ -167,14 +173,14 @@ Bootstrapper::LinLevel plan(const Diags &D, long m) {
     std::map<long, size_t> bidx;
     for (long i : ib) {
         bidx[i] = lv.baby.size();
-        lv.baby.push_back((i * step) % m);
+        lv.baby.push_back(baby_rot(i));
     }
     std::map<long, Bootstrapper::Giant> giants;
     size_t j = 0;
     for (const auto &kv : D) {
         const long x = e[j++];
         const long i = (x - emin) % best_b;
-        const long G = (((x - i) * step) % m + m) % m;
+        const long G = (((x - emin - i) * step) % m + m) % m;
         Bootstrapper::Giant &g = giants[G];
         g.shift = G;
         g.baby.push_back((int)bidx[i]);
@@ -271,43 +277,22 @@ CtPtr Bootstrapper::linear(const Ciphertext &x, const LinLevel &lv, int tag) {
     const int m = 2 * cfg.slots;
     auto key = std::make_pair(tag, x.level);
     auto it = pts.find(key);
-    if (it == pts.end()) {
+    if (it == pts.end()) {  // diagonals over Q_level u P (products in the extended basis)
         std::vector<std::vector<Plaintext>> P;
         for (const Giant &g : lv.giants) {
             std::vector<Plaintext> row;
-            for (const auto &v : g.v) row.push_back(cc.encode_complex(v, m, x.level, cc.delta(x.level)));
+            for (const auto &v : g.v) row.push_back(cc.encode_complex(v, m, x.level, cc.delta(x.level), true));
             P.push_back(std::move(row));
         }
         it = pts.emplace(key, std::move(P)).first;
     }
-    const auto babies = cc.rotate_hoisted(x, lv.baby);
-    CtPtr acc;
-    std::vector<CtPtr> inner;
-    std::vector<long> shifts;
+    std::vector<Context::LtGiant> G(lv.giants.size());
     for (size_t gi = 0; gi < lv.giants.size(); ++gi) {
-        const Giant &g = lv.giants[gi];
-        std::vector<const Ciphertext *> a;
-        std::vector<const Plaintext *> p;
-        for (size_t j = 0; j < g.baby.size(); ++j) {
-            a.push_back(babies[(size_t)g.baby[j]].get());
-            p.push_back(&it->second[gi][j]);
-        }
-        CtPtr t = cc.mul_plain_sum(a, p);
-        if (g.shift) {
-            inner.push_back(t);
-            shifts.push_back(g.shift);
-        } else {
-            acc = t;
-        }
+        G[gi].shift = lv.giants[gi].shift;
+        G[gi].baby = lv.giants[gi].baby;
+        for (const Plaintext &p : it->second[gi]) G[gi].pts.push_back(&p);
     }
-    // the giant steps: their key products summed over QP, one ModDown (rotate_sum)
-    if (!inner.empty()) {
-        std::vector<const Ciphertext *> ptrs;
-        for (auto &c : inner) ptrs.push_back(c.get());
-        CtPtr r = cc.rotate_sum(ptrs, shifts);
-        acc = acc ? cc.add(*acc, *r) : r;
-    }
-    return acc;
+    return cc.linear_transform_ext(x, lv.baby, G);
 }
 
 CtPtr Bootstrapper::coeffs_to_slots(const Ciphertext &raised) {

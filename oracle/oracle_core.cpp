@@ -398,7 +398,7 @@ Plaintext Context::encode_scaled(const std::vector<double> &v, int slots, int le
     for (size_t i = 0; i < v.size() && i < (size_t)std::max(slots, 0); ++i) z.push_back(cd(v[i], 0));
     return encode_complex(z, slots, level, scale);
 }
-Plaintext Context::encode_complex(const std::vector<cd> &v, int slots, int level, double scale) const {
+Plaintext Context::encode_complex(const std::vector<cd> &v, int slots, int level, double scale, bool ext) const {
     const size_t n = P.n;
     if (slots <= 0 || (slots & (slots - 1)) || (size_t)slots > n / 2)
         throw std::invalid_argument("encode: slots must be a power of two <= n/2");
@@ -420,13 +420,15 @@ Plaintext Context::encode_complex(const std::vector<cd> &v, int slots, int level
     pt.level = level;
     pt.slots = slots;
     pt.scale = scale;
-    pt.limbs = P.limbs_at(level);
+    const size_t ell = P.limbs_at(level);
+    pt.limbs = ext ? ell + P.K : ell;
     pt.m.assign(pt.limbs * n, 0);
 #pragma omp parallel for
     for (size_t l = 0; l < pt.limbs; ++l) {
+        const size_t pi = l < ell ? l : P.nq() + (l - ell);
         u64 *d = pt.m.data() + l * n;
-        for (size_t k = 0; k < n; ++k) d[k] = signed_to_mod(coef[k], P.primes[l]);
-        ntt_forward(d, tab[l], n);
+        for (size_t k = 0; k < n; ++k) d[k] = signed_to_mod(coef[k], P.primes[pi]);
+        ntt_forward(d, tab[pi], n);
     }
     return pt;
 }
@@ -1173,6 +1175,98 @@ CtPtr Context::rotate_sum(const std::vector<const Ciphertext *> &xs, const std::
         for (size_t k = 0; k < n; ++k) o[k] = mod_add(o[k], c[k], q);
     }
     return r;
+}
+
+CtPtr Context::linear_transform_ext(const Ciphertext &x, const std::vector<long> &baby,
+                                    const std::vector<LtGiant> &giants) {
+    const size_t n = P.n, nq = P.nq(), K = P.K, ell = x.limbs, W = ell + K;
+    if (x.level >= P.L) throw std::runtime_error("linear_transform_ext: no levels left");
+    auto prime = [&](size_t t) { return t < ell ? t : nq + (t - ell); };
+    std::vector<u64> Pq(ell);  // P mod q_t
+    for (size_t t = 0; t < ell; ++t) {
+        u64 v = 1;
+        for (size_t k = 0; k < K; ++k) v = mod_mul(v, P.primes[nq + k] % P.primes[t], tab[t].mod);
+        Pq[t] = v;
+    }
+    // babies over Q u P: (P sigma(c0), 0) + <sigma(ext), key>, or (P c0, P c1) unrotated
+    std::vector<u64> ext;
+    modup(x.poly(1, n), ell, ext);
+    std::vector<std::vector<u64>> B(baby.size());
+    for (size_t b = 0; b < baby.size(); ++b) {
+        auto &acc = B[b];
+        acc.assign(2 * W * n, 0);
+        const u64 g = galois_for_rotation(P.logN, baby[b]);
+        std::vector<uint32_t> perm;
+        if (g == 1) {
+            for (size_t t = 0; t < ell; ++t)
+                for (int c = 0; c < 2; ++c)
+                    for (size_t k = 0; k < n; ++k)
+                        acc[(c * W + t) * n + k] = mod_mul(x.poly(c, n)[t * n + k], Pq[t], tab[t].mod);
+            continue;
+        }
+        auto it = rotkeys.find(g);
+        if (it == rotkeys.end()) throw std::out_of_range("linear_transform_ext: no rotation key for " + std::to_string(baby[b]));
+        ctr.keyswitch++;
+        ctr.rotations++;
+        perm = automorphism_perm(P.logN, g);
+        keyswitch_acc(ext, ell, it->second, &perm, acc);
+        for (size_t t = 0; t < ell; ++t)
+            for (size_t k = 0; k < n; ++k)
+                acc[t * n + k] = mod_add(acc[t * n + k], mod_mul(x.poly(0, n)[t * n + perm[k]], Pq[t], tab[t].mod),
+                                         P.primes[t]);
+    }
+    // inner sums over Q u P
+    auto inner = [&](const LtGiant &G) {
+        std::vector<u64> r(2 * W * n, 0);
+        for (size_t j = 0; j < G.baby.size(); ++j) {
+            const auto &b = B[(size_t)G.baby[j]];
+            const Plaintext &pt = *G.pts[j];
+            if (pt.limbs != W) throw std::invalid_argument("linear_transform_ext: plaintexts must be extended");
+            ctr.ptmult++;
+#pragma omp parallel for
+            for (size_t t = 0; t < W; ++t) {
+                const Modulus &m = tab[prime(t)].mod;
+                for (int c = 0; c < 2; ++c)
+                    for (size_t k = 0; k < n; ++k) {
+                        u64 &o = r[(c * W + t) * n + k];
+                        o = mod_add(o, mod_mul(b[(c * W + t) * n + k], pt.m[t * n + k], m), m.q);
+                    }
+            }
+        }
+        return r;
+    };
+    std::vector<u64> acc(2 * W * n, 0), c0(ell * n, 0);
+    for (const LtGiant &G : giants)
+        if (G.shift == 0) acc = inner(G);
+    for (const LtGiant &G : giants) {
+        if (G.shift == 0) continue;
+        const auto in = inner(G);
+        auto q = make_ct(x.level, x.slots, x.scale, ell, n);  // ModDown of the giant's inner sum
+        moddown(in.data(), ell, q->poly(0, n));
+        moddown(in.data() + W * n, ell, q->poly(1, n));
+        const u64 g = galois_for_rotation(P.logN, G.shift);
+        auto it = rotkeys.find(g);
+        if (g == 1 || it == rotkeys.end())
+            throw std::out_of_range("linear_transform_ext: no rotation key for " + std::to_string(G.shift));
+        ctr.keyswitch++;
+        ctr.rotations++;
+        const auto perm = automorphism_perm(P.logN, g);
+        std::vector<u64> e2;
+        modup(q->poly(1, n), ell, e2);
+        keyswitch_acc(e2, ell, it->second, &perm, acc);
+        for (size_t t = 0; t < ell; ++t)
+            for (size_t k = 0; k < n; ++k)
+                c0[t * n + k] = mod_add(c0[t * n + k], q->poly(0, n)[t * n + perm[k]], P.primes[t]);
+    }
+    auto r = make_ct(x.level, x.slots, x.scale, ell, n);
+    moddown(acc.data(), ell, r->poly(0, n));
+    moddown(acc.data() + W * n, ell, r->poly(1, n));
+    for (size_t t = 0; t < ell; ++t)
+        for (size_t k = 0; k < n; ++k)
+            r->poly(0, n)[t * n + k] = mod_add(r->poly(0, n)[t * n + k], c0[t * n + k], P.primes[t]);
+    auto out = rescale(*r);
+    out->scale = P.delta[x.level + 1];
+    return out;
 }
 
 CtPtr Context::mod_raise(const Ciphertext &a) {
