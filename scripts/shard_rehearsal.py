@@ -17,22 +17,24 @@ _last = {'hdr': None}
 
 
 def noop(ptr, count, _user):
-    """No exchange; a 2-word level header with no local partial gets the level
-    of the last one seen (the partials of one phase share a level), so rank 0
-    proceeds as if another rank had contributed."""
-    if count != 2:
+    """No exchange; a 4-word header (presence, level + 1, (level + 1)^2, limbs)
+    with no local partial gets the one of the last partial seen (the partials
+    of one phase share a level), so rank 0 proceeds as if another rank had
+    contributed."""
+    if count != 4:
         return
-    h = (C.c_uint64 * 2)()
-    _hip.hipMemcpy(h, C.cast(ptr, C.c_void_p), 16, 2)
-    if h[1]:
-        _last['hdr'] = (h[0], h[1])
+    h = (C.c_uint64 * 4)()
+    _hip.hipMemcpy(h, C.cast(ptr, C.c_void_p), 32, 2)
+    if h[0]:
+        _last['hdr'] = tuple(h)
     elif _last['hdr']:
-        h[0], h[1] = _last['hdr']
-        _hip.hipMemcpy(C.cast(ptr, C.c_void_p), h, 16, 1)
+        for i in range(4):
+            h[i] = _last['hdr'][i]
+        _hip.hipMemcpy(C.cast(ptr, C.c_void_p), h, 32, 1)
 if kind == 'direct':
     N = 1024
     depth, rots = F.size_parameters(N)
-    ctx = F.Context(16, depth, 50, 60, 3, seed=1)
+    ctx = F.Context(16, depth, 40, 60, 3, seed=1)  # the bench config: 40-bit scaling, OpenFHE PS split
     ctx.gen_rotation_keys(rots)
     x = np.random.default_rng(1).permutation(N) / N
     ct = ctx.encrypt(x, N)
