@@ -45,6 +45,18 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
     return COLS ? idx * (NB + 1) + tr : tr * ((1 << PB) + (1 << PB) / 16) + idx + (idx >> 4);
 }
 
+// Split exchange (column passes with G = E / T >= 2 groups per lane: the
+// 512-point columns of ring 2^17).  The L1 -> L2 re-deal runs in G phases
+// through a tile of 1/G the size: phase g moves the L1 registers r = G u + g
+// (exactly the elements of every lane's L2 group g) and the lane reads its group
+// g back into those same registers, so no second register set is needed.  L2
+// group g element r therefore lives in register G r + g.  Halving the tile
+// (69.6 -> 34.8 KB) doubles the blocks an LDS holds.
+template <int G, int T, bool SPLIT>
+__device__ constexpr int l2reg(int g, int r) {
+    return SPLIT ? G * r + g : g * T + r;
+}
+
 // Lazy Shoup product a * w mod q in [0, 2q): a*w - floor(a*w'/2^64)*q taken
 // mod 2^64, written as a*w + h*nq with nq = 2^64 - q so both low products
 // share one multiply-accumulate chain (2 v_mad_u64_u32 + 4 v_mul_lo_u32) and
@@ -325,7 +337,9 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     constexpr int NB = NTB / T;         // transforms per block
     constexpr int G = E >> RB;          // round-2 groups per lane
     constexpr int LEN = 1 << PB;
-    __shared__ u64 tile[SH ? 1 : lds_words<PB, NB, COLS>()];
+    constexpr bool SPLIT = COLS && G >= 2;
+    constexpr int TPB = SPLIT ? PB - (EB - RB) : PB;  // points per exchange phase (log2)
+    __shared__ u64 tile[SH ? 1 : lds_words<TPB, NB, COLS>()];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
@@ -470,13 +484,25 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
             }
     }
     // ---- exchange through LDS: L1 -> L2 (idx = (t*G + g) * 2^RB + r)
+    if constexpr (SPLIT) {
 #pragma unroll
-    for (int r = 0; r < E; ++r) tile[lds_at<PB, NB, COLS>(tr, t + T * r)] = x[r];
-    __syncthreads();
+        for (int g = 0; g < G; ++g) {
+            if (g) __syncthreads();  // the previous phase's reads are done
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+            for (int u = 0; u < T; ++u) tile[lds_at<TPB, NB, COLS>(tr, u * T + t)] = x[G * u + g];
+            __syncthreads();
 #pragma unroll
-        for (int r = 0; r < T; ++r) x[g * T + r] = tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)];
+            for (int r = 0; r < T; ++r) x[G * r + g] = tile[lds_at<TPB, NB, COLS>(tr, t * T + r)];
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < E; ++r) tile[lds_at<PB, NB, COLS>(tr, t + T * r)] = x[r];
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < T; ++r) x[g * T + r] = tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)];
+    }
     // ---- round 2: local stages EB..PB-1 (pair bit PB-1-s < RB)
 #pragma unroll
     for (int s = EB; s < PB; ++s) {
@@ -491,7 +517,8 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
                 const size_t wi = ((size_t)1 << (S0 + s)) + i;
                 const ulonglong2 w =
                     PRE ? tw2[PRE ? ((1 << (s - EB)) - 1) + (r0 >> (PB - s)) : 0] : tw[wi];
-                ct_stage<PB>(COLS, s, x[g * T + r0], x[g * T + r0 + (1 << hb)], w, q4, nq);
+                ct_stage<PB>(COLS, s, x[l2reg<G, T, SPLIT>(g, r0)], x[l2reg<G, T, SPLIT>(g, r0 + (1 << hb))], w, q4,
+                             nq);
             }
     }
     // ---- store.  COLS: layout L2 is already lane-contiguous in memory
@@ -505,7 +532,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
 #pragma unroll
             for (int r = 0; r < T; ++r) {
                 const int idx = (t * G + g) * T + r;
-                if (valid) a[(size_t)idx * ((size_t)1 << k2) + tid_global] = x[g * T + r];
+                if (valid) a[(size_t)idx * ((size_t)1 << k2) + tid_global] = x[l2reg<G, T, SPLIT>(g, r)];
             }
     } else {
 #pragma unroll
@@ -538,7 +565,9 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     constexpr int NB = NTB / T;
     constexpr int G = E >> RB;
     constexpr int LEN = 1 << PB;
-    __shared__ u64 tile[SH ? 1 : lds_words<PB, NB, COLS>()];
+    constexpr bool SPLIT = COLS && G >= 2;  // split exchange (see l2reg)
+    constexpr int TPB = SPLIT ? PB - (EB - RB) : PB;
+    __shared__ u64 tile[SH ? 1 : lds_words<TPB, NB, COLS>()];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
@@ -590,7 +619,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
             for (int r = 0; r < T; ++r) {
                 const int idx = (t * G + g) * T + r;
                 const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
-                x[g * T + r] = valid ? ain[off] : 0;
+                x[l2reg<G, T, SPLIT>(g, r)] = valid ? ain[off] : 0;
             }
     } else {
 #pragma unroll
@@ -618,17 +647,30 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
 #pragma unroll
             for (int r0 = 0; r0 < T; ++r0) {
                 if (r0 & (1 << s)) continue;
-                gs_bfly(x[g * T + r0], x[g * T + r0 + (1 << s)], tws[(g * T + r0) >> (s + 1)], q4, nq);
+                gs_bfly(x[l2reg<G, T, SPLIT>(g, r0)], x[l2reg<G, T, SPLIT>(g, r0 + (1 << s))],
+                        tws[(g * T + r0) >> (s + 1)], q4, nq);
             }
     }
     // ---- exchange L2 -> L1 (idx = t + T * r)
+    if constexpr (SPLIT) {
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g) {
+            if (g) __syncthreads();
 #pragma unroll
-        for (int r = 0; r < T; ++r) tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] = x[g * T + r];
-    __syncthreads();
+            for (int r = 0; r < T; ++r) tile[lds_at<TPB, NB, COLS>(tr, t * T + r)] = x[G * r + g];
+            __syncthreads();
 #pragma unroll
-    for (int r = 0; r < E; ++r) x[r] = tile[lds_at<PB, NB, COLS>(tr, t + T * r)];
+            for (int u = 0; u < T; ++u) x[G * u + g] = tile[lds_at<TPB, NB, COLS>(tr, u * T + t)];
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < T; ++r) tile[lds_at<PB, NB, COLS>(tr, (t * G + g) * T + r)] = x[g * T + r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < E; ++r) x[r] = tile[lds_at<PB, NB, COLS>(tr, t + T * r)];
+    }
     // ---- round B: local stages RB..PB-1 (pair bit s >= RB, i.e. bit s-RB of r)
 #pragma unroll
     for (int s = RB; s < PB; ++s) {
