@@ -1016,14 +1016,28 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
     const int W = ell + K;
     // ext (+ own digit) and 2 accumulators per member; the key once
     const double B = 8.0 * ((double)members * (digits * W + 2.0 * W) + 2.0 * digits * W) * ((size_t)1 << logN);
-    if (members >= 4) {  // member groups of 4 (8 measured the same): the key words stay in registers
-        constexpr int MC = 4;
-        const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W, (unsigned)((members + MC - 1) / MC));
-        dispatch_int<1, 8>(digits, [&](auto c) {
-            constexpr int D = decltype(c)::value;
-            launch_clocked("k_ks_inner", B, k_ks_inner_mc<D, MC>, grid, dim3(NT), st, acc, ext, dntt, key, ell, W,
-                           nall, alpha, members, perm, pmap_ext, mods, logN, str, fold);
-        });
+    // member groups of MC (FHE_KS_MC=4 for A/B): the key words stay in registers
+    // for the MC members of a thread; 8 reads the key half as often as 4
+    // (MEHP24 12.74 -> 12.69 s, DirectSort 690.8 -> 689.0 ms, profiles/r3_h)
+    static const int mc_env = [] {
+        const char *e = std::getenv("FHE_KS_MC");
+        return e && std::atoi(e) == 4 ? 4 : 8;
+    }();
+    if (members >= 4) {
+        auto go = [&](auto mcc) {
+            constexpr int MC = decltype(mcc)::value;
+            const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W,
+                            (unsigned)((members + MC - 1) / MC));
+            dispatch_int<1, 8>(digits, [&](auto c) {
+                constexpr int D = decltype(c)::value;
+                launch_clocked("k_ks_inner", B, k_ks_inner_mc<D, MC>, grid, dim3(NT), st, acc, ext, dntt, key, ell, W,
+                               nall, alpha, members, perm, pmap_ext, mods, logN, str, fold);
+            });
+        };
+        if (mc_env == 8 && members >= 8)
+            go(std::integral_constant<int, 8>{});
+        else
+            go(std::integral_constant<int, 4>{});
         return;
     }
     const dim3 grid((unsigned)members, (unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
