@@ -1167,15 +1167,15 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
         Engine &E = *L.eng;
         CtPtr acc;
         for (size_t c0 = 0; c0 < bs.size(); c0 += chunk) {
-            std::vector<CtPtr> diffs;
+            std::vector<CtPtr> shifted;
             std::vector<const Ciphertext *> ptrs;
             for (size_t i = c0; i < std::min(bs.size(), c0 + chunk); ++i) {
-                CtPtr shifted = vecRotsOpt(L, baby, s.num_partition, s.num_slots, s.np, bs[i]);
-                diffs.push_back(E.sub(*dup, *shifted));
-                ptrs.push_back(diffs.back().get());
+                shifted.push_back(vecRotsOpt(L, baby, s.num_partition, s.num_slots, s.np, bs[i]));
+                ptrs.push_back(shifted.back().get());
             }
-            CtPtr d = ptrs.size() == 1 ? diffs[0] : E.stack(ptrs);
-            diffs.clear();
+            // x - s_b of every batch written straight into the stacked ciphertext
+            CtPtr d = ptrs.size() == 1 ? E.sub(*dup, *shifted[0]) : E.sub_stacked(*dup, ptrs);
+            shifted.clear();
             CtPtr sg = sign(*d, E, f, cfg);
             CtPtr c = E.mul_const(*E.add_const(*sg, 1.0), 0.5);
             E.add_inplace(acc, c->batch == 1 ? *c : *E.sum_members(*c));
@@ -1243,19 +1243,17 @@ CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext 
         Engine &E = *L.eng;
         CtPtr acc;
         for (size_t c0 = 0; c0 < bs.size(); c0 += chunk) {
-            std::vector<CtPtr> ris;
-            std::vector<const Ciphertext *> ptrs;
+            std::vector<const Plaintext *> chks;
             std::vector<int> ibs;
             for (size_t i = c0; i < std::min(bs.size(), c0 + chunk); ++i) {
                 const int b = bs[i];
-                const Plaintext &chk = mask(E, 1, s.num_slots, b * s.num_partition, 0, imr->level);
-                CtPtr ri = E.sub_plain(*imr, chk);
-                ris.push_back(E.mul_const(*ri, 1.0 / N / 2));
-                ptrs.push_back(ris.back().get());
+                chks.push_back(&mask(E, 1, s.num_slots, b * s.num_partition, 0, imr->level));
                 ibs.push_back(b);
             }
-            CtPtr r = ptrs.size() == 1 ? ris[0] : E.stack(ptrs);
-            ris.clear();
+            // (imr - checking vector_b) / 2N of every batch: the differences written
+            // straight into one stacked ciphertext, one scaling for all of them
+            CtPtr r = E.mul_const(*(chks.size() == 1 ? E.sub_plain(*imr, *chks[0]) : E.sub_plain_stacked(*imr, chks)),
+                                  1.0 / N / 2);
             r = evalChebyshevSeriesPS(E, *r, coeffs, -1.0, 1.0);
             CtPtr masked = E.mul(*r, *xs);  // xs broadcast over the members
             r.reset();

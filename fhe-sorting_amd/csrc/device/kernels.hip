@@ -127,6 +127,34 @@ __global__ __launch_bounds__(NT) void k_add_scalar(u64 *out, const u64 *a, int64
     const ulonglong2 x = ld2(a + oa);
     st2(out + oo, make_ulonglong2(add_mod(x.x, w, q), add_mod(x.y, w, q)));
 }
+// out = a with the c0 of every member changed (one pass over both polys, no
+// separate copy): segment z = 2 member + poly, ln = limbs n.  mode 0: c0 + K 2^sh;
+// 1: c0 + p; 2: c0 - p; 3: p - c0 and c1 negated (p - a)
+__global__ __launch_bounds__(NT) void k_c0_op(u64 *out, const u64 *a, const u64 *p, int64_t K, int sh, int mode,
+                                              size_t ln_seg, const Mod *mods, int logN) {
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const int z = blockIdx.z;
+    const size_t o = (size_t)z * ln_seg + (size_t)l * n + k;
+    const u64 q = mods[l].q;
+    ulonglong2 x = ld2(a + o);
+    if (!(z & 1)) {
+        if (mode == 0) {
+            const u64 w = smod(K, sh, mods[l]);
+            x = make_ulonglong2(add_mod(x.x, w, q), add_mod(x.y, w, q));
+        } else {
+            const ulonglong2 y = ld2(p + (size_t)l * n + k);
+            x = mode == 1 ? make_ulonglong2(add_mod(x.x, y.x, q), add_mod(x.y, y.y, q))
+              : mode == 2 ? make_ulonglong2(sub_mod(x.x, y.x, q), sub_mod(x.y, y.y, q))
+                          : make_ulonglong2(sub_mod(y.x, x.x, q), sub_mod(y.y, x.y, q));
+        }
+    } else if (mode == 3) {
+        x = make_ulonglong2(sub_mod(0, x.x, q), sub_mod(0, x.y, q));
+    }
+    st2(out + o, x);
+}
 __global__ __launch_bounds__(NT) void k_mul_plain(u64 *out, const u64 *a, const u64 *p, Seg S, const Mod *mods,
                                                   int logN) {
     EW_PROLOGUE
@@ -834,6 +862,12 @@ void ew_add_scalar(u64 *out, const u64 *a, int64_t K, int limbs, int segs, Seg S
                    hipStream_t st, int sh) {
     if (limbs <= 0 || segs <= 0) return;
     hipLaunchKernelGGL(k_add_scalar, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, K, sh, S, mods, logN);
+}
+void ew_c0_op(u64 *out, const u64 *a, const u64 *p, int64_t K, int sh, int mode, int limbs, int members,
+              const Mod *mods, int logN, hipStream_t st) {
+    if (limbs <= 0 || members <= 0) return;
+    hipLaunchKernelGGL(k_c0_op, ew_grid(logN, limbs, 2 * members), dim3(NT), 0, st, out, a, p, K, sh, mode,
+                       (size_t)limbs << logN, mods, logN);
 }
 void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, Seg S, const Mod *mods, int logN,
                   hipStream_t st) {

@@ -167,6 +167,10 @@ void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, in
 void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,
                 hipStream_t st);
 // out[l][k] = coef[k] mod q_{pmap[l]} (signed 64-bit coefficients)
+// out = a ([members][2][limbs][n]) with every member's c0 changed: mode 0 c0 + K 2^sh,
+// 1 c0 + p, 2 c0 - p, 3 (p - c0, -c1); p [limbs][n] shared by the members
+void ew_c0_op(u64 *out, const u64 *a, const u64 *p, int64_t K, int sh, int mode, int limbs, int members,
+              const Mod *mods, int logN, hipStream_t st);
 void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap, const Mod *mods, int logN,
                       hipStream_t st);
 

@@ -992,34 +992,32 @@ CtPtr Engine::negate(const Ciphertext &a) {
     return r;
 }
 // plaintext ops touch c0 of every member: segments 0, 2, 4, ... (stride 2 limbs n)
+// plaintext and constant ops change c0 only; one pass writes the whole result
+// (k_c0_op: c1 copied through), so no clone precedes them
 CtPtr Engine::add_plain(const Ciphertext &a, const Plaintext &p) {
     if (p.level != a.level) throw std::invalid_argument("add_plain: level mismatch");
-    auto r = clone(a);
-    const size_t l2 = 2 * a.limbs * n();
-    dev::ew_add(r->data, r->data, p.data, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
+    dev::ew_c0_op(r->data, a.data, p.data, 0, 0, 1, (int)a.limbs, a.batch, MODS, LOGN, ST);
     count_bytes(5.0 * a.limbs, a.batch);
     return r;
 }
 CtPtr Engine::sub_plain(const Ciphertext &a, const Plaintext &p) {
     if (p.level != a.level) throw std::invalid_argument("sub_plain: level mismatch");
-    auto r = clone(a);
-    const size_t l2 = 2 * a.limbs * n();
-    dev::ew_sub(r->data, r->data, p.data, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
+    dev::ew_c0_op(r->data, a.data, p.data, 0, 0, 2, (int)a.limbs, a.batch, MODS, LOGN, ST);
     count_bytes(5.0 * a.limbs, a.batch);
     return r;
 }
 CtPtr Engine::plain_sub(const Plaintext &p, const Ciphertext &a) {
     if (p.level != a.level) throw std::invalid_argument("plain_sub: level mismatch");
-    auto r = negate(a);
-    const size_t l2 = 2 * a.limbs * n();
-    dev::ew_add(r->data, r->data, p.data, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST);
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
+    dev::ew_c0_op(r->data, a.data, p.data, 0, 0, 3, (int)a.limbs, a.batch, MODS, LOGN, ST);
     return r;
 }
 CtPtr Engine::add_const(const Ciphertext &a, double c) {
-    auto r = clone(a);
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);
     const host::SConst K = host::const_at_scale(c, a.scale);
-    const size_t l2 = 2 * a.limbs * n();
-    dev::ew_add_scalar(r->data, r->data, K.k, (int)a.limbs, a.batch, seg3(l2, l2, 0), MODS, LOGN, ST, K.sh);
+    dev::ew_c0_op(r->data, a.data, nullptr, K.k, K.sh, 0, (int)a.limbs, a.batch, MODS, LOGN, ST);
     count_bytes(4.0 * a.limbs, a.batch);
     return r;
 }
@@ -1619,6 +1617,42 @@ CtPtr Engine::member(const Ciphertext &a, int m) {
     auto r = std::make_shared<Ciphertext>(a);
     r->data = a.data + (size_t)m * 2 * a.limbs * n();
     r->batch = 1;
+    return r;
+}
+CtPtr Engine::sub_stacked(const Ciphertext &a0, const std::vector<const Ciphertext *> &bs) {
+    if (bs.empty()) throw std::invalid_argument("sub_stacked: no operands");
+    if (a0.batch != 1) throw std::invalid_argument("sub_stacked: a must be one ciphertext");
+    const int level = bs[0]->level;
+    for (auto *b : bs)
+        if (b->level != level || b->batch != 1) throw std::invalid_argument("sub_stacked: operands differ in level");
+    CtPtr a = std::make_shared<Ciphertext>(a0);
+    if (a->level < level) a = level_adjust(*a, level);  // sub(a, b) adjusts a the same way
+    if (a->level > level) {                             // ... or every b: not stackable in place
+        std::vector<CtPtr> d;
+        std::vector<const Ciphertext *> p;
+        for (auto *b : bs) {
+            d.push_back(sub(a0, *b));
+            p.push_back(d.back().get());
+        }
+        return stack(p);
+    }
+    const size_t ln = a->limbs * n();
+    auto r = new_ct(a->level, a->slots, a->scale, a->limbs, (int)bs.size());
+    for (size_t i = 0; i < bs.size(); ++i)
+        dev::ew_sub(r->data + i * 2 * ln, a->data, bs[i]->data, (int)a->limbs, 2, seg3(ln, ln, ln), MODS, LOGN, ST);
+    count_bytes(6.0 * a->limbs, (int)bs.size());
+    return r;
+}
+CtPtr Engine::sub_plain_stacked(const Ciphertext &a, const std::vector<const Plaintext *> &ps) {
+    if (ps.empty()) throw std::invalid_argument("sub_plain_stacked: no plaintexts");
+    if (a.batch != 1) throw std::invalid_argument("sub_plain_stacked: a must be one ciphertext");
+    for (auto *p : ps)
+        if (p->level != a.level) throw std::invalid_argument("sub_plain_stacked: level mismatch");
+    const size_t ln = a.limbs * n();
+    auto r = new_ct(a.level, a.slots, a.scale, a.limbs, (int)ps.size());
+    for (size_t i = 0; i < ps.size(); ++i)
+        dev::ew_c0_op(r->data + i * 2 * ln, a.data, ps[i]->data, 0, 0, 2, (int)a.limbs, 1, MODS, LOGN, ST);
+    count_bytes(5.0 * a.limbs, (int)ps.size());
     return r;
 }
 CtPtr Engine::sum_members(const Ciphertext &a) {

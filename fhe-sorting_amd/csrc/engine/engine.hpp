@@ -201,6 +201,10 @@ class Engine {
     // batches: stack (copies; equal levels), member view (no copy), member sum
     CtPtr stack(const std::vector<const Ciphertext *> &xs);
     CtPtr member(const Ciphertext &a, int m);
+    // batches built in place (no stack copies): member i = a - bs[i] (a brought to
+    // the bs' level once), and member i = a - ps[i]
+    CtPtr sub_stacked(const Ciphertext &a, const std::vector<const Ciphertext *> &bs);
+    CtPtr sub_plain_stacked(const Ciphertext &a, const std::vector<const Plaintext *> &ps);
     CtPtr sum_members(const Ciphertext &a);
     // sum over ranks already done into ct (u64 add, no reduction): reduce mod q
     void reduce_after_allreduce(Ciphertext &ct);

@@ -1,0 +1,14 @@
+#!/bin/bash
+# c0 ops in one pass, stacked batches built in place: full GPU suite + benches
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$R"
+O=gpurun_out/r3w
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 400 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error" $O/gpu_tests.log | head -20; tail -30 $O/gpu_tests.log; exit 1; }
+tail -3 $O/gpu_tests.log
+timeout -k 10 300 python bench.py --steps 10 --warmup 1 --no-cpu-baseline --no-roofline > $O/bench_direct.json 2> $O/bench_direct.err || { echo "direct failed"; tail -5 $O/bench_direct.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench_direct.json'));print('direct', d['ms_per_step'], d['value'], d['max_abs_err'])"
+timeout -k 10 400 python bench.py --workload kway --steps 2 --warmup 1 --no-cpu-baseline --no-roofline > $O/bench_kway.json 2> $O/bench_kway.err || { echo "kway failed"; tail -5 $O/bench_kway.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench_kway.json'));print('kway', d['ms_per_step'], d['value'], d['max_abs_err'])"
+echo ALLOK
