@@ -1058,20 +1058,25 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
         return e && std::atoi(e) == 4 ? 4 : 8;
     }();
     if (members >= 4) {
-        auto go = [&](auto mcc) {
-            constexpr int MC = decltype(mcc)::value;
-            const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W,
-                            (unsigned)((members + MC - 1) / MC));
-            dispatch_int<1, 8>(digits, [&](auto c) {
-                constexpr int D = decltype(c)::value;
+        dispatch_int<1, 8>(digits, [&](auto c) {
+            constexpr int D = decltype(c)::value;
+            auto go = [&](auto mcc) {
+                constexpr int MC = decltype(mcc)::value;
+                const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W,
+                                (unsigned)((members + MC - 1) / MC));
                 launch_clocked("k_ks_inner", B, k_ks_inner_mc<D, MC>, grid, dim3(NT), st, acc, ext, dntt, key, ell, W,
                                nall, alpha, members, perm, pmap_ext, mods, logN, str, fold);
-            });
-        };
-        if (mc_env == 8 && members >= 8)
-            go(std::integral_constant<int, 8>{});
-        else
-            go(std::integral_constant<int, 4>{});
+            };
+            // 8 members x 5+ digits would spill the x words to scratch
+            if constexpr (D <= 4) {
+                if (mc_env == 8 && members >= 8)
+                    go(std::integral_constant<int, 8>{});
+                else
+                    go(std::integral_constant<int, 4>{});
+            } else {
+                go(std::integral_constant<int, 4>{});
+            }
+        });
         return;
     }
     const dim3 grid((unsigned)members, (unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
