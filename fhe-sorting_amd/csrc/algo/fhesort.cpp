@@ -535,16 +535,18 @@ struct PSOpenFHE {
     }
     // node at depth mm: (T2[mm-1] + c) q + s, output level lk + mm
     CtPtr node(const OFNode &N) {
-        CtPtr a = N.cu >= 0 ? cc.add(*T2[N.mm - 1], *leaf(N.cu))
-                            : (N.c0 != 0.0 ? cc.add_const(*T2[N.mm - 1], N.c0) : T2[N.mm - 1]);
+        // a = T2[mm-1] + c(u): with c(u) a leaf the sum is formed inside the
+        // product's tensor pass (Engine::mul_add's a_add; same words)
+        CtPtr cu = N.cu >= 0 ? leaf(N.cu) : nullptr;
+        CtPtr a = cu ? T2[N.mm - 1] : (N.c0 != 0.0 ? cc.add_const(*T2[N.mm - 1], N.c0) : T2[N.mm - 1]);
         CtPtr qu = N.qn ? node(*N.qn) : leaf(N.qleaf);
         if (N.sn) {
             CtPtr su = node(*N.sn);  // level lk + mm - 1: added before the product's rescale
-            return cc.mul_add(*a, *qu, {su.get()}, {1.0});
+            return cc.mul_add(*a, *qu, {su.get()}, {1.0}, nullptr, cu.get());
         }
         const double s0 = P->leaves[N.sleaf].a[0];
         CtPtr raw = leaf(N.sleaf);
-        CtPtr out = cc.mul_add_raw(*a, *qu, *raw);
+        CtPtr out = cc.mul_add_raw(*a, *qu, *raw, cu.get());
         return s0 != 0.0 ? cc.add_const(*out, s0) : out;
     }
     CtPtr run() {

@@ -165,8 +165,11 @@ __global__ __launch_bounds__(NT) void k_mul_plain(u64 *out, const u64 *a, const 
 }
 // member z: a, b [2][limbs][n] at z * sa / z * sb (sb = 0 broadcasts b);
 // d01 [members][2][limbs][n], d2 [members][limbs][n]
+// a2 (optional, member stride sa2): a + a2 is the left operand (the PS node's
+// T_{k 2^j} + c(u), formed on load instead of in a separate pass)
 __global__ __launch_bounds__(NT) void k_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, size_t ln_all,
-                                               size_t sa, size_t sb, const Mod *mods, int logN) {
+                                               size_t sa, size_t sb, const u64 *a2, size_t sa2, const Mod *mods,
+                                               int logN) {
     const size_t n = (size_t)1 << logN;
     const int l = blockIdx.y;
     const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
@@ -174,7 +177,13 @@ __global__ __launch_bounds__(NT) void k_tensor(u64 *d01, u64 *d2, const u64 *a, 
     const Mod m = mods[l];
     const size_t z = blockIdx.z, o = (size_t)l * n + k;
     const u64 *A = a + z * sa, *Bp = b + z * sb;
-    const ulonglong2 a0 = ld2(A + o), a1 = ld2(A + ln_all + o);
+    ulonglong2 a0 = ld2(A + o), a1 = ld2(A + ln_all + o);
+    if (a2) {
+        const u64 *A2 = a2 + z * sa2;
+        const ulonglong2 c0 = ld2(A2 + o), c1 = ld2(A2 + ln_all + o);
+        a0 = make_ulonglong2(add_mod(a0.x, c0.x, m.q), add_mod(a0.y, c0.y, m.q));
+        a1 = make_ulonglong2(add_mod(a1.x, c1.x, m.q), add_mod(a1.y, c1.y, m.q));
+    }
     const ulonglong2 b0 = ld2(Bp + o), b1 = ld2(Bp + ln_all + o);
     ulonglong2 e0, e1, e2;
     e0.x = mul_barrett(a0.x, b0.x, m);
@@ -875,12 +884,12 @@ void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, Seg
     hipLaunchKernelGGL(k_mul_plain, ew_grid(logN, limbs, segs), dim3(NT), 0, st, out, a, p, S, mods, logN);
 }
 void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int members, size_t sa, size_t sb,
-               const Mod *mods, int logN, hipStream_t st) {
+               const Mod *mods, int logN, hipStream_t st, const u64 *a2, size_t sa2) {
     if (limbs <= 0 || members <= 0) return;
     const size_t ln_all = (size_t)limbs << logN;
-    const double B = 8.0 * (5.0 * members + 2.0 * (sb ? members : 1)) * ln_all;
+    const double B = 8.0 * (5.0 * members + 2.0 * (sb ? members : 1) + (a2 ? 2.0 * members : 0.0)) * ln_all;
     launch_clocked("k_tensor", B, k_tensor, ew_grid(logN, limbs, members), dim3(NT), st, d01, d2, a, b, ln_all, sa, sb,
-                   mods, logN);
+                   a2, sa2, mods, logN);
 }
 void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st) {
     if (limbs <= 0 || members <= 0) return;

@@ -147,7 +147,7 @@ void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, Seg
 // per member m: d0 = a0 b0, d1 = a0 b1 + a1 b0 -> d01 [m][2][limbs][n]; d2 = a1 b1 -> d2 [m][limbs][n]
 // (a member m at m * sa, b member at m * sb; sb = 0 broadcasts one ciphertext)
 void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int members, size_t sa, size_t sb,
-               const Mod *mods, int logN, hipStream_t st);
+               const Mod *mods, int logN, hipStream_t st, const u64 *a2 = nullptr, size_t sa2 = 0);
 // out [2][limbs][n] = sum_m in [m][2][limbs][n]
 void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st);
 // out (+)= sum_i (K_i 2^sh_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride; sh may be null)

@@ -1116,9 +1116,13 @@ CtPtr Engine::mul(const Ciphertext &a0, const Ciphertext &b0) { return mul_add(a
 // pre-rescale scale (the constants of linear_sum_to(xs, c, level+1)) and added
 // to the tensor's (d0, d1) before relinearisation (oracle: Context::mul_add).
 CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vector<const Ciphertext *> &xs,
-                      const std::vector<double> &cs, const Ciphertext *raw) {
+                      const std::vector<double> &cs, const Ciphertext *raw, const Ciphertext *a_add) {
     auto &I = *impl;
     if (a0.batch != b0.batch && b0.batch != 1) throw std::invalid_argument("mul: batch size mismatch");
+    // a + a_add fused into the tensor pass only where add() would not level-adjust
+    // and the sum would not be level-adjusted against b; otherwise formed first
+    if (a_add && (a_add->level != a0.level || a_add->batch != a0.batch || a0.level < b0.level))
+        return mul_add(*add(a0, *a_add), b0, xs, cs, raw);
     auto a = std::make_shared<Ciphertext>(a0), b = std::make_shared<Ciphertext>(b0);
     match_levels(a, b);
     if (a->level >= I.P.L) throw std::runtime_error("mul: no levels left");
@@ -1132,7 +1136,8 @@ CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vec
     auto d01m = I.alloc((size_t)B * 2 * ell * nn * 8), d2m = I.alloc((size_t)B * ell * nn * 8);
     u64 *d01 = static_cast<u64 *>(d01m->p), *d2 = static_cast<u64 *>(d2m->p);
     dev::ew_tensor(d01, d2, a->data, b->data, (int)ell, B, 2 * ell * nn, b->batch == 1 ? 0 : 2 * ell * nn, MODS,
-                   LOGN, ST);
+                   LOGN, ST, a_add ? a_add->data : nullptr, 2 * ell * nn);
+    if (a_add) count_bytes(6.0 * ell, B);  // the add it replaces
     if (!xs.empty()) {
         const int target = a->level + 1;
         const u64 qd = I.P.primes[I.P.L - target + 1];
@@ -1167,8 +1172,8 @@ CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vec
     I.mul_tail(static_cast<u64 *>(extm->p), d01, d2, ell, B, r->data);
     return r;
 }
-CtPtr Engine::mul_add_raw(const Ciphertext &a, const Ciphertext &b, const Ciphertext &raw) {
-    return mul_add(a, b, {}, {}, &raw);
+CtPtr Engine::mul_add_raw(const Ciphertext &a, const Ciphertext &b, const Ciphertext &raw, const Ciphertext *a_add) {
+    return mul_add(a, b, {}, {}, &raw, a_add);
 }
 CtPtr Engine::square(const Ciphertext &a) { return mul(a, a); }
 

@@ -160,10 +160,12 @@ class Engine {
     CtPtr mul_plain_sum(const std::vector<const Ciphertext *> &a, const std::vector<const Plaintext *> &p);
     CtPtr mul(const Ciphertext &a, const Ciphertext &b);
     // a*b + sum_i c_i x_i with one rescale (lazy rescaling of PS remainders)
+    // a_add (optional): the left operand is a + a_add, formed inside the tensor
+    // pass (same words as add(a, a_add) first)
     CtPtr mul_add(const Ciphertext &a, const Ciphertext &b, const std::vector<const Ciphertext *> &xs,
-                  const std::vector<double> &cs, const Ciphertext *raw = nullptr);
+                  const std::vector<double> &cs, const Ciphertext *raw = nullptr, const Ciphertext *a_add = nullptr);
     // same with the sum already formed: raw = linear_sums_to(xs, {c}, level+1, false)[0]
-    CtPtr mul_add_raw(const Ciphertext &a, const Ciphertext &b, const Ciphertext &raw);
+    CtPtr mul_add_raw(const Ciphertext &a, const Ciphertext &b, const Ciphertext &raw, const Ciphertext *a_add = nullptr);
     CtPtr square(const Ciphertext &a);
     CtPtr rotate(const Ciphertext &a, long k);
     std::vector<CtPtr> rotate_hoisted(const Ciphertext &a, const std::vector<long> &ks);
