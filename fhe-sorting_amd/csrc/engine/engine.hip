@@ -1290,52 +1290,6 @@ CtPtr Engine::rotate_members(const Ciphertext &a, const std::vector<long> &ks) {
     return r;
 }
 
-// sum_m rotate(member m, ks[m]) with one ModDown: the key products of all
-// members accumulate over QP, the permuted c0s are summed and added by the
-// ModDown finish (oracle: Context::rotate_sum)
-CtPtr Engine::rotate_members_sum(const Ciphertext &a, const std::vector<long> &ks) {
-    auto &I = *impl;
-    if ((int)ks.size() != a.batch) throw std::invalid_argument("rotate_members_sum: one rotation per member");
-    const size_t nn = n(), ell = a.limbs, ln = ell * nn, W = ell + (size_t)I.P.K;
-    const int B = a.batch;
-    std::vector<u64> gs;
-    for (long k : ks) {
-        const u64 g = host::galois_for_rotation(I.P.logN, k);
-        if (g == 1) throw std::invalid_argument("rotate_members_sum: identity rotation");
-        if (!I.ks->rotkeys.count(g)) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
-        gs.push_back(g);
-    }
-    auto extm = I.modup(a.data + ln, ell, B, 2 * ln);
-    const int digits = I.P.digits_at(ell);
-    const size_t es = (size_t)digits * W * nn;
-    auto accm = I.alloc(2 * W * nn * 8);
-    u64 *acc = static_cast<u64 *>(accm->p);
-    auto c0m = I.alloc(ln * 8);
-    u64 *c0 = static_cast<u64 *>(c0m->p);
-    dev::KsStrides str;
-    str.acc = 0;
-    str.ext = es;
-    str.d = 2 * ln;
-    for (int b0 = 0; b0 < B; b0 += dev::KS_MAXKEYS) {
-        const int cnt = std::min(dev::KS_MAXKEYS, B - b0);
-        dev::KsKeys KK{};
-        for (int i = 0; i < cnt; ++i) {
-            KK.key[i] = static_cast<const u64 *>(I.ks->rotkeys.at(gs[b0 + i])->p);
-            KK.perm[i] = I.perm(gs[b0 + i]);
-        }
-        dev::ew_permute_sum(c0, a.data + b0 * 2 * ln, KK, (int)ell, cnt, b0 > 0, 2 * ln, MODS, LOGN, ST);
-        dev::ks_inner_multikey_sum(acc, static_cast<u64 *>(extm->p) + b0 * es, a.data + b0 * 2 * ln + ln, KK, cnt,
-                                   b0 > 0, (int)ell, I.P.K, (int)I.P.nall(), I.P.alpha, digits, I.ext(ell), MODS, LOGN,
-                                   ST, str);
-    }
-    auto r = new_ct(a.level, a.slots, a.scale, ell, 1);
-    I.ks_moddown(acc, ell, 2, r->data, c0, 0);
-    ctr.keyswitch += B;
-    ctr.rotations += B;
-    count_bytes(4.0 * ell + ks_units(ell), B);
-    return r;
-}
-
 CtPtr Engine::linear_transform_ext(const Ciphertext &x, const std::vector<long> &baby,
                                    const std::vector<LtGiant> &giants) {
     auto &I = *impl;
@@ -1396,7 +1350,7 @@ CtPtr Engine::linear_transform_ext(const Ciphertext &x, const std::vector<long> 
     const int S = (int)shifted.size();
     if (S > 0) {
         // each rotated giant's inner sum brought down to Q, then all of them
-        // rotated with their key products summed into acc (rotate_members_sum)
+        // rotated with their key products summed into acc
         auto qm = I.alloc((size_t)S * 2 * ln * 8), tm = I.alloc(2 * W * nn * 8);
         u64 *q = static_cast<u64 *>(qm->p), *tmp = static_cast<u64 *>(tm->p);
         std::vector<u64> gs;

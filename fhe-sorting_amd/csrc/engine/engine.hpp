@@ -172,8 +172,6 @@ class Engine {
     // member m of a batch rotated by ks[m] (all keyed): the giant steps of a
     // BSGS linear transform as one pipeline
     CtPtr rotate_members(const Ciphertext &a, const std::vector<long> &ks);
-    // sum over members of member m rotated by ks[m], one ModDown (bootstrap giant steps)
-    CtPtr rotate_members_sum(const Ciphertext &a, const std::vector<long> &ks);
     // Double-hoisted baby-step giant-step linear transform (oracle:
     // Context::linear_transform_ext): one ModUp of x, the baby rotations kept
     // over Q u P and multiplied there by extended plaintexts (encode_complex_ext),

@@ -233,15 +233,12 @@ class Context {
     // keyed automorphisms X -> X^g sharing one ModUp (rotations are g = 5^k)
     std::vector<CtPtr> apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs);
     CtPtr conjugate(const Ciphertext &a);                            // g = 2n - 1
-    // sum_m rotate(xs[m], ks[m]) with ONE ModDown: the key products of every
-    // member accumulate over QP and the rotated c0s are added after the ModDown
-    // (the giant steps of a bootstrap's linear transform, OpenFHE's outer sum)
-    CtPtr rotate_sum(const std::vector<const Ciphertext *> &xs, const std::vector<long> &ks);
     // Baby-step giant-step linear transform with double hoisting: one ModUp of
     // x; every baby rotation stays over Q u P (no ModDown); each giant's inner
     // sum sum_j pt_j * baby_j is formed there with extended plaintexts; the
     // unrotated giant is the starting accumulator, every other giant is brought
-    // down (ModDown), rotated and summed as in rotate_sum; one final ModDown,
+    // down (ModDown), rotated and its key products summed over Q u P with the rotated
+    // c0s added after the final ModDown (OpenFHE's outer sum); one final ModDown,
     // then the rescale.  Result: level + 1, canonical scale.
     struct LtGiant {
         long shift = 0;

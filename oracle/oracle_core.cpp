@@ -1141,42 +1141,6 @@ std::vector<CtPtr> Context::apply_galois_hoisted(const Ciphertext &a, const std:
 
 CtPtr Context::rotate(const Ciphertext &a, long k) { return rotate_hoisted(a, {k})[0]; }
 
-CtPtr Context::rotate_sum(const std::vector<const Ciphertext *> &xs, const std::vector<long> &ks) {
-    if (xs.empty() || xs.size() != ks.size()) throw std::invalid_argument("rotate_sum: one rotation per ciphertext");
-    const size_t n = P.n, ell = xs[0]->limbs, W = ell + P.K;
-    for (const Ciphertext *x : xs)
-        if (x->limbs != ell || x->level != xs[0]->level)
-            throw std::invalid_argument("rotate_sum: ciphertexts at different levels");
-    std::vector<u64> acc(2 * W * n, 0), c0(ell * n, 0), ext;
-    for (size_t m = 0; m < xs.size(); ++m) {
-        const u64 g = galois_for_rotation(P.logN, ks[m]);
-        auto it = rotkeys.find(g);
-        if (g == 1 || it == rotkeys.end())
-            throw std::out_of_range("rotate_sum: no rotation key for index " + std::to_string(ks[m]));
-        ctr.keyswitch++;
-        ctr.rotations++;
-        const auto perm = automorphism_perm(P.logN, g);
-        modup(xs[m]->poly(1, n), ell, ext);
-        keyswitch_acc(ext, ell, it->second, &perm, acc);
-        for (size_t l = 0; l < ell; ++l) {
-            const u64 q = P.primes[l];
-            const u64 *a0 = xs[m]->poly(0, n) + l * n;
-            u64 *o = c0.data() + l * n;
-            for (size_t c = 0; c < n; ++c) o[c] = mod_add(o[c], a0[perm[c]], q);
-        }
-    }
-    auto r = make_ct(xs[0]->level, xs[0]->slots, xs[0]->scale, ell, n);
-    moddown(acc.data(), ell, r->poly(0, n));
-    moddown(acc.data() + W * n, ell, r->poly(1, n));
-    for (size_t l = 0; l < ell; ++l) {
-        const u64 q = P.primes[l];
-        u64 *o = r->poly(0, n) + l * n;
-        const u64 *c = c0.data() + l * n;
-        for (size_t k = 0; k < n; ++k) o[k] = mod_add(o[k], c[k], q);
-    }
-    return r;
-}
-
 CtPtr Context::linear_transform_ext(const Ciphertext &x, const std::vector<long> &baby,
                                     const std::vector<LtGiant> &giants) {
     const size_t n = P.n, nq = P.nq(), K = P.K, ell = x.limbs, W = ell + K;
