@@ -94,6 +94,22 @@ DiagMap compose(const DiagMap &A, const DiagMap &B, long m) {
     return C;
 }
 
+// Partial trace: log2(n / 2s) doubling steps x += rot(x, 2^b s), taken three at
+// a time as one hoisted sum x + sum_{0 < j < 8} rot(x, j 2^b0 s) (one ModUp and
+// one ModDown per chunk instead of one of each per step)
+std::vector<std::vector<long>> traceChunks(size_t n, long s) {
+    int t = 0;
+    while (((size_t)s << (t + 1)) <= n / 2) ++t;
+    std::vector<std::vector<long>> out;
+    for (int b0 = 0; b0 < t; b0 += 3) {
+        const int c = std::min(3, t - b0);
+        std::vector<long> ks;
+        for (long j = 1; j < (1L << c); ++j) ks.push_back(j * (s << b0));
+        out.push_back(std::move(ks));
+    }
+    return out;
+}
+
 // stages per level: the first (stages mod budget) levels take one more
 std::vector<int> level_sizes(int stages, int budget) {
     budget = std::max(1, std::min(budget, stages));
@@ -220,7 +236,8 @@ Bootstrapper::Bootstrapper(Engine &c, const BootstrapConfig &cf) : cc(c), cfg(cf
 std::vector<int> Bootstrapper::rotationIndices() const {
     std::set<long> r;
     const long s = cfg.slots;
-    for (long j = 1; (size_t)(j * s) < cc.params().n / 2; j <<= 1) r.insert(j * s);
+    for (const auto &ks : traceChunks(cc.params().n, s))
+        for (long k : ks) r.insert(k);
     for (const auto *levels : {&enc, &dec})
         for (const Level &lv : *levels) {
             for (long b : lv.baby)
@@ -299,8 +316,7 @@ CtPtr Bootstrapper::evalBootstrap(const Ciphertext &in) {
     const double q0 = (double)cc.params().primes[0];
     CtPtr x = cc.mul_const_to(in, std::ldexp(q0, -cfg.correctionBits) / cc.delta(L), L);
     x = cc.mod_raise(*x);
-    for (long j = 1; (size_t)(j * cfg.slots) < cc.params().n / 2; j <<= 1)  // partial trace
-        x = cc.add(*x, *cc.rotate(*x, j * cfg.slots));
+    for (const auto &ks : traceChunks(cc.params().n, cfg.slots)) x = cc.rotate_sum_hoisted(*x, ks);  // partial trace
     x = coeffsToSlots(*x);
     x = evalMod(*x);
     return slotsToCoeffs(*x);

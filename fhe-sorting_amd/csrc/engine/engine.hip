@@ -1290,6 +1290,43 @@ CtPtr Engine::rotate_members(const Ciphertext &a, const std::vector<long> &ks) {
     return r;
 }
 
+CtPtr Engine::rotate_sum_hoisted(const Ciphertext &x, const std::vector<long> &ks) {
+    auto &I = *impl;
+    if (x.batch != 1) throw std::invalid_argument("rotate_sum_hoisted: one ciphertext at a time");
+    if (ks.empty()) return clone(x);
+    const size_t nn = n(), ell = x.limbs, ln = ell * nn, W = ell + (size_t)I.P.K;
+    const int digits = I.P.digits_at(ell);
+    std::vector<u64> gs;
+    for (long k : ks) {
+        const u64 g = host::galois_for_rotation(I.P.logN, k);
+        if (g == 1) throw std::invalid_argument("rotate_sum_hoisted: identity rotation");
+        if (!I.ks->rotkeys.count(g)) throw NoKeyError("rotate: no rotation key for index " + std::to_string(k));
+        gs.push_back(g);
+    }
+    auto extm = I.modup(x.data + ln, ell, 1, 2 * ln);
+    auto accm = I.alloc(2 * W * nn * 8), c0m = I.alloc(ln * 8);
+    u64 *acc = static_cast<u64 *>(accm->p), *c0 = static_cast<u64 *>(c0m->p);
+    dev::KsStrides str;  // every rotation reads the one hoisted ModUp and x's c1
+    for (size_t b0 = 0; b0 < gs.size(); b0 += dev::KS_MAXKEYS) {
+        const int cnt = (int)std::min<size_t>(dev::KS_MAXKEYS, gs.size() - b0);
+        dev::KsKeys KK{};
+        for (int i = 0; i < cnt; ++i) {
+            KK.key[i] = static_cast<const u64 *>(I.ks->rotkeys.at(gs[b0 + i])->p);
+            KK.perm[i] = I.perm(gs[b0 + i]);
+        }
+        dev::ew_permute_sum(c0, x.data, KK, (int)ell, cnt, b0 > 0, 0, MODS, LOGN, ST);
+        dev::ks_inner_multikey_sum(acc, static_cast<u64 *>(extm->p), x.data + ln, KK, cnt, b0 > 0, (int)ell, I.P.K,
+                                   (int)I.P.nall(), I.P.alpha, digits, I.ext(ell), MODS, LOGN, ST, str);
+    }
+    auto t = new_ct(x.level, x.slots, x.scale, ell, 1);
+    I.ks_moddown(acc, ell, 2, t->data, c0, 0);
+    dev::ew_add(t->data, t->data, x.data, (int)ell, 2, seg3(ln, ln, ln), MODS, LOGN, ST);
+    ctr.keyswitch += gs.size();
+    ctr.rotations += gs.size();
+    count_bytes((4.0 * ell + ks_units(ell)) * (double)gs.size() + 6.0 * ell, 1);
+    return t;
+}
+
 CtPtr Engine::linear_transform_ext(const Ciphertext &x, const std::vector<long> &baby,
                                    const std::vector<LtGiant> &giants) {
     auto &I = *impl;

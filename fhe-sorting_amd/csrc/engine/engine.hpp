@@ -172,6 +172,10 @@ class Engine {
     // member m of a batch rotated by ks[m] (all keyed): the giant steps of a
     // BSGS linear transform as one pipeline
     CtPtr rotate_members(const Ciphertext &a, const std::vector<long> &ks);
+    // x + sum_k rotate(x, k) with one ModUp and one ModDown (the key products of
+    // every rotation summed over Q u P, the rotated c0s added after the ModDown;
+    // oracle: Context::rotate_sum_hoisted) -- the bootstrap's partial trace
+    CtPtr rotate_sum_hoisted(const Ciphertext &x, const std::vector<long> &ks);
     // Double-hoisted baby-step giant-step linear transform (oracle:
     // Context::linear_transform_ext): one ModUp of x, the baby rotations kept
     // over Q u P and multiplied there by extended plaintexts (encode_complex_ext),

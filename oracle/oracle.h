@@ -233,6 +233,10 @@ class Context {
     // keyed automorphisms X -> X^g sharing one ModUp (rotations are g = 5^k)
     std::vector<CtPtr> apply_galois_hoisted(const Ciphertext &a, const std::vector<u64> &gs);
     CtPtr conjugate(const Ciphertext &a);                            // g = 2n - 1
+    // x + sum_k rotate(x, k) with one ModUp and one ModDown: the key products of
+    // every rotation accumulate over Q u P, the rotated c0s are added after the
+    // ModDown (the bootstrap's partial trace)
+    CtPtr rotate_sum_hoisted(const Ciphertext &x, const std::vector<long> &ks);
     // Baby-step giant-step linear transform with double hoisting: one ModUp of
     // x; every baby rotation stays over Q u P (no ModDown); each giant's inner
     // sum sum_j pt_j * baby_j is formed there with extended plaintexts; the

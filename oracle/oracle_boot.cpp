@@ -139,6 +139,21 @@ std::vector<int> split_levels(int stages, int budget) {
     return g;
 }
 
+// partial trace: the log2(n / 2s) doubling steps three at a time, each chunk the
+// hoisted sum x + sum_{0 < j < 2^c} rot(x, j 2^b0 s) (engine: traceChunks)
+std::vector<std::vector<long>> trace_chunks(size_t n, long s) {
+    int t = 0;
+    while (((size_t)s << (t + 1)) <= n / 2) ++t;
+    std::vector<std::vector<long>> out;
+    for (int b0 = 0; b0 < t; b0 += 3) {
+        const int c = std::min(3, t - b0);
+        std::vector<long> ks;
+        for (long j = 1; j < (1L << c); ++j) ks.push_back(j * (s << b0));
+        out.push_back(std::move(ks));
+    }
+    return out;
+}
+
 // baby-step giant-step plan of one level: diagonal x step = G + (emin + i) step,
 // baby i < b.  A baby costs one key product inside linear_transform_ext (no
 // ModDown); a rotated giant a ModDown, a ModUp and a key switch of its own,
@@ -253,7 +268,8 @@ Bootstrapper::Bootstrapper(Context &c, const BootConfig &cf) : cc(c), cfg(cf) {
 std::vector<int> Bootstrapper::rotation_indices() const {
     std::set<long> r;
     const long s = cfg.slots;
-    for (long j = 1; (size_t)(j * s) < cc.P.n / 2; j <<= 1) r.insert(j * s);
+    for (const auto &ks : trace_chunks(cc.P.n, s))
+        for (long k : ks) r.insert(k);
     for (const auto *set : {&cts, &stc})
         for (const LinLevel &lv : *set) {
             for (long b : lv.baby)
@@ -330,7 +346,7 @@ CtPtr Bootstrapper::bootstrap(const Ciphertext &in) {
     const double q0 = (double)cc.P.primes[0];
     CtPtr x = cc.mul_const_to(in, std::ldexp(q0, -cfg.correction_bits) / cc.delta(L), L);
     x = cc.mod_raise(*x);
-    for (long j = 1; (size_t)(j * cfg.slots) < cc.P.n / 2; j <<= 1) x = cc.add(*x, *cc.rotate(*x, j * cfg.slots));
+    for (const auto &ks : trace_chunks(cc.P.n, cfg.slots)) x = cc.rotate_sum_hoisted(*x, ks);
     x = coeffs_to_slots(*x);
     x = eval_mod(*x);
     return slots_to_coeffs(*x);

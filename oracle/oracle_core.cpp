@@ -1141,6 +1141,36 @@ std::vector<CtPtr> Context::apply_galois_hoisted(const Ciphertext &a, const std:
 
 CtPtr Context::rotate(const Ciphertext &a, long k) { return rotate_hoisted(a, {k})[0]; }
 
+CtPtr Context::rotate_sum_hoisted(const Ciphertext &x, const std::vector<long> &ks) {
+    if (ks.empty()) return clone(x);
+    const size_t n = P.n, ell = x.limbs, W = ell + P.K;
+    std::vector<u64> ext, acc(2 * W * n, 0), c0(ell * n, 0);
+    modup(x.poly(1, n), ell, ext);
+    for (long k : ks) {
+        const u64 g = galois_for_rotation(P.logN, k);
+        auto it = rotkeys.find(g);
+        if (g == 1 || it == rotkeys.end())
+            throw std::out_of_range("rotate_sum_hoisted: no rotation key for index " + std::to_string(k));
+        ctr.keyswitch++;
+        ctr.rotations++;
+        const auto perm = automorphism_perm(P.logN, g);
+        keyswitch_acc(ext, ell, it->second, &perm, acc);
+        for (size_t t = 0; t < ell; ++t)
+            for (size_t c = 0; c < n; ++c)
+                c0[t * n + c] = mod_add(c0[t * n + c], x.poly(0, n)[t * n + perm[c]], P.primes[t]);
+    }
+    auto r = make_ct(x.level, x.slots, x.scale, ell, n);
+    moddown(acc.data(), ell, r->poly(0, n));
+    moddown(acc.data() + W * n, ell, r->poly(1, n));
+    for (size_t t = 0; t < ell; ++t)
+        for (size_t c = 0; c < n; ++c) {
+            u64 &o0 = r->poly(0, n)[t * n + c], &o1 = r->poly(1, n)[t * n + c];
+            o0 = mod_add(mod_add(o0, c0[t * n + c], P.primes[t]), x.poly(0, n)[t * n + c], P.primes[t]);
+            o1 = mod_add(o1, x.poly(1, n)[t * n + c], P.primes[t]);
+        }
+    return r;
+}
+
 CtPtr Context::linear_transform_ext(const Ciphertext &x, const std::vector<long> &baby,
                                     const std::vector<LtGiant> &giants) {
     const size_t n = P.n, nq = P.nq(), K = P.K, ell = x.limbs, W = ell + K;

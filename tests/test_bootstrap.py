@@ -34,8 +34,11 @@ def test_bootstrap_rotation_set(ctx):
     B = O.Bootstrapper(ctx, 8, (2, 2), keygen=False)
     r = B.rotations()
     assert r == sorted(set(r)) and all(0 < k < 16 or k % 8 == 0 for k in r)
-    # partial trace over the n/2s copies of the 8 slots: rotations by 8, 16, ..., n/4
-    assert [k for k in r if k >= 16] == [8 * 2 ** j for j in range(1, 7)]
+    # partial trace over the n/2s = 128 copies of the 8 slots: its 7 doubling steps
+    # three at a time as hoisted sums, x + sum_{0<j<2^c} rot(x, j 2^b0 8), so the
+    # keys are j 8 (j < 8), j 64 (j < 8) and 512
+    trace = sorted({j * (8 << b0) for b0, c in ((0, 3), (3, 3), (6, 1)) for j in range(1, 1 << c)})
+    assert [k for k in r if k >= 16] == [k for k in trace if k >= 16]
 
 
 def test_bootstrap_level_and_slot_checks(ctx):
