@@ -399,6 +399,26 @@ def cpu_baseline(logN, depth, N, sample_mults, scale_bits, dnum=3):
             'kind': 'port', 'sample': sample, 'seconds': round(dt, 2), 'hmults': c['hmult']}
 
 
+def oracle_full_sort(N, logN, depth, scale_bits, ps_split):
+    """The CPU oracle's whole sort of this exact configuration, when a golden
+    digest recorded one (tests/golden/make_digests.py runs it once, about an
+    hour on the build container's CPU; the GPU reproduces its output words,
+    tests/test_gpu_digests.py).  Reported beside the bounded sample, never
+    re-run here."""
+    try:
+        with open(os.path.join(REPO, 'tests', 'golden', 'sort_digests.json')) as f:
+            digests = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for name, c in digests.items():
+        if (c.get('N'), c.get('logN'), c.get('depth'), c.get('scale_bits'), c.get('ps_split', 0)) == \
+                (N, logN, depth, scale_bits, 1 if ps_split == 'openfhe' else 0) and 'oracle_sort_s' in c:
+            return {'seconds': c['oracle_sort_s'], 'threads': c.get('oracle_threads'), 'digest': name,
+                    'where': 'build container (not the GPU box), tests/golden/sort_digests.json',
+                    'output': 'word-identical to the GPU sort'}
+    return None
+
+
 def make_allreduce(ctx, d):
     """RCCL when every rank has its own GPU, else a host + gloo exchange."""
     if d.world > 1 and d.rccl:
@@ -744,6 +764,9 @@ def main():
         if d.world == 1 and not a.no_cpu_baseline:
             try:
                 res['cpu_baseline'] = cpu_baseline(logN, depth, N, a.cpu_sample_mults, a.scale_bits)
+                full = oracle_full_sort(N, logN, depth, a.scale_bits, a.ps_split)
+                if full:
+                    res['cpu_baseline']['full_sort'] = full
             except Exception as e:
                 res['cpu_baseline'] = {'error': str(e)}
         print(json.dumps(res), flush=True)
