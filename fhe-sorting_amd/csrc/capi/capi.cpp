@@ -11,6 +11,7 @@
 #include "../../../include/fhe_gpu.h"
 #include "../algo/bootstrap.hpp"
 #include "../algo/fhesort.hpp"
+#include "../device/kernels.hpp"
 #include "../algo/kway.hpp"
 #include "../engine/engine.hpp"
 #include "../wire/wire.hpp"
@@ -888,6 +889,7 @@ int fhe_automorph_dev(fhe_ctx *ctx, const uint64_t *dev_in, int limbs, uint64_t 
         ctx->eng->automorph_dev(dev_in, dev_out, (size_t)limbs, galois, stream);
     });
 }
+int fhe_set_mfma_sums(int mask) { return fhe::dev::set_mfma_sums(mask); }
 int fhe_modup(fhe_ctx *ctx, const uint64_t *d, int ell, uint64_t *ext) {
     return guard([&] { ctx->eng->modup_host(d, (size_t)ell, ext); });
 }

@@ -52,6 +52,36 @@ inline int conv_chunk(int logN, int targets, int zdim) {
     return std::max(4, (targets + chunks - 1) / chunks);
 }
 
+// compile-time dispatch of a small runtime integer (digit size, special-prime count)
+template <int Lo, int Hi, typename F>
+void dispatch_int(int v, F &&f) {
+    if constexpr (Lo > Hi) {
+        throw std::invalid_argument("unsupported basis size " + std::to_string(v));
+    } else {
+        if (v == Lo)
+            f(std::integral_constant<int, Lo>{});
+        else
+            dispatch_int<Lo + 1, Hi>(v, std::forward<F>(f));
+    }
+}
+
+// i8-MFMA sums of products; FHE_MFMA is a mask of the kernels that use them
+// (1: PS linear sums, 2: ModUp, 4: ModDown+rescale; 0 = the VALU kernels --
+// the words are the same either way; fhe_set_mfma_sums sets it at run time)
+enum { MF_LIN = 1, MF_MODUP = 2, MF_MODDOWN = 4 };
+constexpr int MFMA_DEFAULT = MF_LIN;  // measured: linear sums gain on MFMA, the conversions do not
+std::atomic<int> g_mfma_mask{-1};  // -1: not yet read from FHE_MFMA
+inline int mfma_mask() {
+    int m = g_mfma_mask.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char *e = std::getenv("FHE_MFMA");
+        m = e ? std::atoi(e) & 7 : MFMA_DEFAULT;
+        g_mfma_mask.store(m, std::memory_order_relaxed);
+    }
+    return m;
+}
+inline bool use_mfma_sums(int which) { return (mfma_mask() & which) != 0; }
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
 
 // --------------------------------------------------------- element-wise ----
@@ -307,6 +337,191 @@ __global__ __launch_bounds__(NT) void k_linear_sum_multi(MultiLinArgs A, size_t 
     for (int g = 0; g < G; ++g) A.out[g][oo] = reduce128(run[g], md);
 }
 
+// ------------------------------------------------ RNS sums of products on MFMA ----
+// A sum of products out_t = sum_i c_{t,i} y_i mod q with word-sized residues is
+// a GEMM over the integers followed by one reduction per output, so it runs on
+// the i8 matrix cores (v_mfma_i32_16x16x64_i8):
+//   * y (< 2^60) is split into 8 bytes u_a; bytes 0..6 are XORed with 0x80,
+//     which makes them the signed bytes u_a - 128 (byte 7 < 16 stays as it is):
+//     sum_a s_a 256^a = y - C0, C0 = 0x0080808080808080;
+//   * c (< 2^60) is written in balanced base-256 digits e_0..e_7 in [-128, 128);
+//   * the K index runs over (source i, byte a) and the M index over (output t,
+//     shift s = a + c'), with A[(t, s), (i, a)] = e_{s-a}(c_{t,i}), so row s of
+//     output t accumulates sum_{i, a} s_{i,a} e_{s-a} exactly in int32 (at most
+//     256 terms of magnitude <= 2^14 per row);
+//   * out_t = sum_s v_s 256^s + C0 sum_i c_{t,i}: sixteen int32 rows combined
+//     into a signed 128-bit value (|value| < 32 * 2^120) and reduced once.
+// Rows are ordered so that one lane holds all sixteen shifts of one output: a
+// 16x16 tile kk of a group of four outputs has row 4 g + r = (output g, shift
+// 4 kk + r), and the C/D layout (col = lane & 15, row = 4 (lane >> 4) + reg)
+// puts output g = lane >> 4, shifts 4 kk .. 4 kk + 3 into lane `lane`'s four
+// accumulator registers of tile kk.  A and B take their k index from the same
+// (lane >> 4, byte) pair, so the sum is over matching (i, a) whatever order the
+// hardware gives the 64 k slots.  The words equal the VALU sums' (one exact
+// integer sum, one canonical reduction).
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr u64 XMASK = 0x0080808080808080ull;  // bytes 0..6 -> signed (u - 128); also C0
+
+// balanced base-256 digits of c < 2^60 as bytes (digit d in byte d)
+__device__ __forceinline__ u64 balanced_digits(u64 c) {
+    u64 e = 0;
+    int64_t v = (int64_t)c;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        int dig = (int)(v & 255);
+        if (dig >= 128) dig -= 256;
+        v = (v - dig) >> 8;
+        e |= (u64)(uint8_t)(int8_t)dig << (8 * d);
+    }
+    return e;
+}
+// the 8 A bytes of row shift s for one source: byte a = e_{s-a} (0 outside 0..7)
+__device__ __forceinline__ u64 shift_window(u64 e, int s) {
+    const u64 r = __builtin_bswap64(e);  // byte p = e_{7-p}
+    if (s <= 7) return r >> (8 * (7 - s));
+    return s == 15 ? 0 : r << (8 * (s - 7));
+}
+// sum_{kk, r} v[kk][r] 256^(4 kk + r) + 2^126, reduced mod q.  |v| < 2^22, so
+// v0 + 256 v1 fits an int32 and each four-row group L_kk an int64 (< 2^47); the
+// signed 128-bit sum (|sum| < 2^125) is biased by 2^126 so the reduction sees
+// a non-negative value -- the caller's per-output constant takes 2^126 off again.
+__device__ __forceinline__ u64 combine_rows(const v4i (&v)[4], const Mod &m) {
+    int64_t L[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        const int32_t p = v[kk][0] + (v[kk][1] << 8), q = v[kk][2] + (v[kk][3] << 8);
+        L[kk] = (int64_t)p + ((int64_t)q << 16);
+    }
+    Acc128 a;
+    a.lo = (u64)L[0] + ((u64)L[1] << 32);
+    const u64 c = a.lo < (u64)L[0];
+    a.hi = (u64)(L[0] >> 63) + (u64)(L[1] >> 32) + c + (u64)L[2] + ((u64)L[3] << 32) + (1ull << 62);
+    return reduce128(a, m);
+}
+// the per-output constant C0 * sum_i c_i - 2^126 mod q
+__device__ __forceinline__ u64 sums_constant(u64 csum, const Mod &m) {
+    const u64 b126 = mul_shoup(reduce64(1ull << 62, m), m.r64, m.r64s, m.q);
+    return sub_mod(mul_barrett(csum, reduce64(XMASK, m), m), b126, m.q);
+}
+
+// A fragments in LDS: [group][kk][ks][lane] x 16 B; one wave reads 1 KB contiguous.
+// Window (output t, source i, shift s) -> its 8 bytes in that image.
+template <int KS>
+__device__ __forceinline__ int afrag_offset(int t, int i, int s) {
+    const int grp = t >> 2, row = 4 * (t & 3) + (s & 3), lane = 16 * ((i & 7) >> 1) + row;
+    return ((((grp * 4 + (s >> 2)) * KS + (i >> 3)) * 64 + lane) * 16 + 8 * (i & 1)) >> 3;  // u64 units
+}
+
+// One group of four outputs for four column tiles: acc[c][kk] = tile kk of
+// column tile c, from the group's A image in LDS ([kk][ks][lane] x 16 B).
+template <int KS>
+__device__ __forceinline__ void mfma_group(const u64 *img, const v4i (&bf)[4][KS], v4i (&acc)[4][4], int lane) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) acc[c][kk] = v4i{0, 0, 0, 0};
+    // the A fragments of row block kk + 1 are read while row block kk multiplies
+    v4i af[2][KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) af[0][ks] = *reinterpret_cast<const v4i *>(&img[(ks * 64 + lane) * 2]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        if (kk < 3) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                af[(kk + 1) & 1][ks] = *reinterpret_cast<const v4i *>(&img[(((kk + 1) * KS + ks) * 64 + lane) * 2]);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this block's products
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                acc[c][kk] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kk & 1][ks], bf[c][ks], acc[c][kk], 0, 0, 0);
+    }
+}
+// a pointer read back from LDS is generic (flat loads, which also wait on LDS
+// traffic); the sources are global memory
+typedef __attribute__((address_space(1))) const u64 gu64;
+__device__ __forceinline__ gu64 *to_global(const u64 *p) { return (gu64 *)p; }
+__device__ __forceinline__ v4i bytes_of(u64 y0, u64 y1) {
+    return v4i{(int)(uint32_t)y0, (int)(uint32_t)(y0 >> 32), (int)(uint32_t)y1, (int)(uint32_t)(y1 >> 32)};
+}
+
+// Linear sums (PS leaves) on MFMA.  Same arguments and outputs as
+// k_linear_sum_multi; KS = ceil(m / 8) source steps, NG = ceil(G / 4) groups.
+// Block: 4 waves x 4 column tiles of 16 coefficients = 256 coefficients per
+// iteration, LS_CH coefficients per block (the LDS image is built once per block).
+// grid: x = n / LS_CH, y = limb, z = segment.
+constexpr int LS_CH = 1024;
+template <int KS, int NG>
+__global__ __launch_bounds__(NT) void k_linear_sum_mfma(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
+    __shared__ u64 tab[NG * 4 * KS * 64 * 2];
+    __shared__ u64 cval[4 * NG][8 * KS];
+    __shared__ u64 corr[4 * NG];
+    __shared__ const u64 *xptr[8 * KS];
+    __shared__ size_t xoff[8 * KS];
+    __shared__ u64 *optr[4 * NG];
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const Mod md = mods[l];
+    const int tid = threadIdx.x;
+    // constants (zero for padding outputs / sources), then their A windows
+    for (int p = tid; p < 4 * NG * 8 * KS; p += NT) {
+        const int t = p / (8 * KS), i = p % (8 * KS);
+        const u64 c = (t < A.G && i < A.m) ? smod(A.K[t * MLS_M + i], A.sh[t * MLS_M + i], md) : 0;
+        cval[t][i] = c;
+        const u64 e = balanced_digits(c);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) tab[afrag_offset<KS>(t, i, s)] = shift_window(e, s);
+    }
+    if (tid < 8 * KS) {  // padding sources read source 0 (their constants are zero)
+        const int i = tid < A.m ? tid : 0;
+        xptr[tid] = A.x[i];
+        xoff[tid] = (size_t)blockIdx.z * A.xseg[i] + (size_t)l * n;
+    }
+    __syncthreads();
+    if (tid < 4 * NG) {
+        optr[tid] = tid < A.G ? A.out[tid] : nullptr;
+        u64 s = 0;
+        for (int i = 0; i < A.m; ++i) s = add_mod(s, cval[tid][i], md.q);
+        corr[tid] = sums_constant(s, md);
+    }
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
+    const size_t oo_l = (size_t)blockIdx.z * seg + (size_t)l * n;
+    for (size_t nb = (size_t)blockIdx.x * LS_CH + wave * 64; nb < (size_t)(blockIdx.x + 1) * LS_CH && nb < n;
+         nb += 4 * 64) {
+        // B fragments: sources 8 ks + 2 lg, +1 of coefficient nb + 16 c + col
+        v4i bf[4][KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int i0 = 8 * ks + 2 * lg;
+            const gu64 *p0 = to_global(xptr[i0]) + xoff[i0] + nb + col;
+            const gu64 *p1 = to_global(xptr[i0 + 1]) + xoff[i0 + 1] + nb + col;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) bf[c][ks] = bytes_of(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
+        }
+#pragma unroll 1
+        for (int grp = 0; grp < NG; ++grp) {
+            v4i acc[4][4];  // [column tile][kk]
+            mfma_group<KS>(tab + grp * 4 * KS * 64 * 2, bf, acc, lane);
+            const int t = 4 * grp + lg;
+            if (t < A.G) {
+                u64 *o = optr[t] + oo_l;
+                const u64 cr = corr[t];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const size_t k = nb + 16 * c + col;
+                    u64 r = add_mod(combine_rows(acc[c], md), cr, md.q);
+                    if (A.accumulate) r = add_mod(r, o[k], md.q);
+                    o[k] = r;
+                }
+            }
+        }
+    }
+}
+
 // out[m][c] = sum_i ct_i[m][c] * pt_i  (accumulate: + out), lazy 128-bit.
 // Segment z = 2m + c; ct_i member m at m * cmember (0 = broadcast), its c1 at
 // + cpoly; plaintexts are shared by all members.
@@ -441,6 +656,83 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
         }
         fold4(r, acc);
         ext[((size_t)j * W + t) * n + k] = reduce128(r, mt);
+    }
+}
+
+// ModUp basis conversion on MFMA (the sums of products above with c_{t,i} =
+// qhat[t][i], y_i = [x_i qhinv_i]_{q_i}); same arguments and outputs as
+// k_modup_convert.  Block: 256 coefficients (4 waves x 4 column tiles), groups
+// of four targets [blockIdx.y * gpc, +gpc) of the digit's T = W - alpha_j
+// targets (target index tau skips the digit's own limbs).  Each group's A
+// image is built in LDS (double-buffered: one barrier per group).
+// grid: x = n / 256, y = group chunks, z = member * digits + digit.
+template <int KS>
+__global__ __launch_bounds__(NT) void k_modup_mfma(u64 *__restrict__ ext, const u64 *__restrict__ coef, int W, int ell,
+                                                   ModUpArgs A, const int *pmap_ext, const Mod *mods, int logN,
+                                                   int gpc) {
+    __shared__ u64 img[2][4 * KS * 64 * 2];
+    __shared__ Mod tm[2][4];
+    __shared__ u64 corr[2][4];
+    const size_t n = (size_t)1 << logN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
+    const int j = (int)(blockIdx.z % (unsigned)A.digits);
+    const size_t mb = blockIdx.z / (unsigned)A.digits;
+    coef += mb * A.coef_stride;
+    ext += mb * A.ext_stride;
+    const int lo = A.lo[j], hi = A.hi[j], na = hi - lo, T = W - na;
+    const int g0 = blockIdx.y * gpc, g1 = min((T + 3) / 4, g0 + gpc);
+    const size_t nb = (size_t)blockIdx.x * 256 + wave * 64;
+    // B fragments: scaled source residues of sources 8 ks + 2 lg, +1
+    v4i bf[4][KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        u64 y[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            // padding sources (i >= na) read the digit's last limb: zero constants
+            const int i = min(8 * ks + 2 * lg + h, na - 1);
+            const u64 w = A.qhinv[j][i], wp = A.qhinv_s[j][i], q = mods[lo + i].q;
+            const u64 *src = coef + (size_t)(lo + i) * n + nb + col;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) y[h][c] = mul_shoup(src[16 * c], w, wp, q) ^ XMASK;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bf[c][ks] = bytes_of(y[0][c], y[1][c]);
+    }
+    const u64 *qh = A.qhat[j];
+    for (int grp = g0; grp < g1; ++grp) {
+        const int b = grp & 1;
+        // A windows of the group's 4 x 8 KS constants
+        for (int p = tid; p < 4 * 8 * KS; p += NT) {
+            const int tl = p / (8 * KS), i = p % (8 * KS), tau = 4 * grp + tl;
+            const int t = tau < lo ? tau : tau + na;
+            const u64 c = (tau < T && i < na) ? qh[(size_t)t * A.qstride + i] : 0;
+            const u64 e = balanced_digits(c);
+#pragma unroll
+            for (int s = 0; s < 16; ++s) img[b][afrag_offset<KS>(tl, i, s)] = shift_window(e, s);
+        }
+        if (tid < 4) {
+            const int tau = 4 * grp + tid, t = tau < lo ? tau : tau + na;
+            if (tau < T) {
+                const Mod mt = mods[pmap_ext[t]];
+                u64 s = 0;
+                for (int i = 0; i < na; ++i) s = add_mod(s, qh[(size_t)t * A.qstride + i], mt.q);
+                tm[b][tid] = mt;
+                corr[b][tid] = sums_constant(s, mt);
+            }
+        }
+        __syncthreads();
+        v4i acc[4][4];
+        mfma_group<KS>(img[b], bf, acc, lane);
+        const int tau = 4 * grp + lg;
+        if (tau < T) {
+            const int t = tau < lo ? tau : tau + na;
+            const Mod mt = tm[b][lg];
+            const u64 cr = corr[b][lg];
+            u64 *o = ext + ((size_t)j * W + t) * n + nb + col;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) o[16 * c] = add_mod(combine_rows(acc[c], mt), cr, mt.q);
+        }
     }
 }
 
@@ -827,6 +1119,121 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict_
         dst[(size_t)i * n + k] = reduce128(r, mi);
     }
 }
+
+// The same on MFMA: the K-source conversion of the special limbs to the ell-1
+// remaining Q limbs runs as the i8 sums of products (c_{i,k} = phat[i][k]); the
+// per-coefficient part (scaled special residues, the centred count, the last
+// limb's conversion and y) is computed once per coefficient by the lane that
+// owns it and handed to the lanes of its column by __shfl; the P (lift - v)
+// term is one Shoup product in the epilogue.  Same words as the VALU kernel.
+// grid: x = n / 256, y = group chunks of the ell-1 targets, z = segment.
+template <int KS, int KT>
+__global__ __launch_bounds__(NT) void k_moddown_rescale_mfma(u64 *__restrict__ corr_out, const u64 *__restrict__ acc,
+                                                             int ell, int nq, size_t seg_acc, size_t seg_corr,
+                                                             const u64 *phinv, const u64 *phinv_s, const u64 *phat,
+                                                             const u64 *pinv, const u64 *pinv_s, const u64 *pmod,
+                                                             const u64 *pmod_s, const double *pinvd, const u64 *ninv,
+                                                             const u64 *ninv_s, const Mod *mods, int logN, int gpc) {
+    __shared__ u64 img[2][4 * KS * 64 * 2];
+    __shared__ Mod tm[2][4];
+    __shared__ u64 cadd[2][4], pm[2][4], pms[2][4];
+    const size_t n = (size_t)1 << logN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
+    const int last = ell - 1, T = last;
+    const u64 *src = acc + (size_t)blockIdx.z * seg_acc + (size_t)last * n;
+    u64 *dst = corr_out + (size_t)blockIdx.z * seg_corr;
+    const size_t nb = (size_t)blockIdx.x * 256 + wave * 64;
+    // per-coefficient part, coefficient nb + lane
+    u64 y, cntv;
+    {
+        const size_t k = nb + lane;
+        u64 yk[KT];
+        Split30 v[KT];
+#pragma unroll
+        for (int i = 0; i < KT; ++i) {
+            yk[i] = mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+            v[i] = split30(yk[i]);
+        }
+        cntv = centre_count<KT>(yk, pinvd);
+        const Mod ml = mods[last];
+        const u64 ql = ml.q;
+        Acc4 cacc;
+        Acc128 cr;
+#pragma unroll
+        for (int kk = 0; kk < KT; ++kk) {
+            mac4(cacc, v[kk], split30(phat[(size_t)last * KT + kk]));
+            spill4<KT + 1>(cr, cacc, kk);
+        }
+        mac4(cacc, split30(cntv), split30(ql - pmod[last]));
+        fold4(cr, cacc);
+        const u64 cl = reduce128(cr, ml);
+        const u64 xl = mul_shoup(src[k], ninv[last], ninv_s[last], ql);
+        y = mul_shoup(sub_mod(xl, cl, ql), pinv[last], pinv_s[last], ql);
+    }
+    const u64 ql = mods[last].q;
+    u64 yc[4], cc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        yc[c] = __shfl(y, 16 * c + col);
+        cc[c] = __shfl(cntv, 16 * c + col);
+    }
+    // B fragments: scaled special residues, sources 8 ks + 2 lg, +1
+    v4i bf[4][KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        u64 yy[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = min(8 * ks + 2 * lg + h, KT - 1);  // padding: zero constants
+            const u64 w = phinv[i], wp = phinv_s[i], q = mods[nq + i].q;
+            const u64 *sp = src + (size_t)(1 + i) * n + nb + col;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) yy[h][c] = mul_shoup(sp[16 * c], w, wp, q) ^ XMASK;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bf[c][ks] = bytes_of(yy[0][c], yy[1][c]);
+    }
+    const int g0 = blockIdx.y * gpc, g1 = min((T + 3) / 4, g0 + gpc);
+    for (int grp = g0; grp < g1; ++grp) {
+        const int b = grp & 1;
+        for (int p = tid; p < 4 * 8 * KS; p += NT) {
+            const int tl = p / (8 * KS), i = p % (8 * KS), t = 4 * grp + tl;
+            const u64 c = (t < T && i < KT) ? phat[(size_t)t * KT + i] : 0;
+            const u64 e = balanced_digits(c);
+#pragma unroll
+            for (int s = 0; s < 16; ++s) img[b][afrag_offset<KS>(tl, i, s)] = shift_window(e, s);
+        }
+        if (tid < 4) {
+            const int t = 4 * grp + tid;
+            if (t < T) {
+                const Mod mt = mods[t];
+                u64 sum = 0;
+                for (int i = 0; i < KT; ++i) sum = add_mod(sum, phat[(size_t)t * KT + i], mt.q);
+                tm[b][tid] = mt;
+                cadd[b][tid] = sums_constant(sum, mt);
+                pm[b][tid] = pmod[t];
+                pms[b][tid] = pmod_s[t];
+            }
+        }
+        __syncthreads();
+        v4i a4[4][4];
+        mfma_group<KS>(img[b], bf, a4, lane);
+        const int t = 4 * grp + lg;
+        if (t < T) {
+            const Mod mt = tm[b][lg];
+            const u64 ca = cadd[b][lg], w = pm[b][lg], wp = pms[b][lg];
+            u64 *o = dst + (size_t)t * n + nb + col;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                // centred lift of y: q_last / 2 < q_t (checked at context creation)
+                const u64 lift = yc[c] > (ql >> 1) ? mt.q - (ql - yc[c]) : yc[c];
+                const u64 lv = lift >= cc[c] ? lift - cc[c] : lift + mt.q - cc[c];
+                const u64 conv = add_mod(combine_rows(a4[c], mt), ca, mt.q);
+                o[16 * c] = add_mod(conv, mul_shoup(lv, w, wp, mt.q), mt.q);
+            }
+        }
+    }
+}
 inline dim3 ew_grid(int logN, int limbs, int segs) {
     const size_t n = (size_t)1 << logN;
     return dim3((unsigned)((n / 2 + NT - 1) / NT), (unsigned)limbs, (unsigned)segs);
@@ -836,6 +1243,12 @@ inline dim3 pt_grid(int logN, int y, int z) {
     return dim3((unsigned)((n + NT - 1) / NT), (unsigned)y, (unsigned)z);
 }
 }  // namespace
+
+int set_mfma_sums(int mask) {
+    const int prev = mfma_mask();
+    if (mask >= 0) g_mfma_mask.store(mask & 7, std::memory_order_relaxed);
+    return prev;
+}
 
 // ============================================================ wrappers =====
 void ew_add(u64 *out, const u64 *a, const u64 *b, int limbs, int segs, Seg S, const Mod *mods, int logN,
@@ -935,6 +1348,18 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
             }
         }
         const double B = 8.0 * (A.m + (double)G * (1 + A.accumulate)) * limbs * segs * ((size_t)1 << logN);
+        const size_t n = (size_t)1 << logN;
+        if (use_mfma_sums(MF_LIN) && n >= 256) {
+            const dim3 grid((unsigned)((n + LS_CH - 1) / LS_CH), (unsigned)limbs, (unsigned)segs);
+            dispatch_int<1, 4>((A.m + 7) / 8, [&](auto ks) {
+                dispatch_int<1, 3>((G + 3) / 4, [&](auto ng) {
+                    constexpr int KS = decltype(ks)::value, NG = decltype(ng)::value;
+                    launch_clocked("k_linear_sum_mfma", B, k_linear_sum_mfma<KS, NG>, grid, dim3(NT), st, A, seg, mods,
+                                   logN);
+                });
+            });
+            continue;
+        }
         const dim3 grid = pt_grid(logN, limbs, segs);
         switch (G) {
 #define MLS_CASE(g)                                                                                          \
@@ -989,19 +1414,6 @@ void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int log
     hipLaunchKernelGGL(k_reduce, ew_grid(logN, limbs, segs), dim3(NT), 0, st, x, Seg{seg, seg, 0}, mods, logN);
 }
 
-// compile-time dispatch of a small runtime integer (digit size, special-prime count)
-template <int Lo, int Hi, typename F>
-void dispatch_int(int v, F &&f) {
-    if constexpr (Lo > Hi) {
-        throw std::invalid_argument("unsupported basis size " + std::to_string(v));
-    } else {
-        if (v == Lo)
-            f(std::integral_constant<int, Lo>{});
-        else
-            dispatch_int<Lo + 1, Hi>(v, std::forward<F>(f));
-    }
-}
-
 void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
                    size_t coef_stride, size_t ext_stride, const int *pmap_ext, const u64 *tabs,
                    const size_t *tab_off, const Mod *mods, int logN, hipStream_t st) {
@@ -1028,6 +1440,20 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
     const size_t n = (size_t)1 << logN;
     auto launch = [&](int nd, int at, const ModUpArgs &Ar, u64 *ext0) {
         const double B = 8.0 * members * (double)((size_t)nd * W) * (double)n;  // sources in + targets out
+        if (use_mfma_sums(MF_MODUP) && n >= 256) {
+            // groups of four targets, chunked over grid.y when the launch is narrow
+            const int ngt = (W - at + 3) / 4;
+            const size_t base = n / 256 * (size_t)(nd * members);
+            const int chunks = base >= 2048 ? 1 : std::min(ngt, (int)((2048 + base - 1) / base));
+            const int gpc = (ngt + chunks - 1) / chunks;
+            dispatch_int<1, 3>((at + 7) / 8, [&](auto c) {
+                constexpr int KS = decltype(c)::value;
+                launch_clocked("k_modup_mfma", B, k_modup_mfma<KS>,
+                               dim3((unsigned)(n / 256), (unsigned)((ngt + gpc - 1) / gpc), (unsigned)(nd * members)),
+                               dim3(NT), st, ext0, coef, W, ell, Ar, pmap_ext, mods, logN, gpc);
+            });
+            return;
+        }
         dispatch_int<1, 24>(at, [&](auto c) {
             constexpr int AT = decltype(c)::value;
             const int tch = conv_chunk(logN, W, nd * members);
@@ -1162,9 +1588,24 @@ void ew_permute_multi(u64 *out, const u64 *in, const KsKeys &keys, int limbs, in
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                              const u64 *pinv_s, const u64 *pmod, const double *pinvd, const u64 *ninv,
-                             const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st) {
+                             const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st, const u64 *pmod_s) {
     if (ell <= 1) return;
     const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
+    const size_t n = (size_t)1 << logN;
+    if (use_mfma_sums(MF_MODDOWN) && n >= 256 && pmod_s) {
+        const int ngt = (ell - 1 + 3) / 4;
+        const size_t base = n / 256 * (size_t)segs;
+        const int chunks = base >= 2048 ? 1 : std::min(ngt, (int)((2048 + base - 1) / base));
+        const int gpc = (ngt + chunks - 1) / chunks;
+        dispatch_int<1, 16>(K, [&](auto c) {
+            constexpr int KT = decltype(c)::value, KS = (KT + 7) / 8;
+            launch_clocked("k_moddown_rescale_mfma", B, k_moddown_rescale_mfma<KS, KT>,
+                           dim3((unsigned)(n / 256), (unsigned)((ngt + gpc - 1) / gpc), (unsigned)segs), dim3(NT), st,
+                           corr, acc, ell, nq, seg_acc, seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, pmod_s,
+                           pinvd, ninv, ninv_s, mods, logN, gpc);
+        });
+        return;
+    }
     dispatch_int<1, 16>(K, [&](auto c) {
         constexpr int KT = decltype(c)::value;
         const int tch = conv_chunk(logN, ell - 1, segs);

@@ -178,6 +178,10 @@ void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap,
 // ext[m][j][t][k] for every member m, digit j and target t not in digit j
 // (coefficient in, unscaled: the q-hat^-1 constants carry n^-1; NTT NOT applied);
 // coef member stride coef_stride, ext member stride ext_stride
+// mask of the sums-of-products kernels that run on the i8 matrix cores (1 PS
+// linear sums, 2 ModUp, 4 ModDown+rescale); mask < 0 only reads it.  Returns
+// the previous mask.
+int set_mfma_sums(int mask);
 void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
                    size_t coef_stride, size_t ext_stride, const int *pmap_ext,
                    const u64 *tabs /* packed, see engine */, const size_t *tab_off, const Mod *mods, int logN,
@@ -237,7 +241,8 @@ void ew_permute_multi(u64 *out, const u64 *in, const KsKeys &keys, int limbs, in
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                              const u64 *pinv_s, const u64 *pmod, const double *pinvd, const u64 *ninv,
-                             const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st);
+                             const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st,
+                             const u64 *pmod_s = nullptr);  // given: the MFMA kernel
 // conv[s][i][k] = (sum_k' y_k' phat[i][k'] - v P) mod q_i for i < ell, y_k' =
 // pc[s][k'] * phinv_k' (pc: unscaled inverse NTT, phinv carries n^-1),
 // v = round(sum_k' y_k' pinvd_k'): the centred Conv_{P->q_i}

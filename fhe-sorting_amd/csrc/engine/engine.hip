@@ -332,7 +332,8 @@ struct Engine::Impl {
         auto corrm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *corr = static_cast<u64 *>(corrm->p);
         dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, segs, phinv,
-                                     phinv_s, phat, pinv, pinv_s, pmod, pinvd, T.ninv, T.ninv_s, mods, P.logN, st);
+                                     phinv_s, phat, pinv, pinv_s, pmod, pinvd, T.ninv, T.ninv_s, mods, P.logN, st,
+                                     pmod_s);
         // forward NTT of corr whose row pass finishes (acc + d P - corr) (P q_last)^-1 into `out`
         dev::NttFuse F;
         F.out = out;

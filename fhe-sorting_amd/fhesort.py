@@ -171,6 +171,7 @@ _SIGS = {
     'fhe_ntt_dev': (C.c_int, [vp, vp, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, vp]),
     'fhe_automorph_dev': (C.c_int, [vp, vp, C.c_int, C.c_uint64, vp, vp]),
     'fhe_host_stats': (C.c_int, [dp]),
+    'fhe_set_mfma_sums': (C.c_int, [C.c_int]),
     'fhe_host_stats_reset': (C.c_int, []),
     'fhe_prng_block': (C.c_int, [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     'fhe_get_ps_split': (C.c_int, [vp]),
@@ -202,6 +203,13 @@ class WireInfo(C.Structure):
 
 WIRE_KINDS = {1: 'context', 2: 'public_key', 3: 'eval_mult_key', 4: 'eval_automorphism_key', 5: 'ciphertext',
               6: 'secret_key'}
+
+
+def set_mfma_sums(mask):
+    """Process-wide choice of the i8-MFMA sums-of-products kernels (1 PS linear
+    sums, 2 ModUp, 4 ModDown+rescale; fhe_set_mfma_sums).  mask < 0 only
+    queries.  Returns the previous mask.  The output words do not change."""
+    return lib().fhe_set_mfma_sums(int(mask))
 
 
 def wire_inspect(path):

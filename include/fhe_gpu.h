@@ -379,6 +379,13 @@ int fhe_ntt_dev(fhe_ctx *ctx, uint64_t *dev_limbs, int first_prime, int nlimbs, 
                 int inverse, void *stream);
 int fhe_automorph_dev(fhe_ctx *ctx, const uint64_t *dev_in, int limbs, uint64_t galois, uint64_t *dev_out,
                       void *stream);
+/* Process-wide choice of the sums-of-products kernels (PS linear sums = 1,
+ * ModUp conversion = 2, fused ModDown+rescale conversion = 4): a set bit runs
+ * that conversion on the i8 matrix cores (v_mfma_i32_16x16x64_i8),
+ * a clear bit on the 64-bit VALU kernels.  The output words are the same
+ * either way.  mask < 0 only queries.  Returns the previous mask (initially
+ * FHE_MFMA from the environment, else the build default). */
+int fhe_set_mfma_sums(int mask);
 /* op counters: hmult, keyswitch, rotations, rescale, ptmult, constmult, and
  * the op-level algorithmic HBM bytes of SURVEY §8(d) (HMult, rotation, ct x pt,
  * ct x const, add, linear sum formulas, each op at its own level) */
