@@ -43,6 +43,8 @@ sys.path.insert(0, os.path.join(REPO, 'fhe-sorting_amd'))
 import fhesort as F  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MFMA_SIMDS = 1024           # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+PEAK_CLOCK_HZ = 2.4e9      # peak engine clock
 N_SIMD = 256 * 4        # 256 CUs x 4 SIMDs
 F_CLK = 2.4e9           # peak engine clock (the effective clock under load is lower: valu_frac is a lower bound)
 
@@ -275,9 +277,16 @@ def valu_fraction(name, avg_s, sq_file, mix_file='valu_mix.json'):
     wc = sum(sq[k]['launches'] * sq[k].get('SQ_WAVE_CYCLES', 0) for k in keys) / n or 1
     wait = sum(sq[k]['launches'] * sq[k].get('SQ_WAIT_ANY', 0) for k in keys) / n
     stall = sum(sq[k]['launches'] * sq[k].get('SQ_WAIT_INST_ANY', 0) for k in keys) / n
-    return {'valu_frac': round(valu_s / avg_s, 4), 'valu_insts_per_launch': round(insts),
-            'valu_seconds_per_launch': valu_s, 'valu_source': f'profiles/{sq_file} + profiles/{mix_file}',
-            'wave_cycle_split': {'waitcnt': round(wait / wc, 3), 'issue_stall': round(stall / wc, 3)}}
+    out = {'valu_frac': round(valu_s / avg_s, 4), 'valu_insts_per_launch': round(insts),
+           'valu_seconds_per_launch': valu_s, 'valu_source': f'profiles/{sq_file} + profiles/{mix_file}',
+           'wave_cycle_split': {'waitcnt': round(wait / wc, 3), 'issue_stall': round(stall / wc, 3)}}
+    # matrix-core kernels (the i8 sums of products): SQ_VALU_MFMA_BUSY_CYCLES is
+    # the MFMA pipe's busy SIMD-cycles per launch (16 per v_mfma_i32_16x16x64_i8);
+    # over 1024 SIMDs x the 2.4 GHz peak clock x the live launch duration
+    busy = sum(sq[k]['launches'] * sq[k].get('SQ_VALU_MFMA_BUSY_CYCLES', 0) for k in keys) / n
+    if busy > 0:
+        out['mfma_frac'] = round(busy / (MFMA_SIMDS * PEAK_CLOCK_HZ * avg_s), 4)
+    return out
 
 
 def pmc_lookup_all(table, name):
@@ -335,15 +344,20 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
         return {n: {'share': round(v['ms'] / total_ms, 3), 'avg_us': round(v['ms'] / v['launches'] * 1e3, 1),
                     'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1)} for n, v in top}
     run_bytes = sum(v['bytes'] for v in stats.values())
-    # roofline priced against HBM (integer modular work, no MFMA); what limits
+    # roofline priced against HBM (integer modular work; the i8-MFMA linear sums
+    # also report mfma_frac); what limits
     # the kernel below it: VALU issue for the NTT passes, the
     # basis conversions and the PS linear sums, HBM for the streaming kernels
     limiter = 'hbm' if name.split('<')[0] in ('k_tensor', 'k_add', 'k_sub', 'k_ks_inner', 'k_mul_plain_sum') \
         else 'valu'
+    vf = valu_fraction(name, avg_s, sq_file)
+    split = vf.get('wave_cycle_split', {})
+    if split.get('waitcnt', 0) >= max(0.3, split.get('issue_stall', 0)) and limiter == 'valu':
+        limiter = 'memory latency'  # waves parked in s_waitcnt more than stalled on issue
     return {'kernel': name, 'bound': 'hbm', 'limiter': limiter, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
             'unit': 'GB/s',
             'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_source': src,
-            **valu_fraction(name, avg_s, sq_file),
+            **vf,
             'avg_us': round(avg_s * 1e6, 2), 'launches': st['launches'],
             'algorithmic_bytes_per_launch': per_launch, 'clocked_ms_per_sort': round(total_ms, 1),
             'kernels': table(by_sym.items()), 'kernels_by_caller': table(stats.items()),

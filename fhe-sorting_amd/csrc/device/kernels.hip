@@ -1,7 +1,8 @@
 // gfx950 kernels for the RNS-CKKS ciphertext-op engine.
 //
-// Everything here is 64-bit integer modular arithmetic (no MFMA: the hot path
-// is HBM/VALU-bound integer work).  Design notes:
+// 64-bit integer modular arithmetic on the VALU, except the sums of products
+// that can run as an integer GEMM on the i8 matrix cores (k_*_mfma, see
+// "RNS sums of products on MFMA" below and DESIGN.md §5).  Design notes:
 //   * the NTT lives in ntt.hip (register-blocked, two passes per transform).
 //   * element-wise kernels move 16 B per lane (ulonglong2) and are launched
 //     3-D: x = coefficient blocks, y = limb (prime), z = polynomial segment.
@@ -455,7 +456,18 @@ __device__ __forceinline__ v4i bytes_of(u64 y0, u64 y1) {
 // grid: x = n / LS_CH, y = limb, z = segment.
 constexpr int LS_CH = 1024;
 template <int KS, int NG>
-__global__ __launch_bounds__(NT) void k_linear_sum_mfma(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
+// three waves per SIMD (164 registers, accumulators in VGPRs, no spills) instead
+// of the compiler's two; the LDS image of the widest instantiation allows three
+// blocks per CU.  FHE_LS_WPE=0 at build time drops the hint (A/B).
+#ifndef FHE_LS_WPE
+#define FHE_LS_WPE 3
+#endif
+#if FHE_LS_WPE
+#define LS_WAVES __attribute__((amdgpu_waves_per_eu(FHE_LS_WPE, 8)))
+#else
+#define LS_WAVES
+#endif
+__global__ __launch_bounds__(NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
     __shared__ u64 tab[NG * 4 * KS * 64 * 2];
     __shared__ u64 cval[4 * NG][8 * KS];
     __shared__ u64 corr[4 * NG];

@@ -19,7 +19,7 @@ gzip -f $O/trace/run_kernel_trace.csv
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 600 rocprofv3 --pmc $C --kernel-include-regex 'k_[a-z]' --output-format csv -d "$R/$O/pmc_$C" -o run -- python3 "$R/bench.py" $B --no-roofline > $O/pmc_$C.log 2>&1 || { echo "pmc $C failed"; tail -5 $O/pmc_$C.log; exit 1; }
 done
-timeout -s KILL 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --kernel-include-regex 'k_[a-z]' --output-format csv -d "$R/$O/pmc_SQ" -o run -- python3 "$R/bench.py" $B --no-roofline > $O/pmc_SQ.log 2>&1 || { echo "pmc SQ failed"; tail -5 $O/pmc_SQ.log; exit 1; }
+timeout -s KILL 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --kernel-include-regex 'k_[a-z]' --output-format csv -d "$R/$O/pmc_SQ" -o run -- python3 "$R/bench.py" $B --no-roofline > $O/pmc_SQ.log 2>&1 || { echo "pmc SQ failed"; tail -5 $O/pmc_SQ.log; exit 1; }
 python scripts/pmc_summary.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv $O/pmc_traffic.json > $O/pmc_traffic.txt || exit 1
 python scripts/pmc_sq_summary.py $O/pmc_SQ/run_counter_collection.csv $O/pmc_sq.json > $O/pmc_sq.txt || exit 1
 gzip -f $O/pmc_*/run_counter_collection.csv
