@@ -3,7 +3,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd "$R"
-O=gpurun_out/r3v2
+O=gpurun_out/${1:-r3v2}
 mkdir -p $O
 (while sleep 50; do echo "tick $(date +%T)"; done) & TICK=$!
 trap 'kill $TICK 2>/dev/null' EXIT
