@@ -516,19 +516,22 @@ __global__ __launch_bounds__(NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A,
         }
 #pragma unroll 1
         for (int grp = 0; grp < NG; ++grp) {
+            const int t = 4 * grp + lg;
+            // padding outputs (t >= G) load output 0's words and store nothing
+            u64 *o = optr[t < A.G ? t : 0] + oo_l + nb + col;
+            // a second pass adds the first pass's outputs: loaded before the
+            // products so the load latency hides under them
+            u64 prev[4] = {0, 0, 0, 0};
+            if (A.accumulate) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) prev[c] = o[16 * c];
+            }
             v4i acc[4][4];  // [column tile][kk]
             mfma_group<KS>(tab + grp * 4 * KS * 64 * 2, bf, acc, lane);
-            const int t = 4 * grp + lg;
             if (t < A.G) {
-                u64 *o = optr[t] + oo_l;
                 const u64 cr = corr[t];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const size_t k = nb + 16 * c + col;
-                    u64 r = add_mod(combine_rows(acc[c], md), cr, md.q);
-                    if (A.accumulate) r = add_mod(r, o[k], md.q);
-                    o[k] = r;
-                }
+                for (int c = 0; c < 4; ++c) o[16 * c] = add_mod(add_mod(combine_rows(acc[c], md), cr, md.q), prev[c], md.q);
             }
         }
     }
