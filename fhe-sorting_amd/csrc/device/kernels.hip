@@ -415,10 +415,10 @@ __device__ __forceinline__ int afrag_offset(int t, int i, int s) {
 
 // One group of four outputs for four column tiles: acc[c][kk] = tile kk of
 // column tile c, from the group's A image in LDS ([kk][ks][lane] x 16 B).
-template <int KS>
-__device__ __forceinline__ void mfma_group(const u64 *img, const v4i (&bf)[4][KS], v4i (&acc)[4][4], int lane) {
+template <int KS, int NC = 4>
+__device__ __forceinline__ void mfma_group(const u64 *img, const v4i (&bf)[NC][KS], v4i (&acc)[NC][4], int lane) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) acc[c][kk] = v4i{0, 0, 0, 0};
     // the A fragments of row block kk + 1 are read while row block kk multiplies
@@ -437,7 +437,7 @@ __device__ __forceinline__ void mfma_group(const u64 *img, const v4i (&bf)[4][KS
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
+            for (int c = 0; c < NC; ++c)
                 acc[c][kk] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kk & 1][ks], bf[c][ks], acc[c][kk], 0, 0, 0);
     }
 }
@@ -455,6 +455,14 @@ __device__ __forceinline__ v4i bytes_of(u64 y0, u64 y1) {
 // iteration, LS_CH coefficients per block (the LDS image is built once per block).
 // grid: x = n / LS_CH, y = limb, z = segment.
 constexpr int LS_CH = 1024;
+// column tiles per wave and threads per block (A/B: -DFHE_LS_NC=2 -DFHE_LS_NT=512)
+#ifndef FHE_LS_NC
+#define FHE_LS_NC 4
+#endif
+#ifndef FHE_LS_NT
+#define FHE_LS_NT 256
+#endif
+constexpr int LS_NC = FHE_LS_NC, LS_NT = FHE_LS_NT;
 template <int KS, int NG>
 // three waves per SIMD (164 registers, accumulators in VGPRs, no spills) instead
 // of the compiler's two; the LDS image of the widest instantiation allows three
@@ -467,7 +475,7 @@ template <int KS, int NG>
 #else
 #define LS_WAVES
 #endif
-__global__ __launch_bounds__(NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
+__global__ __launch_bounds__(LS_NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
     __shared__ u64 tab[NG * 4 * KS * 64 * 2];
     __shared__ u64 cval[4 * NG][8 * KS];
     __shared__ u64 corr[4 * NG];
@@ -479,7 +487,7 @@ __global__ __launch_bounds__(NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A,
     const Mod md = mods[l];
     const int tid = threadIdx.x;
     // constants (zero for padding outputs / sources), then their A windows
-    for (int p = tid; p < 4 * NG * 8 * KS; p += NT) {
+    for (int p = tid; p < 4 * NG * 8 * KS; p += LS_NT) {
         const int t = p / (8 * KS), i = p % (8 * KS);
         const u64 c = (t < A.G && i < A.m) ? smod(A.K[t * MLS_M + i], A.sh[t * MLS_M + i], md) : 0;
         cval[t][i] = c;
@@ -502,17 +510,17 @@ __global__ __launch_bounds__(NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A,
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
     const size_t oo_l = (size_t)blockIdx.z * seg + (size_t)l * n;
-    for (size_t nb = (size_t)blockIdx.x * LS_CH + wave * 64; nb < (size_t)(blockIdx.x + 1) * LS_CH && nb < n;
-         nb += 4 * 64) {
+    for (size_t nb = (size_t)blockIdx.x * LS_CH + wave * 16 * LS_NC; nb < (size_t)(blockIdx.x + 1) * LS_CH && nb < n;
+         nb += LS_NT / 4 * LS_NC) {
         // B fragments: sources 8 ks + 2 lg, +1 of coefficient nb + 16 c + col
-        v4i bf[4][KS];
+        v4i bf[LS_NC][KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const int i0 = 8 * ks + 2 * lg;
             const gu64 *p0 = to_global(xptr[i0]) + xoff[i0] + nb + col;
             const gu64 *p1 = to_global(xptr[i0 + 1]) + xoff[i0 + 1] + nb + col;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) bf[c][ks] = bytes_of(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
+            for (int c = 0; c < LS_NC; ++c) bf[c][ks] = bytes_of(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
         }
 #pragma unroll 1
         for (int grp = 0; grp < NG; ++grp) {
@@ -521,17 +529,17 @@ __global__ __launch_bounds__(NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A,
             u64 *o = optr[t < A.G ? t : 0] + oo_l + nb + col;
             // a second pass adds the first pass's outputs: loaded before the
             // products so the load latency hides under them
-            u64 prev[4] = {0, 0, 0, 0};
+            u64 prev[LS_NC] = {};
             if (A.accumulate) {
 #pragma unroll
-                for (int c = 0; c < 4; ++c) prev[c] = o[16 * c];
+                for (int c = 0; c < LS_NC; ++c) prev[c] = o[16 * c];
             }
-            v4i acc[4][4];  // [column tile][kk]
-            mfma_group<KS>(tab + grp * 4 * KS * 64 * 2, bf, acc, lane);
+            v4i acc[LS_NC][4];  // [column tile][kk]
+            mfma_group<KS, LS_NC>(tab + grp * 4 * KS * 64 * 2, bf, acc, lane);
             if (t < A.G) {
                 const u64 cr = corr[t];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) o[16 * c] = add_mod(add_mod(combine_rows(acc[c], md), cr, md.q), prev[c], md.q);
+                for (int c = 0; c < LS_NC; ++c) o[16 * c] = add_mod(add_mod(combine_rows(acc[c], md), cr, md.q), prev[c], md.q);
             }
         }
     }
@@ -1369,7 +1377,7 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
             dispatch_int<1, 4>((A.m + 7) / 8, [&](auto ks) {
                 dispatch_int<1, 3>((G + 3) / 4, [&](auto ng) {
                     constexpr int KS = decltype(ks)::value, NG = decltype(ng)::value;
-                    launch_clocked("k_linear_sum_mfma", B, k_linear_sum_mfma<KS, NG>, grid, dim3(NT), st, A, seg, mods,
+                    launch_clocked("k_linear_sum_mfma", B, k_linear_sum_mfma<KS, NG>, grid, dim3(LS_NT), st, A, seg, mods,
                                    logN);
                 });
             });
