@@ -452,9 +452,13 @@ __device__ __forceinline__ v4i bytes_of(u64 y0, u64 y1) {
 // Linear sums (PS leaves) on MFMA.  Same arguments and outputs as
 // k_linear_sum_multi; KS = ceil(m / 8) source steps, NG = ceil(G / 4) groups.
 // Block: 4 waves x 4 column tiles of 16 coefficients = 256 coefficients per
-// iteration, LS_CH coefficients per block (the LDS image is built once per block).
-// grid: x = n / LS_CH, y = limb, z = segment.
-constexpr int LS_CH = 1024;
+// iteration, `chunk` coefficients per block (the LDS image is built once per block).
+// grid: x = n / chunk, y = limb, z = segment.
+// Coefficients per block: the LDS image is built once per block, so wide
+// launches take 4096 (2238-2245 us against 2303-2305 us at 1024 on the headline's
+// leaf sums, profiles/r3_mfma/bench_ch_*.json); narrow ones (one ciphertext: the
+// bootstrap's series) halve it until the grid has >= 2048 blocks, down to 256.
+constexpr int LS_CH_MAX = 4096;
 // column tiles per wave and threads per block (A/B: -DFHE_LS_NC=2 -DFHE_LS_NT=512)
 #ifndef FHE_LS_NC
 #define FHE_LS_NC 4
@@ -475,7 +479,8 @@ template <int KS, int NG>
 #else
 #define LS_WAVES
 #endif
-__global__ __launch_bounds__(LS_NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A, size_t seg, const Mod *mods, int logN) {
+__global__ __launch_bounds__(LS_NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A, size_t seg, const Mod *mods, int logN,
+                                                                 int chunk) {
     __shared__ u64 tab[NG * 4 * KS * 64 * 2];
     __shared__ u64 cval[4 * NG][8 * KS];
     __shared__ u64 corr[4 * NG];
@@ -510,7 +515,7 @@ __global__ __launch_bounds__(LS_NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
     const size_t oo_l = (size_t)blockIdx.z * seg + (size_t)l * n;
-    for (size_t nb = (size_t)blockIdx.x * LS_CH + wave * 16 * LS_NC; nb < (size_t)(blockIdx.x + 1) * LS_CH && nb < n;
+    for (size_t nb = (size_t)blockIdx.x * chunk + wave * 16 * LS_NC; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
          nb += LS_NT / 4 * LS_NC) {
         // B fragments: sources 8 ks + 2 lg, +1 of coefficient nb + 16 c + col
         v4i bf[LS_NC][KS];
@@ -1373,12 +1378,14 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
         const double B = 8.0 * (A.m + (double)G * (1 + A.accumulate)) * limbs * segs * ((size_t)1 << logN);
         const size_t n = (size_t)1 << logN;
         if (use_mfma_sums(MF_LIN) && n >= 256) {
-            const dim3 grid((unsigned)((n + LS_CH - 1) / LS_CH), (unsigned)limbs, (unsigned)segs);
+            size_t ch = std::min<size_t>(LS_CH_MAX, n);
+            while (ch > 256 && (n / ch) * (size_t)limbs * (size_t)segs < 2048) ch /= 2;
+            const dim3 grid((unsigned)((n + ch - 1) / ch), (unsigned)limbs, (unsigned)segs);
             dispatch_int<1, 4>((A.m + 7) / 8, [&](auto ks) {
                 dispatch_int<1, 3>((G + 3) / 4, [&](auto ng) {
                     constexpr int KS = decltype(ks)::value, NG = decltype(ng)::value;
                     launch_clocked("k_linear_sum_mfma", B, k_linear_sum_mfma<KS, NG>, grid, dim3(LS_NT), st, A, seg, mods,
-                                   logN);
+                                   logN, (int)ch);
                 });
             });
             continue;
