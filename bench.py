@@ -27,7 +27,7 @@ it does not shard: --gpus N runs N independent replicas (weak scaling).
 Output: one JSON line.  value = ciphertext-mults/s (relinearised ct x ct
 products, incl. those in the Chebyshev PS, summed over ranks / wall time);
 ms_per_step = sort wall time.  Also: roofline of the dominant kernel (HIP
-events on the engine stream) and the CPU-oracle baseline (rank 0, N=1 only).
+events on the engine stream) and the CPU-oracle baseline (rank 0, every world size).
 """
 import argparse
 import json
@@ -153,6 +153,36 @@ def sign_cfg(N):  # tests/DirectSortTest.cpp:104-112
     return (3, 5, 2)
 
 
+def collective_for(world, ndev, local_world):
+    """The partial-sum exchange of a sharded run: 'none' for one rank; 'rccl'
+    when every local rank has a GPU of its own (ndev 0 = not probed: trust the
+    launcher); 'gloo' (host memory) otherwise -- RCCL refuses two ranks on one
+    device (rccl.h), so a rehearsal with more ranks than GPUs goes through the host"""
+    if world <= 1:
+        return 'none'
+    return 'rccl' if ndev == 0 or ndev >= local_world else 'gloo'
+
+
+class ProfRegion:
+    """FHE_PROF_REGION=1: empty marker kernels (k_region_begin / k_region_end,
+    fhe_region_marker) on the engine stream bracket the timed sorts, so a
+    rocprofv3 kernel trace or PMC pass of this run can be cut to the sort alone
+    (scripts/pmc_meta.py region filter: key generation, encryption and the
+    warmup sort stay out of profiles/r4_*).  Without the variable: nothing."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx if os.environ.get('FHE_PROF_REGION') == '1' else None
+
+    def resume(self):
+        if self.ctx:
+            self.ctx.region_marker(True)
+
+    def pause(self):
+        if self.ctx:
+            self.ctx.region_marker(False)
+            self.ctx.sync()
+
+
 class Dist:
     def __init__(self, world, probe_devices=True):
         self.world = world
@@ -166,9 +196,8 @@ class Dist:
             except Exception:
                 ndev = 0
         self.device = self.local % ndev if ndev > 0 else self.local
-        # RCCL needs distinct devices; a rehearsal with more ranks than GPUs
-        # exchanges the partial sums through host memory and gloo instead
-        self.rccl = world > 1 and (ndev == 0 or ndev >= int(os.environ.get('LOCAL_WORLD_SIZE', world)))
+        self.collective = collective_for(world, ndev, int(os.environ.get('LOCAL_WORLD_SIZE', world)))
+        self.rccl = self.collective == 'rccl'
         self.pg = None
         if world > 1:
             import torch.distributed as dist
@@ -229,89 +258,141 @@ def device_sync(ctx):
         pass
 
 
-def pmc_lookup(table, name):
-    """PMC entry for a clocked kernel name: the clock tags launches with their
-    caller phase ('k_ntt_fwd<8, 4, false, 2, 0, false>@rescale') and omits template
-    arguments of the conversion kernels ('k_modup_convert'); rocprofv3 names
-    the instantiation."""
-    base = name.split('@')[0]
-    if base in table:
-        return table[base]
-    hits = [v for k, v in table.items() if k.split('<')[0] == base]
-    if not hits:
-        return None
-    # several instantiations booked under one clock name (k_linear_sum_multi<G>):
-    # launch-weighted mean, like the clock's own per-launch average
-    n = sum(v['launches'] for v in hits)
-    return {'launches': n, 'hbm_bytes_per_launch': sum(v['hbm_bytes_per_launch'] * v['launches'] for v in hits) / n}
+_LIB_SHA = None
 
 
-def valu_fraction(name, avg_s, sq_file, mix_file='valu_mix.json'):
-    """The compute roof of the dominant kernel: the share of the chip's measured
-    VALU throughput its launches use.  valu_frac = SQ_INSTS_VALU per launch (the
-    committed SQ pass of the same workload, profiles/pmc_sq*.json,
+def lib_sha256():
+    """SHA-256 of the loaded engine library: the committed PMC tables carry the
+    hash of the build they were collected on (scripts/pmc_summary.py --lib), and
+    counters of another build are not reported as this one's"""
+    global _LIB_SHA
+    if _LIB_SHA is None:
+        import hashlib
+        h = hashlib.sha256()
+        with open(F.LIB_PATH, 'rb') as f:
+            for chunk in iter(lambda: f.read(1 << 20), b''):
+                h.update(chunk)
+        _LIB_SHA = h.hexdigest()
+    return _LIB_SHA
+
+
+def load_table(fname):
+    """(table, source) of a committed profiles/ table (PMC traffic, SQ counters);
+    (None, reason) when absent or collected on a different libfhesort.so"""
+    path = os.path.join(REPO, 'profiles', fname)
+    if not os.path.exists(path):
+        return None, f'profiles/{fname} absent'
+    with open(path) as f:
+        t = json.load(f)
+    meta = t.pop('_meta', {})
+    want = lib_sha256()
+    if meta.get('lib_sha256') != want:
+        return None, (f'profiles/{fname} is stale: collected on libfhesort.so {str(meta.get("lib_sha256"))[:12]}, '
+                      f'loaded {want[:12]}')
+    return t, f'profiles/{fname}'
+
+
+def family(name):
+    """'k_ntt_fwd<8, 4, true, 0, true>@modup' -> 'k_ntt_fwd'"""
+    return name.split('@')[0].split('<')[0]
+
+
+def table_keys(table, name, by_family):
+    if table is None:
+        return []
+    if by_family:
+        return [k for k in table if family(k) == name]
+    return [name] if name in table else []
+
+
+def weighted(table, keys, field):
+    n = sum(table[k]['launches'] for k in keys)
+    return sum(table[k].get(field, 0) * table[k]['launches'] for k in keys) / n if n else 0.0
+
+
+def valu_fraction(sq, mix, keys, avg_s):
+    """The compute roof: the share of the chip's measured VALU throughput the
+    launches use.  valu_frac = SQ_INSTS_VALU per launch (the committed SQ pass
+    of the same workload and build, profiles/pmc_sq*.json,
     scripts/pmc_sq_summary.py) x 64 lanes x the seconds one lane-instruction of
     the kernel's instruction mix costs at the measured MI355X rates
     (profiles/valu_mix.json, scripts/valu_mix.py: full-rate 67.5 T, half-rate
     36 T, v_mad_u64_u32 23 T, carry/compare pairs 39 T lane-instructions/s) /
-    the live average launch duration.  Near 1: VALU-bound (the HBM fraction
-    cannot rise without fewer instructions).  Instantiations booked under one
-    clock name are launch-weighted."""
-    sq_path = os.path.join(REPO, 'profiles', sq_file)
-    mix_path = os.path.join(REPO, 'profiles', mix_file)
-    if not (os.path.exists(sq_path) and os.path.exists(mix_path)):
-        return {}
-    with open(sq_path) as f:
-        sq = json.load(f)
-    with open(mix_path) as f:
-        mix = json.load(f)
-    base = name.split('@')[0]
-    keys = [k for k in sq if k == base or k.split('<')[0] == base]
+    the live average launch duration.  Near 1: VALU-bound.  Instantiations of
+    one family are launch-weighted."""
     keys = [k for k in keys if k in mix and 'SQ_INSTS_VALU' in sq[k]]
     if not keys:
         return {}
     n = sum(sq[k]['launches'] for k in keys)
     valu_s = sum(sq[k]['launches'] * sq[k]['SQ_INSTS_VALU'] * 64 * mix[k]['ps_per_lane_instr'] * 1e-12
                  for k in keys) / n
-    insts = sum(sq[k]['launches'] * sq[k]['SQ_INSTS_VALU'] for k in keys) / n
-    wc = sum(sq[k]['launches'] * sq[k].get('SQ_WAVE_CYCLES', 0) for k in keys) / n or 1
-    wait = sum(sq[k]['launches'] * sq[k].get('SQ_WAIT_ANY', 0) for k in keys) / n
-    stall = sum(sq[k]['launches'] * sq[k].get('SQ_WAIT_INST_ANY', 0) for k in keys) / n
-    out = {'valu_frac': round(valu_s / avg_s, 4), 'valu_insts_per_launch': round(insts),
-           'valu_seconds_per_launch': valu_s, 'valu_source': f'profiles/{sq_file} + profiles/{mix_file}',
-           'wave_cycle_split': {'waitcnt': round(wait / wc, 3), 'issue_stall': round(stall / wc, 3)}}
+    wc = weighted(sq, keys, 'SQ_WAVE_CYCLES') or 1
+    out = {'valu_frac': round(valu_s / avg_s, 4), 'valu_insts_per_launch': round(weighted(sq, keys, 'SQ_INSTS_VALU')),
+           'valu_seconds_per_launch': valu_s,
+           'wave_cycle_split': {'waitcnt': round(weighted(sq, keys, 'SQ_WAIT_ANY') / wc, 3),
+                                'issue_stall': round(weighted(sq, keys, 'SQ_WAIT_INST_ANY') / wc, 3)}}
     # matrix-core kernels (the i8 sums of products): SQ_VALU_MFMA_BUSY_CYCLES is
     # the MFMA pipe's busy SIMD-cycles per launch (16 per v_mfma_i32_16x16x64_i8);
     # over 1024 SIMDs x the 2.4 GHz peak clock x the live launch duration
-    busy = sum(sq[k]['launches'] * sq[k].get('SQ_VALU_MFMA_BUSY_CYCLES', 0) for k in keys) / n
+    busy = weighted(sq, keys, 'SQ_VALU_MFMA_BUSY_CYCLES')
     if busy > 0:
         out['mfma_frac'] = round(busy / (MFMA_SIMDS * PEAK_CLOCK_HZ * avg_s), 4)
     return out
 
 
-def pmc_lookup_all(table, name):
-    """like pmc_lookup, averaging every field over instantiations (launch-weighted)"""
-    base = name.split('@')[0]
-    if base in table:
-        return table[base]
-    hits = [v for k, v in table.items() if k.split('<')[0] == base]
-    if not hits:
-        return None
-    n = sum(v['launches'] for v in hits)
-    keys = set().union(*[v.keys() for v in hits]) - {'launches'}
-    return {'launches': n, **{k: sum(v.get(k, 0) * v['launches'] for v in hits) / n for k in keys}}
+STREAMING = ('k_tensor', 'k_add', 'k_sub', 'k_ks_inner', 'k_ks_inner_mc', 'k_ks_inner_mk', 'k_ks_inner_mk_sum',
+             'k_mul_plain_sum', 'k_linear_sum')
+
+
+def limiter_of(name, frac, vf):
+    """What bounds the kernel below the HBM roof: 'hbm' for the streaming kernels
+    (or any kernel at >= 0.85 of HBM peak); 'valu' at >= 0.85 of the measured
+    VALU throughput (whatever its waits); 'memory latency' when the SQ pass puts
+    >= 0.3 of its wave cycles in s_waitcnt, more than in issue stalls; else
+    'valu' (issue-bound at low occupancy)"""
+    if family(name) in STREAMING or frac >= 0.85:
+        return 'hbm'
+    if vf.get('valu_frac', 0) >= 0.85:
+        return 'valu'
+    split = vf.get('wave_cycle_split', {})
+    if split.get('waitcnt', 0) >= max(0.3, split.get('issue_stall', 0)):
+        return 'memory latency'
+    return 'valu'
+
+
+def kernel_view(name, st, pmc, sq, mix, by_family):
+    """frac, traffic and compute roof of one kernel (an exact rocprofv3 symbol, or
+    every instantiation of a family) from the live clock + committed tables"""
+    avg_s = st['ms'] / st['launches'] * 1e-3
+    per_launch = st['bytes'] / st['launches']
+    achieved = per_launch / avg_s / 1e9
+    frac = achieved / HBM_PEAK_GBS
+    pk = table_keys(pmc, name, by_family)
+    traffic = round(weighted(pmc, pk, 'hbm_bytes_per_launch')) if pk else None
+    vf = valu_fraction(sq, mix, table_keys(sq, name, by_family), avg_s) if sq and mix else {}
+    return {'kernel': name, 'achieved': round(achieved, 1), 'frac': round(frac, 4), 'traffic': traffic,
+            'traffic_ratio': round(traffic / per_launch, 3) if traffic else None,
+            'limiter': limiter_of(name, frac, vf), **vf,
+            'avg_us': round(avg_s * 1e6, 2), 'launches': st['launches'], 'algorithmic_bytes_per_launch': per_launch}
 
 
 def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc_sq.json'):
     """Roofline of the dominant kernel, measured live: one more (untimed) sort
     runs with every hot kernel launched through hipExtLaunchKernelGGL with
     start/stop events on the engine stream (the stream it runs on), one lane so
-    no other kernel overlaps the measured span; the kernel
-    with the largest total time is reported.  achieved = its algorithmic bytes
-    per launch / its average launch duration.  traffic = HBM bytes
-    per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950
-    + WRITE_SIZE) when profiles/ holds them for this kernel.  `kernels` lists
-    the top kernels by time with their achieved GB/s."""
+    no other kernel overlaps the measured span.  Two dominance views:
+      * the headline (`kernel`, `frac`, ...) is the kernel with the largest total
+        time by exact rocprofv3 symbol (template instantiation; the clock's
+        caller tags '@modup' are aggregated the way rocprofv3 --stats does), so
+        profiles/<run>/run_kernel_stats.csv reproduces it directly;
+      * `by_family`: the largest family when a family's instantiations are
+        aggregated (e.g. the six k_linear_sum_mfma<KS, NG>).
+    achieved = algorithmic bytes per launch / average launch
+    duration.  traffic = HBM bytes per launch from the committed rocprofv3 PMC
+    passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE), valu_frac / mfma_frac from
+    the committed SQ pass -- both only when collected on the loaded
+    libfhesort.so (its SHA-256 is stamped in the table; otherwise null and
+    `pmc_source` says why)."""
     with F.KernelClock(ctx) as clk:
         run_once()  # single lane: concurrent lanes would inflate each kernel's event span
     stats = clk.stats
@@ -319,48 +400,36 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
         with open(dump, 'w') as f:
             json.dump(stats, f, indent=1)
     total_ms = sum(v['ms'] for v in stats.values())
-    # the dominant kernel by rocprof symbol: the clock tags NTT launches with
-    # their caller ('k_ntt_inv_row<0>@mul_tail'); aggregate the tags the
-    # way rocprofv3 --stats does before choosing
-    by_sym = {}
+    by_sym, by_fam = {}, {}
     for k, v in stats.items():
-        a = by_sym.setdefault(k.split('@')[0], {'ms': 0.0, 'launches': 0, 'bytes': 0.0})
-        a['ms'] += v['ms']
-        a['launches'] += v['launches']
-        a['bytes'] += v['bytes']
-    name, st = max(by_sym.items(), key=lambda kv: kv[1]['ms'])
-    avg_s = st['ms'] / st['launches'] * 1e-3
-    per_launch = st['bytes'] / st['launches']
-    achieved = per_launch / avg_s / 1e9
-    traffic, src = None, None
-    pmc = os.path.join(REPO, 'profiles', pmc_file)  # PMC passes of this same workload only
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            t = pmc_lookup(json.load(f), name)
-        if t:
-            traffic, src = t['hbm_bytes_per_launch'], 'profiles/' + pmc_file
-    def table(items, k=8):
+        for agg, key in ((by_sym, k.split('@')[0]), (by_fam, family(k))):
+            a = agg.setdefault(key, {'ms': 0.0, 'launches': 0, 'bytes': 0.0})
+            a['ms'] += v['ms']
+            a['launches'] += v['launches']
+            a['bytes'] += v['bytes']
+    pmc, pmc_src = load_table(pmc_file)
+    sq, sq_src = load_table(sq_file)
+    mix_path = os.path.join(REPO, 'profiles', 'valu_mix.json')
+    mix = json.load(open(mix_path)) if os.path.exists(mix_path) else None
+    sym, st = max(by_sym.items(), key=lambda kv: kv[1]['ms'])
+    fam, fst = max(by_fam.items(), key=lambda kv: kv[1]['ms'])
+    head = kernel_view(sym, st, pmc, sq, mix, False)
+    head['share'] = round(st['ms'] / total_ms, 4)
+    fv = kernel_view(fam, fst, pmc, sq, mix, True)
+    fv['share'] = round(fst['ms'] / total_ms, 4)
+
+    def table(items, k=10):
         top = sorted(items, key=lambda kv: -kv[1]['ms'])[:k]
         return {n: {'share': round(v['ms'] / total_ms, 3), 'avg_us': round(v['ms'] / v['launches'] * 1e3, 1),
-                    'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1)} for n, v in top}
+                    'launches': v['launches'], 'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1)} for n, v in top}
     run_bytes = sum(v['bytes'] for v in stats.values())
-    # roofline priced against HBM (integer modular work; the i8-MFMA linear sums
-    # also report mfma_frac); what limits
-    # the kernel below it: VALU issue for the NTT passes, the
-    # basis conversions and the PS linear sums, HBM for the streaming kernels
-    limiter = 'hbm' if name.split('<')[0] in ('k_tensor', 'k_add', 'k_sub', 'k_ks_inner', 'k_mul_plain_sum') \
-        else 'valu'
-    vf = valu_fraction(name, avg_s, sq_file)
-    split = vf.get('wave_cycle_split', {})
-    if split.get('waitcnt', 0) >= max(0.3, split.get('issue_stall', 0)) and limiter == 'valu':
-        limiter = 'memory latency'  # waves parked in s_waitcnt more than stalled on issue
-    return {'kernel': name, 'bound': 'hbm', 'limiter': limiter, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-            'unit': 'GB/s',
-            'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic, 'traffic_source': src,
-            **vf,
-            'avg_us': round(avg_s * 1e6, 2), 'launches': st['launches'],
-            'algorithmic_bytes_per_launch': per_launch, 'clocked_ms_per_sort': round(total_ms, 1),
-            'kernels': table(by_sym.items()), 'kernels_by_caller': table(stats.items()),
+    return {**head, 'bound': 'hbm', 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'pmc_source': {'traffic': pmc_src, 'sq': sq_src, 'lib_sha256': lib_sha256()},
+            'by_symbol': {'kernel': sym, 'note': 'the headline fields above are this kernel'},
+            'by_family': fv,
+            'clocked_ms_per_sort': round(total_ms, 1),
+            'kernels': table(by_sym.items()), 'families': table(by_fam.items(), 8),
+            'kernels_by_caller': table(stats.items()),
             # whole sort: every clocked kernel's algorithmic bytes,
             # over its summed kernel time here and over the timed wall in with_run()
             'run': {'algorithmic_bytes_per_sort': run_bytes,
@@ -433,6 +502,17 @@ def oracle_full_sort(N, logN, depth, scale_bits, ps_split):
     return None
 
 
+def collective_split(ctx, d, dt_rank, steps):
+    """rank_compute_ms / allreduce_ms per step, each the max over ranks: the
+    engine times every partial-sum exchange from a drained stream to the reduced
+    data (fhe_collective_stats), so compute = this rank's wall minus that"""
+    st = ctx.collective_stats()
+    ar = st['allreduce_s']
+    return {'rank_compute_ms': round(d.max(dt_rank - ar) / steps * 1e3, 2),
+            'allreduce_ms': round(d.max(ar) / steps * 1e3, 3),
+            'allreduce_calls_per_step': round(d.max(float(st['allreduce_calls'])) / steps, 2)}
+
+
 def make_allreduce(ctx, d):
     """RCCL when every rank has its own GPU, else a host + gloo exchange."""
     if d.world > 1 and d.rccl:
@@ -476,13 +556,18 @@ def run_mehp24(a, d):
     ctx.reset_counters()
     device_sync(ctx)
     d.barrier()
+    prof = ProfRegion(ctx)
+    prof.resume()
     t = time.perf_counter()
     for _ in range(a.steps):
         out = run()
     device_sync(ctx)
     d.barrier()
-    dt = d.max(time.perf_counter() - t)
+    dt_rank = time.perf_counter() - t
+    prof.pause()
+    dt = d.max(dt_rank)
     cnt = ctx.counters()
+    split = collective_split(ctx, d, dt_rank, a.steps)
     peak_gb = ctx.pool_stats()['peak'] / 1e9
     hm_total = d.sum(cnt['hmult'])
     ks_total = d.sum(cnt['keyswitch'])
@@ -513,12 +598,13 @@ def run_mehp24(a, d):
                        'N': N, 'ring_dim': 1 << p['log_ring'], 'mult_depth': p['depth'],
                        'pair_compares': P * (P + 1) // 2, 'indicators': P * P, 'max_stack': a.stack,
                        'parallelism': f'pair/indicator-shard x{d.world}',
-                       'collective': 'none' if d.world == 1 else ('rccl' if d.rccl else 'host+gloo (more ranks than GPUs)')},
+                       'collective': {'none': 'none', 'rccl': 'rccl', 'gloo': 'host+gloo (more ranks than GPUs)'}[d.collective]},
             'max_abs_err': float(np.max(np.abs(y - np.sort(x)))),
             'output_level': out.level,
             'hmult_per_sort': int(hm_total / a.steps),
             'setup_s': round(setup_s, 1),
             'hbm_peak_gb_rank0': round(peak_gb, 1),
+            **split,
             'roofline': None,
         }
         if not a.no_roofline and d.world == 1:
@@ -528,7 +614,7 @@ def run_mehp24(a, d):
                                            res['ms_per_step'], 1, op_total / a.steps)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
-        if d.world == 1 and not a.no_cpu_baseline:
+        if not a.no_cpu_baseline:
             try:
                 res['cpu_baseline'] = cpu_baseline(p['log_ring'], p['depth'] + 1, N, a.cpu_sample_mults or 6,
                                                    p['scale_bits'], dnum=p['dnum'])
@@ -597,11 +683,14 @@ def run_kway(a, d):
     ctx.reset_counters()
     device_sync(ctx)
     d.barrier()
+    prof = ProfRegion(ctx)
+    prof.resume()
     t = time.perf_counter()
     for _ in range(a.steps):
         out = run()
     device_sync(ctx)
     d.barrier()
+    prof.pause()
     dt = d.max(time.perf_counter() - t)
     cnt = ctx.counters()
     boots = ctx.kway_bootstraps
@@ -650,7 +739,7 @@ def run_kway(a, d):
                 ctx.set_sort_lanes(a.lanes)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
-        if d.world == 1 and not a.no_cpu_baseline:
+        if not a.no_cpu_baseline:
             try:
                 res['cpu_baseline'] = cpu_bootstrap_baseline(logN, depth, s, budget)
             except Exception as e:
@@ -708,15 +797,19 @@ def main():
     device_sync(ctx)
     d.barrier()
     F.host_stats(reset=True)
+    prof = ProfRegion(ctx)
+    prof.resume()
     t = time.perf_counter()
     for _ in range(a.steps):
         out = ctx.direct_sort(ct, N, rots, cfg, shard=shard, allreduce=allreduce)
     device_sync(ctx)
     d.barrier()
-    dt = time.perf_counter() - t
-    dt = d.max(dt)
+    dt_rank = time.perf_counter() - t
+    prof.pause()
+    dt = d.max(dt_rank)
     warm_parts = F.host_stats(reset=True)
     cnt = ctx.counters()
+    split = collective_split(ctx, d, dt_rank, a.steps)
     peak_gb = ctx.pool_stats()['peak'] / 1e9
     ctx.pool_trim()  # ranks idle at the final barrier hold no cache while rank 0 measures
     d.barrier()
@@ -750,7 +843,7 @@ def main():
                        'N': N, 'ring_dim': 1 << logN, 'mult_depth': depth, 'scale_bits': a.scale_bits,
                        'ps_split': a.ps_split, 'special_primes': ctx.K, 'lanes_per_gpu': a.lanes,
                        'max_stack': a.stack, 'parallelism': f'batch-shard x{d.world}',
-                       'collective': 'none' if d.world == 1 else ('rccl' if d.rccl else 'host+gloo (more ranks than GPUs)')},
+                       'collective': {'none': 'none', 'rccl': 'rccl', 'gloo': 'host+gloo (more ranks than GPUs)'}[d.collective]},
             'max_abs_err': max_err,
             'output_level': out.level,
             'hmult_per_sort': int(hm_total / a.steps),
@@ -764,6 +857,9 @@ def main():
             'cold_breakdown': cold_parts,
             'timed_host_costs': warm_parts,
             'hbm_peak_gb_rank0': round(peak_gb, 1),
+            # per sort, max over ranks: a rank's wall outside the partial-sum
+            # exchanges, and inside them (header + data all-reduce of both phases)
+            **split,
         }
         res['roofline'] = None
         if not a.no_roofline:
@@ -775,7 +871,7 @@ def main():
                 ctx.set_sort_lanes(a.lanes)
             except Exception as e:  # never hide the main number
                 res['roofline'] = {'error': str(e)}
-        if d.world == 1 and not a.no_cpu_baseline:
+        if not a.no_cpu_baseline:  # rank 0 only, at every world size (the other ranks wait at the barrier)
             try:
                 res['cpu_baseline'] = cpu_baseline(logN, depth, N, a.cpu_sample_mults, a.scale_bits)
                 full = oracle_full_sort(N, logN, depth, a.scale_bits, a.ps_split)

@@ -254,7 +254,7 @@ void Bootstrapper::keyGen() {
 }
 
 int Bootstrapper::depth() const {
-    return (int)(enc.size() + dec.size()) + chebPSDepthSplit((int)cheb.size() - 1, cc.ps_split) + cfg.r;
+    return (int)(enc.size() + dec.size()) + chebPSDepthSplit((int)cheb.size() - 1, cc.ps_split()) + cfg.r;
 }
 
 CtPtr Bootstrapper::transform(const Ciphertext &x, const Level &lv, int tag) {

@@ -10,6 +10,7 @@
 #include "fhesort.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -427,19 +428,15 @@ std::unique_ptr<OFNode> of_build(OFPlan &P, const std::vector<double> &f, int mm
     return node;
 }
 
-std::shared_ptr<const OFPlan> of_plan(const std::vector<double> &c) {
-    static std::mutex mu;
-    static std::map<std::vector<double>, std::shared_ptr<const OFPlan>> cache;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = cache.find(c);
-    if (it != cache.end()) return it->second;
+// Division trees cached by coefficient vector: built outside the lock (the
+// degree-6510 series' first build does not block other lanes' lookups), least
+// recently used entries evicted beyond OF_CACHE_MAX series.
+constexpr size_t OF_CACHE_MAX = 64;
+std::shared_ptr<const OFPlan> of_plan_build(const std::vector<double> &c) {
     auto P = std::make_shared<OFPlan>();
     const int n = degree_of(c);
     openfhe_degrees_ps(n, P->k, P->m);
-    if (P->m < 2) {
-        cache[c] = nullptr;
-        return nullptr;
-    }
+    if (P->m < 2) return nullptr;
     const int k2m2k = P->k * (1 << (P->m - 1)) - P->k;
     std::vector<double> f2(c.begin(), c.begin() + n + 1);
     f2.resize(2 * k2m2k + P->k + 1, 0.0);
@@ -449,10 +446,39 @@ std::shared_ptr<const OFPlan> of_plan(const std::vector<double> &c) {
     } catch (const std::invalid_argument &) {
         P->cmax = INFINITY;
     }
-    std::shared_ptr<const OFPlan> out = P;
-    if (!(P->cmax <= OF_CMAX)) out = nullptr;  // ill-conditioned: power-of-two split
-    cache[c] = out;
-    return out;
+    if (!(P->cmax <= OF_CMAX)) return nullptr;  // ill-conditioned: power-of-two split
+    return P;
+}
+std::shared_ptr<const OFPlan> of_plan(const std::vector<double> &c) {
+    struct Entry {
+        std::shared_ptr<const OFPlan> plan;
+        uint64_t used;
+    };
+    static std::mutex mu;
+    static std::map<std::vector<double>, Entry> cache;
+    static uint64_t tick = 0;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(c);
+        if (it != cache.end()) {
+            it->second.used = ++tick;
+            return it->second.plan;
+        }
+    }
+    std::shared_ptr<const OFPlan> plan = of_plan_build(c);  // deterministic: a racing build gives the same plan
+    std::lock_guard<std::mutex> g(mu);
+    auto ins = cache.emplace(c, Entry{plan, ++tick});
+    if (!ins.second) {
+        ins.first->second.used = tick;
+        return ins.first->second.plan;
+    }
+    while (cache.size() > OF_CACHE_MAX) {
+        auto lru = cache.begin();
+        for (auto it = cache.begin(); it != cache.end(); ++it)
+            if (it->second.used < lru->second.used) lru = it;
+        cache.erase(lru);
+    }
+    return plan;
 }
 
 struct PSOpenFHE {
@@ -571,6 +597,12 @@ int chebPSDepthSplit(int d, int split) {
 }
 int chebPSDepth(int d) { return chebPSDepthSplit(d, PS_SPLIT_OPENFHE); }
 
+bool chebPSUsesOpenFHE(const std::vector<double> &coeffs) {
+    std::vector<double> c(coeffs);
+    trim_zeros(c);
+    return c.size() >= 6 && of_plan(c) != nullptr;
+}
+
 CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<double> &coeffs, double a,
                             double b) {
     std::vector<double> c(coeffs);
@@ -582,7 +614,7 @@ CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<
         x = cc.add_const(*x, -(a + b) / (b - a));
     }
     const int d = (int)c.size() - 1;
-    if (cc.ps_split == PS_SPLIT_OPENFHE && d >= 5) {
+    if (cc.ps_split() == PS_SPLIT_OPENFHE && d >= 5) {
         if (auto plan = of_plan(c)) {
             PSOpenFHE ev(cc, *x, plan);
             return ev.run();
@@ -1099,6 +1131,10 @@ void reducePartial(Engine &cc, const Shard &sh, CtPtr &acc, int slots) {
     if (acc && acc->batch != 1) throw std::invalid_argument("sharded run: a partial must be a single ciphertext");
     // header: presence, level + 1, (level + 1)^2, limbs -- summed over ranks.
     // Every rank sees the same sums, so every rank takes the same branch below.
+    // the exchange's time (bench.py: allreduce_ms beside rank_compute_ms) runs
+    // from a drained stream -- this rank's compute is done -- to the reduced data
+    cc.sync();
+    const auto t0 = std::chrono::steady_clock::now();
     auto hdr = cc.alloc_u64(4);
     const u64 l1 = acc ? (u64)(acc->level + 1) : 0;
     u64 h[4] = {acc ? 1ULL : 0ULL, l1, l1 * l1, acc ? (u64)acc->limbs : 0};
@@ -1110,6 +1146,10 @@ void reducePartial(Engine &cc, const Shard &sh, CtPtr &acc, int slots) {
     if (acc->limbs != H.limbs) throw std::runtime_error("sharded run: partial limb count differs from the header");
     sh.allreduce(acc->data, 2 * acc->limbs * cc.n());
     cc.reduce_after_allreduce(*acc);
+    cc.sync();
+    cc.ctr.allreduce_ns += (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now() - t0).count();
+    cc.ctr.allreduce_calls += 1;
 }
 void DirectSortN::reducePartial(CtPtr &acc, int slots) {
     Shard sh;

@@ -49,6 +49,10 @@ CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x, const std::vector<d
 // levels evalChebyshevSeriesPS consumes for a degree-d series (OpenFHE split /
 // given split)
 int chebPSDepth(int degree);
+// true iff evalChebyshevSeriesPS under PS_SPLIT_OPENFHE evaluates these
+// coefficients with OpenFHE's division tree (false: the power-of-two fallback
+// of an ill-conditioned or degree < 5 series)
+bool chebPSUsesOpenFHE(const std::vector<double> &coeffs);
 int chebPSDepthSplit(int degree, int split);
 
 CtPtr compositeSignN(Engine &cc, const Ciphertext &x, int n, const SignConfig &cfg);

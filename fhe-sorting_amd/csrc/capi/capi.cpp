@@ -807,11 +807,11 @@ int fhe_set_ps_split(fhe_ctx *ctx, int split) {
         NEED(ctx);
         if (split != FHE_PS_SPLIT_ENGINE && split != FHE_PS_SPLIT_OPENFHE)
             throw std::invalid_argument("ps split must be FHE_PS_SPLIT_ENGINE or FHE_PS_SPLIT_OPENFHE");
-        ctx->eng->ps_split = split;
+        ctx->eng->set_ps_split(split);
     });
 }
 
-int fhe_get_ps_split(const fhe_ctx *ctx) { return ctx ? ctx->eng->ps_split : -FHE_EINVAL; }
+int fhe_get_ps_split(const fhe_ctx *ctx) { return ctx ? ctx->eng->ps_split() : -FHE_EINVAL; }
 
 int fhe_cheb_ps_depth(int degree, int split) {
     int d = -1;
@@ -821,6 +821,16 @@ int fhe_cheb_ps_depth(int degree, int split) {
         d = chebPSDepthSplit(degree, split);
     });
     return rc ? -rc : d;
+}
+
+int fhe_cheb_ps_plan(const double *coeffs, int ncoeffs) {
+    int r = -1;
+    const int rc = guard([&] {
+        NEED(coeffs);
+        if (ncoeffs < 1) throw std::invalid_argument("fhe_cheb_ps_plan: no coefficients");
+        r = chebPSUsesOpenFHE(std::vector<double>(coeffs, coeffs + ncoeffs)) ? 1 : 0;
+    });
+    return rc ? -rc : r;
 }
 
 int fhe_comm_get_unique_id(uint8_t id[128]) {
@@ -911,10 +921,23 @@ int fhe_counters(fhe_ctx *ctx, uint64_t out[7]) {
         out[6] = c.opbytes;
     });
 }
+int fhe_collective_stats(fhe_ctx *ctx, uint64_t out[2]) {
+    return guard([&] {
+        NEED(ctx);
+        out[0] = ctx->eng->ctr.allreduce_ns;
+        out[1] = ctx->eng->ctr.allreduce_calls;
+    });
+}
 int fhe_reset_counters(fhe_ctx *ctx) {
     return guard([&] { ctx->eng->ctr = Counters(); });
 }
 int fhe_sync(fhe_ctx *ctx) { return guard([&] { ctx->eng->sync(); }); }
+int fhe_region_marker(fhe_ctx *ctx, int begin) {
+    return guard([&] {
+        NEED(ctx);
+        fhe::dev::region_marker(begin != 0, static_cast<hipStream_t>(ctx->eng->stream_handle()));
+    });
+}
 void *fhe_stream(fhe_ctx *ctx) { return ctx ? ctx->eng->stream_handle() : nullptr; }
 int fhe_time_kernel(fhe_ctx *ctx, const char *name, int limbs, int iters, double *avg_ms, double *bytes) {
     return guard([&] {

@@ -7,6 +7,7 @@
 //   * a "prime map" (pmap) gives the prime index of each limb of a batch when
 //     the limbs are not Q primes 0..ell-1 (extended Q u P basis).
 #pragma once
+#include <string>
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <cstddef>
@@ -38,6 +39,21 @@ struct LaunchClock {
 LaunchClock *&launch_clock();
 // caller tag appended to clocked NTT names ("k_ntt_fwd<8, 4, true>@modup"); per thread
 const char *&launch_phase();
+// a stable, process-lifetime copy of s (thread-safe)
+const char *intern_name(const std::string &s);
+// "base<V0, V1, ...>", the instantiation as rocprofv3 spells it, so the clock
+// books template instantiations apart (bench.py roofline.by_symbol); the plain
+// base name when no clock is installed (no string work on the hot path)
+template <int... V>
+inline const char *inst_name(const char *base) {
+    if (!launch_clock()) return base;
+    std::string r(base);
+    r += '<';
+    const int v[] = {V...};
+    for (size_t i = 0; i < sizeof...(V); ++i) r += (i ? ", " : "") + std::to_string(v[i]);
+    r += '>';
+    return intern_name(r);
+}
 
 // Fault diagnostics (environment FHE_FAULT_REPORT=1): every launch notes its
 // kernel and grid in a process-global record, and install_fault_report() (the
@@ -260,6 +276,8 @@ void ew_lift_centered(u64 *out, const u64 *in, int src, int limbs, int segs, siz
                       const Mod *mods, int logN, hipStream_t st);
 // u64 all-reduce fix-up: x mod q_l per limb
 void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st);
+// k_region_begin / k_region_end on `st` (profiling region delimiters)
+void region_marker(bool begin, hipStream_t st);
 
 }  // namespace dev
 }  // namespace fhe

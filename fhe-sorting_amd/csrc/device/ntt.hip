@@ -45,6 +45,34 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
     return COLS ? idx * (NB + 1) + tr : tr * ((1 << PB) + (1 << PB) / 16) + idx + (idx >> 4);
 }
 
+// 32-bit exchanges (FHE_NTT_LDS32, default on): a non-split exchange moves the
+// low and then the high halves of the coefficients through a tile of 32-bit
+// words, half the LDS of a 64-bit tile, so twice the blocks fit a CU: the
+// 256-point passes' 34.8 KB tile held 4 blocks (4 waves per SIMD) where their
+// 52-64 VGPRs allow 8.  Two more barriers; no more registers (the low halves
+// are dead once written).
+#ifndef FHE_NTT_LDS32
+#define FHE_NTT_LDS32 1
+#endif
+constexpr bool LDS32 = FHE_NTT_LDS32 != 0;
+// x'[j] = coefficient at tile position rpos(j), after every lane stored its x[r]
+// at wpos(r)
+template <int E, class WP, class RP>
+__device__ __forceinline__ void exchange32(uint32_t *t32, u64 (&x)[E], WP wpos, RP rpos) {
+#pragma unroll
+    for (int r = 0; r < E; ++r) t32[wpos(r)] = (uint32_t)x[r];
+    __syncthreads();
+    uint32_t lo[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) lo[j] = t32[rpos(j)];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < E; ++r) t32[wpos(r)] = (uint32_t)(x[r] >> 32);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < E; ++j) x[j] = (u64)lo[j] | ((u64)t32[rpos(j)] << 32);
+}
+
 // Split exchange (column passes with G = E / T >= 2 groups per lane: the
 // 512-point columns of ring 2^17).  The L1 -> L2 re-deal runs in G phases
 // through a tile of 1/G the size: phase g moves the L1 registers r = G u + g
@@ -339,7 +367,9 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     constexpr int LEN = 1 << PB;
     constexpr bool SPLIT = COLS && G >= 2;
     constexpr int TPB = SPLIT ? PB - (EB - RB) : PB;  // points per exchange phase (log2)
-    __shared__ u64 tile[SH ? 1 : lds_words<TPB, NB, COLS>()];
+    constexpr bool X32 = LDS32 && !SPLIT;
+    __shared__ u64 tile[SH ? 1 : X32 ? (lds_words<TPB, NB, COLS>() + 1) / 2 : lds_words<TPB, NB, COLS>()];
+    uint32_t *const t32 = reinterpret_cast<uint32_t *>(tile);
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
@@ -494,6 +524,10 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
 #pragma unroll
             for (int r = 0; r < T; ++r) x[G * r + g] = tile[lds_at<TPB, NB, COLS>(tr, t * T + r)];
         }
+    } else if constexpr (X32) {
+        exchange32<E>(
+            t32, x, [&](int r) { return lds_at<PB, NB, COLS>(tr, t + T * r); },
+            [&](int j) { return lds_at<PB, NB, COLS>(tr, (t * G + j / T) * T + j % T); });
     } else {
 #pragma unroll
         for (int r = 0; r < E; ++r) tile[lds_at<PB, NB, COLS>(tr, t + T * r)] = x[r];
@@ -534,6 +568,15 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
                 const int idx = (t * G + g) * T + r;
                 if (valid) a[(size_t)idx * ((size_t)1 << k2) + tid_global] = x[l2reg<G, T, SPLIT>(g, r)];
             }
+    } else if constexpr (X32) {
+        // each lane rewrites only tile words it read itself in the L1 -> L2
+        // exchange (a permutation), so no barrier is needed before it
+        exchange32<E>(
+            t32, x, [&](int j) { return lds_at<PB, NB, COLS>(tr, (t * G + j / T) * T + j % T); },
+            [&](int r) { return lds_at<PB, NB, COLS>(tr, t + T * r); });
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            if (valid) store_row(r, t + T * r, x[r]);
     } else {
 #pragma unroll
         for (int g = 0; g < G; ++g)
@@ -567,7 +610,9 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     constexpr int LEN = 1 << PB;
     constexpr bool SPLIT = COLS && G >= 2;  // split exchange (see l2reg)
     constexpr int TPB = SPLIT ? PB - (EB - RB) : PB;
-    __shared__ u64 tile[SH ? 1 : lds_words<TPB, NB, COLS>()];
+    constexpr bool X32 = LDS32 && !SPLIT;
+    __shared__ u64 tile[SH ? 1 : X32 ? (lds_words<TPB, NB, COLS>() + 1) / 2 : lds_words<TPB, NB, COLS>()];
+    uint32_t *const t32 = reinterpret_cast<uint32_t *>(tile);
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
@@ -662,6 +707,10 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
 #pragma unroll
             for (int u = 0; u < T; ++u) x[G * u + g] = tile[lds_at<TPB, NB, COLS>(tr, u * T + t)];
         }
+    } else if constexpr (X32) {
+        exchange32<E>(
+            t32, x, [&](int j) { return lds_at<PB, NB, COLS>(tr, (t * G + j / T) * T + j % T); },
+            [&](int r) { return lds_at<PB, NB, COLS>(tr, t + T * r); });
     } else {
 #pragma unroll
         for (int g = 0; g < G; ++g)
@@ -835,6 +884,14 @@ LaunchClock *&launch_clock() {
 const char *&launch_phase() {
     static thread_local const char *ph = nullptr;
     return ph;
+}
+const char *intern_name(const std::string &s) {
+    static std::map<std::string, std::string> names;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = names.find(s);
+    if (it == names.end()) it = names.emplace(s, s).first;
+    return it->second.c_str();
 }
 
 void ntt_forward(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const NttTables &T, hipStream_t st) {

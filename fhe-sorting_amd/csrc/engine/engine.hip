@@ -467,7 +467,7 @@ Engine::Engine(ForkTag) {}
 
 std::unique_ptr<Engine> Engine::fork() const {
     std::unique_ptr<Engine> e(new Engine(ForkTag{}));
-    e->ps_split = ps_split;
+    e->ps_split_ = ps_split_;  // shared, not copied
     e->impl.reset(new Impl(*impl));  // shares tables and keys (shared_ptr / raw device pointers)
     auto &I = *e->impl;
     HIP_OK(hipSetDevice(I.device));

@@ -61,8 +61,13 @@ struct Counters {
     // rotation (2l + 2 digits(l)(l+K) + 2l) B, ct x pt 5l B, ct x const 4l B,
     // add 6l B, linear sum of m terms (2l m + 2l) B -- per ciphertext
     u64 opbytes = 0;
+    // sharded runs: host wall time inside the partial-sum exchanges (header +
+    // data all-reduce, from a drained stream to the reduced data), and their count
+    u64 allreduce_ns = 0, allreduce_calls = 0;
     Counters &operator+=(const Counters &o) {
         opbytes += o.opbytes;
+        allreduce_ns += o.allreduce_ns;
+        allreduce_calls += o.allreduce_calls;
         hmult += o.hmult;
         keyswitch += o.keyswitch;
         rotations += o.rotations;
@@ -81,7 +86,11 @@ enum : int { PS_SPLIT_ENGINE = 0, PS_SPLIT_OPENFHE = 1 };
 class Engine {
   public:
     Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int device, u64 seed);
-    int ps_split = PS_SPLIT_OPENFHE;  // copied by fork()
+    // the Paterson-Stockmeyer split, one value shared by this engine and every
+    // fork of it (lane engines cached by the sorters read the current split, so
+    // a change after a sort cannot leave lanes on the old one)
+    int ps_split() const { return *ps_split_; }
+    void set_ps_split(int split) { *ps_split_ = split; }
     ~Engine();
     // A second engine on its own HIP stream and memory pool sharing this one's
     // keys and tables: independent work issued to both (from two host threads)
@@ -264,6 +273,7 @@ class Engine {
     explicit Engine(ForkTag);
 
   private:
+    std::shared_ptr<int> ps_split_ = std::make_shared<int>(PS_SPLIT_OPENFHE);
     CtPtr new_ct(int level, int slots, double scale, size_t limbs, int batch = 1);
 };
 

@@ -4,6 +4,7 @@
 #include "wire.hpp"
 
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <cmath>
@@ -41,17 +42,46 @@ struct File {
     }
 };
 
-// Writes go to a temporary file beside the target (created with mode 0600 for
-// a secret key, 0644 otherwise, before the umask) that replaces the target by
+// the process umask without changing it (umask(2) can only be read by setting
+// it, which would race with other threads creating files): /proc/self/status
+mode_t current_umask() {
+    if (FILE *f = std::fopen("/proc/self/status", "r")) {
+        char line[256];
+        unsigned m = 022;
+        bool found = false;
+        while (std::fgets(line, sizeof line, f))
+            if (std::sscanf(line, "Umask: %o", &m) == 1) {
+                found = true;
+                break;
+            }
+        std::fclose(f);
+        if (found) return (mode_t)m;
+    }
+    return 022;
+}
+
+// Writes go to a temporary file beside the target that replaces the target by
 // rename() only once the whole object is written: a failed write never leaves
-// a truncated file in place of a good one.
+// a truncated file in place of a good one.  The temporary name has a random
+// suffix and is created exclusively (mkostemp: O_CREAT | O_EXCL, never through
+// an existing file or symlink, so concurrent writers of one path and other
+// users of the directory cannot hand it an inode of theirs); its mode is set
+// on the descriptor before any byte is written: 0600 for a secret key, 0644
+// less the umask otherwise.
 class Writer {
   public:
     Writer(const std::string &path, Kind kind, uint64_t pid, const host::Params &P, uint64_t body_words)
         : target_(path) {
-        tmp_ = path + ".tmp." + std::to_string((long)getpid());
-        const int fd = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, kind == SecretKey ? 0600 : 0644);
+        std::string tmpl = path + ".tmp.XXXXXX";
+        const int fd = ::mkostemp(&tmpl[0], O_CLOEXEC);
         if (fd < 0) throw IoError("cannot open " + path + " for writing");
+        tmp_ = tmpl;
+        const mode_t mode = kind == SecretKey ? 0600 : 0644 & ~current_umask();
+        if (::fchmod(fd, mode) != 0) {
+            ::close(fd);
+            ::unlink(tmp_.c_str());
+            throw IoError("cannot set the mode of " + path);
+        }
         file_.path = path;
         file_.f = ::fdopen(fd, "wb");
         if (!file_.f) {
@@ -59,10 +89,19 @@ class Writer {
             ::unlink(tmp_.c_str());
             throw IoError("cannot open " + path + " for writing");
         }
-        const uint64_t h[kHeaderWords] = {kMagic, (uint64_t)kVersion | ((uint64_t)kind << 32), pid, (uint64_t)P.logN,
-                                          P.nq(), (uint64_t)P.K, body_words, 0};
-        raw(h, 1);
-        put(h + 1, kHeaderWords - 1);
+        // the destructor does not run for a throwing constructor: a failed header
+        // write removes the temporary file here
+        try {
+            const uint64_t h[kHeaderWords] = {kMagic, (uint64_t)kVersion | ((uint64_t)kind << 32), pid,
+                                              (uint64_t)P.logN, P.nq(), (uint64_t)P.K, body_words, 0};
+            raw(h, 1);
+            put(h + 1, kHeaderWords - 1);
+        } catch (...) {
+            std::fclose(file_.f);
+            file_.f = nullptr;
+            ::unlink(tmp_.c_str());
+            throw;
+        }
         left_ = body_words;
     }
     ~Writer() {

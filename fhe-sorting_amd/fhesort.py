@@ -160,6 +160,8 @@ _SIGS = {
     'fhe_moddown': (C.c_int, [vp, u64p, C.c_int, u64p]),
     'fhe_automorph': (C.c_int, [vp, u64p, C.c_int, C.c_uint64, u64p]),
     'fhe_counters': (C.c_int, [vp, u64p]),
+    'fhe_collective_stats': (C.c_int, [vp, u64p]),
+    'fhe_region_marker': (C.c_int, [vp, C.c_int]),
     'fhe_reset_counters': (C.c_int, [vp]),
     'fhe_sync': (C.c_int, [vp]),
     'fhe_stream': (vp, [vp]),
@@ -176,6 +178,7 @@ _SIGS = {
     'fhe_prng_block': (C.c_int, [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     'fhe_get_ps_split': (C.c_int, [vp]),
     'fhe_cheb_ps_depth': (C.c_int, [C.c_int, C.c_int]),
+    'fhe_cheb_ps_plan': (C.c_int, [C.POINTER(C.c_double), C.c_int]),
     'fhe_pool_trim': (C.c_int, [vp]),
     'fhe_pool_stats': (C.c_int, [vp, u64p, u64p, u64p]),
     'fhe_ct_stack': (C.c_int, [vp, C.POINTER(C.c_void_p), C.c_int, C.POINTER(C.c_void_p)]),
@@ -760,6 +763,17 @@ class Context:
         return dict(zip(['hmult', 'keyswitch', 'rotations', 'rescale', 'ptmult', 'constmult', 'opbytes'],
                         map(int, out)))
 
+    def collective_stats(self):
+        """{'allreduce_s': host seconds inside the sharded sorts' partial-sum
+        exchanges since reset_counters(), 'allreduce_calls': their count}"""
+        out = np.zeros(2, dtype=np.uint64)
+        _chk(lib().fhe_collective_stats(self.h, _u64(out)))
+        return {'allreduce_s': int(out[0]) * 1e-9, 'allreduce_calls': int(out[1])}
+
+    def region_marker(self, begin):
+        """k_region_begin / k_region_end on the context stream (profiling)"""
+        _chk(lib().fhe_region_marker(self.h, 1 if begin else 0))
+
     def reset_counters(self):
         _chk(lib().fhe_reset_counters(self.h))
 
@@ -790,7 +804,7 @@ class KernelClock:
     def __exit__(self, *exc):
         import json
         need = C.c_size_t()
-        buf = C.create_string_buffer(1 << 16)
+        buf = C.create_string_buffer(1 << 20)
         _chk(lib().fhe_kernel_clock_stop(self.ctx.h, buf, len(buf), C.byref(need)))
         if need.value > len(buf):
             raise FheError(FHE_EINTERNAL, 'kernel clock report truncated')
@@ -816,6 +830,16 @@ def prng_block(key, counter, nonce):
     P32 = C.POINTER(C.c_uint32)
     _chk(lib().fhe_prng_block(k.ctypes.data_as(P32), int(counter), nn.ctypes.data_as(P32), out.ctypes.data_as(P32)))
     return out
+
+
+def cheb_ps_uses_openfhe(coeffs):
+    """True iff the OpenFHE split evaluates these coefficients with its division
+    tree (fhe_cheb_ps_plan; False: the power-of-two fallback)"""
+    c = np.ascontiguousarray(coeffs, dtype=np.float64)
+    r = lib().fhe_cheb_ps_plan(c.ctypes.data_as(C.POINTER(C.c_double)), len(c))
+    if r < 0:
+        raise FheError(-r, lib().fhe_last_error().decode())
+    return r == 1
 
 
 def cheb_ps_depth(degree, split=PS_SPLIT_OPENFHE):

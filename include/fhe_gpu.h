@@ -224,6 +224,11 @@ int fhe_get_ps_split(const fhe_ctx *ctx);
 /* levels a degree-`degree` series consumes under `split` (the output level of
  * fhe_cheb_ps is the input level plus this); < 0 on bad arguments */
 int fhe_cheb_ps_depth(int degree, int split);
+/* 1 if fhe_cheb_ps under FHE_PS_SPLIT_OPENFHE evaluates these coefficients
+ * with OpenFHE's division tree, 0 if it falls back to the power-of-two split
+ * (degree < 5, or a quotient coefficient above 1024: DESIGN.md §3); < 0 on bad
+ * arguments.  Host only. */
+int fhe_cheb_ps_plan(const double *coeffs, int ncoeffs);
 
 /* ------------------------------------------------------------ hybrid sort */
 /* DirectSort<N>::sort_hybrid (src/sort_algo.h:1050-1064; mode 0) or
@@ -391,7 +396,17 @@ int fhe_set_mfma_sums(int mask);
  * ct x const, add, linear sum formulas, each op at its own level) */
 int fhe_counters(fhe_ctx *ctx, uint64_t out[7]);
 int fhe_reset_counters(fhe_ctx *ctx);
+/* sharded sorts' partial-sum exchanges since the last fhe_reset_counters:
+ * out = {host nanoseconds inside them (header + data all-reduce, measured from a
+ * drained stream to the reduced data), exchanges}.  The reference's reduction
+ * points are the rank sums after its batch loops (src/sort_algo.h:489-490,
+ * 740-741); a bench splits a rank's wall into compute and collective with it. */
+int fhe_collective_stats(fhe_ctx *ctx, uint64_t out[2]);
 int fhe_sync(fhe_ctx *ctx);
+/* enqueue an empty marker kernel (k_region_begin if begin != 0, else
+ * k_region_end) on the context stream: it delimits a measured region in a
+ * rocprofv3 kernel trace or PMC pass (bench.py FHE_PROF_REGION=1) */
+int fhe_region_marker(fhe_ctx *ctx, int begin);
 /* opaque hipStream_t of the context (for event timing by the caller) */
 void *fhe_stream(fhe_ctx *ctx);
 /* time `iters` launches of one hot kernel ("ks_inner", "ntt_fwd",

@@ -13,10 +13,15 @@ import json
 import re
 import sys
 
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+from pmc_meta import meta, region  # noqa: E402
+
 
 def load(path, counter):
     acc = collections.defaultdict(lambda: [0, 0.0])
-    for r in csv.DictReader(open(path)):
+    rows, found = region(list(csv.DictReader(open(path))))
+    print(f'{path}: {"region markers found" if found else "no region markers: every dispatch"}', file=sys.stderr)
+    for r in rows:
         if r['Counter_Name'] != counter:
             continue
         m = re.search(r'(k_[a-z0-9_]+(<[^>]*>)?)\(', r['Kernel_Name'])
@@ -35,6 +40,7 @@ for k in sorted(set(f) & set(w)):
     wk = w[k][1] / w[k][0]
     out[k] = {'launches': f[k][0], 'fetch_size_kib': round(fk, 1), 'write_size_kib': round(wk, 1),
               'hbm_bytes_per_launch': round((2 * fk + wk) * 1024)}
-json.dump(out, open(sys.argv[3], 'w'), indent=1)
 for k, v in out.items():
     print(k, v)
+out['_meta'] = meta()
+json.dump(out, open(sys.argv[3], 'w'), indent=1)

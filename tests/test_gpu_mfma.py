@@ -51,8 +51,15 @@ def test_chebyshev_ps_mfma(deg, split, mask):
     gpu = F.Context(12, L, 40, 60, 3, seed=9, keygen=False, ps_split=split)
     gpu.load_keys_from(orc)
     ox = orc.encrypt(np.linspace(-1, 1, 16), 16)
-    c = np.random.default_rng(deg).normal(size=deg + 1) / (1 + np.arange(deg + 1))
-    same(gpu.cheb(gpu.from_oracle(ox), c), orc.cheb(ox, c))
+    # a well-conditioned series (coefficients decaying like 1/i^2): OpenFHE's
+    # division tree takes it (a slowly decaying one could fall back
+    # to the power-of-two split and run the same path twice)
+    c = np.random.default_rng(deg).normal(size=deg + 1) / (1 + np.arange(deg + 1)) ** 2
+    if deg >= 5:
+        assert F.cheb_ps_uses_openfhe(c)
+    out = gpu.cheb(gpu.from_oracle(ox), c)
+    same(out, orc.cheb(ox, c))
+    assert out.level == ox.level + F.cheb_ps_depth(deg, split)
 
 
 @pytest.mark.parametrize('L', [12, 65])
@@ -101,3 +108,31 @@ def test_ring16_products_mfma():
     st = gpu.mul(gpu.stack(gx), gx[2])
     for m in range(3):
         same(gpu.member(st, m), orc.mul(xs[m], xs[2]))
+
+
+def test_leaf_sums_4096_blocks_ring16_stack32():
+    """k_linear_sum_mfma at the width the bench runs it: ring 2^16 and a
+    32-member stack (64 segments), so the launches take the 4096-coefficient
+    blocks (kernels.hip ew_linear_sum_multi: n / 4096 x limbs x segments >= 2048)
+    and passes of more than 8 baby steps (KS >= 2) and more than 4 leaves
+    (NG >= 2).  Every member word-identical to the oracle's series on that
+    member (four distinct inputs, each stacked eight times)."""
+    L = 10
+    orc = O.Context(16, L, 40, 60, 3, seed=61)
+    gpu = F.Context(16, L, 40, 60, 3, seed=61, keygen=False)
+    gpu.load_keys_from(orc, [])
+    rng = np.random.default_rng(61)
+    xs = [orc.encrypt(rng.uniform(-1, 1, 64), 64) for _ in range(4)]
+    c = rng.normal(size=120) / (1 + np.arange(120)) ** 2
+    assert F.cheb_ps_uses_openfhe(c)
+    st = gpu.stack([gpu.from_oracle(xs[m % 4]) for m in range(32)])
+    clk_ok = False
+    with F.KernelClock(gpu) as clk:
+        out = gpu.cheb(st, c)
+    for name in clk.stats:
+        if name.startswith('k_linear_sum_mfma<'):
+            clk_ok = True
+    assert clk_ok, f'no k_linear_sum_mfma launch: {sorted(clk.stats)}'
+    ref = [orc.cheb(x, c) for x in xs]
+    for m in range(32):
+        same(gpu.member(out, m), ref[m % 4])

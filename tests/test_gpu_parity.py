@@ -462,6 +462,29 @@ def test_direct_sort_multi_batch_stacked(stack, lanes):
     assert np.max(np.abs(gpu.decrypt(gout) - np.sort(x))) < 0.01
 
 
+def test_ps_split_change_reaches_cached_lanes():
+    """the sorters cache forked lane engines; switching the
+    Paterson-Stockmeyer split after a sort must reach them too (the split is
+    shared by an engine and its forks), so a second sort on two lanes matches
+    the oracle under the new split, and switching back matches the first."""
+    N, cfg = 64, (3, 3, 2)
+    depth, rots = O.size_parameters(N)
+    orcs = {s: O.Context(11, depth, 40, 60, 3, seed=7, ps_split=s) for s in (F.PS_SPLIT_OPENFHE, F.PS_SPLIT_ENGINE)}
+    for o in orcs.values():
+        o.gen_rotation_keys(rots)
+    gpu = F.Context(11, depth, 40, 60, 3, seed=7, keygen=False)
+    gpu.load_keys_from(orcs[F.PS_SPLIT_OPENFHE], rots)
+    gpu.set_sort_stack(1)
+    gpu.set_sort_lanes(2)
+    x = np.random.default_rng(65).permutation(N) / N
+    ox = orcs[F.PS_SPLIT_OPENFHE].encrypt(x, N)
+    gx = gpu.from_oracle(ox)
+    for split in (F.PS_SPLIT_OPENFHE, F.PS_SPLIT_ENGINE, F.PS_SPLIT_OPENFHE):
+        gpu.set_ps_split(split)
+        assert gpu.ps_split == split
+        same(gpu.direct_sort(gx, N, rots, cfg), orcs[split].direct_sort(ox, N, rots, cfg))
+
+
 def test_ring_2_17_ops_match_oracle():
     """Ring 2^17 (the reference's MEHP24 ring; 2^8 x 2^9 NTT passes): encryption,
     products, rescales, rotations and plaintext products bit-exact."""

@@ -203,3 +203,28 @@ def test_secret_key_file_mode_and_atomic_replace(tmp_path):
     assert os.stat(sk).st_mode & 0o077 == 0
     assert sorted(os.listdir(tmp_path)) == ['sk.bin']
     ctx.close()
+
+
+def test_temp_file_is_exclusive_and_mode_set_on_descriptor(tmp_path):
+    """the temporary file is created exclusively under a random
+    name (a pre-planted world-readable '<path>.tmp.<pid>' file or symlink is never
+    reused), and the secret key's 0600 is applied to the descriptor whatever the
+    umask; a public key gets 0644 less the umask.  No temporary file is left."""
+    ctx = F.Context(12, 6, 40, 60, 3, seed=3)
+    sk = str(tmp_path / 'sk.bin')
+    planted = sk + '.tmp.' + str(os.getpid())
+    with open(planted, 'w') as f:
+        f.write('planted')
+    os.chmod(planted, 0o666)
+    old = os.umask(0)
+    try:
+        ctx.serialize_secret_key(sk)
+        pk = str(tmp_path / 'pk.bin')
+        ctx.serialize_public_key(pk)
+    finally:
+        os.umask(old)
+    assert os.stat(sk).st_mode & 0o777 == 0o600
+    assert os.stat(pk).st_mode & 0o777 == 0o644
+    assert open(planted).read() == 'planted'  # untouched
+    assert sorted(os.listdir(tmp_path)) == sorted(['sk.bin', 'pk.bin', os.path.basename(planted)])
+    ctx.close()
