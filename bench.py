@@ -428,8 +428,8 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
             'by_symbol': {'kernel': sym, 'note': 'the headline fields above are this kernel'},
             'by_family': fv,
             'clocked_ms_per_sort': round(total_ms, 1),
-            'kernels': table(by_sym.items()), 'families': table(by_fam.items(), 8),
-            'kernels_by_caller': table(stats.items()),
+            'kernels': table(by_sym.items(), 16), 'families': table(by_fam.items(), 8),
+            'kernels_by_caller': table(stats.items(), 24),
             # whole sort: every clocked kernel's algorithmic bytes,
             # over its summed kernel time here and over the timed wall in with_run()
             'run': {'algorithmic_bytes_per_sort': run_bytes,

@@ -165,12 +165,12 @@ struct PSEval {
     void evaluate_chunk(size_t first) {
         const int target = leaves[first].target;
         const bool raw = leaves[first].raw;
-        // up to 10 leaves per linear-sum pass (one read of the baby steps for all
+        // up to 16 leaves per linear-sum pass (one read of the baby steps for all
         // of them; FHE_PS_CHUNK for A/B timing)
         static const size_t max_chunk = [] {
             const char *e = std::getenv("FHE_PS_CHUNK");
-            const int v = e ? std::atoi(e) : 10;
-            return (size_t)std::min(10, std::max(1, v));
+            const int v = e ? std::atoi(e) : 16;
+            return (size_t)std::min(16, std::max(1, v));
         }();
         std::vector<size_t> chunk;
         for (size_t i = first; i < leaves.size() && chunk.size() < max_chunk; ++i)
@@ -522,11 +522,12 @@ struct PSOpenFHE {
         for (int j = 1; j < m; ++j) t = twice_prod(*t, *T2[j], T2[0].get(), -1.0);
         return t;
     }
-    // leaves sharing (target, raw) are evaluated up to 10 per linear-sum pass
+    // leaves sharing (target, raw) are evaluated up to 16 per linear-sum pass
+    // (the leaf-sum kernel's outputs; any grouping gives the same words)
     void evaluate_chunk(size_t first) {
         const OFLeaf &L0 = P->leaves[first];
         std::vector<size_t> chunk;
-        for (size_t i = first; i < P->leaves.size() && chunk.size() < 10; ++i)
+        for (size_t i = first; i < P->leaves.size() && chunk.size() < 16; ++i)
             if (P->leaves[i].mm == L0.mm && P->leaves[i].raw == L0.raw && !ready.count(i)) chunk.push_back(i);
         std::vector<int> idx;
         for (size_t c : chunk)

@@ -449,39 +449,37 @@ __device__ __forceinline__ v4i bytes_of(u64 y0, u64 y1) {
     return v4i{(int)(uint32_t)y0, (int)(uint32_t)(y0 >> 32), (int)(uint32_t)y1, (int)(uint32_t)(y1 >> 32)};
 }
 
-// Linear sums (PS leaves) on MFMA.  Same arguments and outputs as
-// k_linear_sum_multi; KS = ceil(m / 8) source steps, NG = ceil(G / 4) groups.
-// Block: 4 waves x 4 column tiles of 16 coefficients = 256 coefficients per
-// iteration, `chunk` coefficients per block (the LDS image is built once per block).
-// grid: x = n / chunk, y = limb, z = segment.
-// Coefficients per block: the LDS image is built once per block, so wide
-// launches take 4096 (2238-2245 us against 2303-2305 us at 1024 on the headline's
-// leaf sums, profiles/r3_mfma/bench_ch_*.json); narrow ones (one ciphertext: the
-// bootstrap's series) halve it until the grid has >= 2048 blocks, down to 256.
+// Coefficients per block of the leaf sums: wide launches take 4096 (round 3:
+// 2238-2245 us against 2303-2305 us at 1024 per launch, profiles/r3_mfma); narrow
+// ones (one ciphertext: the bootstrap's series) halve it until the grid has
+// >= 2048 blocks, down to 256.
 constexpr int LS_CH_MAX = 4096;
-// column tiles per wave and threads per block (A/B: -DFHE_LS_NC=2 -DFHE_LS_NT=512)
-#ifndef FHE_LS_NC
-#define FHE_LS_NC 4
-#endif
-#ifndef FHE_LS_NT
-#define FHE_LS_NT 256
-#endif
-constexpr int LS_NC = FHE_LS_NC, LS_NT = FHE_LS_NT;
+// Paterson-Stockmeyer leaf sums in one pass (round 4): up to 16 outputs x 64
+// baby steps per launch, so the degree-6510 doubled sinc's 52 baby steps and a
+// level's leaves are read once (round 3: passes of 10 leaves x 32 steps, the
+// second pass re-reading and re-writing its outputs).  The constants come from
+// a device table ([G][m] K and shift, cached by the engine per series and level)
+// instead of the 4-KB argument block.  The A fragments are no longer an LDS image
+// of every 16-shift window (G m 128 B: 114 KB at 16 x 56): a lane reads the two
+// byte-reversed digit words of its (output, source pair) -- 16 B from a G m 8-B
+// LDS table -- and shifts its window out of them per row block (two 64-bit
+// shifts), so the LDS holds 16 KB and never bounds occupancy.  Each wave owns two
+// 16-coefficient column tiles; every source's B fragment stays in registers
+// across the output groups.  Same exact sums and reductions as
+// round 3's LDS-image kernel and k_linear_sum_multi (word-identical).
+struct LeafArgs {
+    u64 *out[LEAF_G];
+    const u64 *x[LEAF_M];
+    uint32_t xseg[LEAF_M];  // segment strides in words (limbs * n < 2^32)
+    const int64_t *K;       // device [G][m]
+    const uint8_t *sh;      // device [G][m]
+    int m, G, accumulate;
+};
+constexpr int LF_NC = 2, LF_NT = 256;
 template <int KS, int NG>
-// three waves per SIMD (164 registers, accumulators in VGPRs, no spills) instead
-// of the compiler's two; the LDS image of the widest instantiation allows three
-// blocks per CU.  FHE_LS_WPE=0 at build time drops the hint (A/B).
-#ifndef FHE_LS_WPE
-#define FHE_LS_WPE 3
-#endif
-#if FHE_LS_WPE
-#define LS_WAVES __attribute__((amdgpu_waves_per_eu(FHE_LS_WPE, 8)))
-#else
-#define LS_WAVES
-#endif
-__global__ __launch_bounds__(LS_NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs A, size_t seg, const Mod *mods, int logN,
-                                                                 int chunk) {
-    __shared__ u64 tab[NG * 4 * KS * 64 * 2];
+__global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_leaf_sums_mfma(LeafArgs A, size_t seg, const Mod *mods, int logN,
+                                                          int chunk) {
+    __shared__ u64 etab[4 * NG][8 * KS];  // byte-reversed balanced digits of each constant
     __shared__ u64 cval[4 * NG][8 * KS];
     __shared__ u64 corr[4 * NG];
     __shared__ const u64 *xptr[8 * KS];
@@ -491,14 +489,11 @@ __global__ __launch_bounds__(LS_NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs
     const int l = blockIdx.y;
     const Mod md = mods[l];
     const int tid = threadIdx.x;
-    // constants (zero for padding outputs / sources), then their A windows
-    for (int p = tid; p < 4 * NG * 8 * KS; p += LS_NT) {
+    for (int p = tid; p < 4 * NG * 8 * KS; p += LF_NT) {
         const int t = p / (8 * KS), i = p % (8 * KS);
-        const u64 c = (t < A.G && i < A.m) ? smod(A.K[t * MLS_M + i], A.sh[t * MLS_M + i], md) : 0;
+        const u64 c = (t < A.G && i < A.m) ? smod(A.K[t * A.m + i], A.sh[t * A.m + i], md) : 0;
         cval[t][i] = c;
-        const u64 e = balanced_digits(c);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) tab[afrag_offset<KS>(t, i, s)] = shift_window(e, s);
+        etab[t][i] = __builtin_bswap64(balanced_digits(c));
     }
     if (tid < 8 * KS) {  // padding sources read source 0 (their constants are zero)
         const int i = tid < A.m ? tid : 0;
@@ -514,37 +509,61 @@ __global__ __launch_bounds__(LS_NT) LS_WAVES void k_linear_sum_mfma(MultiLinArgs
     }
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
+    const int ta = (lane & 15) >> 2, rr = lane & 3;  // A row: output ta of the group, shift 4 kk + rr
     const size_t oo_l = (size_t)blockIdx.z * seg + (size_t)l * n;
-    for (size_t nb = (size_t)blockIdx.x * chunk + wave * 16 * LS_NC; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
-         nb += LS_NT / 4 * LS_NC) {
+    for (size_t nb = (size_t)blockIdx.x * chunk + wave * 16 * LF_NC; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
+         nb += LF_NT / 4 * LF_NC) {
         // B fragments: sources 8 ks + 2 lg, +1 of coefficient nb + 16 c + col
-        v4i bf[LS_NC][KS];
+        v4i bf[LF_NC][KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const int i0 = 8 * ks + 2 * lg;
             const gu64 *p0 = to_global(xptr[i0]) + xoff[i0] + nb + col;
             const gu64 *p1 = to_global(xptr[i0 + 1]) + xoff[i0 + 1] + nb + col;
 #pragma unroll
-            for (int c = 0; c < LS_NC; ++c) bf[c][ks] = bytes_of(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
+            for (int c = 0; c < LF_NC; ++c) bf[c][ks] = bytes_of(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
         }
 #pragma unroll 1
         for (int grp = 0; grp < NG; ++grp) {
             const int t = 4 * grp + lg;
-            // padding outputs (t >= G) load output 0's words and store nothing
             u64 *o = optr[t < A.G ? t : 0] + oo_l + nb + col;
-            // a second pass adds the first pass's outputs: loaded before the
-            // products so the load latency hides under them
-            u64 prev[LS_NC] = {};
+            u64 prev[LF_NC] = {};
             if (A.accumulate) {
 #pragma unroll
-                for (int c = 0; c < LS_NC; ++c) prev[c] = o[16 * c];
+                for (int c = 0; c < LF_NC; ++c) prev[c] = o[16 * c];
             }
-            v4i acc[LS_NC][4];  // [column tile][kk]
-            mfma_group<KS, LS_NC>(tab + grp * 4 * KS * 64 * 2, bf, acc, lane);
+            v4i acc[LF_NC][4];
+#pragma unroll
+            for (int c = 0; c < LF_NC; ++c)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) acc[c][kk] = v4i{0, 0, 0, 0};
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(&etab[4 * grp + ta][8 * ks + 2 * lg]);
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const int s = 4 * kk + rr;  // shift_window(e, s) of both sources
+                    u64 w0, w1;
+                    if (kk < 2) {
+                        w0 = e.x >> (8 * (7 - s));
+                        w1 = e.y >> (8 * (7 - s));
+                    } else {
+                        w0 = s == 15 ? 0 : e.x << (8 * (s - 7));
+                        w1 = s == 15 ? 0 : e.y << (8 * (s - 7));
+                    }
+                    const v4i af = bytes_of(w0, w1);
+#pragma unroll
+                    for (int c = 0; c < LF_NC; ++c)
+                        acc[c][kk] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[c][ks], acc[c][kk], 0, 0, 0);
+                }
+                // one source step's windows at a time (hoisting every step's
+                // fragments ahead spilled the one-group instantiations)
+                __builtin_amdgcn_sched_barrier(0);
+            }
             if (t < A.G) {
                 const u64 cr = corr[t];
 #pragma unroll
-                for (int c = 0; c < LS_NC; ++c) o[16 * c] = add_mod(add_mod(combine_rows(acc[c], md), cr, md.q), prev[c], md.q);
+                for (int c = 0; c < LF_NC; ++c) o[16 * c] = add_mod(add_mod(combine_rows(acc[c], md), cr, md.q), prev[c], md.q);
             }
         }
     }
@@ -592,11 +611,13 @@ __global__ __launch_bounds__(NT) void k_permute(u64 *out, const u64 *in, const u
     out[(size_t)blockIdx.z * S.o + ln + k] = in[(size_t)blockIdx.z * S.a + ln + perm[k]];
 }
 __global__ __launch_bounds__(NT) void k_signed_to_rns(u64 *out, const int64_t *coef, const int *pmap,
-                                                      const Mod *mods, int logN) {
+                                                      const Mod *mods, int logN, size_t os, size_t cs) {
     const size_t n = (size_t)1 << logN;
     const int l = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
+    out += blockIdx.z * os;  // member z (batched device encodes)
+    coef += blockIdx.z * cs;
     const Mod m = mods[pmap ? pmap[l] : l];
     const int64_t v = coef[k];
     u64 r;
@@ -1356,49 +1377,71 @@ void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int 
         if (m == 0) break;
     }
 }
+bool linear_sums_on_mfma(int logN) { return use_mfma_sums(MF_LIN) && logN >= 8; }
 void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,
                          int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st,
-                         const uint8_t *sh) {
+                         const uint8_t *sh, const int64_t *dK, const uint8_t *dsh) {
     if (limbs <= 0 || segs <= 0 || G <= 0 || m <= 0) return;
-    if (G > MLS_G) throw std::invalid_argument("ew_linear_sum_multi: at most 10 outputs per pass");
-    for (int base = 0; base < m; base += MLS_M) {
-        MultiLinArgs A{};
-        A.m = std::min(MLS_M, m - base);
-        A.G = G;
-        A.accumulate = base > 0;
-        for (int g = 0; g < G; ++g) A.out[g] = outs[g];
-        for (int i = 0; i < A.m; ++i) {
-            A.x[i] = xs[base + i];
-            A.xseg[i] = xseg[base + i];
-            for (int g = 0; g < G; ++g) {
-                A.K[g * MLS_M + i] = K[(size_t)g * m + base + i];
-                A.sh[g * MLS_M + i] = sh ? sh[(size_t)g * m + base + i] : 0;
+    if (G > LEAF_G) throw std::invalid_argument("ew_linear_sum_multi: at most 16 outputs per call");
+    const size_t n = (size_t)1 << logN;
+    if (linear_sums_on_mfma(logN) && dK && dsh && m <= LEAF_M) {
+        // one pass: every series the sorts evaluate has k <= 52 baby steps (more
+        // than 64 inputs take the VALU passes below)
+        {
+            LeafArgs A{};
+            A.m = m;
+            A.G = G;
+            A.accumulate = 0;
+            for (int g = 0; g < G; ++g) A.out[g] = outs[g];
+            for (int i = 0; i < A.m; ++i) {
+                A.x[i] = xs[i];
+                A.xseg[i] = (uint32_t)xseg[i];
             }
-        }
-        const double B = 8.0 * (A.m + (double)G * (1 + A.accumulate)) * limbs * segs * ((size_t)1 << logN);
-        const size_t n = (size_t)1 << logN;
-        if (use_mfma_sums(MF_LIN) && n >= 256) {
+            A.K = dK;
+            A.sh = dsh;
+            const double B = 8.0 * (A.m + (double)G * (1 + A.accumulate)) * limbs * segs * (double)n;
             size_t ch = std::min<size_t>(LS_CH_MAX, n);
             while (ch > 256 && (n / ch) * (size_t)limbs * (size_t)segs < 2048) ch /= 2;
             const dim3 grid((unsigned)((n + ch - 1) / ch), (unsigned)limbs, (unsigned)segs);
-            dispatch_int<1, 4>((A.m + 7) / 8, [&](auto ks) {
-                dispatch_int<1, 3>((G + 3) / 4, [&](auto ng) {
+            dispatch_int<1, 8>((A.m + 7) / 8, [&](auto ks) {
+                dispatch_int<1, 4>((G + 3) / 4, [&](auto ng) {
                     constexpr int KS = decltype(ks)::value, NG = decltype(ng)::value;
-                    launch_clocked(inst_name<KS, NG>("k_linear_sum_mfma"), B, k_linear_sum_mfma<KS, NG>, grid, dim3(LS_NT), st, A, seg, mods,
-                                   logN, (int)ch);
+                    launch_clocked(inst_name<KS, NG>("k_leaf_sums_mfma"), B, k_leaf_sums_mfma<KS, NG>, grid, dim3(LF_NT),
+                                   st, A, seg, mods, logN, (int)ch);
                 });
             });
-            continue;
         }
-        const dim3 grid = pt_grid(logN, limbs, segs);
-        switch (G) {
-#define MLS_CASE(g)                                                                                          \
-    case g:                                                                                                  \
-        launch_clocked(inst_name<g>("k_linear_sum_multi"), B, k_linear_sum_multi<g>, grid, dim3(NT), st, A, seg, mods, logN); \
+        return;
+    }
+    // VALU: passes of <= 10 outputs x 32 inputs
+    for (int g0 = 0; g0 < G; g0 += MLS_G) {
+        const int Gp = std::min(MLS_G, G - g0);
+        for (int base = 0; base < m; base += MLS_M) {
+            MultiLinArgs A{};
+            A.m = std::min(MLS_M, m - base);
+            A.G = Gp;
+            A.accumulate = base > 0;
+            for (int g = 0; g < Gp; ++g) A.out[g] = outs[g0 + g];
+            for (int i = 0; i < A.m; ++i) {
+                A.x[i] = xs[base + i];
+                A.xseg[i] = xseg[base + i];
+                for (int g = 0; g < Gp; ++g) {
+                    A.K[g * MLS_M + i] = K[(size_t)(g0 + g) * m + base + i];
+                    A.sh[g * MLS_M + i] = sh ? sh[(size_t)(g0 + g) * m + base + i] : 0;
+                }
+            }
+            const double B = 8.0 * (A.m + (double)Gp * (1 + A.accumulate)) * limbs * segs * (double)n;
+            const dim3 grid = pt_grid(logN, limbs, segs);
+            switch (Gp) {
+#define MLS_CASE(g)                                                                                               \
+    case g:                                                                                                       \
+        launch_clocked(inst_name<g>("k_linear_sum_multi"), B, k_linear_sum_multi<g>, grid, dim3(NT), st, A, seg, mods, \
+                       logN);                                                                                     \
         break;
-            MLS_CASE(1) MLS_CASE(2) MLS_CASE(3) MLS_CASE(4) MLS_CASE(5) MLS_CASE(6) MLS_CASE(7) MLS_CASE(8) MLS_CASE(9)
-                MLS_CASE(10)
+                MLS_CASE(1) MLS_CASE(2) MLS_CASE(3) MLS_CASE(4) MLS_CASE(5) MLS_CASE(6) MLS_CASE(7) MLS_CASE(8) MLS_CASE(9)
+                    MLS_CASE(10)
 #undef MLS_CASE
+            }
         }
     }
 }
@@ -1429,9 +1472,10 @@ void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int se
     hipLaunchKernelGGL(k_permute, pt_grid(logN, limbs, segs), dim3(NT), 0, st, out, in, perm, S, logN);
 }
 void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap, const Mod *mods, int logN,
-                      hipStream_t st) {
-    if (limbs <= 0) return;
-    hipLaunchKernelGGL(k_signed_to_rns, pt_grid(logN, limbs, 1), dim3(NT), 0, st, out, coef, pmap, mods, logN);
+                      hipStream_t st, int members, size_t out_stride, size_t coef_stride) {
+    if (limbs <= 0 || members <= 0) return;
+    hipLaunchKernelGGL(k_signed_to_rns, pt_grid(logN, limbs, members), dim3(NT), 0, st, out, coef, pmap, mods, logN,
+                       out_stride, coef_stride);
 }
 void ew_lift_centered(u64 *out, const u64 *in, int src, int limbs, int segs, size_t seg_in, size_t seg_out,
                       const Mod *mods, int logN, hipStream_t st) {

@@ -170,11 +170,19 @@ void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
                    size_t xseg, const Mod *mods, int logN, hipStream_t st, bool accumulate = false,
                    const uint8_t *sh = nullptr);
-// outs[g] = sum_i (K[g*m + i] mod q_l) * x_i for g < G <= 8 in one pass over the
-// inputs (x_i: [segs][limbs][n] with segment stride xseg[i]; outs: stride seg)
+// outs[g] = sum_i (K[g*m + i] 2^sh[g*m + i] mod q_l) * x_i for g < G <= 16 (the
+// Paterson-Stockmeyer leaves of one level; x_i: [segs][limbs][n] with segment
+// stride xseg[i]; outs: stride seg).  On the matrix cores (set_mfma_sums bit 1)
+// one pass reads every input once for up to 16 outputs and 64 inputs; the
+// constants then come from the device copies dK / dsh of K / sh ([G][m]).  The
+// VALU kernel (mask bit clear, no device copies, or m > 64) takes passes of
+// <= 10 outputs x 32 inputs from the host arrays.
+constexpr int LEAF_G = 16, LEAF_M = 64;
 void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,
                          int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st,
-                         const uint8_t *sh = nullptr);
+                         const uint8_t *sh, const int64_t *dK, const uint8_t *dsh);
+// true iff ew_linear_sum_multi runs on the matrix cores at this ring (it then reads dK / dsh)
+bool linear_sums_on_mfma(int logN);
 // out [members][2][limbs][n] = sum_i ct_i * pt_i  (ct_i member stride cmember, 0 = broadcast;
 // c1 at + cpoly; pt_i [limbs][n] shared), lazy 128-bit accumulation
 void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, int m, int limbs, int members,
@@ -188,7 +196,18 @@ void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int se
 void ew_c0_op(u64 *out, const u64 *a, const u64 *p, int64_t K, int sh, int mode, int limbs, int members,
               const Mod *mods, int logN, hipStream_t st);
 void ew_signed_to_rns(u64 *out, const int64_t *coef, int limbs, const int *pmap, const Mod *mods, int logN,
-                      hipStream_t st);
+                      hipStream_t st, int members = 1, size_t out_stride = 0, size_t coef_stride = 0);
+
+// ------------------------------------------------------------ device encode
+// (encode.hip) special inverse FFT of B members of S slots in place (v [B][S]),
+// then coef [B][n] = round(scale[b] * coefficients), word-identical to
+// host::encode_coeffs_complex; ksi [2n + 1], rot [n / 2] are the host encoder's
+// tables; *overflow |= 1 if a scaled coefficient reaches 9.2e18
+void encode_ifft(double2 *v, int64_t *coef, int B, int S, int n, const double2 *ksi, const uint32_t *rot,
+                 const double *scale, unsigned *overflow, hipStream_t st);
+// the sort's masks as slot values: spec [B][3] = {kind, k, r}: kind 0
+// mask_vector(S, N, k) rotated by r, kind 1 checking_vector(S, N, k)
+void mask_slots(double2 *v, int B, int S, int N, const int *spec, hipStream_t st);
 
 // ---------------------------------------------------------------- keyswitch
 // ext[m][j][t][k] for every member m, digit j and target t not in digit j

@@ -28,7 +28,20 @@ namespace dev {
 
 namespace {
 
-constexpr int NTB = 256;  // threads per block
+constexpr int NTB = 256;  // threads per block (row passes, small rings)
+// Wide column passes (FHE_NTT_COL_WIDE, default on): a 256-point column pass
+// runs 64 columns per 1024-thread block, so lane = column and wave = t, the
+// lane's position in its transform: every twiddle of both rounds is then
+// wave-uniform (scalar loads, no VGPRs -- the 16-column blocks held up to 60
+// VGPRs of per-lane round-2 twiddles), a wave's loads and stores are 512-B
+// runs, and the 32-bit exchange tile (66.5 KB) leaves room for two blocks per CU.
+#ifndef FHE_NTT_COL_WIDE
+#define FHE_NTT_COL_WIDE 0
+#endif
+template <int PB, bool COLS>
+constexpr int nthreads() {
+    return (FHE_NTT_COL_WIDE && COLS && PB == 8) ? 1024 : NTB;
+}
 
 // LDS exchange tile.  ROWS: the lanes of one transform are adjacent, so each
 // transform owns a contiguous run padded by one u64 per 16.  COLS: adjacent
@@ -52,9 +65,14 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
 // 52-64 VGPRs allow 8.  Two more barriers; no more registers (the low halves
 // are dead once written).
 #ifndef FHE_NTT_LDS32
-#define FHE_NTT_LDS32 1
+#define FHE_NTT_LDS32 0
 #endif
-constexpr bool LDS32 = FHE_NTT_LDS32 != 0;
+// (row passes keep the 64-bit tile: with theirs at 32 bits the rescale and
+// HMult-tail row passes ran 461 -> 530 and 385 -> 403 us, profiles/r4_a)
+template <bool COLS>
+constexpr bool lds32() {
+    return FHE_NTT_LDS32 != 0 && COLS;
+}
 // x'[j] = coefficient at tile position rpos(j), after every lane stored its x[r]
 // at wpos(r)
 template <int E, class WP, class RP>
@@ -362,12 +380,12 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     constexpr int E = 1 << EB;          // coefficients per lane
     constexpr int RB = PB - EB;         // bits of round 2
     constexpr int T = 1 << RB;          // lanes per transform
-    constexpr int NB = NTB / T;         // transforms per block
+    constexpr int NB = nthreads<PB, COLS>() / T;  // transforms per block
     constexpr int G = E >> RB;          // round-2 groups per lane
     constexpr int LEN = 1 << PB;
     constexpr bool SPLIT = COLS && G >= 2;
     constexpr int TPB = SPLIT ? PB - (EB - RB) : PB;  // points per exchange phase (log2)
-    constexpr bool X32 = LDS32 && !SPLIT;
+    constexpr bool X32 = lds32<COLS>() && !SPLIT;
     __shared__ u64 tile[SH ? 1 : X32 ? (lds_words<TPB, NB, COLS>() + 1) / 2 : lds_words<TPB, NB, COLS>()];
     uint32_t *const t32 = reinterpret_cast<uint32_t *>(tile);
 
@@ -381,7 +399,9 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     int t, tr;  // lane within its transform, transform within the block
     if (COLS) {
         tr = threadIdx.x % NB;
-        t = threadIdx.x / NB;
+        // NB = 64: t is the wave index -- said so, so the twiddle addresses
+        // built from it are scalar
+        t = NB == 64 ? __builtin_amdgcn_readfirstlane(threadIdx.x / NB) : threadIdx.x / NB;
     } else {
         tr = threadIdx.x / T;
         t = threadIdx.x % T;
@@ -605,12 +625,12 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     constexpr int E = 1 << EB;
     constexpr int RB = PB - EB;
     constexpr int T = 1 << RB;
-    constexpr int NB = NTB / T;
+    constexpr int NB = nthreads<PB, COLS>() / T;
     constexpr int G = E >> RB;
     constexpr int LEN = 1 << PB;
     constexpr bool SPLIT = COLS && G >= 2;  // split exchange (see l2reg)
     constexpr int TPB = SPLIT ? PB - (EB - RB) : PB;
-    constexpr bool X32 = LDS32 && !SPLIT;
+    constexpr bool X32 = lds32<COLS>() && !SPLIT;
     __shared__ u64 tile[SH ? 1 : X32 ? (lds_words<TPB, NB, COLS>() + 1) / 2 : lds_words<TPB, NB, COLS>()];
     uint32_t *const t32 = reinterpret_cast<uint32_t *>(tile);
 
@@ -624,7 +644,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     int t, tr;
     if (COLS) {
         tr = threadIdx.x % NB;
-        t = threadIdx.x / NB;
+        t = NB == 64 ? __builtin_amdgcn_readfirstlane(threadIdx.x / NB) : threadIdx.x / NB;
     } else {
         tr = threadIdx.x / T;
         t = threadIdx.x % T;
@@ -755,13 +775,18 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
 // so no lane needs the bounds check and the loads / stores carry no exec-mask
 // branches.  (Waves-per-EU hints and "lean" epilogue variants were measured
 // slower in round 2 and removed)
+// minimum waves per SIMD the compiler must allow (register budget) for the
+// forward column passes (A/B: -DFHE_NTT_COL_WPE=n)
+#ifndef FHE_NTT_COL_WPE
+#define FHE_NTT_COL_WPE 1
+#endif
 template <int PB, int EB, bool COLS, int MODE, bool FULL>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_ntt_fwd(
+__global__ __launch_bounds__((nthreads<PB, COLS>())) __attribute__((amdgpu_waves_per_eu(COLS ? FHE_NTT_COL_WPE : 1, 8))) void k_ntt_fwd(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
     ntt_fwd_body<PB, EB, COLS, MODE, false, FULL>(data, seg, pmap, smap, logN, Tb, F);
 }
 template <int PB, int EB, bool COLS, bool FULL>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_ntt_inv(
+__global__ __launch_bounds__((nthreads<PB, COLS>())) __attribute__((amdgpu_waves_per_eu(COLS ? FHE_NTT_COL_WPE : 1, 8))) void k_ntt_inv(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
     ntt_inv_body<PB, EB, COLS, false, FULL>(data, seg, pmap, smap, logN, Tb, F);
 }
@@ -797,7 +822,8 @@ constexpr int full_bit() {
 template <int PB, int EB, bool COLS, bool FWD, int MODE>
 void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap, const NttTables &T,
                  const NttFuse &F, hipStream_t st) {
-    constexpr int NB = NTB >> (PB - EB);
+    constexpr int NTHR = nthreads<PB, COLS>();
+    constexpr int NB = NTHR >> (PB - EB);
     constexpr bool CAN_SH = !COLS && PB == 8 && EB == 4;
     const int mode = row_shfl_enabled();
     const bool sh = CAN_SH && (mode & (FWD ? 2 : 1)) != 0;
@@ -819,9 +845,9 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const int slot = clk ? clk->events(e0, e1) : -1;
     note_launch(FWD ? (COLS ? "k_ntt_fwd(col)" : "k_ntt_fwd(row)") : (COLS ? "k_ntt_inv(col)" : "k_ntt_inv(row)"), grid,
-                dim3(NTB));
+                dim3(NTHR));
 #define FHE_NTT_LAUNCH(K, FF) \
-    hipExtLaunchKernelGGL((K), grid, dim3(NTB), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
+    hipExtLaunchKernelGGL((K), grid, dim3(NTHR), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
     if (FWD && sh) {
         if (full) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true>), Fs);
         else FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false>), Fs);

@@ -191,6 +191,45 @@ struct Engine::Impl {
     std::map<u64, std::shared_ptr<DevMem>> perms;
     int key_digits = 0;
 
+    // device copies of the leaf sums' constant tables ([G][m] K and shift),
+    // keyed by their bytes: a series at a level uploads once per engine (first
+    // sort), the sums read them from HBM (kernels.hip k_leaf_sums_mfma)
+    struct ConstTab {
+        std::shared_ptr<DevMem> mem;
+        std::vector<int64_t> K;  // host copies stay alive for the asynchronous upload
+        std::vector<uint8_t> sh;
+        u64 used = 0;
+    };
+    std::map<std::string, ConstTab> ctabs;
+    u64 ctab_tick = 0;
+    std::pair<const int64_t *, const uint8_t *> const_table(const std::vector<int64_t> &K,
+                                                           const std::vector<uint8_t> &sh) {
+        std::string key(reinterpret_cast<const char *>(K.data()), K.size() * sizeof(int64_t));
+        key.append(reinterpret_cast<const char *>(sh.data()), sh.size());
+        key.append(std::to_string(K.size()));
+        auto it = ctabs.find(key);
+        if (it == ctabs.end()) {
+            if (ctabs.size() >= 4096) {  // bound the cache: drop the least recently used
+                auto lru = ctabs.begin();
+                for (auto j = ctabs.begin(); j != ctabs.end(); ++j)
+                    if (j->second.used < lru->second.used) lru = j;
+                HIP_OK(hipStreamSynchronize(st));  // its upload / readers are done
+                ctabs.erase(lru);
+            }
+            ConstTab t;
+            t.K = K;
+            t.sh = sh;
+            const size_t kb = K.size() * sizeof(int64_t);
+            t.mem = alloc(kb + sh.size());
+            HIP_OK(hipMemcpyAsync(t.mem->p, t.K.data(), kb, hipMemcpyHostToDevice, st));
+            HIP_OK(hipMemcpyAsync(static_cast<char *>(t.mem->p) + kb, t.sh.data(), sh.size(), hipMemcpyHostToDevice, st));
+            it = ctabs.emplace(std::move(key), std::move(t)).first;
+        }
+        it->second.used = ++ctab_tick;
+        const char *b = static_cast<const char *>(it->second.mem->p);
+        return {reinterpret_cast<const int64_t *>(b), reinterpret_cast<const uint8_t *>(b + K.size() * sizeof(int64_t))};
+    }
+
     std::shared_ptr<DevMem> alloc(size_t bytes) {
         auto m = std::make_shared<DevMem>();
         m->pool = pool;
@@ -1521,8 +1560,9 @@ std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> 
         xseg[i] = xs[i]->limbs * nn;
     }
     std::vector<CtPtr> outs;
-    // passes of at most 10 outputs (the kernel's limit), balanced: 18 -> 9 + 9
-    const size_t passes = (c.size() + 9) / 10, per = (c.size() + passes - 1) / passes;
+    // passes of at most 16 outputs (the kernel's limit), balanced: 18 -> 9 + 9
+    const size_t passes = (c.size() + dev::LEAF_G - 1) / dev::LEAF_G, per = (c.size() + passes - 1) / passes;
+    const bool mfma = dev::linear_sums_on_mfma(LOGN) && m <= (size_t)dev::LEAF_M;
     for (size_t g0 = 0; g0 < c.size(); g0 += per) {
         const int G = (int)std::min<size_t>(per, c.size() - g0);
         std::vector<int64_t> K((size_t)G * m);
@@ -1539,8 +1579,10 @@ std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> 
         u64 *t = static_cast<u64 *>(tm->p);
         std::vector<u64 *> op(G);
         for (int g = 0; g < G; ++g) op[g] = t + (size_t)g * segs * ell * nn;
+        std::pair<const int64_t *, const uint8_t *> dk{nullptr, nullptr};
+        if (mfma) dk = I.const_table(K, sh);
         dev::ew_linear_sum_multi(op.data(), G, xp.data(), xseg.data(), K.data(), (int)m, (int)ell, segs, ell * nn,
-                                 MODS, LOGN, ST, sh.data());
+                                 MODS, LOGN, ST, sh.data(), dk.first, dk.second);
         if (!rescale) {  // raw sums at the pre-rescale scale, views into one allocation
             for (int g = 0; g < G; ++g) {
                 auto r = std::make_shared<Ciphertext>();

@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../fhe-sorting_amd"
 make -s -j8 lib/libfhesort.so >/dev/null
-OBJS=$(ls build/device/ntt.o build/engine/engine.o build/host/*.o build/algo/*.o build/wire/*.o build/capi/*.o)
+OBJS=$(ls build/device/ntt.o build/device/encode.o build/engine/engine.o build/host/*.o build/algo/*.o build/wire/*.o build/capi/*.o)
 while [ $# -ge 2 ]; do
   mkdir -p build/ab
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-unused-function $2 -c csrc/device/kernels.hip -o build/ab/kernels_$1.o 2>/dev/null

@@ -1,4 +1,4 @@
-"""The i8-MFMA sums of products (kernels.hip: k_linear_sum_mfma, k_modup_mfma,
+"""The i8-MFMA sums of products (kernels.hip: k_leaf_sums_mfma, k_modup_mfma,
 k_moddown_rescale_mfma; fhe_set_mfma_sums) against the CPU oracle.
 
 The build default runs the PS linear sums on MFMA and the basis conversions on
@@ -43,7 +43,7 @@ def test_mask_query_and_set():
 @pytest.mark.parametrize('split', [F.PS_SPLIT_OPENFHE, F.PS_SPLIT_ENGINE])
 @pytest.mark.parametrize('deg', [7, 70, 200])
 def test_chebyshev_ps_mfma(deg, split, mask):
-    """Paterson-Stockmeyer leaves through k_linear_sum_mfma (mask 7) and the
+    """Paterson-Stockmeyer leaves through k_leaf_sums_mfma (mask 7) and the
     VALU k_linear_sum_multi (mask 0): word-identical to the oracle."""
     F.set_mfma_sums(mask)
     L = 10 if deg <= 119 else 11
@@ -111,28 +111,27 @@ def test_ring16_products_mfma():
 
 
 def test_leaf_sums_4096_blocks_ring16_stack32():
-    """k_linear_sum_mfma at the width the bench runs it: ring 2^16 and a
+    """k_leaf_sums_mfma at the width the bench runs it: ring 2^16 and a
     32-member stack (64 segments), so the launches take the 4096-coefficient
-    blocks (kernels.hip ew_linear_sum_multi: n / 4096 x limbs x segments >= 2048)
-    and passes of more than 8 baby steps (KS >= 2) and more than 4 leaves
-    (NG >= 2).  Every member word-identical to the oracle's series on that
-    member (four distinct inputs, each stacked eight times)."""
-    L = 10
+    blocks (kernels.hip ew_linear_sum_multi: n / 4096 x limbs x segments >= 2048),
+    passes of more than 8 baby steps (KS >= 2) and more than 4 leaves (NG >= 2):
+    a degree-848 series, the doubled sinc's degree at N = 128.  Every member
+    word-identical to the oracle's series on that member (four distinct inputs,
+    each stacked eight times)."""
+    L = 12
     orc = O.Context(16, L, 40, 60, 3, seed=61)
     gpu = F.Context(16, L, 40, 60, 3, seed=61, keygen=False)
     gpu.load_keys_from(orc, [])
     rng = np.random.default_rng(61)
     xs = [orc.encrypt(rng.uniform(-1, 1, 64), 64) for _ in range(4)]
-    c = rng.normal(size=120) / (1 + np.arange(120)) ** 2
+    c = rng.normal(size=849) / (1 + np.arange(849)) ** 2
     assert F.cheb_ps_uses_openfhe(c)
     st = gpu.stack([gpu.from_oracle(xs[m % 4]) for m in range(32)])
-    clk_ok = False
     with F.KernelClock(gpu) as clk:
         out = gpu.cheb(st, c)
-    for name in clk.stats:
-        if name.startswith('k_linear_sum_mfma<'):
-            clk_ok = True
-    assert clk_ok, f'no k_linear_sum_mfma launch: {sorted(clk.stats)}'
+    shapes = [tuple(int(v) for v in k.split('<')[1].rstrip('>').split(','))
+              for k in clk.stats if k.startswith('k_leaf_sums_mfma<')]
+    assert any(ks >= 2 and ng >= 2 for ks, ng in shapes), f'leaf-sum launches: {sorted(clk.stats)}'
     ref = [orc.cheb(x, c) for x in xs]
     for m in range(32):
         same(gpu.member(out, m), ref[m % 4])
