@@ -75,6 +75,8 @@ def parse():
     ap.add_argument('--dnum', type=int, default=0, help='MEHP24: key-switch digits (0: the parameter table, OpenFHE default 3)')
     ap.add_argument('--lanes', type=int, default=3, help='concurrent batch lanes (forked engines) per GPU (3: 885 vs 898 ms for 2)')
     ap.add_argument('--stack', type=int, default=32, help='max batches stacked into one ciphertext batch')
+    ap.add_argument('--mask-steps', type=int, default=2,
+                    help='extra sorts timed with every mask re-encoded per sort (0: skip)')
     ap.add_argument('--rendezvous-check', action='store_true',
                     help='launch/rendezvous only: ranks meet over gloo, exchange a max and a sum, rank 0 prints '
                          'one JSON line (no GPU work; the multi-rank launcher test)')
@@ -810,6 +812,21 @@ def main():
     warm_parts = F.host_stats(reset=True)
     cnt = ctx.counters()
     split = collective_split(ctx, d, dt_rank, a.steps)
+    # the reference's per-sort encoding: every mask and checking vector
+    # re-encoded (on the device, in batches) at the start of each sort
+    masks_ms = None
+    if a.mask_steps > 0:
+        ctx.set_mask_cache(False)
+        device_sync(ctx)
+        d.barrier()
+        tm = time.perf_counter()
+        for _ in range(a.mask_steps):
+            ctx.direct_sort(ct, N, rots, cfg, shard=shard, allreduce=allreduce)
+        device_sync(ctx)
+        d.barrier()
+        masks_ms = d.max(time.perf_counter() - tm) / a.mask_steps * 1e3
+        mask_parts = F.host_stats(reset=True)
+        ctx.set_mask_cache(True)
     peak_gb = ctx.pool_stats()['peak'] / 1e9
     ctx.pool_trim()  # ranks idle at the final barrier hold no cache while rank 0 measures
     d.barrier()
@@ -853,9 +870,14 @@ def main():
             # allocation pool's first growth; null without a warmup step
             'cold_sort_s': round(cold_s, 4) if cold_s is not None else None,
             # rank 0's host costs inside the cold sort (mask / checking-vector
-            # encodes, pool-miss hipMallocs) and inside the timed sorts (none)
+            # encodes -- on the device -- and pool-miss hipMallocs) and inside
+            # the timed sorts (none)
             'cold_breakdown': cold_parts,
             'timed_host_costs': warm_parts,
+            # wall per sort when every sort re-encodes all its masks on the
+            # device first (fhe_set_mask_cache(0)); ms_per_step keeps them cached
+            'ms_per_step_masks_per_sort': round(masks_ms, 2) if masks_ms is not None else None,
+            'masks_per_sort_breakdown': mask_parts if masks_ms is not None else None,
             'hbm_peak_gb_rank0': round(peak_gb, 1),
             # per sort, max over ranks: a rank's wall outside the partial-sum
             # exchanges, and inside them (header + data all-reduce of both phases)

@@ -1097,8 +1097,18 @@ const Plaintext &DirectSortN::mask(Engine &E, int kind, int num_slots, int k, in
         auto it = mask_cache.find(key);
         if (it != mask_cache.end()) return *it->second;
     }
-    std::vector<double> v = kind == 0 ? vector_rotate(mask_vector(num_slots, N, k), r) : checking_vector(num_slots, N, k);
-    PtPtr p = E.encode(v, num_slots, level);
+    static const bool host_masks = [] {
+        const char *e = std::getenv("FHE_HOST_MASKS");
+        return e && std::atoi(e) == 1;
+    }();
+    PtPtr p;
+    if (host_masks) {
+        std::vector<double> v =
+            kind == 0 ? vector_rotate(mask_vector(num_slots, N, k), r) : checking_vector(num_slots, N, k);
+        p = E.encode(v, num_slots, level);
+    } else {
+        p = E.encode_masks({Engine::MaskSpec{kind, k, r, level}}, num_slots, N)[0];  // word-identical
+    }
     E.sync();  // complete before another lane's stream reads it
     std::lock_guard<std::mutex> lk(mask_mu);
     auto ins = mask_cache.emplace(key, p);
@@ -1318,7 +1328,26 @@ CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext 
     return out;
 }
 
+void DirectSortN::refresh_masks() {
+    cc.sync();
+    for (auto &e : lane_eng) e->sync();  // nothing of the last sort still reads the old masks
+    std::map<int, std::vector<std::tuple<int, int, int, int, int>>> by_slots;
+    {
+        std::lock_guard<std::mutex> lk(mask_mu);
+        for (auto &kv : mask_cache) by_slots[std::get<1>(kv.first)].push_back(kv.first);
+    }
+    for (auto &g : by_slots) {
+        std::vector<Engine::MaskSpec> specs;
+        for (auto &key : g.second)
+            specs.push_back(Engine::MaskSpec{std::get<0>(key), std::get<2>(key), std::get<3>(key), std::get<4>(key)});
+        auto pts = cc.encode_masks(specs, g.first, N);  // synchronises the main stream
+        std::lock_guard<std::mutex> lk(mask_mu);
+        for (size_t i = 0; i < pts.size(); ++i) mask_cache[g.second[i]] = pts[i];
+    }
+}
+
 CtPtr DirectSortN::sort(const Ciphertext &x, SignFunc f, const SignConfig &cfg) {
+    if (!cache_masks) refresh_masks();
     CtPtr rank = constructRank(x, f, cfg);
     return rotationIndexCheckN(*rank, x);
 }

@@ -218,6 +218,12 @@ class DirectSortN {
     // concurrent lanes: the rank's batches are split over `lanes` host threads,
     // each driving a forked engine (own HIP stream and pool, shared keys)
     int lanes = 2;
+    // public masks and checking vectors: true = encoded once per context and
+    // kept; false = every sort re-encodes all of them on the device before it
+    // starts (the reference encodes them on every use, src/sort_algo.h:341-342,
+    // 714-716); masks are encoded on the device either way (FHE_HOST_MASKS=1:
+    // the host encoder, A/B)
+    bool cache_masks = true;
 
   private:
     struct Lane {
@@ -236,6 +242,8 @@ class DirectSortN {
     std::vector<CtPtr> babySteps(const Ciphertext &x, int np);
     // encoded on the calling lane's engine, published once complete (thread-safe)
     const Plaintext &mask(Engine &E, int kind, int num_slots, int k, int rot, int level);
+    // re-encode every cached mask in device batches on the main engine
+    void refresh_masks();
     std::map<std::tuple<int, int, int, int, int>, PtPtr> mask_cache;
     std::mutex mask_mu;
     std::vector<int> rot_indices;

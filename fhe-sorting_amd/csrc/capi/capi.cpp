@@ -28,6 +28,7 @@ struct fhe_ctx {
     std::map<std::pair<int, std::vector<int>>, std::unique_ptr<DirectSortN>> sorters;
     int sort_stack = 32;
     int sort_lanes = 2;
+    bool mask_cache = true;  // fhe_set_mask_cache
     std::unique_ptr<Engine> kway_lane;  // the k-way sorter's second lane (forked on first use)
 };
 struct fhe_ct {
@@ -227,6 +228,39 @@ int fhe_ct_sum_members(fhe_ctx *ctx, const fhe_ct *a, fhe_ct **out) {
 int fhe_pt_encode(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_pt **out) {
     return guard([&] { *out = new fhe_pt{ctx->eng->encode(std::vector<double>(v, v + len), slots, level)}; });
 }
+int fhe_pt_limbs(const fhe_pt *pt) { return pt && pt->p ? (int)pt->p->limbs : -FHE_EINVAL; }
+int fhe_pt_download(fhe_ctx *ctx, const fhe_pt *pt, uint64_t *out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(pt);
+        NEED(out);
+        ctx->eng->sync();
+        if (hipMemcpy(out, pt->p->data, pt->p->limbs * ctx->eng->n() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+            throw std::runtime_error("HIP error: plaintext download");
+    });
+}
+int fhe_pt_encode_device(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_pt **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(v);
+        *out = new fhe_pt{ctx->eng->encode_device({std::vector<double>(v, v + len)}, slots, {level})[0]};
+    });
+}
+int fhe_pt_encode_masks(fhe_ctx *ctx, const int32_t *spec, int count, int num_slots, int N, fhe_pt **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(spec);
+        NEED(out);
+        if (count < 0) throw std::invalid_argument("fhe_pt_encode_masks: negative count");
+        std::vector<Engine::MaskSpec> m(count);
+        for (int i = 0; i < count; ++i) {
+            if (spec[4 * i] != 0 && spec[4 * i] != 1) throw std::invalid_argument("fhe_pt_encode_masks: kind must be 0 or 1");
+            m[i] = Engine::MaskSpec{spec[4 * i], spec[4 * i + 1], spec[4 * i + 2], spec[4 * i + 3]};
+        }
+        auto pts = ctx->eng->encode_masks(m, num_slots, N);
+        for (int i = 0; i < count; ++i) out[i] = new fhe_pt{pts[i]};
+    });
+}
 int fhe_pt_upload(fhe_ctx *ctx, const uint64_t *h, int limbs, int level, int slots, double scale, fhe_pt **out) {
     return guard([&] { *out = new fhe_pt{ctx->eng->upload_pt(h, (size_t)limbs, level, slots, scale)}; });
 }
@@ -423,6 +457,7 @@ int fhe_direct_sort(fhe_ctx *ctx, const fhe_ct *x, const fhe_ct *rank, int N, co
         DirectSortN &ds = *slot;
         ds.max_stack = ctx->sort_stack;
         ds.lanes = ctx->sort_lanes;
+        ds.cache_masks = ctx->mask_cache;
         ds.shard_rank = shard_rank;
         ds.shard_world = shard_world;
         ds.allreduce = std::move(reduce);
@@ -784,6 +819,13 @@ int fhe_kway_rotation_indices(int N, int32_t *rots, int max_rots) {
         for (int i = 0; i < count && i < max_rots; ++i) rots[i] = r[(size_t)i];
     });
     return rc ? -rc : count;
+}
+
+int fhe_set_mask_cache(fhe_ctx *ctx, int cache) {
+    return guard([&] {
+        NEED(ctx);
+        ctx->mask_cache = cache != 0;
+    });
 }
 
 int fhe_set_sort_stack(fhe_ctx *ctx, int max_stack) {

@@ -305,7 +305,27 @@ __device__ constexpr int reg_of(const RowLayout &L, int b) {
         if (L.reg[k] == b) p = k;
     return p;
 }
-template <bool FWD, int S>
+// LDS offset of stage S's twiddles in a row's table (row_twiddles): forward
+// stage S uses 2^S of them, inverse stage S 2^(7 - S)
+template <bool FWD>
+__device__ constexpr int twl_off(int S) {
+    return FWD ? (1 << S) - 1 : 256 - (256 >> S);
+}
+// The 255 twiddle pairs of one row (every stage of a 256-point row pass) into
+// LDS, by the block's first 255 threads; the caller synchronises.  Used when
+// every transform of the block is the same row (16 segments per block), so
+// the row's twiddles are read from HBM / L2 once per block and from LDS per
+// butterfly instead of from the vector cache.
+template <bool FWD>
+__device__ __forceinline__ void row_twiddles(ulonglong2 *twl, const ulonglong2 *tw, size_t row, size_t n, int S0) {
+    const int e = threadIdx.x;
+    if (e >= 255) return;
+    int S = 0;
+    while (S < 7 && e >= twl_off<FWD>(S + 1)) ++S;
+    const int j = e - twl_off<FWD>(S);
+    twl[e] = FWD ? tw[((size_t)1 << (S0 + S)) + (row << S) + j] : tw[(n >> (S + 1)) + (row << (7 - S)) + j];
+}
+template <bool FWD, int S, bool TWL>
 __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulonglong2 *tw, size_t n, int S0,
                                           u64 q4, u64 nq) {
     constexpr RowSwap w = FWD ? fwd_swap(S) : inv_swap(S);
@@ -319,8 +339,9 @@ __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulong
     // lane and register bits are disjoint, so the shift splits into a per-lane
     // offset and a compile-time one -> one address per stage, immediate offsets
     constexpr int SH = FWD ? 8 - S : S + 1;
-    const ulonglong2 *tws = FWD ? tw + ((size_t)1 << (S0 + S)) + (row << S) + (uint32_t)(li >> SH)
-                                : tw + (n >> (S + 1)) + (row << (7 - S)) + (uint32_t)(li >> SH);
+    const ulonglong2 *tws = TWL ? tw + twl_off<FWD>(S) + (li >> SH)  // tw: the row's LDS table
+                            : FWD ? tw + ((size_t)1 << (S0 + S)) + (row << S) + (uint32_t)(li >> SH)
+                                  : tw + (n >> (S + 1)) + (row << (7 - S)) + (uint32_t)(li >> SH);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         if (j & (1 << P)) continue;
@@ -329,18 +350,18 @@ __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulong
         else gs_bfly(x[j], x[j + (1 << P)], w, q4, nq);
     }
 }
-template <bool FWD>
+template <bool FWD, bool TWL>
 __device__ __forceinline__ void row_pass_shfl(u64 *x, int t, size_t row, const ulonglong2 *tw, size_t n, int S0,
                                               u64 q4, u64 nq) {
-    row_stage<FWD, 0>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 1>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 2>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 3>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 4>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 5>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 6>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 7>(x, t, row, tw, n, S0, q4, nq);
-    if (FWD) row_stage<FWD, 8>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 0, TWL>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 1, TWL>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 2, TWL>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 3, TWL>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 4, TWL>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 5, TWL>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 6, TWL>(x, t, row, tw, n, S0, q4, nq);
+    row_stage<FWD, 7, TWL>(x, t, row, tw, n, S0, q4, nq);
+    if (FWD) row_stage<FWD, 8, TWL>(x, t, row, tw, n, S0, q4, nq);
 }
 // in-row index of lane t's register r after a pass (both passes end in this layout)
 template <bool FWD>
@@ -348,8 +369,9 @@ __device__ __forceinline__ int row_final_index(int t, int r) {
     constexpr RowLayout L = row_layout<FWD>(FWD ? 8 : 7);
     return lane_index(L, t) + reg_index(L, r);
 }
-// FHE_NTT_ROW_SHFL bit mask (A/B timing): 1 inverse row pass, 2 forward row
-// pass use the register-only DPP passes.  0 keeps both on the LDS-exchange passes.
+// FHE_NTT_ROW_SHFL bit mask (A/B timing): 1 inverse row pass, 2 every forward row
+// pass, 4 / 8 / 16 only the fused HMult-tail / rescale / key-switch-finish forward
+// rows use the register-only DPP passes.  0 keeps all on the LDS-exchange passes.
 int &row_shfl_enabled() {
     static int v = [] {
         const char *e = std::getenv("FHE_NTT_ROW_SHFL");
@@ -373,7 +395,7 @@ enum { NTT_PLAIN = 0, NTT_LIFT = 1, NTT_RESCALE = 2, NTT_MULTAIL = 3, NTT_KSFINI
 // ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
 // SH (row passes with PB = 8 only): register-only stages with DPP lane swaps
 // (row_pass_shfl) instead of the two LDS exchanges.
-template <int PB, int EB, bool COLS, int MODE, bool SH, bool FULL>
+template <int PB, int EB, bool COLS, int MODE, bool SH, bool FULL, bool TWL = false>
 __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
                                              const NttTables &Tb, const NttFuse &F) {
     static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
@@ -498,7 +520,14 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
         }
     };
     if constexpr (SH) {
-        row_pass_shfl<true>(x, t, tid_global, tw, n, S0, q4, nq);
+        if constexpr (TWL) {  // every transform of the block is row blockIdx.y
+            __shared__ ulonglong2 twl[256];
+            row_twiddles<true>(twl, tw, tid_global, n, S0);
+            __syncthreads();
+            row_pass_shfl<true, true>(x, t, tid_global, twl, n, S0, q4, nq);
+        } else {
+            row_pass_shfl<true, false>(x, t, tid_global, tw, n, S0, q4, nq);
+        }
         if (!valid) return;
 #pragma unroll
         for (int r = 0; r < E; ++r) store_row(r, row_final_index<true>(t, r), x[r]);
@@ -618,7 +647,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
 // COLS covers sg in [logN - PB, logN) and multiplies by n^-1 on the way out.
 // F.src (optional): read the input from there instead (out-of-place first
 // pass; segment z, limb l at F.src + z * F.seg_src + l * n)
-template <int PB, int EB, bool COLS, bool SH, bool FULL>
+template <int PB, int EB, bool COLS, bool SH, bool FULL, bool TWL = false>
 __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
                                              const NttTables &Tb, const NttFuse &F) {
     static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
@@ -668,7 +697,14 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
             x[2 * m] = v.x;
             x[2 * m + 1] = v.y;
         }
-        row_pass_shfl<false>(x, t, tid_global, tw, n, 0, q4, nq);
+        if constexpr (TWL) {  // every transform of the block is row blockIdx.y
+            __shared__ ulonglong2 twl[256];
+            row_twiddles<false>(twl, tw, tid_global, n, 0);
+            __syncthreads();
+            row_pass_shfl<false, true>(x, t, tid_global, twl, n, 0, q4, nq);
+        } else {
+            row_pass_shfl<false, false>(x, t, tid_global, tw, n, 0, q4, nq);
+        }
         if (!valid) return;
 #pragma unroll
         for (int r = 0; r < E; ++r) a[tid_global * LEN + row_final_index<false>(t, r)] = x[r];
@@ -791,15 +827,29 @@ __global__ __launch_bounds__((nthreads<PB, COLS>())) __attribute__((amdgpu_waves
     ntt_inv_body<PB, EB, COLS, false, FULL>(data, seg, pmap, smap, logN, Tb, F);
 }
 // register-only row passes (PB = 8)
-template <int MODE, bool FULL>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_ntt_fwd_row(
+// minimum waves per SIMD for the register-only row passes with LDS twiddles
+// (their twiddles are cheap to re-read, so a register budget need not spill)
+#ifndef FHE_NTT_ROW_WPE
+#define FHE_NTT_ROW_WPE 1
+#endif
+template <int MODE, bool FULL, bool TWL>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(TWL ? FHE_NTT_ROW_WPE : 1, 8))) void k_ntt_fwd_row(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_fwd_body<8, 4, false, MODE, true, FULL>(data, seg, pmap, smap, logN, Tb, F);
+    ntt_fwd_body<8, 4, false, MODE, true, FULL, TWL>(data, seg, pmap, smap, logN, Tb, F);
 }
-template <bool FULL>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(1, 8))) void k_ntt_inv_row(
+template <bool FULL, bool TWL>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(TWL ? FHE_NTT_ROW_WPE : 1, 8))) void k_ntt_inv_row(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_inv_body<8, 4, false, true, FULL>(data, seg, pmap, smap, logN, Tb, F);
+    ntt_inv_body<8, 4, false, true, FULL, TWL>(data, seg, pmap, smap, logN, Tb, F);
+}
+// FHE_NTT_TWL (A/B, default 1): the register-only row passes stage a row's
+// twiddles in LDS when the block is one row of 16 segments
+int &row_twl_enabled() {
+    static int v = [] {
+        const char *e = std::getenv("FHE_NTT_TWL");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
 }
 
 // FHE_NTT_FULL (A/B timing): which passes take the exact-grid variant (bit mask:
@@ -825,8 +875,11 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     constexpr int NTHR = nthreads<PB, COLS>();
     constexpr int NB = NTHR >> (PB - EB);
     constexpr bool CAN_SH = !COLS && PB == 8 && EB == 4;
+    // bits: 1 inverse rows, 2 every forward row, 4 / 8 / 16 the forward HMult-tail /
+    // rescale / key-switch-finish rows only
     const int mode = row_shfl_enabled();
-    const bool sh = CAN_SH && (mode & (FWD ? 2 : 1)) != 0;
+    const int fwd_bit = MODE == NTT_MULTAIL ? 4 : MODE == NTT_RESCALE ? 8 : MODE == NTT_KSFINISH ? 16 : 0;
+    const bool sh = CAN_SH && (mode & (FWD ? 2 | fwd_bit : 1)) != 0;
     const int count = 1 << (T.logN - PB);  // columns (COLS) or rows (ROWS)
     dim3 grid((unsigned)segs, (unsigned)((count + NB - 1) / NB), (unsigned)limbs);
     const bool want_full = (ntt_full_mask() & full_bit<COLS, FWD, MODE>()) != 0;
@@ -848,15 +901,20 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
                 dim3(NTHR));
 #define FHE_NTT_LAUNCH(K, FF) \
     hipExtLaunchKernelGGL((K), grid, dim3(NTHR), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
+    const bool twl = sh && Fs.lsegb == 4 && row_twl_enabled() != 0;
     if (FWD && sh) {
-        if (full) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true>), Fs);
-        else FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false>), Fs);
+        if (full && twl) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, true>), Fs);
+        else if (full) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, false>), Fs);
+        else if (twl) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false, true>), Fs);
+        else FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false, false>), Fs);
     } else if (FWD) {
         if (full) FHE_NTT_LAUNCH((k_ntt_fwd<PB, EB, COLS, MODE, true>), F);
         else FHE_NTT_LAUNCH((k_ntt_fwd<PB, EB, COLS, MODE, false>), F);
     } else if (sh) {
-        if (full) FHE_NTT_LAUNCH((k_ntt_inv_row<true>), Fs);
-        else FHE_NTT_LAUNCH((k_ntt_inv_row<false>), Fs);
+        if (full && twl) FHE_NTT_LAUNCH((k_ntt_inv_row<true, true>), Fs);
+        else if (full) FHE_NTT_LAUNCH((k_ntt_inv_row<true, false>), Fs);
+        else if (twl) FHE_NTT_LAUNCH((k_ntt_inv_row<false, true>), Fs);
+        else FHE_NTT_LAUNCH((k_ntt_inv_row<false, false>), Fs);
     } else {
         if (full) FHE_NTT_LAUNCH((k_ntt_inv<PB, EB, COLS, true>), F);
         else FHE_NTT_LAUNCH((k_ntt_inv<PB, EB, COLS, false>), F);
@@ -867,9 +925,10 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
         // (the instantiation the branches above launched)
         const std::string pe = std::to_string(PB) + ", " + std::to_string(EB) + (COLS ? ", true" : ", false");
         const std::string fl = full ? "true>" : "false>";
-        const std::string base = FWD && sh ? "k_ntt_fwd_row<" + std::to_string(MODE) + ", " + fl
+        const std::string fl2 = (full ? "true, " : "false, ") + std::string(twl ? "true>" : "false>");
+        const std::string base = FWD && sh ? "k_ntt_fwd_row<" + std::to_string(MODE) + ", " + fl2
                                  : FWD     ? "k_ntt_fwd<" + pe + ", " + std::to_string(MODE) + ", " + fl
-                                 : sh      ? "k_ntt_inv_row<" + fl
+                                 : sh      ? "k_ntt_inv_row<" + fl2
                                            : "k_ntt_inv<" + pe + ", " + fl;
         static std::map<std::string, std::string> names;  // stable c_str() per (kernel, caller)
         static std::mutex mu;

@@ -230,6 +230,58 @@ struct Engine::Impl {
         return {reinterpret_cast<const int64_t *>(b), reinterpret_cast<const uint8_t *>(b + K.size() * sizeof(int64_t))};
     }
 
+    // device encoder tables (the host encoder's ksi / rot, uploaded on first use)
+    const double2 *enc_ksi = nullptr;
+    const uint32_t *enc_rot = nullptr;
+    void enc_tables() {
+        if (enc_ksi) return;
+        std::vector<double> ksi;
+        std::vector<uint32_t> rot;
+        host::embedding_tables(P.n, ksi, rot);
+        enc_ksi = reinterpret_cast<const double2 *>(upload_static(ksi));
+        enc_rot = upload_static(rot);
+    }
+    // v [B][S] slot values on the device, member order sorted by level:
+    // plaintexts (one allocation per level, member views) in that order
+    std::vector<PtPtr> encode_sorted(double2 *v, int B, int S, const std::vector<int> &levels,
+                                     const std::vector<double> &scales) {
+        const size_t nn = n();
+        auto coefm = alloc((size_t)B * nn * 8);
+        int64_t *coef = static_cast<int64_t *>(coefm->p);
+        auto scm = alloc((size_t)B * 8 + 8);
+        double *sc = static_cast<double *>(scm->p);
+        unsigned *ovf = reinterpret_cast<unsigned *>(sc + B);
+        HIP_OK(hipMemcpyAsync(sc, scales.data(), (size_t)B * 8, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemsetAsync(ovf, 0, 4, st));
+        dev::encode_ifft(v, coef, B, S, (int)nn, enc_ksi, enc_rot, sc, ovf, st);
+        std::vector<PtPtr> out(B);
+        for (int a = 0; a < B;) {
+            int b = a;
+            while (b < B && levels[b] == levels[a]) ++b;
+            const size_t ell = P.limbs_at(levels[a]);
+            auto blk = alloc((size_t)(b - a) * ell * nn * 8);
+            u64 *d = static_cast<u64 *>(blk->p);
+            dev::ew_signed_to_rns(d, coef + (size_t)a * nn, (int)ell, nullptr, mods, P.logN, st, b - a, ell * nn, nn);
+            dev::ntt_forward(d, (int)ell, b - a, ell * nn, nullptr, T, st);
+            for (int i = a; i < b; ++i) {
+                auto pt = std::make_shared<Plaintext>();
+                pt->mem = blk;
+                pt->data = d + (size_t)(i - a) * ell * nn;
+                pt->level = levels[a];
+                pt->slots = S;
+                pt->scale = scales[i];
+                pt->limbs = ell;
+                out[i] = pt;
+            }
+            a = b;
+        }
+        unsigned flag = 0;
+        HIP_OK(hipMemcpyAsync(&flag, ovf, 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));  // also: the scale table's host source outlives its copy
+        if (flag) throw std::overflow_error("encode: scaled coefficient exceeds 63 bits");
+        return out;
+    }
+
     std::shared_ptr<DevMem> alloc(size_t bytes) {
         auto m = std::make_shared<DevMem>();
         m->pool = pool;
@@ -796,6 +848,70 @@ PtPtr Engine::encode_scaled(const std::vector<double> &v, int slots, int level, 
     host_stats().encode_ns += now_ns() - t0;
     host_stats().encodes++;
     return pt;
+}
+
+std::vector<PtPtr> Engine::encode_masks(const std::vector<MaskSpec> &specs, int num_slots, int N) {
+    auto &I = *impl;
+    const int B = (int)specs.size();
+    if (B == 0) return {};
+    if (num_slots <= 0 || (num_slots & (num_slots - 1)) || (size_t)num_slots > I.n() / 2 || N <= 0)
+        throw std::invalid_argument("encode_masks: slots must be a power of two <= n/2");
+    const u64 t0 = now_ns();
+    I.enc_tables();
+    std::vector<int> ord(B);
+    for (int i = 0; i < B; ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return specs[a].level < specs[b].level; });
+    std::vector<int> spec(3 * B), levels(B);
+    std::vector<double> scales(B);
+    for (int j = 0; j < B; ++j) {
+        const MaskSpec &m = specs[ord[j]];
+        if (m.level < 0 || m.level > I.P.L) throw std::invalid_argument("encode_masks: level out of range");
+        spec[3 * j] = m.kind;
+        spec[3 * j + 1] = m.k;
+        spec[3 * j + 2] = m.r;
+        levels[j] = m.level;
+        scales[j] = I.P.delta[m.level];
+    }
+    auto vm = I.alloc((size_t)B * num_slots * sizeof(double2));
+    double2 *v = static_cast<double2 *>(vm->p);
+    auto sm = I.alloc(spec.size() * 4);
+    HIP_OK(hipMemcpyAsync(sm->p, spec.data(), spec.size() * 4, hipMemcpyHostToDevice, I.st));
+    dev::mask_slots(v, B, num_slots, N, static_cast<const int *>(sm->p), I.st);
+    auto sorted = I.encode_sorted(v, B, num_slots, levels, scales);  // synchronises: `spec` outlives its copy
+    std::vector<PtPtr> out(B);
+    for (int j = 0; j < B; ++j) out[ord[j]] = sorted[j];
+    host_stats().encode_ns += now_ns() - t0;
+    host_stats().encodes += B;
+    return out;
+}
+
+std::vector<PtPtr> Engine::encode_device(const std::vector<std::vector<double>> &vs, int slots,
+                                         const std::vector<int> &levels) {
+    auto &I = *impl;
+    const int B = (int)vs.size();
+    if (B == 0) return {};
+    if ((int)levels.size() != B) throw std::invalid_argument("encode_device: one level per vector");
+    if (slots <= 0 || (slots & (slots - 1)) || (size_t)slots > I.n() / 2)
+        throw std::invalid_argument("encode: slots must be a power of two <= n/2");
+    I.enc_tables();
+    std::vector<int> ord(B);
+    for (int i = 0; i < B; ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return levels[a] < levels[b]; });
+    std::vector<double> h((size_t)2 * B * slots, 0.0), scales(B);
+    std::vector<int> lv(B);
+    for (int j = 0; j < B; ++j) {
+        const auto &x = vs[ord[j]];
+        for (size_t i = 0; i < x.size() && i < (size_t)slots; ++i) h[2 * ((size_t)j * slots + i)] = x[i];
+        lv[j] = levels[ord[j]];
+        if (lv[j] < 0 || lv[j] > I.P.L) throw std::invalid_argument("encode_device: level out of range");
+        scales[j] = I.P.delta[lv[j]];
+    }
+    auto vm = I.alloc(h.size() * 8);
+    HIP_OK(hipMemcpyAsync(vm->p, h.data(), h.size() * 8, hipMemcpyHostToDevice, I.st));
+    auto sorted = I.encode_sorted(static_cast<double2 *>(vm->p), B, slots, lv, scales);
+    std::vector<PtPtr> out(B);
+    for (int j = 0; j < B; ++j) out[ord[j]] = sorted[j];
+    return out;
 }
 
 void Engine::host_stats_get(double out[4]) {

@@ -137,6 +137,17 @@ class Engine {
     PtPtr encode_complex(const std::vector<std::complex<double>> &v, int slots, int level, double scale);
     // the same plaintext over Q_level u P (ell + K limbs, special primes last)
     PtPtr encode_complex_ext(const std::vector<std::complex<double>> &v, int slots, int level, double scale);
+    // Device encoding (csrc/device/encode.hip), word-identical to encode():
+    // the special inverse FFT, rounding, RNS split and NTT of a batch in a few
+    // launches.  encode_masks generates the sort's public masks on the device
+    // (kind 0: mask_vector(k) rotated by r, kind 1: checking_vector(k),
+    // src/sort_algo.h:206-233, 272-286; slots num_slots, block size N);
+    // encode_device takes arbitrary real slot vectors.
+    struct MaskSpec {
+        int kind, k, r, level;
+    };
+    std::vector<PtPtr> encode_masks(const std::vector<MaskSpec> &specs, int num_slots, int N);
+    std::vector<PtPtr> encode_device(const std::vector<std::vector<double>> &vs, int slots, const std::vector<int> &levels);
     CtPtr encrypt(const std::vector<double> &v, int slots, int level = 0);
     CtPtr encrypt_pt(const Plaintext &pt);
     // OpenFHE FLEXIBLEAUTOEXT-style encryption: one extra level absorbs the

@@ -285,6 +285,16 @@ void special_fft(std::vector<cd> &v, const Emb &E, size_t n) {
 }
 }  // namespace
 
+void embedding_tables(size_t n, std::vector<double> &ksi, std::vector<uint32_t> &rot) {
+    const Emb &E = emb_tables(n);
+    ksi.resize(2 * E.ksi.size());
+    for (size_t k = 0; k < E.ksi.size(); ++k) {
+        ksi[2 * k] = E.ksi[k].real();
+        ksi[2 * k + 1] = E.ksi[k].imag();
+    }
+    rot.assign(E.rot.begin(), E.rot.end());
+}
+
 std::vector<i64> encode_coeffs(const std::vector<double> &v, size_t n, int slots, double scale) {
     std::vector<cd> z;
     for (size_t i = 0; i < v.size() && i < (size_t)std::max(slots, 0); ++i) z.push_back(cd(v[i], 0));

@@ -53,6 +53,9 @@ NttTable make_ntt_table(u64 q, int logN);
 std::vector<uint32_t> automorphism_perm(int logN, u64 g);
 u64 galois_for_rotation(int logN, long k);
 
+// the encoder's tables, for the device encoder (engine encode_masks): ksi
+// [2n + 1] interleaved (cos, sin) of 2 pi k / 2n, rot [n / 2] = 5^j mod 2n
+void embedding_tables(size_t n, std::vector<double> &ksi, std::vector<uint32_t> &rot);
 // canonical embedding (special FFT, fp64) -> signed integer coefficients
 std::vector<i64> encode_coeffs(const std::vector<double> &v, size_t n, int slots, double scale);
 std::vector<i64> encode_coeffs_complex(const std::vector<std::complex<double>> &v, size_t n, int slots,

@@ -162,6 +162,11 @@ _SIGS = {
     'fhe_counters': (C.c_int, [vp, u64p]),
     'fhe_collective_stats': (C.c_int, [vp, u64p]),
     'fhe_region_marker': (C.c_int, [vp, C.c_int]),
+    'fhe_set_mask_cache': (C.c_int, [vp, C.c_int]),
+    'fhe_pt_limbs': (C.c_int, [vp]),
+    'fhe_pt_download': (C.c_int, [vp, vp, u64p]),
+    'fhe_pt_encode_device': (C.c_int, [vp, dp, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_pt_encode_masks': (C.c_int, [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, C.c_int, PP]),
     'fhe_reset_counters': (C.c_int, [vp]),
     'fhe_sync': (C.c_int, [vp]),
     'fhe_stream': (vp, [vp]),
@@ -384,6 +389,12 @@ class Pt:
     def __init__(self, ctx, h):
         self.ctx, self.h = ctx, h
 
+    def data(self):
+        """the plaintext's words [limbs][n] (NTT form)"""
+        out = np.empty((lib().fhe_pt_limbs(self.h), self.ctx.n), dtype=np.uint64)
+        _chk(lib().fhe_pt_download(self.ctx.h, self.h, _u64(out)))
+        return out
+
     def __del__(self):
         try:
             if self.h:
@@ -531,6 +542,25 @@ class Context:
         out = C.c_void_p()
         _chk(lib().fhe_pt_encode(self.h, _dbl(v), len(v), slots, level, C.byref(out)))
         return Pt(self, out.value)
+
+    def encode_device(self, v, slots, level=0):
+        """fhe_pt_encode_device: encode(v) on the device, word for word"""
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        out = C.c_void_p()
+        _chk(lib().fhe_pt_encode_device(self.h, _dbl(v), len(v), slots, level, C.byref(out)))
+        return Pt(self, out.value)
+
+    def encode_masks(self, specs, num_slots, N):
+        """fhe_pt_encode_masks: specs = [(kind, k, r, level), ...] -> plaintexts"""
+        sp = np.ascontiguousarray(np.asarray(specs, dtype=np.int32).reshape(-1, 4))
+        outs = (C.c_void_p * len(sp))()
+        _chk(lib().fhe_pt_encode_masks(self.h, sp.ctypes.data_as(C.POINTER(C.c_int32)), len(sp), num_slots, N, outs))
+        return [Pt(self, outs[i]) for i in range(len(sp))]
+
+    def set_mask_cache(self, cache):
+        """True (default): masks encoded once per context; False: re-encoded on the
+        device at the start of every sort (the reference's per-sort encoding)"""
+        _chk(lib().fhe_set_mask_cache(self.h, 1 if cache else 0))
 
     def upload_pt(self, data, level, slots, scale=None):
         data = np.ascontiguousarray(data, dtype=np.uint64)

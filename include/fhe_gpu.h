@@ -119,6 +119,19 @@ int fhe_pt_encode(fhe_ctx *ctx, const double *v, int len, int slots, int level, 
 int fhe_pt_upload(fhe_ctx *ctx, const uint64_t *host, int limbs, int level, int slots, double scale,
                   fhe_pt **out);
 int fhe_pt_free(fhe_pt *pt);
+/* limbs of a plaintext (< 0 on a null handle), and its words [limbs][n] (NTT form) */
+int fhe_pt_limbs(const fhe_pt *pt);
+int fhe_pt_download(fhe_ctx *ctx, const fhe_pt *pt, uint64_t *out);
+/* the same plaintext as fhe_pt_encode, word for word, encoded on the device
+ * (special inverse FFT in fp64 restating the host encoder's operations,
+ * rounding, RNS split, NTT: csrc/device/encode.hip) */
+int fhe_pt_encode_device(fhe_ctx *ctx, const double *v, int len, int slots, int level, fhe_pt **out);
+/* `count` DirectSort masks generated and encoded on the device in one batch:
+ * spec[4 i .. 4 i + 3] = {kind, k, r, level}; kind 0 = mask_vector(num_slots,
+ * N, k) rotated by r (src/sort_algo.h:206-233, 289-306), kind 1 =
+ * checking_vector(num_slots, N, k) (src/sort_algo.h:272-286); each equals
+ * fhe_pt_encode of that vector word for word.  out: `count` handles */
+int fhe_pt_encode_masks(fhe_ctx *ctx, const int32_t *spec, int count, int num_slots, int N, fhe_pt **out);
 
 /* -------------------------------------------------------------------- ops */
 /* EvalAdd / EvalSub (src/comparison.cpp:13,19; src/sort_algo.h:454,495,504) */
@@ -396,6 +409,11 @@ int fhe_set_mfma_sums(int mask);
  * ct x const, add, linear sum formulas, each op at its own level) */
 int fhe_counters(fhe_ctx *ctx, uint64_t out[7]);
 int fhe_reset_counters(fhe_ctx *ctx);
+/* DirectSort's public masks and checking vectors: cache != 0 (default) encodes
+ * each once per context and keeps it; cache == 0 re-encodes all of a sort's
+ * masks on the device at the start of every sort, as the reference encodes
+ * them on every use (src/sort_algo.h:341-342, 714-716) */
+int fhe_set_mask_cache(fhe_ctx *ctx, int cache);
 /* sharded sorts' partial-sum exchanges since the last fhe_reset_counters:
  * out = {host nanoseconds inside them (header + data all-reduce, measured from a
  * drained stream to the reduced data), exchanges}.  The reference's reduction

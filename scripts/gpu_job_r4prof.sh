@@ -19,7 +19,7 @@ export TMPDIR=/tmp
 export FHE_PROF_REGION=1
 (while sleep 60; do echo "tick $(date +%T)"; done) & TICK=$!
 trap 'kill $TICK 2>/dev/null' EXIT
-B="--steps 1 --warmup 1 --no-cpu-baseline --no-roofline --lanes 1"
+B="--steps 1 --warmup 1 --no-cpu-baseline --no-roofline --lanes 1 --mask-steps 0"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/trace" -o run -- python3 "$R/bench.py" $B "$@" > $O/trace.log 2>&1 || { echo "trace failed"; tail -5 $O/trace.log; exit 1; }
 python scripts/trace_summary.py $O/trace/run_kernel_trace.csv --stats-out $O/region_kernel_stats.csv > $O/trace_summary.txt && head -40 $O/trace_summary.txt || exit 1
 cp $O/trace/run_kernel_stats.csv $O/run_kernel_stats.csv
