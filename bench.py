@@ -401,6 +401,10 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
     if dump:
         with open(dump, 'w') as f:
             json.dump(stats, f, indent=1)
+    # 'phase:<name>' rows: the same kernels booked under the algorithm phase that
+    # launched them (MEHP24: split / replicate / compare / rank_sums / indicator /
+    # select / recombine), with the SURVEY §8(d) op-level bytes of that phase
+    phase_rows = {k[6:]: stats.pop(k) for k in [k for k in stats if k.startswith('phase:')]}
     total_ms = sum(v['ms'] for v in stats.values())
     by_sym, by_fam = {}, {}
     for k, v in stats.items():
@@ -425,7 +429,13 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
         return {n: {'share': round(v['ms'] / total_ms, 3), 'avg_us': round(v['ms'] / v['launches'] * 1e3, 1),
                     'launches': v['launches'], 'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1)} for n, v in top}
     run_bytes = sum(v['bytes'] for v in stats.values())
-    return {**head, 'bound': 'hbm', 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+    phases = {n: {'ms': round(v['ms'], 2), 'share': round(v['ms'] / total_ms, 3), 'launches': v['launches'],
+                  'kernel_bytes': v['bytes'], 'op_bytes': v.get('op_bytes', 0.0),
+                  'kernel_over_op_bytes': round(v['bytes'] / v['op_bytes'], 2) if v.get('op_bytes') else None,
+                  'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1) if v['ms'] else None}
+              for n, v in sorted(phase_rows.items(), key=lambda kv: -kv[1]['ms'])}
+    extra = {'phases': phases} if phases else {}
+    return {**extra, **head, 'bound': 'hbm', 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'pmc_source': {'traffic': pmc_src, 'sq': sq_src, 'lib_sha256': lib_sha256()},
             'by_symbol': {'kernel': sym, 'note': 'the headline fields above are this kernel'},
             'by_family': fv,

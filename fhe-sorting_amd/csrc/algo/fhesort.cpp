@@ -17,6 +17,7 @@
 #include <fstream>
 #include <map>
 #include <mutex>
+#include <optional>
 #include <stdexcept>
 #include <tuple>
 #include <exception>
@@ -1517,6 +1518,12 @@ namespace mehp24 {
 
 namespace {
 size_t lg(size_t x) { return (size_t)ceil_log2((long)x); }  // LOG2 (mehp24_utils.h:25)
+// algorithm phase of the clocked kernels (bench.py --workload mehp24: roofline.phases)
+struct AlgoPhase {
+    const char *prev;
+    explicit AlgoPhase(const char *p) : prev(Engine::set_algo_phase(p)) {}
+    ~AlgoPhase() { Engine::set_algo_phase(prev); }
+};
 }  // namespace
 
 namespace utils {
@@ -1709,6 +1716,8 @@ std::vector<CtPtr> sortFG(const std::vector<CtPtr> &c, size_t sub, SignFunc f, c
     std::vector<const Ciphertext *> cv;
     for (auto &x : c) cv.push_back(x.get());
     CtPtr parts = P > 1 ? cc.stack(cv) : cc.clone(*c[0]);
+    std::optional<AlgoPhase> ph;
+    ph.emplace("replicate");
     auto R = members(cc, *replicateRow(cc, parts, sub));
     auto Cc = members(cc, *replicateColumn(cc, transposeRow(cc, mk, parts, sub, true), sub));
     parts.reset();
@@ -1723,9 +1732,13 @@ std::vector<CtPtr> sortFG(const std::vector<CtPtr> &c, size_t sub, SignFunc f, c
             A.push_back(R[j]);
             B.push_back(Cc[k]);
         }
+    ph.reset();
+    ph.emplace("compare");
     auto Cjk = stacked2(cc, A, B, max_stack, [&](const Ciphertext &a, const Ciphertext &b) {
         return Comparison().compare(cc, a, b, f, cfg);
     });
+    ph.reset();
+    ph.emplace("rank_sums");
     A.clear();
     B.clear();
     std::vector<CtPtr> Cv(P), Ch(P);
@@ -1750,6 +1763,8 @@ std::vector<CtPtr> sortFG(const std::vector<CtPtr> &c, size_t sub, SignFunc f, c
     Cv.clear();
     Ch.clear();
 
+    ph.reset();
+    ph.emplace("indicator");
     std::vector<CtPtr> X, RR;
     for (size_t j = 0; j < P; ++j) {
         std::vector<double> sm(sub * sub);
@@ -1766,6 +1781,8 @@ std::vector<CtPtr> sortFG(const std::vector<CtPtr> &c, size_t sub, SignFunc f, c
     }
     auto ind = indicators(cc, X, (double)m, dg_i, df_i, max_stack);
     X.clear();
+    ph.reset();
+    ph.emplace("select");
     auto prod = stacked2(cc, ind, RR, max_stack, [&](const Ciphertext &a, const Ciphertext &b) { return cc.mul(a, b); });
     ind.clear();
     std::vector<CtPtr> acc(P);
@@ -1774,6 +1791,8 @@ std::vector<CtPtr> sortFG(const std::vector<CtPtr> &c, size_t sub, SignFunc f, c
             if (sh.mine(j * P + k)) cc.add_inplace(acc[j], *prod[i++]);
     prod.clear();
     for (size_t j = 0; j < P; ++j) reducePartial(cc, sh, acc[j], slots);
+    ph.reset();
+    ph.emplace("recombine");
     std::vector<const Ciphertext *> av;
     for (auto &x : acc) av.push_back(x.get());
     CtPtr out = P > 1 ? cc.stack(av) : acc[0];
@@ -1788,6 +1807,8 @@ CtPtr sortLargeArrayFG(const Ciphertext &c, size_t total, size_t sub, SignFunc f
     const size_t P = total / sub;
     if (P * sub != total || P == 0) throw std::invalid_argument("sortLargeArrayFG: totalLength % subLength != 0");
     std::vector<CtPtr> parts(P);
+    std::optional<AlgoPhase> ph;
+    ph.emplace("split");
     for (size_t i = 0; i < P; ++i) {  // splitCiphertext
         std::vector<double> mask(total, 0.0);
         for (size_t j = 0; j < sub; ++j) mask[i * sub + j] = 1.0;
@@ -1795,7 +1816,9 @@ CtPtr sortLargeArrayFG(const Ciphertext &c, size_t total, size_t sub, SignFunc f
         if (i > 0) part = cc.rotate(*part, (long)(i * sub));
         parts[i] = part;
     }
+    ph.reset();
     auto sorted = sortFG(parts, sub, f, cfg, dg_i, df_i, cc, max_stack, sh);
+    ph.emplace("recombine");
     CtPtr r = sorted[0];  // combineCiphertext
     for (size_t i = 1; i < P; ++i) r = cc.add(*r, *cc.rotate(*sorted[i], -(long)(i * sub)));
     return r;

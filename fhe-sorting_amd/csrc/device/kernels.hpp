@@ -39,6 +39,9 @@ struct LaunchClock {
 LaunchClock *&launch_clock();
 // caller tag appended to clocked NTT names ("k_ntt_fwd<8, 4, true>@modup"); per thread
 const char *&launch_phase();
+// algorithm phase of the calling thread ("compare", "indicator", ...; null:
+// none), booked by the live clock beside each kernel (bench.py roofline.phases)
+const char *&algo_phase();
 // a stable, process-lifetime copy of s (thread-safe)
 const char *intern_name(const std::string &s);
 // "base<V0, V1, ...>", the instantiation as rocprofv3 spells it, so the clock

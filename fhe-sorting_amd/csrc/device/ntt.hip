@@ -69,6 +69,16 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
 #endif
 // (row passes keep the 64-bit tile: with theirs at 32 bits the rescale and
 // HMult-tail row passes ran 461 -> 530 and 385 -> 403 us, profiles/r4_a)
+// LDS twiddles for the 256-point column passes (FHE_NTT_COL_TWL, default on): a
+// column pass of prime p uses table entries 1..255 only (forward: stage s reads
+// [2^s, 2^(s+1)); inverse: [2^(7-s), 2^(8-s))), the same for every block of the
+// limb, so each thread stages one of them into LDS at the start and the
+// per-lane twiddles (forward round 2, inverse round A, which depend on the
+// lane's place t in its transform) are LDS reads instead of vector-cache loads
+// the round had to wait for.
+#ifndef FHE_NTT_COL_TWL
+#define FHE_NTT_COL_TWL 1
+#endif
 template <bool COLS>
 constexpr bool lds32() {
     return FHE_NTT_LDS32 != 0 && COLS;
@@ -410,6 +420,8 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     constexpr bool X32 = lds32<COLS>() && !SPLIT;
     __shared__ u64 tile[SH ? 1 : X32 ? (lds_words<TPB, NB, COLS>() + 1) / 2 : lds_words<TPB, NB, COLS>()];
     uint32_t *const t32 = reinterpret_cast<uint32_t *>(tile);
+    constexpr bool CTW = FHE_NTT_COL_TWL && COLS && !SPLIT && PB == 8 && nthreads<PB, COLS>() == 256;
+    __shared__ ulonglong2 twc[CTW ? 256 : 1];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
@@ -438,6 +450,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
     const int S0 = COLS ? 0 : logN - PB;                      // global stage of local stage 0
+    if (CTW) twc[threadIdx.x] = tw[threadIdx.x];  // read after the exchange's barrier (round 2)
 
     u64 x[E];
     // ---- load, layout L1: idx = t + T * r
@@ -599,7 +612,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
                 const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
                 const size_t wi = ((size_t)1 << (S0 + s)) + i;
                 const ulonglong2 w =
-                    PRE ? tw2[PRE ? ((1 << (s - EB)) - 1) + (r0 >> (PB - s)) : 0] : tw[wi];
+                    PRE ? tw2[PRE ? ((1 << (s - EB)) - 1) + (r0 >> (PB - s)) : 0] : CTW ? twc[wi] : tw[wi];
                 ct_stage<PB>(COLS, s, x[l2reg<G, T, SPLIT>(g, r0)], x[l2reg<G, T, SPLIT>(g, r0 + (1 << hb))], w, q4,
                              nq);
             }
@@ -662,6 +675,8 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     constexpr bool X32 = lds32<COLS>() && !SPLIT;
     __shared__ u64 tile[SH ? 1 : X32 ? (lds_words<TPB, NB, COLS>() + 1) / 2 : lds_words<TPB, NB, COLS>()];
     uint32_t *const t32 = reinterpret_cast<uint32_t *>(tile);
+    constexpr bool CTW = FHE_NTT_COL_TWL && COLS && !SPLIT && PB == 8 && nthreads<PB, COLS>() == 256;
+    __shared__ ulonglong2 twc[CTW ? 256 : 1];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
@@ -686,6 +701,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
     const int SG0 = COLS ? logN - PB : 0;  // global GS stage of local stage 0
+    if (CTW) twc[threadIdx.x] = tw[threadIdx.x];  // round A reads it after the barrier below
 
     const u64 *ain = F.src ? F.src + (size_t)zseg * F.seg_src + (size_t)limb * n : a;
     u64 x[E];
@@ -735,6 +751,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
             }
     }
     // ---- round A: local stages 0..RB-1 (pair bit s)
+    if (CTW) __syncthreads();  // the staged twiddle table (the data loads are in flight)
 #pragma unroll
     for (int s = 0; s < RB; ++s) {
         // twiddle index (row offset + idx0) >> (s + 1) with idx0 = t E + c, c < E:
@@ -742,7 +759,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
         // compile-time c >> (s + 1) (COLS: the column bits of idx0 << k2 vanish)
         const int sg = SG0 + s;
         const size_t lane_base = ((COLS ? 0 : tid_global * LEN) + (size_t)t * E) >> (s + 1);
-        const ulonglong2 *tws = tw + (n >> (sg + 1)) + lane_base;
+        const ulonglong2 *tws = (CTW ? twc : tw) + (n >> (sg + 1)) + lane_base;
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -967,6 +984,10 @@ LaunchClock *&launch_clock() {
     return clk;
 }
 const char *&launch_phase() {
+    static thread_local const char *ph = nullptr;
+    return ph;
+}
+const char *&algo_phase() {
     static thread_local const char *ph = nullptr;
     return ph;
 }

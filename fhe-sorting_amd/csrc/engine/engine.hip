@@ -1093,7 +1093,12 @@ CtPtr Engine::drop_to(const Ciphertext &a, int level) {
 }
 
 // op-level byte model (Counters::opbytes): `limb_units` limbs of n words per ciphertext, times members
-void Engine::count_bytes(double limb_units, int members) { ctr.opbytes += (u64)(limb_units * members * 8.0 * n()); }
+void clock_phase_opbytes(const char *phase, u64 b);
+void Engine::count_bytes(double limb_units, int members) {
+    const u64 b = (u64)(limb_units * members * 8.0 * n());
+    ctr.opbytes += b;
+    if (dev::launch_clock() && dev::algo_phase()) clock_phase_opbytes(dev::algo_phase(), b);
+}
 double Engine::ks_units(size_t ell) const {  // 2 digits(l) (l + K): the key read of one key switch
     const auto &P = impl->P;
     return 2.0 * P.digits_at(ell) * (double)(ell + P.K);
@@ -1907,8 +1912,10 @@ struct EventClock final : dev::LaunchClock {
     struct Rec {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         const char *name = nullptr;
+        const char *phase = nullptr;  // the launching thread's algorithm phase
         double bytes = 0;
     };
+    std::map<std::string, double> phase_opbytes;  // op-level bytes per algorithm phase
     std::mutex mu;
     std::vector<Rec> recs;
     size_t used = 0;
@@ -1927,6 +1934,7 @@ struct EventClock final : dev::LaunchClock {
     void record(int slot, const char *kernel, double bytes) override {
         std::lock_guard<std::mutex> lk(mu);
         recs[(size_t)slot].name = kernel;
+        recs[(size_t)slot].phase = dev::algo_phase();
         recs[(size_t)slot].bytes = bytes;
     }
     ~EventClock() override {
@@ -1939,6 +1947,13 @@ struct EventClock final : dev::LaunchClock {
 std::unique_ptr<EventClock> g_clock;
 }  // namespace
 
+// live clock running: op-level bytes per algorithm phase (Engine::count_bytes)
+void clock_phase_opbytes(const char *phase, u64 b) {
+    if (!g_clock) return;
+    std::lock_guard<std::mutex> lk(g_clock->mu);
+    g_clock->phase_opbytes[phase] += (double)b;
+}
+
 void Engine::pool_trim() {  // this engine's pool and those of its forks (all pools of the process)
     HIP_OK(hipStreamSynchronize(impl->st));
     trim_all_pools();
@@ -1948,6 +1963,12 @@ void Engine::pool_stats(size_t &live, size_t &cached, size_t &peak) const {
     live = impl->pool->live;
     cached = impl->pool->cached;
     peak = impl->pool->peak;
+}
+
+const char *Engine::set_algo_phase(const char *phase) {
+    const char *prev = dev::algo_phase();
+    dev::algo_phase() = phase;
+    return prev;
 }
 
 void Engine::kernel_clock_start() {
@@ -1973,14 +1994,24 @@ std::string Engine::kernel_clock_stop() {
         a.launches += 1;
         a.ms += ms;
         a.bytes += r.bytes;
+        if (r.phase) {  // "phase:<name>": every clocked kernel of an algorithm phase
+            auto &pa = agg[std::string("phase:") + r.phase];
+            pa.launches += 1;
+            pa.ms += ms;
+            pa.bytes += r.bytes;
+        }
     }
+    std::map<std::string, double> phase_op = std::move(g_clock->phase_opbytes);
     g_clock.reset();
     std::string out = "{";
     char buf[512];
     bool first = true;
     for (auto &kv : agg) {
-        snprintf(buf, sizeof buf, "%s\"%s\": {\"launches\": %ld, \"ms\": %.6f, \"bytes\": %.0f}", first ? "" : ", ",
-                 kv.first.c_str(), kv.second.launches, kv.second.ms, kv.second.bytes);
+        const bool ph = kv.first.rfind("phase:", 0) == 0;
+        const double op = ph ? phase_op[kv.first.substr(6)] : 0.0;
+        snprintf(buf, sizeof buf, "%s\"%s\": {\"launches\": %ld, \"ms\": %.6f, \"bytes\": %.0f%s%.0f%s}",
+                 first ? "" : ", ", kv.first.c_str(), kv.second.launches, kv.second.ms, kv.second.bytes,
+                 ph ? ", \"op_bytes\": " : "", ph ? op : 0.0, "");
         out += buf;
         first = false;
     }

@@ -261,6 +261,9 @@ class Engine {
     void pool_stats(size_t &live, size_t &cached, size_t &peak) const;
     void kernel_clock_start();
     std::string kernel_clock_stop();
+    // algorithm phase the clocked kernels and op bytes are booked under
+    // (nullptr = none); returns the previous one
+    static const char *set_algo_phase(const char *phase);
 
     // small device scratch (for collectives / headers); copies are synchronous
     struct DevBuf {

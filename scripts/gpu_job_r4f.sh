@@ -21,5 +21,5 @@ print(sys.argv[2], 'wall', d['ms_per_step'], 'clocked', r['clocked_ms_per_sort']
       {k.split('@')[0].replace('k_ntt_', '') + '@' + k.split('@')[-1]: v['avg_us'] for k, v in ks.items() if 'row' in k})
 PY
 }
-run base default FHE_NTT_TWL=0 && run twl default && run twl_wpe6 rwpe6 && run twl_mt default FHE_NTT_ROW_SHFL=5 && run base2 default FHE_NTT_TWL=0 && run twl2 default || exit 1
+run all default && run norowtwl default FHE_NTT_TWL=0 && run nocoltwl nocoltwl && run rowwpe6 rwpe6 && run rowdpp_mt default FHE_NTT_ROW_SHFL=5 && run all2 default && run norowtwl2 default FHE_NTT_TWL=0 && run nocoltwl2 nocoltwl || exit 1
 echo ALLOK
