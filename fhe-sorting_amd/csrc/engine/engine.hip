@@ -2009,10 +2009,14 @@ std::string Engine::kernel_clock_stop() {
     for (auto &kv : agg) {
         const bool ph = kv.first.rfind("phase:", 0) == 0;
         const double op = ph ? phase_op[kv.first.substr(6)] : 0.0;
-        snprintf(buf, sizeof buf, "%s\"%s\": {\"launches\": %ld, \"ms\": %.6f, \"bytes\": %.0f%s%.0f%s}",
-                 first ? "" : ", ", kv.first.c_str(), kv.second.launches, kv.second.ms, kv.second.bytes,
-                 ph ? ", \"op_bytes\": " : "", ph ? op : 0.0, "");
+        snprintf(buf, sizeof buf, "%s\"%s\": {\"launches\": %ld, \"ms\": %.6f, \"bytes\": %.0f", first ? "" : ", ",
+                 kv.first.c_str(), kv.second.launches, kv.second.ms, kv.second.bytes);
         out += buf;
+        if (ph) {
+            snprintf(buf, sizeof buf, ", \"op_bytes\": %.0f", op);
+            out += buf;
+        }
+        out += "}";
         first = false;
     }
     return out + "}";

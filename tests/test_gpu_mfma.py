@@ -135,3 +135,27 @@ def test_leaf_sums_4096_blocks_ring16_stack32():
     ref = [orc.cheb(x, c) for x in xs]
     for m in range(32):
         same(gpu.member(out, m), ref[m % 4])
+
+
+def test_kernel_clock_bytes_are_algorithmic():
+    """The live clock the bench's roofline reads: a ciphertext add at level l of
+    ring 2^12 books exactly 3 x 2 x (l+1) x n x 8 algorithmic bytes (two inputs,
+    one output, two polynomials) on one k_add launch, and no kernel of an HMult
+    claims more than 10 TB/s (the JSON once appended a stray digit to every byte
+    count, a 10x error)"""
+    L = 6
+    orc = O.Context(12, L, 40, 60, 3, seed=62)
+    gpu = F.Context(12, L, 40, 60, 3, seed=62, keygen=False)
+    gpu.load_keys_from(orc, [])
+    rng = np.random.default_rng(62)
+    x = gpu.from_oracle(orc.encrypt(rng.uniform(-1, 1, 64), 64))
+    y = gpu.from_oracle(orc.encrypt(rng.uniform(-1, 1, 64), 64))
+    with F.KernelClock(gpu) as clk:
+        gpu.add(x, y)
+    st = clk.stats
+    assert st['k_add']['launches'] == 1
+    assert st['k_add']['bytes'] == 3 * 2 * x.info()['limbs'] * 4096 * 8
+    with F.KernelClock(gpu) as clk:
+        gpu.mul(x, y)
+    for k, v in clk.stats.items():
+        assert v['bytes'] > 0 and v['bytes'] / (v['ms'] * 1e-3) < 10e12, (k, v)
