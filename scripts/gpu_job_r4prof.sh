@@ -17,6 +17,10 @@ O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 export FHE_PROF_REGION=1
+# an 8 MiB AQL ring: the profiler's dispatch interception faults when HIP's
+# default 16,384-packet ring wraps under a --pmc pass (the
+# device mask encoder's launches made the N=1024 sort wrap it too)
+export ROC_AQL_QUEUE_SIZE=131072
 (while sleep 60; do echo "tick $(date +%T)"; done) & TICK=$!
 trap 'kill $TICK 2>/dev/null' EXIT
 B="--steps 1 --warmup 1 --no-cpu-baseline --no-roofline --lanes 1 --mask-steps 0"
@@ -33,7 +37,7 @@ python scripts/pmc_summary.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pm
 python scripts/pmc_sq_summary.py $O/pmc_sq/run_counter_collection.csv $O/pmc_sq${PMCSFX}.json > $O/pmc_sq.txt || exit 1
 gzip -f $O/pmc_*/run_counter_collection.csv
 cp $O/pmc_traffic${PMCSFX}.json $O/pmc_sq${PMCSFX}.json profiles/
-unset FHE_PROF_REGION
+unset FHE_PROF_REGION ROC_AQL_QUEUE_SIZE
 timeout -k 10 600 python bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
 python - "$O/bench.json" <<'PY'
 import json, sys

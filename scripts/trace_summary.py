@@ -1,6 +1,4 @@
-"""Summarise a rocprofv3 kernel-trace CSV: time share per kernel and the
-achieved HBM bandwidth of the NTT passes (algorithmic bytes: every limb is
-read and written once per pass).
+"""Summarise a rocprofv3 kernel-trace CSV: time share per kernel.
 
 When the run carries region markers (bench.py FHE_PROF_REGION=1: k_region_begin
 / k_region_end around the timed sort), only the dispatches inside the region are
@@ -8,7 +6,7 @@ counted, and `--stats-out PATH` writes them in rocprofv3's --stats layout
 (Name, Calls, TotalDurationNs, AverageNs, Percentage, MinNs, MaxNs, StdDev):
 profiles/r4_*/region_kernel_stats.csv, from which bench.py's roofline line can
 be recomputed (its live clock runs the same one-lane sort).
-usage: trace_summary.py run_kernel_trace.csv [n] [--stats-out PATH]
+usage: trace_summary.py run_kernel_trace.csv [--stats-out PATH]
 """
 import collections
 import csv
@@ -27,7 +25,6 @@ if '--stats-out' in args:
     stats_out = args[i + 1]
     del args[i:i + 2]
 rows, found = region(list(csv.DictReader(open(args[0]))))
-n = int(args[1]) if len(args) > 1 else 65536
 print(f'region: {"k_region_begin..k_region_end" if found else "none (every dispatch)"}')
 stat = collections.defaultdict(list)
 full = {}
@@ -46,16 +43,9 @@ for k, v in sorted(stat.items(), key=lambda kv: -sum(x[0] for x in kv[1]))[:24]:
     tot = sum(x[0] for x in v)
     print(f'{k:34s} n={len(v):6d} {tot / 1e6:9.2f} ms {100 * tot / tot_all:5.1f}%  avg {tot / len(v) / 1e3:7.2f} us'
           f'  vgpr={v[0][4]} agpr={v[0][6]} sgpr={v[0][7]} lds={v[0][5]}')
-# NTT passes launch grid (segments x 256 threads, blocks per limb, limbs)
-for k in sorted(stat):
-    if not k.startswith('k_ntt'):
-        continue
-    v = stat[k]
-    limbs = [gx // 256 * gz for _, gx, _, gz, _, _, _, _ in v]
-    tb = sum(L * n * 16 for L in limbs)
-    tt = sum(x[0] for x in v)
-    print(f'{k}: {tb / tt:.1f} GB/s algorithmic (one read + one write per coefficient), '
-          f'avg {sum(limbs) / len(v):.1f} limbs/launch, avg {tt / len(v) / 1e3:.2f} us')
+# (algorithmic bytes per launch come from the engine's own launch wrappers --
+# bench.py's live clock, `roofline.kernels` -- not from grid shapes here: the
+# register-only row passes and the column passes lay their grids out differently)
 if stats_out:
     with open(stats_out, 'w', newline='') as f:
         w = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
