@@ -848,6 +848,52 @@ std::vector<CtPtr> RotationComposerN::rotateMany(const Ciphertext &in, const std
     return out;
 }
 
+std::vector<CtPtr> RotationComposerN::rotateMembers(const Ciphertext &in, const std::vector<int> &rotations) {
+    const int B = in.batch;
+    if ((int)rotations.size() != B) throw std::invalid_argument("rotateMembers: one rotation per member");
+    const long half = (long)cc.n() / 2;
+    std::vector<std::vector<int>> steps(B);  // the keyed steps rotate() would apply
+    size_t depth = 0;
+    for (int m = 0; m < B; ++m) {
+        const int r = rotations[m];
+        if (r % in.slots == 0)
+            ;
+        else if (avail.count(r))
+            steps[m].push_back(r);
+        else
+            for (const Step &st : dec.decompose(r, in.slots, algo))
+                if (st.stepSize % half) steps[m].push_back(st.stepSize);  // (a step = 0 mod n/2 is the identity)
+        depth = std::max(depth, steps[m].size());
+    }
+    std::vector<CtPtr> cur(B);
+    for (int m = 0; m < B; ++m) cur[m] = cc.member(in, m);
+    for (size_t j = 0; j < depth; ++j) {
+        std::vector<int> act;
+        std::vector<long> ks;
+        for (int m = 0; m < B; ++m)
+            if (steps[m].size() > j) {
+                act.push_back(m);
+                ks.push_back(steps[m][j]);
+            }
+        if (act.size() == 1) {
+            cur[act[0]] = cc.rotate(*cur[act[0]], ks[0]);
+            continue;
+        }
+        CtPtr r;
+        if (j == 0 && (int)act.size() == B) {
+            r = cc.rotate_members(in, ks);
+        } else {
+            std::vector<const Ciphertext *> v;
+            for (int m : act) v.push_back(cur[m].get());
+            r = cc.rotate_members(*cc.stack(v), ks);
+        }
+        for (size_t i = 0; i < act.size(); ++i) cur[act[i]] = cc.member(*r, (int)i);
+    }
+    for (int m = 0; m < B; ++m)
+        if (steps[m].empty()) cur[m] = cc.clone(*cur[m]);  // as rotate(): a copy, not a view
+    return cur;
+}
+
 // ============================================================ DirectSort ===
 // ---------------------------------------------------------- RotationTree ----
 RotationTreeN::RotationTreeN(Engine &c, int N, const std::vector<int> &rotIndices, DecomposeAlgo a)
@@ -1200,6 +1246,31 @@ CtPtr DirectSortN::vecRotsOpt(Lane L, const std::vector<CtPtr> &baby, int num_pa
     return result;
 }
 
+std::vector<CtPtr> DirectSortN::vecRotsOptMany(Lane L, const std::vector<CtPtr> &baby, int num_partition,
+                                               int num_slots, int np, const std::vector<int> &iss) {
+    if (iss.size() == 1) return {vecRotsOpt(L, baby, num_partition, num_slots, np, iss[0])};
+    std::vector<CtPtr> result(iss.size());
+    for (int j = 0; j < num_partition / np; ++j) {
+        std::vector<CtPtr> T(iss.size());
+        std::vector<const Ciphertext *> tp;
+        std::vector<int> rots;
+        for (size_t b = 0; b < iss.size(); ++b) {
+            std::vector<const Ciphertext *> cs;
+            std::vector<const Plaintext *> ps;
+            for (int i = 0; i < np; ++i) {
+                cs.push_back(baby[i].get());
+                ps.push_back(&mask(*L.eng, 0, num_slots, np * j + i, -iss[b] * num_partition - j * np, baby[i]->level));
+            }
+            T[b] = L.eng->mul_plain_sum(cs, ps);
+            tp.push_back(T[b].get());
+            rots.push_back(iss[b] * num_partition + j * np);
+        }
+        auto o = L.rot->rotateMembers(*L.eng->stack(tp), rots);
+        for (size_t b = 0; b < iss.size(); ++b) L.eng->add_inplace(result[b], *o[b]);
+    }
+    return result;
+}
+
 // The comparator batches run stacked: their inputs differ, but the sign() op
 // sequence is identical, so one compare over a ciphertext batch replaces
 // max_stack sequential ones, on `lanes` concurrent streams.
@@ -1221,12 +1292,10 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
         Engine &E = *L.eng;
         CtPtr acc;
         for (size_t c0 = 0; c0 < bs.size(); c0 += chunk) {
-            std::vector<CtPtr> shifted;
+            std::vector<int> iss(bs.begin() + c0, bs.begin() + std::min(bs.size(), c0 + chunk));
+            std::vector<CtPtr> shifted = vecRotsOptMany(L, baby, s.num_partition, s.num_slots, s.np, iss);
             std::vector<const Ciphertext *> ptrs;
-            for (size_t i = c0; i < std::min(bs.size(), c0 + chunk); ++i) {
-                shifted.push_back(vecRotsOpt(L, baby, s.num_partition, s.num_slots, s.np, bs[i]));
-                ptrs.push_back(shifted.back().get());
-            }
+            for (auto &x : shifted) ptrs.push_back(x.get());
             // x - s_b of every batch written straight into the stacked ciphertext
             CtPtr d = ptrs.size() == 1 ? E.sub(*dup, *shifted[0]) : E.sub_stacked(*dup, ptrs);
             shifted.clear();
@@ -1264,10 +1333,15 @@ CtPtr DirectSortN::blindRotationStacked(Lane L, const std::vector<CtPtr> &mi, in
             ps.push_back(&mask(E, 0, num_slots, np * i + j, j, mi[j]->level));
         }
         CtPtr tmp = E.mul_plain_sum(cs, ps);  // src/sort_algo.h:573-577
-        for (size_t m = 0; m < ibs.size(); ++m) {
-            CtPtr one = tmp->batch == 1 ? tmp : E.member(*tmp, (int)m);
-            E.add_inplace(result, *L.rot->rotate(*one, ibs[m] * num_partition + i * np));
+        if (tmp->batch == 1) {
+            E.add_inplace(result, *L.rot->rotate(*tmp, ibs[0] * num_partition + i * np));
+            continue;
         }
+        // every batch's giant-step rotation (its own amount) in shared launches;
+        // the sum mod q does not depend on the order of the terms
+        std::vector<int> rots;
+        for (size_t m = 0; m < ibs.size(); ++m) rots.push_back(ibs[m] * num_partition + i * np);
+        for (auto &o : L.rot->rotateMembers(*tmp, rots)) E.add_inplace(result, *o);
     }
     return result;
 }

@@ -95,6 +95,11 @@ class RotationComposerN {
     CtPtr rotate(const Ciphertext &in, int rotation);
     // several rotations of one input; single keyed steps share one ModUp
     std::vector<CtPtr> rotateMany(const Ciphertext &in, const std::vector<int> &rotations);
+    // member m of the batch `in` rotated by rotations[m] through the same keyed
+    // steps rotate() takes; step j of every member that has one runs in one
+    // multi-key launch sequence (Engine::rotate_members).  Same words as
+    // rotate() member by member.
+    std::vector<CtPtr> rotateMembers(const Ciphertext &in, const std::vector<int> &rotations);
     Engine &cc;
     DecomposerN dec;
     DecomposeAlgo algo;
@@ -234,6 +239,10 @@ class DirectSortN {
     template <class F>
     std::vector<CtPtr> run_lanes(const std::vector<int> &batches, F &&work);
     CtPtr vecRotsOpt(Lane L, const std::vector<CtPtr> &baby, int num_partition, int num_slots, int np, int is);
+    // vecRotsOpt of several batches: the giant-step rotations of all of them
+    // (one amount per batch) run in shared launches (RotationComposerN::rotateMembers)
+    std::vector<CtPtr> vecRotsOptMany(Lane L, const std::vector<CtPtr> &baby, int num_partition, int num_slots,
+                                      int np, const std::vector<int> &iss);
     CtPtr blindRotationOptN(const std::vector<CtPtr> &masked, int num_slots, int np, int ib, int num_partition);
     // blindRotationOptN over a stacked `masked` (member m belongs to batch ibs[m]), summed over members
     CtPtr blindRotationStacked(Lane L, const std::vector<CtPtr> &masked, int num_slots, int np,
