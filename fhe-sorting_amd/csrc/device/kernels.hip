@@ -476,8 +476,11 @@ struct LeafArgs {
     int m, G, accumulate;
 };
 constexpr int LF_NC = 2, LF_NT = 256;
+#ifndef FHE_LF_WPE  // waves per SIMD asked of the compiler (A/B: -DFHE_LF_WPE=4)
+#define FHE_LF_WPE 3
+#endif
 template <int KS, int NG>
-__global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_leaf_sums_mfma(LeafArgs A, size_t seg, const Mod *mods, int logN,
+__global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(FHE_LF_WPE, 8))) void k_leaf_sums_mfma(LeafArgs A, size_t seg, const Mod *mods, int logN,
                                                           int chunk) {
     __shared__ u64 etab[4 * NG][8 * KS];  // byte-reversed balanced digits of each constant
     __shared__ u64 cval[4 * NG][8 * KS];
@@ -527,11 +530,6 @@ __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(3, 8))) v
         for (int grp = 0; grp < NG; ++grp) {
             const int t = 4 * grp + lg;
             u64 *o = optr[t < A.G ? t : 0] + oo_l + nb + col;
-            u64 prev[LF_NC] = {};
-            if (A.accumulate) {
-#pragma unroll
-                for (int c = 0; c < LF_NC; ++c) prev[c] = o[16 * c];
-            }
             v4i acc[LF_NC][4];
 #pragma unroll
             for (int c = 0; c < LF_NC; ++c)
@@ -561,6 +559,13 @@ __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(3, 8))) v
                 __builtin_amdgcn_sched_barrier(0);
             }
             if (t < A.G) {
+                // (accumulating launches read the running sums only now: loaded
+                // before the products they held 4 VGPRs across the MFMA loop)
+                u64 prev[LF_NC] = {};
+                if (A.accumulate) {
+#pragma unroll
+                    for (int c = 0; c < LF_NC; ++c) prev[c] = o[16 * c];
+                }
                 const u64 cr = corr[t];
 #pragma unroll
                 for (int c = 0; c < LF_NC; ++c) o[16 * c] = add_mod(add_mod(combine_rows(acc[c], md), cr, md.q), prev[c], md.q);
