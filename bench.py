@@ -73,7 +73,9 @@ def parse():
     ap.add_argument('--cpu-sample-mults', type=int, default=0, help='override CPU sample size')
     ap.add_argument('--clock-json', default=None, help='write the full per-kernel clock of the roofline sort here')
     ap.add_argument('--dnum', type=int, default=0, help='MEHP24: key-switch digits (0: the parameter table, OpenFHE default 3)')
-    ap.add_argument('--lanes', type=int, default=3, help='concurrent batch lanes (forked engines) per GPU (3: 885 vs 898 ms for 2)')
+    ap.add_argument('--lanes', type=int, default=2,
+                    help='concurrent batch lanes (forked engines) per GPU (round 4, batched rotations: 2 lanes 589.6 ms, '
+                         '3 lanes 604.0, 4 lanes 611.9, 1 lane 613.8; profiles/r4_lanes)')
     ap.add_argument('--stack', type=int, default=32, help='max batches stacked into one ciphertext batch')
     ap.add_argument('--mask-steps', type=int, default=2,
                     help='extra sorts timed with every mask re-encoded per sort (0: skip)')
