@@ -382,13 +382,15 @@ __device__ __forceinline__ int row_final_index(int t, int r) {
 // FHE_NTT_ROW_SHFL bit mask (A/B timing): 1 inverse row pass, 2 every forward row
 // pass, 4 / 8 / 16 only the fused HMult-tail / rescale / key-switch-finish forward
 // rows use the register-only DPP passes.  0 keeps all on the LDS-exchange passes.
-// Default 5 (inverse rows + HMult-tail rows): at two lanes the DPP HMult tail
-// (66-175 VGPRs instead of 220) took the sort 590.9 / 589.2 -> 584.9 / 582.5 ms
-// (profiles/r4_j; at three lanes it had measured even, profiles/r4_f).
+// Default 13 (inverse rows + HMult-tail and rescale rows): at two lanes the DPP
+// HMult tail (66-175 VGPRs instead of 220) took the sort 590.9 / 589.2 -> 584.9 /
+// 582.5 ms (profiles/r4_j; at three lanes it had measured even, profiles/r4_f),
+// the DPP rescale rows 575.4 / 577.5 -> 572.4 / 574.6 ms (profiles/r4_k; the
+// key-switch-finish rows were neutral and stay on the LDS passes).
 int &row_shfl_enabled() {
     static int v = [] {
         const char *e = std::getenv("FHE_NTT_ROW_SHFL");
-        return e ? std::atoi(e) : 5;
+        return e ? std::atoi(e) : 13;
     }();
     return v;
 }
