@@ -58,14 +58,16 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
     return COLS ? idx * (NB + 1) + tr : tr * ((1 << PB) + (1 << PB) / 16) + idx + (idx >> 4);
 }
 
-// 32-bit exchanges (FHE_NTT_LDS32, default on): a non-split exchange moves the
-// low and then the high halves of the coefficients through a tile of 32-bit
-// words, half the LDS of a 64-bit tile, so twice the blocks fit a CU: the
-// 256-point passes' 34.8 KB tile held 4 blocks (4 waves per SIMD) where their
-// 52-64 VGPRs allow 8.  Two more barriers; no more registers (the low halves
-// are dead once written).
+// 32-bit exchanges (FHE_NTT_LDS32, default on for the column passes): a
+// non-split exchange moves the low and then the high halves of the coefficients
+// through a tile of 32-bit words, half the LDS of a 64-bit tile, so twice the
+// blocks fit a CU: with the 4-KB column twiddle table the inverse column pass
+// (70-72 VGPRs) goes from 4 blocks (38.9 KB) to 7 (21.5 KB) per CU.  Two more
+// barriers; no more registers (the low halves are dead once written).  Measured
+// neutral in r4_a, before the column twiddles moved to LDS; since then 577.8 /
+// 576.0 -> 572.6 / 574.7 ms, inverse column 98 -> 95 us (profiles/r4_l).
 #ifndef FHE_NTT_LDS32
-#define FHE_NTT_LDS32 0
+#define FHE_NTT_LDS32 1
 #endif
 // (row passes keep the 64-bit tile: with theirs at 32 bits the rescale and
 // HMult-tail row passes ran 461 -> 530 and 385 -> 403 us, profiles/r4_a)
@@ -79,6 +81,39 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
 #ifndef FHE_NTT_COL_TWL
 #define FHE_NTT_COL_TWL 1
 #endif
+// Buffer-addressed column passes (FHE_NTT_COL_BUF): a lane's E coefficients of a
+// column sit 2^k2 words apart, too far for a global load's 13-bit immediate, so
+// every global_load / global_store carried its own 64-bit VGPR address (32 VGPRs
+// of addresses with all 16 loads in flight).  As buffer_load / buffer_store the
+// limb base is one scalar resource, the lane's offset one VGPR and the per-register
+// offset r T 2^k2 8 an SGPR.
+#ifndef FHE_NTT_COL_BUF
+#define FHE_NTT_COL_BUF 1
+#endif
+// Wave-uniform twiddles of the column passes (forward round 1, inverse round B)
+// read through the constant address space, i.e. scalar loads into SGPRs (the
+// tables never change while a kernel runs); as vector loads they held 4 VGPRs
+// each.  A/B: -DFHE_NTT_COL_SCALAR=0.
+#ifndef FHE_NTT_COL_SCALAR
+#define FHE_NTT_COL_SCALAR 1
+#endif
+typedef const __attribute__((address_space(4))) u64 const_u64_t;
+__device__ __forceinline__ ulonglong2 scalar_tw(const ulonglong2 *p, size_t i) {
+    const const_u64_t *q = (const const_u64_t *)p + 2 * i;
+    return make_ulonglong2(q[0], q[1]);
+}
+// raw buffer resource over one limb (wave-uniform base; CDNA word 3)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t limb_rsrc(const u64 *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<u64 *>(base), 0, 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ u64 bload64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    return ((u64)v[1] << 32) | v[0];
+}
+__device__ __forceinline__ void bstore64(__amdgpu_buffer_rsrc_t r, int voff, int soff, u64 x) {
+    typedef unsigned v2u __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(v2u{(unsigned)x, (unsigned)(x >> 32)}, r, voff, soff, 0);
+}
 template <bool COLS>
 constexpr bool lds32() {
     return FHE_NTT_LDS32 != 0 && COLS;
@@ -434,7 +469,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // block across all segments run back to back and share its twiddles in
     // L2), y = block within the limb, z = limb
     const int limb = blockIdx.z;
-    const int p = pmap ? pmap[limb] : limb;
+    const int p = pmap ? __builtin_amdgcn_readfirstlane(pmap[limb]) : limb;
     int t, tr;  // lane within its transform, transform within the block
     if (COLS) {
         tr = threadIdx.x % NB;
@@ -451,9 +486,10 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     const size_t tid_global = SH ? (size_t)blockIdx.y * (NB >> F.lsegb) + (tr >> F.lsegb)
                                  : (size_t)blockIdx.y * NB + tr;  // column or row index
     const bool valid = FULL || (tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs));
-    u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
+    u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)__builtin_amdgcn_readfirstlane(smap[limb]) : (size_t)limb) * n;
     const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
+    constexpr bool CBUF = FHE_NTT_COL_BUF && COLS && FULL;  // (FULL: no bounds check; COLS: zseg is blockIdx.x)
     const int S0 = COLS ? 0 : logN - PB;                      // global stage of local stage 0
     if (CTW) twc[threadIdx.x] = tw[threadIdx.x];  // read after the exchange's barrier (round 2)
 
@@ -466,13 +502,21 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
         const u64 ql = ml.q, qh = ql >> 1;
         const u64 kl = F.scalar ? smod64(F.scalar, F.scalar_sh, ml) : 0;  // K mod q_last (scaled rescale)
         const u64 *src = F.last + (size_t)zseg * F.seg_last;
+        const auto rs = limb_rsrc(src);
+        const int vo = (int)((((size_t)t << k2) + tid_global) * 8);
 #pragma unroll
         for (int r = 0; r < E; ++r) {
             const int idx = t + T * r;
-            u64 c = valid ? src[(size_t)idx * ((size_t)1 << k2) + tid_global] : 0;
+            u64 c = CBUF ? bload64(rs, vo, (T * r << k2) * 8)
+                         : valid ? src[(size_t)idx * ((size_t)1 << k2) + tid_global] : 0;
             if (F.scalar) c = mul_barrett(c, kl, ml);
             x[r] = c > qh ? q - (ql - c) : c;
         }
+    } else if constexpr (CBUF) {
+        const auto rs = limb_rsrc(a);
+        const int vo = (int)((((size_t)t << k2) + tid_global) * 8);
+#pragma unroll
+        for (int r = 0; r < E; ++r) x[r] = bload64(rs, vo, (T * r << k2) * 8);
     } else {
 #pragma unroll
         for (int r = 0; r < E; ++r) {
@@ -559,9 +603,13 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
         for (int b = 0; b < E / 2; ++b) {  // butterfly b: r0 = b with a 0 inserted at bit hb
             const int r0 = ((b >> hb) << (hb + 1)) | (b & ((1 << hb) - 1));
             const int idx0 = t + T * r0;
-            const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
+            // COLS: (t + T r0) >> (PB - s) = r0 >> (EB - s) since t < T -- a
+            // compile-time index into the prime's table, so the twiddle is a
+            // scalar load (constant address space) instead of 4 VGPRs
+            const size_t i = COLS ? ((size_t)r0 >> (EB - s)) : (tid_global << s) + (size_t)(idx0 >> (PB - s));
             const size_t wi = ((size_t)1 << (S0 + s)) + i;
-            ct_stage<PB>(COLS, s, x[r0], x[r0 + (1 << hb)], tw[wi], q4, nq);
+            ct_stage<PB>(COLS, s, x[r0], x[r0 + (1 << hb)], (COLS && FHE_NTT_COL_SCALAR) ? scalar_tw(tw, wi) : tw[wi], q4,
+                         nq);
         }
     }
     // round-2 twiddles (G == 1: stage s needs 2^(s-EB) of them per lane, index
@@ -627,7 +675,14 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // consecutive coefficients, so the values go back through LDS to layout
     // L1 and every store instruction writes contiguous 128-B runs.  Each lane
     // rewrites only the tile words it read itself, so one barrier suffices.
-    if (COLS) {
+    if constexpr (CBUF) {
+        const auto rs = limb_rsrc(a);
+        const int vo = (int)((((size_t)t * G * T << k2) + tid_global) * 8);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < T; ++r) bstore64(rs, vo, ((g * T + r) << k2) * 8, x[l2reg<G, T, SPLIT>(g, r)]);
+    } else if (COLS) {
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -689,7 +744,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     // block across all segments run back to back and share its twiddles in
     // L2), y = block within the limb, z = limb
     const int limb = blockIdx.z;
-    const int p = pmap ? pmap[limb] : limb;
+    const int p = pmap ? __builtin_amdgcn_readfirstlane(pmap[limb]) : limb;
     int t, tr;
     if (COLS) {
         tr = threadIdx.x % NB;
@@ -702,9 +757,10 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     const int zseg = SH ? (int)blockIdx.x * (1 << F.lsegb) + (tr & ((1 << F.lsegb) - 1)) : (int)blockIdx.x;
     const size_t tid_global = SH ? (size_t)blockIdx.y * (NB >> F.lsegb) + (tr >> F.lsegb) : (size_t)blockIdx.y * NB + tr;
     const bool valid = FULL || (tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs));
-    u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)smap[limb] : (size_t)limb) * n;
+    u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)__builtin_amdgcn_readfirstlane(smap[limb]) : (size_t)limb) * n;
     const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
     const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
+    constexpr bool CBUF = FHE_NTT_COL_BUF && COLS && FULL;
     const int SG0 = COLS ? logN - PB : 0;  // global GS stage of local stage 0
     if (CTW) twc[threadIdx.x] = tw[threadIdx.x];  // round A reads it after the barrier below
 
@@ -734,7 +790,14 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     // ---- load, layout L2 (low bits within a lane group).  The ROWS pass's
     // per-lane runs of T consecutive words are read 16 B at a time (L1 serves
     // the rest of each line; routing them through LDS measured slower).
-    if (COLS || (T & 1)) {
+    if constexpr (CBUF) {
+        const auto rs = limb_rsrc(ain);
+        const int vo = (int)((((size_t)t * G * T << k2) + tid_global) * 8);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int r = 0; r < T; ++r) x[l2reg<G, T, SPLIT>(g, r)] = bload64(rs, vo, ((g * T + r) << k2) * 8);
+    } else if (COLS || (T & 1)) {
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -813,19 +876,24 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
             const size_t i = COLS ? ((size_t)T * r0) >> (s + 1)
                                   : (j + (size_t)idx0) >> (sg + 1);
             const size_t wi = (n >> (sg + 1)) + i;
-            gs_bfly(x[r0], x[r0 + (1 << hb)], tw[wi], q4, nq);
+            gs_bfly(x[r0], x[r0 + (1 << hb)], (COLS && FHE_NTT_COL_SCALAR) ? scalar_tw(tw, wi) : tw[wi], q4, nq);
         }
     }
     // ---- store, layout L1 (COLS: times n^-1, or raw: reduced to [0, 2q) for
     // the conversions' 30-bit operand split; ROWS: lazy [0, 4q))
     const u64 ni = Tb.ninv[p], nis = Tb.ninv_s[p];
     const bool scale = COLS && !F.raw;
+    const auto rso = limb_rsrc(a);
+    const int vso = (int)((((size_t)t << k2) + tid_global) * 8);
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const int idx = t + T * r;
         const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
         const u64 v = scale ? mul_shoup(x[r], ni, nis, q) : COLS ? (x[r] >= q2 ? x[r] - q2 : x[r]) : x[r];
-        if (valid) a[off] = v;
+        if constexpr (CBUF)
+            bstore64(rso, vso, (T * r << k2) * 8, v);
+        else if (valid)
+            a[off] = v;
     }
 }
 
