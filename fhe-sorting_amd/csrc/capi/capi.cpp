@@ -347,6 +347,19 @@ int fhe_compose_rotate(fhe_ctx *ctx, const fhe_ct *a, int N, const int32_t *rots
         *out = wrap(rc.rotate(*a->p, rotation));
     });
 }
+int fhe_compose_rotate_members(fhe_ctx *ctx, const fhe_ct *a, int N, const int32_t *rots, int nrot, int algo,
+                               const int32_t *rotations, int count, fhe_ct **out) {
+    return guard([&] {
+        NEED(ctx);
+        NEED(a);
+        if (count != a->p->batch) throw std::invalid_argument("compose_rotate_members: one rotation per member");
+        RotationComposerN rc(*ctx->eng, N, std::vector<int>(rots, rots + nrot), (DecomposeAlgo)algo);
+        auto m = rc.rotateMembers(*a->p, std::vector<int>(rotations, rotations + count));
+        std::vector<const Ciphertext *> v;
+        for (auto &x : m) v.push_back(x.get());
+        *out = wrap(v.size() == 1 ? ctx->eng->clone(*m[0]) : ctx->eng->stack(v));
+    });
+}
 int fhe_rotation_tree_create(fhe_ctx *ctx, int N, const int32_t *rots, int nrot, int algo, fhe_rot_tree **out) {
     return guard([&] {
         NEED(ctx);

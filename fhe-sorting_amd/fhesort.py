@@ -111,6 +111,7 @@ _SIGS = {
     'fhe_compare': (C.c_int, [vp, vp, vp, C.c_int, C.c_int, C.c_int, PP]),
     'fhe_indicator': (C.c_int, [vp, vp, C.c_double, C.c_int, C.c_int, C.c_int, PP]),
     'fhe_compose_rotate': (C.c_int, [vp, vp, C.c_int, ip, C.c_int, C.c_int, C.c_int, PP]),
+    'fhe_compose_rotate_members': (C.c_int, [vp, vp, C.c_int, ip, C.c_int, C.c_int, ip, C.c_int, PP]),
     'fhe_decompose': (C.c_int, [C.c_int, ip, C.c_int, C.c_int, C.c_int, C.c_int, ip, ip, C.c_int]),
     'fhe_rotation_tree_create': (C.c_int, [vp, C.c_int, ip, C.c_int, C.c_int, PP]),
     'fhe_rotation_tree_build': (C.c_int, [vp, C.c_int, C.c_int]),
@@ -650,6 +651,12 @@ class Context:
     def compose_rotate(self, a, N, rots, algo, rotation):
         r = np.asarray(rots, dtype=np.int32)
         return self._new(lib().fhe_compose_rotate, a.h, N, _int(r), len(r), algo, rotation)
+
+    def compose_rotate_members(self, a, N, rots, algo, rotations):
+        """member m of the batch `a` rotated by rotations[m], steps batched across members"""
+        r = np.asarray(rots, dtype=np.int32)
+        k = np.asarray(rotations, dtype=np.int32)
+        return self._new(lib().fhe_compose_rotate_members, a.h, N, _int(r), len(r), algo, _int(k), len(k))
 
     def direct_sort(self, x, N, rots, cfg, mode=0, rank=None, shard=(0, 1), allreduce=None):
         r = np.asarray(rots, dtype=np.int32)

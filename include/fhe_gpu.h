@@ -173,6 +173,12 @@ int fhe_indicator(fhe_ctx *ctx, const fhe_ct *x, double c, int n, int dg, int df
  * algo: 0 NAF, 1 BNAF, 2 BINARY */
 int fhe_compose_rotate(fhe_ctx *ctx, const fhe_ct *a, int N, const int32_t *rots, int nrot, int algo,
                        int rotation, fhe_ct **out);
+/* Member m of the ciphertext batch `a` rotated by rotations[m] through the same keyed
+ * steps as fhe_compose_rotate, step j of every member in one multi-key launch sequence
+ * (the batched giant steps of blindRotationOptN / vecRotsOpt, src/sort_algo.h:326-366,
+ * 561-584); *out is the batch of the results, word-identical to member-wise rotation. */
+int fhe_compose_rotate_members(fhe_ctx *ctx, const fhe_ct *a, int N, const int32_t *rots, int nrot, int algo,
+                               const int32_t *rotations, int count, fhe_ct **out);
 /* RotationTree<N>(cc, rots, algo) (src/rotation.h:240-358): buildTree(start, end)
  * (:272-279), treeRotate(ct, rotation) (:281-291) with every node's rotation cached
  * (one tree per input ciphertext, as in the reference) and the children of a node
