@@ -417,15 +417,17 @@ __device__ __forceinline__ int row_final_index(int t, int r) {
 // FHE_NTT_ROW_SHFL bit mask (A/B timing): 1 inverse row pass, 2 every forward row
 // pass, 4 / 8 / 16 only the fused HMult-tail / rescale / key-switch-finish forward
 // rows use the register-only DPP passes.  0 keeps all on the LDS-exchange passes.
-// Default 13 (inverse rows + HMult-tail and rescale rows): at two lanes the DPP
-// HMult tail (66-175 VGPRs instead of 220) took the sort 590.9 / 589.2 -> 584.9 /
-// 582.5 ms (profiles/r4_j; at three lanes it had measured even, profiles/r4_f),
-// the DPP rescale rows 575.4 / 577.5 -> 572.4 / 574.6 ms (profiles/r4_k; the
-// key-switch-finish rows were neutral and stay on the LDS passes).
+// Default 15 (inverse rows, every plain forward row, HMult-tail and rescale rows):
+// at two lanes the DPP HMult tail (66-175 VGPRs instead of 220) took the sort
+// 590.9 / 589.2 -> 584.9 / 582.5 ms (profiles/r4_j; at three lanes it had measured
+// even, profiles/r4_f), the DPP rescale rows 575.4 / 577.5 -> 572.4 / 574.6 ms
+// (profiles/r4_k), the plain forward rows (ModUp; with the LDS row twiddles, so
+// no per-row twiddle re-reads) 573.0 / 575.4 -> 566.6 / 568.4 ms (profiles/r4_n).
+// The key-switch-finish rows were neutral and stay on the LDS passes.
 int &row_shfl_enabled() {
     static int v = [] {
         const char *e = std::getenv("FHE_NTT_ROW_SHFL");
-        return e ? std::atoi(e) : 13;
+        return e ? std::atoi(e) : 15;
     }();
     return v;
 }
