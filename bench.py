@@ -380,6 +380,26 @@ def kernel_view(name, st, pmc, sq, mix, by_family):
             'avg_us': round(avg_s * 1e6, 2), 'launches': st['launches'], 'algorithmic_bytes_per_launch': per_launch}
 
 
+def split_phase_rows(stats):
+    """The live clock's 'phase:<name>' rows -- the same kernels booked again under
+    the algorithm phase that launched them (MEHP24: split / replicate / compare /
+    rank_sums / indicator / select / recombine), with that phase's SURVEY §8(d)
+    op-level bytes -- apart from the per-kernel rows (which alone sum to the sort)"""
+    kernels = {k: v for k, v in stats.items() if not k.startswith('phase:')}
+    phases = {k[6:]: v for k, v in stats.items() if k.startswith('phase:')}
+    return kernels, phases
+
+
+def phase_table(phase_rows, total_ms):
+    """roofline.phases: per phase its kernel time and share, launches, kernel bytes,
+    op-level bytes, their ratio and kernel GB/s, longest first"""
+    return {n: {'ms': round(v['ms'], 2), 'share': round(v['ms'] / total_ms, 3), 'launches': v['launches'],
+                'kernel_bytes': v['bytes'], 'op_bytes': v.get('op_bytes', 0.0),
+                'kernel_over_op_bytes': round(v['bytes'] / v['op_bytes'], 2) if v.get('op_bytes') else None,
+                'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1) if v['ms'] else None}
+            for n, v in sorted(phase_rows.items(), key=lambda kv: -kv[1]['ms'])}
+
+
 def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc_sq.json'):
     """Roofline of the dominant kernel, measured live: one more (untimed) sort
     runs with every hot kernel launched through hipExtLaunchKernelGGL with
@@ -403,10 +423,7 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
     if dump:
         with open(dump, 'w') as f:
             json.dump(stats, f, indent=1)
-    # 'phase:<name>' rows: the same kernels booked under the algorithm phase that
-    # launched them (MEHP24: split / replicate / compare / rank_sums / indicator /
-    # select / recombine), with the SURVEY §8(d) op-level bytes of that phase
-    phase_rows = {k[6:]: stats.pop(k) for k in [k for k in stats if k.startswith('phase:')]}
+    stats, phase_rows = split_phase_rows(stats)
     total_ms = sum(v['ms'] for v in stats.values())
     by_sym, by_fam = {}, {}
     for k, v in stats.items():
@@ -431,11 +448,7 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
         return {n: {'share': round(v['ms'] / total_ms, 3), 'avg_us': round(v['ms'] / v['launches'] * 1e3, 1),
                     'launches': v['launches'], 'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1)} for n, v in top}
     run_bytes = sum(v['bytes'] for v in stats.values())
-    phases = {n: {'ms': round(v['ms'], 2), 'share': round(v['ms'] / total_ms, 3), 'launches': v['launches'],
-                  'kernel_bytes': v['bytes'], 'op_bytes': v.get('op_bytes', 0.0),
-                  'kernel_over_op_bytes': round(v['bytes'] / v['op_bytes'], 2) if v.get('op_bytes') else None,
-                  'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1) if v['ms'] else None}
-              for n, v in sorted(phase_rows.items(), key=lambda kv: -kv[1]['ms'])}
+    phases = phase_table(phase_rows, total_ms)
     extra = {'phases': phases} if phases else {}
     return {**extra, **head, 'bound': 'hbm', 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'pmc_source': {'traffic': pmc_src, 'sq': sq_src, 'lib_sha256': lib_sha256()},

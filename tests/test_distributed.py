@@ -244,3 +244,20 @@ def test_bench_compute_collective_split():
     d = m.Dist(1, probe_devices=False)
     s = m.collective_split(Ctx(), d, 2.0, 2)
     assert s == {'rank_compute_ms': 875.0, 'allreduce_ms': 125.0, 'allreduce_calls_per_step': 2.0}
+
+
+def test_bench_phase_rows_split_from_kernels():
+    """roofline.phases: the clock's 'phase:' rows (MEHP24's sortFG phases) leave the
+    per-kernel table untouched -- kernel time and bytes still sum over the kernel
+    rows only -- and each phase gets its share and kernel / op-level byte ratio"""
+    m = _bench_module()
+    stats = {'k_a': {'launches': 2, 'ms': 3.0, 'bytes': 6e9}, 'k_b@modup': {'launches': 1, 'ms': 1.0, 'bytes': 2e9},
+             'phase:compare': {'launches': 2, 'ms': 3.0, 'bytes': 6e9, 'op_bytes': 2e9},
+             'phase:indicator': {'launches': 1, 'ms': 1.0, 'bytes': 2e9, 'op_bytes': 0.0}}
+    k, ph = m.split_phase_rows(stats)
+    assert set(k) == {'k_a', 'k_b@modup'} and set(ph) == {'compare', 'indicator'}
+    total = sum(v['ms'] for v in k.values())
+    t = m.phase_table(ph, total)
+    assert list(t) == ['compare', 'indicator']
+    assert t['compare']['share'] == 0.75 and t['compare']['kernel_over_op_bytes'] == 3.0
+    assert t['compare']['GBps'] == 2000.0 and t['indicator']['kernel_over_op_bytes'] is None
