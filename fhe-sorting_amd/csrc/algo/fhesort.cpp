@@ -93,7 +93,10 @@ struct PSEval {
             const int a = 1 << (ceil_log2(i) - 1), b = i - a;
             CtPtr t = (a == b) ? cc.square(*T[a]) : cc.mul(*T[a], *T[b]);
             t = cc.add(*t, *t);
-            t = (a == b) ? cc.add_const(*t, -1.0) : cc.sub(*t, *T[a - b]);
+            if (a == b)
+                cc.add_const_inplace(t, -1.0);
+            else
+                t = cc.sub(*t, *T[a - b]);
             T[i] = t;
         }
     }
@@ -103,7 +106,8 @@ struct PSEval {
         const Ciphertext &h = giant(G / 2);
         CtPtr t = cc.square(h);
         t = cc.add(*t, *t);
-        T[G] = cc.add_const(*t, -1.0);
+        cc.add_const_inplace(t, -1.0);
+        T[G] = t;
         return *T[G];
     }
     // ---- leaves.  The recursion below consumes leaves in a fixed order; they
@@ -193,8 +197,8 @@ struct PSEval {
         }
         auto outs = cc.linear_sums_to(xs, rows, target, !raw);
         for (size_t g = 0; g < chunk.size(); ++g) {
-            CtPtr r = outs[g];
-            if (!raw && leaves[chunk[g]].a[0] != 0.0) r = cc.add_const(*r, leaves[chunk[g]].a[0]);
+            CtPtr r = std::move(outs[g]);
+            if (!raw && leaves[chunk[g]].a[0] != 0.0) cc.add_const_inplace(r, leaves[chunk[g]].a[0]);
             ready[chunk[g]] = r;
         }
     }
@@ -203,7 +207,8 @@ struct PSEval {
         const Leaf &L = leaves.at(i);
         if (!has_terms(L.a)) {
             CtPtr r = cc.trivial_const(0.0, L.target, T[1]->slots, T[1]->batch);
-            return L.a[0] != 0.0 ? cc.add_const(*r, L.a[0]) : r;
+            if (L.a[0] != 0.0) cc.add_const_inplace(r, L.a[0]);
+            return r;
         }
         if (!ready.count(i)) evaluate_chunk(i);
         CtPtr r = ready.at(i);
@@ -223,7 +228,8 @@ struct PSEval {
         if (folded(r)) {
             CtPtr rawsum = leaf();  // the collected raw leaf (same order as collect)
             CtPtr out = cc.mul_add_raw(*qv, giant(G), *rawsum);
-            return r[0] != 0.0 ? cc.add_const(*out, r[0]) : out;
+            if (r[0] != 0.0) cc.add_const_inplace(out, r[0]);
+            return out;
         }
         CtPtr prod = cc.mul(*qv, giant(G));
         CtPtr rv = eval(r, target);
@@ -509,13 +515,18 @@ struct PSOpenFHE {
     // T_i: powers of two and even i by 2 T_{i/2}^2 - 1, odd i by 2 T_{i/2} T_{i/2+1} - T_1
     void build() {
         for (int i = 2; i <= k; ++i) {
-            if (i % 2 == 0)
-                T[i] = cc.add_const(*twice_prod(*T[i / 2], *T[i / 2], nullptr, 0.0), -1.0);
-            else
+            if (i % 2 == 0) {
+                T[i] = twice_prod(*T[i / 2], *T[i / 2], nullptr, 0.0);
+                cc.add_const_inplace(T[i], -1.0);
+            } else {
                 T[i] = twice_prod(*T[i / 2], *T[i / 2 + 1], T[1].get(), -1.0);
+            }
         }
         T2.push_back(T[k]);
-        for (int j = 1; j < m; ++j) T2.push_back(cc.add_const(*twice_prod(*T2[j - 1], *T2[j - 1], nullptr, 0.0), -1.0));
+        for (int j = 1; j < m; ++j) {
+            T2.push_back(twice_prod(*T2[j - 1], *T2[j - 1], nullptr, 0.0));
+            cc.add_const_inplace(T2.back(), -1.0);
+        }
     }
     // T_{k(2^m - 1)} = 2 T_{k(2^(j) - 1)} T_{k 2^j} - T_k, j = 1..m-1
     CtPtr t2km1() {
@@ -550,8 +561,8 @@ struct PSOpenFHE {
         }
         auto outs = cc.linear_sums_to(xs, rows, target, !L0.raw);
         for (size_t g = 0; g < chunk.size(); ++g) {
-            CtPtr r = outs[g];
-            if (!L0.raw && P->leaves[chunk[g]].a[0] != 0.0) r = cc.add_const(*r, P->leaves[chunk[g]].a[0]);
+            CtPtr r = std::move(outs[g]);
+            if (!L0.raw && P->leaves[chunk[g]].a[0] != 0.0) cc.add_const_inplace(r, P->leaves[chunk[g]].a[0]);
             ready[chunk[g]] = r;
         }
     }
@@ -575,7 +586,8 @@ struct PSOpenFHE {
         const double s0 = P->leaves[N.sleaf].a[0];
         CtPtr raw = leaf(N.sleaf);
         CtPtr out = cc.mul_add_raw(*a, *qu, *raw, cu.get());
-        return s0 != 0.0 ? cc.add_const(*out, s0) : out;
+        if (s0 != 0.0) cc.add_const_inplace(out, s0);
+        return out;
     }
     CtPtr run() {
         build();
@@ -613,7 +625,7 @@ CtPtr evalChebyshevSeriesPS(Engine &cc, const Ciphertext &x0, const std::vector<
     CtPtr x = cc.clone(x0);
     if (!(a == -1.0 && b == 1.0)) {
         x = cc.mul_const(*x, 2.0 / (b - a));
-        x = cc.add_const(*x, -(a + b) / (b - a));
+        cc.add_const_inplace(x, -(a + b) / (b - a));
     }
     const int d = (int)c.size() - 1;
     if (cc.ps_split() == PS_SPLIT_OPENFHE && d >= 5) {
@@ -733,7 +745,8 @@ CtPtr Comparison::compare(Engine &cc, const Ciphertext &a, const Ciphertext &b, 
         std::fprintf(stderr, "  compare: level %d, max|a - b| %.6g\n", diff->level, mx);
     }
     CtPtr s = sign(*diff, cc, f, cfg);
-    return cc.mul_const(*cc.add_const(*s, 1.0), 0.5);
+    cc.add_const_inplace(s, 1.0);
+    return cc.mul_const(*s, 0.5);
 }
 
 CtPtr Comparison::indicator(Engine &cc, const Ciphertext &x, double c, SignFunc f, const SignConfig &cfg) {
@@ -741,8 +754,10 @@ CtPtr Comparison::indicator(Engine &cc, const Ciphertext &x, double c, SignFunc 
     CtPtr d2 = cc.add_const(x, -c);
     CtPtr s1 = sign(*d1, cc, f, cfg);
     CtPtr s2 = sign(*d2, cc, f, cfg);
-    CtPtr c1 = cc.mul_const(*cc.add_const(*s1, 1.0), 0.5);
-    CtPtr c2 = cc.mul_const(*cc.add_const(*s2, 1.0), 0.5);
+    cc.add_const_inplace(s1, 1.0);
+    cc.add_const_inplace(s2, 1.0);
+    CtPtr c1 = cc.mul_const(*s1, 0.5);
+    CtPtr c2 = cc.mul_const(*s2, 0.5);
     CtPtr om = cc.add_const(*cc.negate(*c2), 1.0);
     return cc.mul(*c1, *om);
 }
@@ -1300,7 +1315,8 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
             CtPtr d = ptrs.size() == 1 ? E.sub(*dup, *shifted[0]) : E.sub_stacked(*dup, ptrs);
             shifted.clear();
             CtPtr sg = sign(*d, E, f, cfg);
-            CtPtr c = E.mul_const(*E.add_const(*sg, 1.0), 0.5);
+            E.add_const_inplace(sg, 1.0);
+            CtPtr c = E.mul_const(*sg, 0.5);
             E.add_inplace(acc, c->batch == 1 ? *c : *E.sum_members(*c));
         }
         return acc;
@@ -1314,7 +1330,8 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
     for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)
         rank = cc.add(*rank, *rot.rotate(*rank, s.num_slots / (1 << i)));
     rank->slots = N;
-    return cc.add_const(*rank, -0.5);
+    cc.add_const_inplace(rank, -0.5);
+    return rank;
 }
 
 CtPtr DirectSortN::blindRotationOptN(const std::vector<CtPtr> &mi, int num_slots, int np, int ib, int num_partition) {
@@ -1668,7 +1685,8 @@ CtPtr signAdv(Engine &cc, CtPtr c, size_t dg, size_t df) {
     for (size_t d = 0; d < dg; ++d) c = g3(cc, *c);
     for (size_t d = 0; d + 1 < df; ++d) c = f3(cc, *c);
     c = odd7(cc, *c, 35.0 / 32.0, -35.0 / 32.0, 21.0 / 32.0, -5.0 / 32.0);
-    return cc.add_const(*c, 0.5);
+    cc.add_const_inplace(c, 0.5);
+    return c;
 }
 
 }  // namespace utils

@@ -1182,6 +1182,20 @@ CtPtr Engine::add_const(const Ciphertext &a, double c) {
     count_bytes(4.0 * a.limbs, a.batch);
     return r;
 }
+// a + c with a exclusively owned (no other handle, no member view of its memory):
+// only the c0 limbs are read and written, in place -- half the traffic of
+// add_const's copy and no allocation; otherwise add_const.  Same words.
+void Engine::add_const_inplace(CtPtr &a, double c) {
+    if (!a) throw std::invalid_argument("add_const_inplace: empty ciphertext");
+    if (a.use_count() != 1 || !a->mem || a->mem.use_count() != 1) {
+        a = add_const(*a, c);
+        return;
+    }
+    const size_t ln = a->limbs * n();
+    const host::SConst K = host::const_at_scale(c, a->scale);
+    dev::ew_add_scalar(a->data, a->data, K.k, (int)a->limbs, a->batch, seg3(2 * ln, 2 * ln, 0), MODS, LOGN, ST, K.sh);
+    count_bytes(2.0 * a->limbs, a->batch);
+}
 CtPtr Engine::mul_int(const Ciphertext &a, i64 K) {
     const size_t ln = a.limbs * n();
     auto r = new_ct(a.level, a.slots, a.scale, a.limbs, a.batch);

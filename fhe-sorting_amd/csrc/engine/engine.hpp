@@ -168,6 +168,8 @@ class Engine {
     CtPtr sub_plain(const Ciphertext &a, const Plaintext &p);
     CtPtr plain_sub(const Plaintext &p, const Ciphertext &a);
     CtPtr add_const(const Ciphertext &a, double c);
+    // a = a + c, in place on the c0 limbs when a is exclusively owned (else add_const)
+    void add_const_inplace(CtPtr &a, double c);
     CtPtr mul_int(const Ciphertext &a, i64 k);
     CtPtr mul_const(const Ciphertext &a, double c);
     CtPtr mul_const_to(const Ciphertext &a, double c, int target);
