@@ -583,11 +583,15 @@ struct PlainSumArgs {
     int m, accumulate;
     size_t cmember, cpoly;
 };
+// grid: x = segment (fastest: the segments that read one plaintext block run
+// back to back, so it is fetched from HBM about once -- with the segment slowest
+// the sort's PMC traffic was 1.32x the algorithmic bytes), y = coefficient block,
+// z = limb
 __global__ __launch_bounds__(NT) void k_mul_plain_sum(u64 *out, PlainSumArgs A, size_t seg, const Mod *mods,
                                                       int logN) {
     const size_t n = (size_t)1 << logN;
-    const int l = blockIdx.y, z = blockIdx.z;
-    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    const int l = blockIdx.z, z = blockIdx.x;
+    const size_t k = ((size_t)blockIdx.y * NT + threadIdx.x) * 2;
     if (k >= n) return;
     const Mod md = mods[l];
     const size_t ln = (size_t)l * n + k;
@@ -1483,8 +1487,9 @@ void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, in
         }
         const double B = 8.0 * ((double)A.m * (cmember ? 2 * members : 2) + A.m + 2.0 * members * (1 + A.accumulate)) *
                          limbs * ((size_t)1 << logN);
-        launch_clocked("k_mul_plain_sum", B, k_mul_plain_sum, ew_grid(logN, limbs, 2 * members), dim3(NT), st, out, A,
-                       seg, mods, logN);
+        const dim3 g0 = ew_grid(logN, limbs, 2 * members);
+        launch_clocked("k_mul_plain_sum", B, k_mul_plain_sum, dim3(g0.z, g0.x, g0.y), dim3(NT), st, out, A, seg, mods,
+                       logN);
     }
 }
 void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,
