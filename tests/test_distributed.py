@@ -261,3 +261,20 @@ def test_bench_phase_rows_split_from_kernels():
     assert list(t) == ['compare', 'indicator']
     assert t['compare']['share'] == 0.75 and t['compare']['kernel_over_op_bytes'] == 3.0
     assert t['compare']['GBps'] == 2000.0 and t['indicator']['kernel_over_op_bytes'] is None
+
+
+def test_bench_limiter_rule():
+    """roofline.limiter (verdict r3: k-way's k_lt_inner at valu_frac 0.98 was
+    labelled 'memory latency'): a kernel at >= 0.85 of the measured VALU
+    throughput is 'valu' whatever its waits; 'memory latency' needs >= 0.3 of the
+    wave cycles in s_waitcnt and more than in issue stalls; streaming kernels and
+    any kernel at >= 0.85 of HBM peak are 'hbm'"""
+    m = _bench_module()
+    lim = m.limiter_of
+    assert lim('k_lt_inner<3>', 0.70, {'valu_frac': 0.98, 'wave_cycle_split': {'waitcnt': 0.5, 'issue_stall': 0.2}}) == 'valu'
+    assert lim('k_ntt_inv_row<false, false>', 0.20,
+               {'valu_frac': 0.32, 'wave_cycle_split': {'waitcnt': 0.52, 'issue_stall': 0.21}}) == 'memory latency'
+    assert lim('k_ntt_fwd_row<3, true, true>', 0.61,
+               {'valu_frac': 0.65, 'wave_cycle_split': {'waitcnt': 0.23, 'issue_stall': 0.57}}) == 'valu'
+    assert lim('k_ntt_fwd<8, 4, true, 0, true>', 0.90, {'valu_frac': 0.5}) == 'hbm'
+    assert lim('k_add', 0.5, {}) == 'hbm'
