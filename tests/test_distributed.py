@@ -12,6 +12,7 @@ i % world, partial Cv / Ch / subSorted sums all-reduced).
 The GPU engine implements the identical hook (fhe_direct_sort allreduce
 callback / RCCL); tests/test_gpu_parity.py checks it against this oracle.
 """
+import json
 import os
 import socket
 
@@ -278,3 +279,23 @@ def test_bench_limiter_rule():
                {'valu_frac': 0.65, 'wave_cycle_split': {'waitcnt': 0.23, 'issue_stall': 0.57}}) == 'valu'
     assert lim('k_ntt_fwd<8, 4, true, 0, true>', 0.90, {'valu_frac': 0.5}) == 'hbm'
     assert lim('k_add', 0.5, {}) == 'hbm'
+
+
+def test_committed_counter_tables_match_the_built_library(tmp_path, monkeypatch):
+    """The PMC / SQ tables in profiles/ carry the SHA-256 of the library they were
+    collected on; bench.py reports their traffic and VALU figures only for that
+    library.  The committed tables must match the in-tree build (a source change
+    to the engine without a new closing profile fails here), and a table stamped
+    with another hash is refused with the reason."""
+    m = _bench_module()
+    if not os.path.exists(m.F.LIB_PATH):
+        pytest.skip('engine library not built')
+    for name in ('pmc_traffic.json', 'pmc_sq.json', 'pmc_traffic_mehp24.json', 'pmc_sq_mehp24.json',
+                 'pmc_traffic_kway.json', 'pmc_sq_kway.json'):
+        t, src = m.load_table(name)
+        assert t is not None, src
+    (tmp_path / 'profiles').mkdir()
+    (tmp_path / 'profiles' / 'pmc_x.json').write_text(json.dumps({'_meta': {'lib_sha256': '0' * 64}, 'k_add': {}}))
+    monkeypatch.setattr(m, 'REPO', str(tmp_path))
+    t, src = m.load_table('pmc_x.json')
+    assert t is None and 'stale' in src
