@@ -344,24 +344,38 @@ def valu_fraction(sq, mix, keys, avg_s):
     return out
 
 
-STREAMING = ('k_tensor', 'k_add', 'k_sub', 'k_ks_inner', 'k_ks_inner_mc', 'k_ks_inner_mk', 'k_ks_inner_mk_sum',
-             'k_mul_plain_sum', 'k_linear_sum')
+def achievable_hbm_frac():
+    """The HBM rate an in-place read + write stream reaches with no arithmetic, as
+    a fraction of the 8 TB/s peak: the best 8-B-per-lane in-place pattern of
+    scripts/row_pattern.hip on one MI355X (profiles/r5_rates/row_pattern.jsonl;
+    the NTT passes and element-wise kernels read and write [segs][limbs][n] in
+    place).  0.786 (the guide's float4 copy, 6.29 TB/s) when absent."""
+    path = os.path.join(REPO, 'profiles', 'r5_rates', 'row_pattern.jsonl')
+    try:
+        rows = [json.loads(l) for l in open(path) if l.strip()]
+        return max(r['frac'] for r in rows if r['pattern'] in ('flat', 'seg16', 'row16', 'seg16x3', 'row16x3'))
+    except (OSError, ValueError, KeyError):
+        return 0.786
 
 
-def limiter_of(name, frac, vf):
-    """What bounds the kernel below the HBM roof: 'hbm' for the streaming kernels
-    (or any kernel at >= 0.85 of HBM peak); 'valu' at >= 0.85 of the measured
-    VALU throughput (whatever its waits); 'memory latency' when the SQ pass puts
-    >= 0.3 of its wave cycles in s_waitcnt, more than in issue stalls; else
-    'valu' (issue-bound at low occupancy)"""
-    if family(name) in STREAMING or frac >= 0.85:
+def limiter_of(name, frac, vf, waves=None, hbm_ach=None):
+    """What bounds the kernel: 'hbm' at >= 0.85 of the achievable in-place HBM
+    rate (achievable_hbm_frac(), whatever the kernel); 'valu' at >= 0.85 of the
+    measured VALU throughput (whatever its waits); 'memory latency' when the SQ
+    pass puts >= 0.3 of its wave cycles in s_waitcnt, at least its issue
+    stalls; else 'issue latency (W waves/SIMD)': dependent-instruction stalls at
+    the compiler's occupancy W (profiles/valu_mix.json), neither roof reached"""
+    ach = achievable_hbm_frac() if hbm_ach is None else hbm_ach
+    if frac >= 0.85 * ach:
         return 'hbm'
     if vf.get('valu_frac', 0) >= 0.85:
         return 'valu'
     split = vf.get('wave_cycle_split', {})
     if split.get('waitcnt', 0) >= max(0.3, split.get('issue_stall', 0)):
         return 'memory latency'
-    return 'valu'
+    if split.get('issue_stall', 0) > split.get('waitcnt', 0):
+        return f'issue latency ({waves} waves/SIMD)' if waves else 'issue latency'
+    return 'memory latency'
 
 
 def kernel_view(name, st, pmc, sq, mix, by_family):
@@ -374,9 +388,12 @@ def kernel_view(name, st, pmc, sq, mix, by_family):
     pk = table_keys(pmc, name, by_family)
     traffic = round(weighted(pmc, pk, 'hbm_bytes_per_launch')) if pk else None
     vf = valu_fraction(sq, mix, table_keys(sq, name, by_family), avg_s) if sq and mix else {}
+    mk = [k for k in table_keys(mix, name, by_family) if 'waves_per_simd' in mix[k]] if mix else []
+    waves = min(mix[k]['waves_per_simd'] for k in mk) if mk else None
     return {'kernel': name, 'achieved': round(achieved, 1), 'frac': round(frac, 4), 'traffic': traffic,
             'traffic_ratio': round(traffic / per_launch, 3) if traffic else None,
-            'limiter': limiter_of(name, frac, vf), **vf,
+            'limiter': limiter_of(name, frac, vf, waves), 'waves_per_simd': waves,
+            'frac_of_achievable': round(frac / achievable_hbm_frac(), 4), **vf,
             'avg_us': round(avg_s * 1e6, 2), 'launches': st['launches'], 'algorithmic_bytes_per_launch': per_launch}
 
 
@@ -448,6 +465,13 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
         return {n: {'share': round(v['ms'] / total_ms, 3), 'avg_us': round(v['ms'] / v['launches'] * 1e3, 1),
                     'launches': v['launches'], 'GBps': round(v['bytes'] / (v['ms'] * 1e-3) / 1e9, 1)} for n, v in top}
     run_bytes = sum(v['bytes'] for v in stats.values())
+    # the sort's VALU work (verdict r4 item 3): every kernel's SQ_INSTS_VALU per
+    # sort (committed SQ pass of this build, sort only) priced at its mix's
+    # measured rate -- the seconds of chip-wide VALU issue the sort needs
+    valu_s = None
+    if sq and mix:
+        valu_s = sum(v['launches'] * v.get('SQ_INSTS_VALU', 0) * 64 * mix[k]['ps_per_lane_instr'] * 1e-12
+                     for k, v in sq.items() if k in mix)
     phases = phase_table(phase_rows, total_ms)
     extra = {'phases': phases} if phases else {}
     return {**extra, **head, 'bound': 'hbm', 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -459,8 +483,10 @@ def roofline(ctx, run_once, dump=None, pmc_file='pmc_traffic.json', sq_file='pmc
             'kernels_by_caller': table(stats.items(), 24),
             # whole sort: every clocked kernel's algorithmic bytes,
             # over its summed kernel time here and over the timed wall in with_run()
+            'hbm_achievable_frac': achievable_hbm_frac(),
             'run': {'algorithmic_bytes_per_sort': run_bytes,
-                    'GBps_over_kernel_time': round(run_bytes / (total_ms * 1e-3) / 1e9, 1)}}
+                    'GBps_over_kernel_time': round(run_bytes / (total_ms * 1e-3) / 1e9, 1),
+                    'valu_s_per_sort': round(valu_s, 5) if valu_s is not None else None}}
 
 
 def with_run(roof, ms_per_step, world, op_bytes=None):
@@ -473,6 +499,8 @@ def with_run(roof, ms_per_step, world, op_bytes=None):
         gbps = roof['run']['algorithmic_bytes_per_sort'] / (ms_per_step * 1e-3) / 1e9
         roof['run']['GBps_over_wall'] = round(gbps, 1)
         roof['run']['frac_over_wall'] = round(gbps / (world * HBM_PEAK_GBS), 4)
+        if roof['run'].get('valu_s_per_sort') is not None:  # one rank's sort over one GPU's VALU
+            roof['run']['valu_frac_over_wall'] = round(roof['run']['valu_s_per_sort'] / (ms_per_step * 1e-3), 4)
     if roof is not None and op_bytes:
         gbps = op_bytes / (ms_per_step * 1e-3) / 1e9
         roof['run_op'] = {'op_bytes_per_sort': int(op_bytes), 'GBps_over_wall': round(gbps, 1),

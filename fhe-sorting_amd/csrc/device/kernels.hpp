@@ -24,7 +24,18 @@ struct NttTables {
     const u64 *ninv, *ninv_s;  // [nprimes]
     const Mod *mods;           // [nprimes]
     int logN;
+    // fp64 butterflies (primes q < 2^41, ntt_fp_prime): twiddles as doubles
+    // ([nprimes][n], entries of other primes unused) and {q, 1/q} per prime
+    const double *fwdd = nullptr, *invd = nullptr;
+    const double2 *qd = nullptr;
+    const uint8_t *fp_host = nullptr;  // HOST array [nprimes]: 1 = the prime takes the FP launches
 };
+// q < 2^41: the NTT passes of this prime run on fp64 butterflies (ntt.hip)
+bool ntt_fp_prime(u64 q);
+// host copy of a device prime map (engine tables), so a launch over mapped
+// limbs can be split by prime class; unknown maps launch on the integer path
+void ntt_register_map(const int *dev, const int *host, size_t count);
+void ntt_unregister_map(const int *dev);
 
 // Optional per-launch clock used by the bench roofline: while one is installed,
 // the NTT passes are bracketed by HIP events on the stream they launch on and
@@ -114,6 +125,10 @@ struct NttFuse {
     int scalar_sh = 0;
     bool raw = false;    // inverse: skip the n^-1 scaling of the last pass
     int lsegb = 0, segs = 0;  // shuffle row passes: log2 segments per block, segment count (set at launch)
+    // limb runs of a launch split by prime class (set at launch): grid limb z is
+    // limb zs0 + z for z < zn0, else zs1 + z - zn0
+    int zs0 = 0, zn0 = 1 << 30, zs1 = 0;
+    __host__ __device__ int limb_of(int z) const { return z < zn0 ? zs0 + z : zs1 + (z - zn0); }
 };
 // inverse NTT reading the input from `src` (segment z, limb l at src + z*seg_src + l*n), writing dst
 void ntt_inverse_from(u64 *dst, const u64 *src, size_t seg_src, int limbs, int segs, size_t seg, const int *pmap,

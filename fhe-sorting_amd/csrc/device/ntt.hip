@@ -20,6 +20,9 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "kernels.hpp"
 
@@ -102,6 +105,8 @@ __device__ __forceinline__ ulonglong2 scalar_tw(const ulonglong2 *p, size_t i) {
     const const_u64_t *q = (const const_u64_t *)p + 2 * i;
     return make_ulonglong2(q[0], q[1]);
 }
+typedef const __attribute__((address_space(4))) double const_f64_t;
+__device__ __forceinline__ double scalar_tw(const double *p, size_t i) { return ((const const_f64_t *)p)[i]; }
 // raw buffer resource over one limb (wave-uniform base; CDNA word 3)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t limb_rsrc(const u64 *base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<u64 *>(base), 0, 0x7ffffff0, 0x00020000);
@@ -222,6 +227,86 @@ __device__ __forceinline__ void gs_bfly(u64 &x, u64 &y, ulonglong2 w, u64 q4, u6
     x = s >= q4 ? s - q4 : s;
     y = shoup_fold4(u + q4 - v, w.x, w.y, nq);
 }
+// ---------------------------------------------------------------------------
+// fp64 butterflies for the primes below 2^41 (the 40-bit scaling primes), run
+// by separate "FP" launches over those limbs (launch_pass splits a launch by
+// prime class; DESIGN.md §5 "fp64 NTT for the 40-bit limbs").  A coefficient
+// is an exactly represented signed integer |v| < 2^52 held as a double; the
+// twiddle product y w mod q is
+//   b = fl(y w), e = y w - b (exact, one FMA), h = rint(fl(b / q)),
+//   r = (b - h q) + e            (the FMA b - h q is exact: |b - h q| < 2^53)
+// = y w - h q with |r| <= (1/2 + eps) q, eps = |y| 3 2^-53 (|y| <= 2^50 keeps
+// eps <= 3/8).  Six fp64 operations (v_fma_f64 / v_mul_f64 / v_rndne_f64 issue
+// at the half rate of v_mul_lo_u32, ~33 T lane-ops/s, against v_mad_u64_u32's
+// ~23 T; profiles/r5_rates) where the integer Shoup product takes 4
+// v_mad_u64_u32 + 2 v_mul_hi_u32 + 4 v_mul_lo_u32, and the butterfly sums are
+// plain fp64 adds with no conditional subtractions: forward values grow by
+// <= q/2 per stage, inverse sums double per stage (bounded per pass below).
+// Loads and stores convert with the 2^52 trick: for an integer 0 <= x < 2^52
+// the double with bits 0x433 << 52 | x is 2^52 + x.
+constexpr double FP_TWO52 = 4503599627370496.0;
+constexpr u64 FP_MAGIC = 0x4330000000000000ull;
+constexpr int FP_QBITS = 41;  // FP launches take primes q < 2^41
+__device__ __forceinline__ double dbits(u64 x) { return __longlong_as_double((long long)x); }
+__device__ __forceinline__ u64 ubits(double d) { return (u64)__double_as_longlong(d); }
+// u64 x < 2^52 -> the double x - off, with c = 2^52 + off (exact)
+__device__ __forceinline__ double fp_in(u64 x, double c) { return dbits(x | FP_MAGIC) - c; }
+// integer-valued v with 0 <= v + off < 2^52 -> the u64 v + off, with c = 2^52 + off
+__device__ __forceinline__ u64 fp_out(double v, double c) { return ubits(v + c) ^ FP_MAGIC; }
+__device__ __forceinline__ double fp_mulmod(double y, double w, double q, double qi) {
+    const double b = y * w;
+    const double e = __builtin_fma(y, w, -b);
+    const double h = __builtin_rint(b * qi);
+    return __builtin_fma(-h, q, b) + e;
+}
+// v - q rint(v / q): |result| <= (1/2 + |v| 3 2^-53) q
+__device__ __forceinline__ double fp_reduce(double v, double q, double qi) {
+    return __builtin_fma(-__builtin_rint(v * qi), q, v);
+}
+// per-launch arithmetic constants of one prime: integer (Shoup butterflies)
+// and fp64 (q and its rounded reciprocal)
+struct Ar {
+    u64 q4, nq;
+    double q, qi;
+};
+template <bool FP>
+using TwT = typename std::conditional<FP, double, ulonglong2>::type;
+__device__ __forceinline__ void ct_bfly_fp(u64 &x, u64 &y, double w, const Ar &A) {
+    const double u = dbits(x), v = fp_mulmod(dbits(y), w, A.q, A.qi);
+    x = ubits(u + v);
+    y = ubits(u - v);
+}
+__device__ __forceinline__ void gs_bfly_fp(u64 &x, u64 &y, double w, const Ar &A) {
+    const double u = dbits(x), v = dbits(y);
+    x = ubits(u + v);
+    y = ubits(fp_mulmod(u - v, w, A.q, A.qi));
+}
+template <bool FP, int PB>
+__device__ __forceinline__ void ct_any(bool cols, int s, u64 &x, u64 &y, TwT<FP> w, const Ar &A) {
+    if constexpr (FP) ct_bfly_fp(x, y, w, A);
+    else if (fwd_reduce(cols, PB, s)) ct_bfly<true>(x, y, w, A.q4, A.nq);
+    else ct_bfly<false>(x, y, w, A.q4, A.nq);
+}
+template <bool FP>
+__device__ __forceinline__ void gs_any(u64 &x, u64 &y, TwT<FP> w, const Ar &A) {
+    if constexpr (FP) gs_bfly_fp(x, y, w, A);
+    else gs_bfly(x, y, w, A.q4, A.nq);
+}
+// Bounds of the FP passes (q < 2^41, so 2^50 = 512 q):
+//   forward column: inputs < 8q loaded as x - 4q (|x| <= 4q); 9 stages add
+//     <= 0.51 q each -> |x| < 8.6 q, stored + 9q (< 18 q);
+//   forward row: loaded - 9q (|x| < 8.6 q), 8 stages -> < 12.7 q, then reduced
+//     (fp_reduce) for the canonical store or the integer epilogues;
+//   inverse row: inputs < 4q loaded - 2q (|x| <= 2q); a GS sum at most doubles
+//     per stage -> |x| <= 2^8 2q = 512 q, twiddle inputs |u - v| <= 512 q;
+//     reduced (|r| <= 0.88 q) and stored + q (< 2q, the integer pass's range);
+//   inverse column: loaded - q (|x| <= 0.88 q), 9 stages -> <= 2^9 0.88 q < 2^50,
+//     then times n^-1 (fp_mulmod, canonicalised) or reduced to [0, 2q) (raw).
+// Every intermediate is an integer below 2^52 and every twiddle input below
+// 2^50, so each operation above is exact (tests/test_fp_mulmod.py checks the
+// product and reduction at these bounds against exact integer arithmetic).
+constexpr double FP_FWD_COL_IN = 4.0, FP_FWD_COL_OUT = 9.0, FP_INV_ROW_IN = 2.0, FP_INV_ROW_OUT = 1.0;
+
 __device__ __forceinline__ u64 smod64(int64_t v, const Mod &m) {  // signed integer -> [0, q)
     if (v >= 0) return reduce64((u64)v, m);
     const u64 r = reduce64((u64)0 - (u64)v, m);
@@ -361,8 +446,8 @@ __device__ constexpr int twl_off(int S) {
 // every transform of the block is the same row (16 segments per block), so
 // the row's twiddles are read from HBM / L2 once per block and from LDS per
 // butterfly instead of from the vector cache.
-template <bool FWD>
-__device__ __forceinline__ void row_twiddles(ulonglong2 *twl, const ulonglong2 *tw, size_t row, size_t n, int S0) {
+template <bool FWD, class TW>
+__device__ __forceinline__ void row_twiddles(TW *twl, const TW *tw, size_t row, size_t n, int S0) {
     const int e = threadIdx.x;
     if (e >= 255) return;
     int S = 0;
@@ -370,9 +455,9 @@ __device__ __forceinline__ void row_twiddles(ulonglong2 *twl, const ulonglong2 *
     const int j = e - twl_off<FWD>(S);
     twl[e] = FWD ? tw[((size_t)1 << (S0 + S)) + (row << S) + j] : tw[(n >> (S + 1)) + (row << (7 - S)) + j];
 }
-template <bool FWD, int S, bool TWL>
-__device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulonglong2 *tw, size_t n, int S0,
-                                          u64 q4, u64 nq) {
+template <bool FWD, int S, bool TWL, bool FP>
+__device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const TwT<FP> *tw, size_t n, int S0,
+                                          const Ar &A) {
     constexpr RowSwap w = FWD ? fwd_swap(S) : inv_swap(S);
     if (w.m >= 0) swap_regs<w.p>(x, t, w.m);
     if (S >= 8) return;  // the forward pass's final fix-up swap
@@ -384,29 +469,29 @@ __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const ulong
     // lane and register bits are disjoint, so the shift splits into a per-lane
     // offset and a compile-time one -> one address per stage, immediate offsets
     constexpr int SH = FWD ? 8 - S : S + 1;
-    const ulonglong2 *tws = TWL ? tw + twl_off<FWD>(S) + (li >> SH)  // tw: the row's LDS table
-                            : FWD ? tw + ((size_t)1 << (S0 + S)) + (row << S) + (uint32_t)(li >> SH)
-                                  : tw + (n >> (S + 1)) + (row << (7 - S)) + (uint32_t)(li >> SH);
+    const TwT<FP> *tws = TWL ? tw + twl_off<FWD>(S) + (li >> SH)  // tw: the row's LDS table
+                         : FWD ? tw + ((size_t)1 << (S0 + S)) + (row << S) + (uint32_t)(li >> SH)
+                               : tw + (n >> (S + 1)) + (row << (7 - S)) + (uint32_t)(li >> SH);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         if (j & (1 << P)) continue;
-        const ulonglong2 w = tws[reg_index(L, j) >> SH];
-        if (FWD) ct_stage<8>(false, S, x[j], x[j + (1 << P)], w, q4, nq);
-        else gs_bfly(x[j], x[j + (1 << P)], w, q4, nq);
+        const TwT<FP> w = tws[reg_index(L, j) >> SH];
+        if (FWD) ct_any<FP, 8>(false, S, x[j], x[j + (1 << P)], w, A);
+        else gs_any<FP>(x[j], x[j + (1 << P)], w, A);
     }
 }
-template <bool FWD, bool TWL>
-__device__ __forceinline__ void row_pass_shfl(u64 *x, int t, size_t row, const ulonglong2 *tw, size_t n, int S0,
-                                              u64 q4, u64 nq) {
-    row_stage<FWD, 0, TWL>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 1, TWL>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 2, TWL>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 3, TWL>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 4, TWL>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 5, TWL>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 6, TWL>(x, t, row, tw, n, S0, q4, nq);
-    row_stage<FWD, 7, TWL>(x, t, row, tw, n, S0, q4, nq);
-    if (FWD) row_stage<FWD, 8, TWL>(x, t, row, tw, n, S0, q4, nq);
+template <bool FWD, bool TWL, bool FP>
+__device__ __forceinline__ void row_pass_shfl(u64 *x, int t, size_t row, const TwT<FP> *tw, size_t n, int S0,
+                                              const Ar &A) {
+    row_stage<FWD, 0, TWL, FP>(x, t, row, tw, n, S0, A);
+    row_stage<FWD, 1, TWL, FP>(x, t, row, tw, n, S0, A);
+    row_stage<FWD, 2, TWL, FP>(x, t, row, tw, n, S0, A);
+    row_stage<FWD, 3, TWL, FP>(x, t, row, tw, n, S0, A);
+    row_stage<FWD, 4, TWL, FP>(x, t, row, tw, n, S0, A);
+    row_stage<FWD, 5, TWL, FP>(x, t, row, tw, n, S0, A);
+    row_stage<FWD, 6, TWL, FP>(x, t, row, tw, n, S0, A);
+    row_stage<FWD, 7, TWL, FP>(x, t, row, tw, n, S0, A);
+    if (FWD) row_stage<FWD, 8, TWL, FP>(x, t, row, tw, n, S0, A);
 }
 // in-row index of lane t's register r after a pass (both passes end in this layout)
 template <bool FWD>
@@ -447,7 +532,7 @@ enum { NTT_PLAIN = 0, NTT_LIFT = 1, NTT_RESCALE = 2, NTT_MULTAIL = 3, NTT_KSFINI
 // ROWS: the transform index is a row `hi`, element idx sits at hi * 2^PB + idx.
 // SH (row passes with PB = 8 only): register-only stages with DPP lane swaps
 // (row_pass_shfl) instead of the two LDS exchanges.
-template <int PB, int EB, bool COLS, int MODE, bool SH, bool FULL, bool TWL = false>
+template <int PB, int EB, bool COLS, int MODE, bool SH, bool FULL, bool TWL = false, bool FP = false>
 __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
                                              const NttTables &Tb, const NttFuse &F) {
     static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
@@ -463,14 +548,15 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     __shared__ u64 tile[SH ? 1 : X32 ? (lds_words<TPB, NB, COLS>() + 1) / 2 : lds_words<TPB, NB, COLS>()];
     uint32_t *const t32 = reinterpret_cast<uint32_t *>(tile);
     constexpr bool CTW = FHE_NTT_COL_TWL && COLS && !SPLIT && PB == 8 && nthreads<PB, COLS>() == 256;
-    __shared__ ulonglong2 twc[CTW ? 256 : 1];
+    using TW = TwT<FP>;
+    __shared__ TW twc[CTW ? 256 : 1];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
     // grid: x = segment (fastest, so the blocks of one prime's row/column
     // block across all segments run back to back and share its twiddles in
-    // L2), y = block within the limb, z = limb
-    const int limb = blockIdx.z;
+    // L2), y = block within the limb, z = limb (through the launch's limb runs)
+    const int limb = F.limb_of(blockIdx.z);
     const int p = pmap ? __builtin_amdgcn_readfirstlane(pmap[limb]) : limb;
     int t, tr;  // lane within its transform, transform within the block
     if (COLS) {
@@ -490,7 +576,18 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     const bool valid = FULL || (tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs));
     u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)__builtin_amdgcn_readfirstlane(smap[limb]) : (size_t)limb) * n;
     const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
-    const ulonglong2 *tw = Tb.fwd2 + (size_t)p * n;
+    const TW *tw;
+    if constexpr (FP) tw = Tb.fwdd + (size_t)p * n;
+    else tw = Tb.fwd2 + (size_t)p * n;
+    Ar A{q4, nq, 0.0, 0.0};
+    if constexpr (FP) {
+        const double2 qd = Tb.qd[p];
+        A.q = qd.x;
+        A.qi = qd.y;
+    }
+    // FP: the load offset (column: inputs < 8q centred by 4q; row: the column
+    // pass's store offset)
+    const double fin = FP ? FP_TWO52 + (COLS ? FP_FWD_COL_IN : FP_FWD_COL_OUT) * A.q : 0.0;
     constexpr bool CBUF = FHE_NTT_COL_BUF && COLS && FULL;  // (FULL: no bounds check; COLS: zseg is blockIdx.x)
     const int S0 = COLS ? 0 : logN - PB;                      // global stage of local stage 0
     if (CTW) twc[threadIdx.x] = tw[threadIdx.x];  // read after the exchange's barrier (round 2)
@@ -527,6 +624,10 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
             x[r] = valid ? a[off] : 0;
         }
     }
+    if constexpr (FP) {
+#pragma unroll
+        for (int r = 0; r < E; ++r) x[r] = ubits(fp_in(x[r], fin));
+    }
     // fused row-pass epilogues: their operands (the rescale input / the HMult
     // accumulators and d) are loaded now, so the loads overlap the butterflies
     // instead of stalling the store loop (the tile's LDS bounds occupancy, the
@@ -556,6 +657,16 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // row-pass store of transform value v (lazy, [0, 12q)) for element r at in-row index idx
     auto store_row = [&](int r, int idx, u64 v) {
         const size_t z = (size_t)zseg, lo = (size_t)limb * n + tid_global * LEN;
+        if constexpr (FP) {
+            // |v| < 12.7 q -> centred residue |r| < 0.51 q; the epilogues take r + q
+            // (< 12q as they require), the plain store the canonical residue
+            const double rr = fp_reduce(dbits(v), A.q, A.qi);
+            if (MODE == NTT_PLAIN) {
+                a[tid_global * LEN + idx] = fp_out(rr < 0.0 ? rr + A.q : rr, FP_TWO52);
+                return;
+            }
+            v = fp_out(rr, FP_TWO52 + A.q);
+        }
         // lazy epilogues: v in [0, 12q), every intermediate < 2^64 (q < 2^60), one
         // final conditional subtraction (the exact Shoup products are in [0, 2q))
         if (MODE == NTT_RESCALE) {
@@ -585,12 +696,12 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     };
     if constexpr (SH) {
         if constexpr (TWL) {  // every transform of the block is row blockIdx.y
-            __shared__ ulonglong2 twl[256];
+            __shared__ TW twl[256];
             row_twiddles<true>(twl, tw, tid_global, n, S0);
             __syncthreads();
-            row_pass_shfl<true, true>(x, t, tid_global, twl, n, S0, q4, nq);
+            row_pass_shfl<true, true, FP>(x, t, tid_global, twl, n, S0, A);
         } else {
-            row_pass_shfl<true, false>(x, t, tid_global, tw, n, S0, q4, nq);
+            row_pass_shfl<true, false, FP>(x, t, tid_global, tw, n, S0, A);
         }
         if (!valid) return;
 #pragma unroll
@@ -610,8 +721,8 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
             // scalar load (constant address space) instead of 4 VGPRs
             const size_t i = COLS ? ((size_t)r0 >> (EB - s)) : (tid_global << s) + (size_t)(idx0 >> (PB - s));
             const size_t wi = ((size_t)1 << (S0 + s)) + i;
-            ct_stage<PB>(COLS, s, x[r0], x[r0 + (1 << hb)], (COLS && FHE_NTT_COL_SCALAR) ? scalar_tw(tw, wi) : tw[wi], q4,
-                         nq);
+            ct_any<FP, PB>(COLS, s, x[r0], x[r0 + (1 << hb)], (COLS && FHE_NTT_COL_SCALAR) ? scalar_tw(tw, wi) : tw[wi],
+                           A);
         }
     }
     // round-2 twiddles (G == 1: stage s needs 2^(s-EB) of them per lane, index
@@ -620,7 +731,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // (row passes only: in the column pass the extra VGPRs cost a wave of occupancy)
     constexpr bool PRE = G == 1 && !COLS;
     constexpr int NT2 = (1 << RB) - 1;
-    ulonglong2 tw2[PRE ? NT2 : 1];
+    TW tw2[PRE ? NT2 : 1];
     if (PRE) {
 #pragma unroll
         for (int s = EB, o = 0; s < PB; ++s)
@@ -666,10 +777,8 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
                 const int idx0 = (t * G + g) * T + r0;
                 const size_t i = (COLS ? 0 : (tid_global << s)) + (size_t)(idx0 >> (PB - s));
                 const size_t wi = ((size_t)1 << (S0 + s)) + i;
-                const ulonglong2 w =
-                    PRE ? tw2[PRE ? ((1 << (s - EB)) - 1) + (r0 >> (PB - s)) : 0] : CTW ? twc[wi] : tw[wi];
-                ct_stage<PB>(COLS, s, x[l2reg<G, T, SPLIT>(g, r0)], x[l2reg<G, T, SPLIT>(g, r0 + (1 << hb))], w, q4,
-                             nq);
+                const TW w = PRE ? tw2[PRE ? ((1 << (s - EB)) - 1) + (r0 >> (PB - s)) : 0] : CTW ? twc[wi] : tw[wi];
+                ct_any<FP, PB>(COLS, s, x[l2reg<G, T, SPLIT>(g, r0)], x[l2reg<G, T, SPLIT>(g, r0 + (1 << hb))], w, A);
             }
     }
     // ---- store.  COLS: layout L2 is already lane-contiguous in memory
@@ -677,6 +786,11 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // consecutive coefficients, so the values go back through LDS to layout
     // L1 and every store instruction writes contiguous 128-B runs.  Each lane
     // rewrites only the tile words it read itself, so one barrier suffices.
+    if constexpr (FP && COLS) {  // the row pass loads them back with the same offset
+        const double fo = FP_TWO52 + FP_FWD_COL_OUT * A.q;
+#pragma unroll
+        for (int r = 0; r < E; ++r) x[r] = fp_out(dbits(x[r]), fo);
+    }
     if constexpr (CBUF) {
         const auto rs = limb_rsrc(a);
         const int vo = (int)((((size_t)t * G * T << k2) + tid_global) * 8);
@@ -722,7 +836,7 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
 // COLS covers sg in [logN - PB, logN) and multiplies by n^-1 on the way out.
 // F.src (optional): read the input from there instead (out-of-place first
 // pass; segment z, limb l at F.src + z * F.seg_src + l * n)
-template <int PB, int EB, bool COLS, bool SH, bool FULL, bool TWL = false>
+template <int PB, int EB, bool COLS, bool SH, bool FULL, bool TWL = false, bool FP = false>
 __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *pmap, const int *smap, int logN,
                                              const NttTables &Tb, const NttFuse &F) {
     static_assert(!SH || (!COLS && PB == 8 && EB == 4), "shuffle row pass: 16 lanes x 16 coefficients");
@@ -738,14 +852,15 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     __shared__ u64 tile[SH ? 1 : X32 ? (lds_words<TPB, NB, COLS>() + 1) / 2 : lds_words<TPB, NB, COLS>()];
     uint32_t *const t32 = reinterpret_cast<uint32_t *>(tile);
     constexpr bool CTW = FHE_NTT_COL_TWL && COLS && !SPLIT && PB == 8 && nthreads<PB, COLS>() == 256;
-    __shared__ ulonglong2 twc[CTW ? 256 : 1];
+    using TW = TwT<FP>;
+    __shared__ TW twc[CTW ? 256 : 1];
 
     const size_t n = (size_t)1 << logN;
     const int k2 = COLS ? logN - PB : 0;
     // grid: x = segment (fastest, so the blocks of one prime's row/column
     // block across all segments run back to back and share its twiddles in
-    // L2), y = block within the limb, z = limb
-    const int limb = blockIdx.z;
+    // L2), y = block within the limb, z = limb (through the launch's limb runs)
+    const int limb = F.limb_of(blockIdx.z);
     const int p = pmap ? __builtin_amdgcn_readfirstlane(pmap[limb]) : limb;
     int t, tr;
     if (COLS) {
@@ -761,7 +876,16 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     const bool valid = FULL || (tid_global < ((size_t)1 << (logN - PB)) && (!SH || zseg < F.segs));
     u64 *a = data + (size_t)zseg * seg + (smap ? (size_t)__builtin_amdgcn_readfirstlane(smap[limb]) : (size_t)limb) * n;
     const u64 q = Tb.mods[p].q, q2 = 2 * q, q4 = 4 * q, nq = (u64)0 - q;
-    const ulonglong2 *tw = Tb.inv2 + (size_t)p * n;
+    const TW *tw;
+    if constexpr (FP) tw = Tb.invd + (size_t)p * n;
+    else tw = Tb.inv2 + (size_t)p * n;
+    Ar A{q4, nq, 0.0, 0.0};
+    if constexpr (FP) {
+        const double2 qd = Tb.qd[p];
+        A.q = qd.x;
+        A.qi = qd.y;
+    }
+    const double fin = FP ? FP_TWO52 + (COLS ? FP_INV_ROW_OUT : FP_INV_ROW_IN) * A.q : 0.0;  // FP load offset
     constexpr bool CBUF = FHE_NTT_COL_BUF && COLS && FULL;
     const int SG0 = COLS ? logN - PB : 0;  // global GS stage of local stage 0
     if (CTW) twc[threadIdx.x] = tw[threadIdx.x];  // round A reads it after the barrier below
@@ -773,20 +897,22 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
         for (int m = 0; m < E / 2; ++m) {
             const ulonglong2 v = valid ? *reinterpret_cast<const ulonglong2 *>(ain + tid_global * LEN + 2 * t + 32 * m)
                                        : make_ulonglong2(0, 0);
-            x[2 * m] = v.x;
-            x[2 * m + 1] = v.y;
+            x[2 * m] = FP ? ubits(fp_in(v.x, fin)) : v.x;
+            x[2 * m + 1] = FP ? ubits(fp_in(v.y, fin)) : v.y;
         }
         if constexpr (TWL) {  // every transform of the block is row blockIdx.y
-            __shared__ ulonglong2 twl[256];
+            __shared__ TW twl[256];
             row_twiddles<false>(twl, tw, tid_global, n, 0);
             __syncthreads();
-            row_pass_shfl<false, true>(x, t, tid_global, twl, n, 0, q4, nq);
+            row_pass_shfl<false, true, FP>(x, t, tid_global, twl, n, 0, A);
         } else {
-            row_pass_shfl<false, false>(x, t, tid_global, tw, n, 0, q4, nq);
+            row_pass_shfl<false, false, FP>(x, t, tid_global, tw, n, 0, A);
         }
         if (!valid) return;
+        const double fo = FP_TWO52 + FP_INV_ROW_OUT * A.q;
 #pragma unroll
-        for (int r = 0; r < E; ++r) a[tid_global * LEN + row_final_index<false>(t, r)] = x[r];
+        for (int r = 0; r < E; ++r)
+            a[tid_global * LEN + row_final_index<false>(t, r)] = FP ? fp_out(fp_reduce(dbits(x[r]), A.q, A.qi), fo) : x[r];
         return;
     }
     // ---- load, layout L2 (low bits within a lane group).  The ROWS pass's
@@ -820,6 +946,10 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
                 x[g * T + r + 1] = v.y;
             }
     }
+    if constexpr (FP) {
+#pragma unroll
+        for (int r = 0; r < E; ++r) x[r] = ubits(fp_in(x[r], fin));
+    }
     // ---- round A: local stages 0..RB-1 (pair bit s)
     if (CTW) __syncthreads();  // the staged twiddle table (the data loads are in flight)
 #pragma unroll
@@ -829,14 +959,14 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
         // compile-time c >> (s + 1) (COLS: the column bits of idx0 << k2 vanish)
         const int sg = SG0 + s;
         const size_t lane_base = ((COLS ? 0 : tid_global * LEN) + (size_t)t * E) >> (s + 1);
-        const ulonglong2 *tws = (CTW ? twc : tw) + (n >> (sg + 1)) + lane_base;
+        const TW *tws = (CTW ? twc : tw) + (n >> (sg + 1)) + lane_base;
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
             for (int r0 = 0; r0 < T; ++r0) {
                 if (r0 & (1 << s)) continue;
-                gs_bfly(x[l2reg<G, T, SPLIT>(g, r0)], x[l2reg<G, T, SPLIT>(g, r0 + (1 << s))],
-                        tws[(g * T + r0) >> (s + 1)], q4, nq);
+                gs_any<FP>(x[l2reg<G, T, SPLIT>(g, r0)], x[l2reg<G, T, SPLIT>(g, r0 + (1 << s))],
+                           tws[(g * T + r0) >> (s + 1)], A);
             }
     }
     // ---- exchange L2 -> L1 (idx = t + T * r)
@@ -878,7 +1008,7 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
             const size_t i = COLS ? ((size_t)T * r0) >> (s + 1)
                                   : (j + (size_t)idx0) >> (sg + 1);
             const size_t wi = (n >> (sg + 1)) + i;
-            gs_bfly(x[r0], x[r0 + (1 << hb)], (COLS && FHE_NTT_COL_SCALAR) ? scalar_tw(tw, wi) : tw[wi], q4, nq);
+            gs_any<FP>(x[r0], x[r0 + (1 << hb)], (COLS && FHE_NTT_COL_SCALAR) ? scalar_tw(tw, wi) : tw[wi], A);
         }
     }
     // ---- store, layout L1 (COLS: times n^-1, or raw: reduced to [0, 2q) for
@@ -887,11 +1017,25 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
     const bool scale = COLS && !F.raw;
     const auto rso = limb_rsrc(a);
     const int vso = (int)((((size_t)t << k2) + tid_global) * 8);
+    const double nid = FP ? fp_in(ni, FP_TWO52) : 0.0;
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const int idx = t + T * r;
         const size_t off = COLS ? (size_t)idx * ((size_t)1 << k2) + tid_global : tid_global * LEN + idx;
-        const u64 v = scale ? mul_shoup(x[r], ni, nis, q) : COLS ? (x[r] >= q2 ? x[r] - q2 : x[r]) : x[r];
+        u64 v;
+        if constexpr (FP) {
+            // column: times n^-1 (|r| <= 0.7 q, canonicalised) or reduced and + q
+            // ([0, 2q), the raw range); row (LDS passes): reduced + q, as the DPP rows
+            const double xr = dbits(x[r]);
+            if (scale) {
+                const double m = fp_mulmod(xr, nid, A.q, A.qi);
+                v = fp_out(m < 0.0 ? m + A.q : m, FP_TWO52);
+            } else {
+                v = fp_out(fp_reduce(xr, A.q, A.qi), FP_TWO52 + FP_INV_ROW_OUT * A.q);
+            }
+        } else {
+            v = scale ? mul_shoup(x[r], ni, nis, q) : COLS ? (x[r] >= q2 ? x[r] - q2 : x[r]) : x[r];
+        }
         if constexpr (CBUF)
             bstore64(rso, vso, (T * r << k2) * 8, v);
         else if (valid)
@@ -908,15 +1052,16 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
 #ifndef FHE_NTT_COL_WPE
 #define FHE_NTT_COL_WPE 1
 #endif
-template <int PB, int EB, bool COLS, int MODE, bool FULL>
+// FP: the fp64 butterflies (every limb of the launch has a prime < 2^FP_QBITS)
+template <int PB, int EB, bool COLS, int MODE, bool FULL, bool FP>
 __global__ __launch_bounds__((nthreads<PB, COLS>())) __attribute__((amdgpu_waves_per_eu(COLS ? FHE_NTT_COL_WPE : 1, 8))) void k_ntt_fwd(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_fwd_body<PB, EB, COLS, MODE, false, FULL>(data, seg, pmap, smap, logN, Tb, F);
+    ntt_fwd_body<PB, EB, COLS, MODE, false, FULL, false, FP>(data, seg, pmap, smap, logN, Tb, F);
 }
-template <int PB, int EB, bool COLS, bool FULL>
+template <int PB, int EB, bool COLS, bool FULL, bool FP>
 __global__ __launch_bounds__((nthreads<PB, COLS>())) __attribute__((amdgpu_waves_per_eu(COLS ? FHE_NTT_COL_WPE : 1, 8))) void k_ntt_inv(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_inv_body<PB, EB, COLS, false, FULL>(data, seg, pmap, smap, logN, Tb, F);
+    ntt_inv_body<PB, EB, COLS, false, FULL, false, FP>(data, seg, pmap, smap, logN, Tb, F);
 }
 // register-only row passes (PB = 8)
 // minimum waves per SIMD for the register-only row passes with LDS twiddles
@@ -924,15 +1069,19 @@ __global__ __launch_bounds__((nthreads<PB, COLS>())) __attribute__((amdgpu_waves
 #ifndef FHE_NTT_ROW_WPE
 #define FHE_NTT_ROW_WPE 1
 #endif
-template <int MODE, bool FULL, bool TWL>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(TWL ? FHE_NTT_ROW_WPE : 1, 8))) void k_ntt_fwd_row(
+// minimum waves per SIMD of the FP forward rows (A/B: -DFHE_NTT_FP_ROW_WPE=n)
+#ifndef FHE_NTT_FP_ROW_WPE
+#define FHE_NTT_FP_ROW_WPE 1
+#endif
+template <int MODE, bool FULL, bool TWL, bool FP>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FP ? FHE_NTT_FP_ROW_WPE : TWL ? FHE_NTT_ROW_WPE : 1, 8))) void k_ntt_fwd_row(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_fwd_body<8, 4, false, MODE, true, FULL, TWL>(data, seg, pmap, smap, logN, Tb, F);
+    ntt_fwd_body<8, 4, false, MODE, true, FULL, TWL, FP>(data, seg, pmap, smap, logN, Tb, F);
 }
-template <bool FULL, bool TWL>
+template <bool FULL, bool TWL, bool FP>
 __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(TWL ? FHE_NTT_ROW_WPE : 1, 8))) void k_ntt_inv_row(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
-    ntt_inv_body<8, 4, false, true, FULL, TWL>(data, seg, pmap, smap, logN, Tb, F);
+    ntt_inv_body<8, 4, false, true, FULL, TWL, FP>(data, seg, pmap, smap, logN, Tb, F);
 }
 // FHE_NTT_TWL (A/B, default 1): the register-only row passes stage a row's
 // twiddles in LDS when the block is one row of 16 segments
@@ -961,9 +1110,9 @@ constexpr int full_bit() {
                : (COLS ? 32 : 64);
 }
 
-template <int PB, int EB, bool COLS, bool FWD, int MODE>
-void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap, const NttTables &T,
-                 const NttFuse &F, hipStream_t st) {
+template <int PB, int EB, bool COLS, bool FWD, int MODE, bool FP>
+void launch_pass_one(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap, const NttTables &T,
+                     const NttFuse &F, hipStream_t st) {
     constexpr int NTHR = nthreads<PB, COLS>();
     constexpr int NB = NTHR >> (PB - EB);
     constexpr bool CAN_SH = !COLS && PB == 8 && EB == 4;
@@ -995,29 +1144,30 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
     hipExtLaunchKernelGGL((K), grid, dim3(NTHR), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
     const bool twl = sh && Fs.lsegb == 4 && row_twl_enabled() != 0;
     if (FWD && sh) {
-        if (full && twl) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, true>), Fs);
-        else if (full) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, false>), Fs);
-        else if (twl) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false, true>), Fs);
-        else FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false, false>), Fs);
+        if (full && twl) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, true, FP>), Fs);
+        else if (full) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, false, FP>), Fs);
+        else if (twl) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false, true, FP>), Fs);
+        else FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, false, false, FP>), Fs);
     } else if (FWD) {
-        if (full) FHE_NTT_LAUNCH((k_ntt_fwd<PB, EB, COLS, MODE, true>), F);
-        else FHE_NTT_LAUNCH((k_ntt_fwd<PB, EB, COLS, MODE, false>), F);
+        if (full) FHE_NTT_LAUNCH((k_ntt_fwd<PB, EB, COLS, MODE, true, FP>), F);
+        else FHE_NTT_LAUNCH((k_ntt_fwd<PB, EB, COLS, MODE, false, FP>), F);
     } else if (sh) {
-        if (full && twl) FHE_NTT_LAUNCH((k_ntt_inv_row<true, true>), Fs);
-        else if (full) FHE_NTT_LAUNCH((k_ntt_inv_row<true, false>), Fs);
-        else if (twl) FHE_NTT_LAUNCH((k_ntt_inv_row<false, true>), Fs);
-        else FHE_NTT_LAUNCH((k_ntt_inv_row<false, false>), Fs);
+        if (full && twl) FHE_NTT_LAUNCH((k_ntt_inv_row<true, true, FP>), Fs);
+        else if (full) FHE_NTT_LAUNCH((k_ntt_inv_row<true, false, FP>), Fs);
+        else if (twl) FHE_NTT_LAUNCH((k_ntt_inv_row<false, true, FP>), Fs);
+        else FHE_NTT_LAUNCH((k_ntt_inv_row<false, false, FP>), Fs);
     } else {
-        if (full) FHE_NTT_LAUNCH((k_ntt_inv<PB, EB, COLS, true>), F);
-        else FHE_NTT_LAUNCH((k_ntt_inv<PB, EB, COLS, false>), F);
+        if (full) FHE_NTT_LAUNCH((k_ntt_inv<PB, EB, COLS, true, FP>), F);
+        else FHE_NTT_LAUNCH((k_ntt_inv<PB, EB, COLS, false, FP>), F);
     }
 #undef FHE_NTT_LAUNCH
     if (clk) {
         // same spelling as the demangled symbol rocprofv3 prints, plus the caller tag
         // (the instantiation the branches above launched)
+        const std::string fps = FP ? "true>" : "false>";
         const std::string pe = std::to_string(PB) + ", " + std::to_string(EB) + (COLS ? ", true" : ", false");
-        const std::string fl = full ? "true>" : "false>";
-        const std::string fl2 = (full ? "true, " : "false, ") + std::string(twl ? "true>" : "false>");
+        const std::string fl = (full ? "true, " : "false, ") + fps;
+        const std::string fl2 = (full ? "true, " : "false, ") + std::string(twl ? "true, " : "false, ") + fps;
         const std::string base = FWD && sh ? "k_ntt_fwd_row<" + std::to_string(MODE) + ", " + fl2
                                  : FWD     ? "k_ntt_fwd<" + pe + ", " + std::to_string(MODE) + ", " + fl
                                  : sh      ? "k_ntt_inv_row<" + fl2
@@ -1032,6 +1182,71 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
         // one read + one write of every limb touched (fused epilogues: + the extra operands)
         const double extra = MODE == NTT_RESCALE ? 1.0 : MODE == NTT_MULTAIL ? 2.0 : MODE == NTT_KSFINISH ? 1.5 : 0.0;
         clk->record(slot, it->second.c_str(), (2.0 + extra) * 8.0 * (double)limbs * segs * ((size_t)1 << T.logN));
+    }
+}
+
+// FHE_NTT_FP (A/B, default 1): limbs whose prime is < 2^FP_QBITS run the fp64
+// butterflies in launches of their own
+int &ntt_fp_enabled() {
+    static int v = [] {
+        const char *e = std::getenv("FHE_NTT_FP");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+// host copies of the device prime maps (ntt_register_map), by device address
+struct MapRegistry {
+    std::mutex mu;
+    std::map<const int *, std::vector<int>> maps;
+};
+MapRegistry &map_registry() {
+    static MapRegistry r;
+    return r;
+}
+// the prime of each limb of a launch, if its map is known on the host
+bool launch_primes(const int *pmap, int limbs, std::vector<int> &out) {
+    out.resize(limbs);
+    if (!pmap) {
+        for (int z = 0; z < limbs; ++z) out[z] = z;
+        return true;
+    }
+    MapRegistry &R = map_registry();
+    std::lock_guard<std::mutex> lk(R.mu);
+    auto it = R.maps.upper_bound(pmap);
+    if (it == R.maps.begin()) return false;
+    --it;
+    const size_t off = (size_t)(pmap - it->first);
+    if (off + (size_t)limbs > it->second.size()) return false;
+    for (int z = 0; z < limbs; ++z) out[z] = it->second[off + z];
+    return true;
+}
+// One launch per class (integer / FP), each over the class's limbs as at most
+// two contiguous runs (NttFuse::limb_of); more runs take more launches.  A
+// launch whose limb map is unknown on the host stays one integer launch.
+template <int PB, int EB, bool COLS, bool FWD, int MODE>
+void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, const int *smap, const NttTables &T,
+                 const NttFuse &F, hipStream_t st) {
+    std::vector<int> pr;
+    if (!ntt_fp_enabled() || !T.fp_host || !launch_primes(pmap, limbs, pr)) {
+        launch_pass_one<PB, EB, COLS, FWD, MODE, false>(data, limbs, segs, seg, pmap, smap, T, F, st);
+        return;
+    }
+    for (int cls = 0; cls < 2; ++cls) {
+        std::vector<std::pair<int, int>> runs;  // (start, length)
+        for (int z = 0; z < limbs; ++z) {
+            if ((T.fp_host[pr[z]] != 0) != (cls == 1)) continue;
+            if (!runs.empty() && runs.back().first + runs.back().second == z) ++runs.back().second;
+            else runs.emplace_back(z, 1);
+        }
+        for (size_t r = 0; r < runs.size(); r += 2) {
+            NttFuse G = F;
+            G.zs0 = runs[r].first;
+            G.zn0 = runs[r].second;
+            G.zs1 = r + 1 < runs.size() ? runs[r + 1].first : 0;
+            const int cnt = runs[r].second + (r + 1 < runs.size() ? runs[r + 1].second : 0);
+            if (cls) launch_pass_one<PB, EB, COLS, FWD, MODE, true>(data, cnt, segs, seg, pmap, smap, T, G, st);
+            else launch_pass_one<PB, EB, COLS, FWD, MODE, false>(data, cnt, segs, seg, pmap, smap, T, G, st);
+        }
     }
 }
 
@@ -1053,6 +1268,18 @@ void dispatch(int PB, u64 *data, int limbs, int segs, size_t seg, const int *pma
 }
 
 }  // namespace
+
+void ntt_register_map(const int *dev, const int *host, size_t count) {
+    MapRegistry &R = map_registry();
+    std::lock_guard<std::mutex> lk(R.mu);
+    R.maps[dev].assign(host, host + count);
+}
+void ntt_unregister_map(const int *dev) {
+    MapRegistry &R = map_registry();
+    std::lock_guard<std::mutex> lk(R.mu);
+    R.maps.erase(dev);
+}
+bool ntt_fp_prime(u64 q) { return (q >> FP_QBITS) == 0; }
 
 LaunchClock *&launch_clock() {
     static LaunchClock *clk = nullptr;

@@ -179,6 +179,21 @@ struct Engine::Impl {
     u64 *pmod = nullptr, *pmod_s = nullptr, *pqlinv = nullptr, *pqlinv_s = nullptr;
     double *pinvd = nullptr;
     int *modup_smap = nullptr, *modup_pmap = nullptr;
+    // the NTT's host-side class table (T.fp_host points into it) and the prime
+    // maps registered with the NTT launcher; shared with forks, released (maps
+    // unregistered) with the last engine holding the tables
+    struct FpState {
+        std::vector<uint8_t> fp_host;
+        std::vector<const int *> maps;
+        void reg(const int *dev, const std::vector<int> &host) {
+            dev::ntt_register_map(dev, host.data(), host.size());
+            maps.push_back(dev);
+        }
+        ~FpState() {
+            for (const int *m : maps) dev::ntt_unregister_map(m);
+        }
+    };
+    std::shared_ptr<FpState> fps = std::make_shared<FpState>();
 
     // keys
     // key material, shared by an engine and its forks (sort lanes): a key load
@@ -505,6 +520,16 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     }
     I.mods = I.upload_static(mods);
     std::vector<u64> fwd(2 * nall * n), inv(2 * nall * n), ninv(nall), ninv_s(nall);
+    // fp64 twiddles of the primes < 2^41 (the FP NTT launches; zero for the others)
+    std::vector<double> fwdd(nall * n, 0.0), invd(nall * n, 0.0);
+    std::vector<double2> qd(nall);
+    std::vector<uint8_t> &fph = I.fps->fp_host;
+    fph.assign(nall, 0);
+    for (size_t i = 0; i < nall; ++i) {
+        const u64 q = I.P.primes[i];
+        fph[i] = dev::ntt_fp_prime(q) ? 1 : 0;
+        qd[i] = make_double2((double)q, 1.0 / (double)q);
+    }
     {
         std::vector<std::thread> th;
         const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -517,6 +542,10 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
                         fwd[2 * (i * n + k) + 1] = t.fwd_s[k];
                         inv[2 * (i * n + k)] = t.inv[k];
                         inv[2 * (i * n + k) + 1] = t.inv_s[k];
+                        if (fph[i]) {
+                            fwdd[i * n + k] = (double)t.fwd[k];
+                            invd[i * n + k] = (double)t.inv[k];
+                        }
                     }
                     ninv[i] = t.ninv;
                     ninv_s[i] = t.ninv_s;
@@ -530,11 +559,17 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.T.ninv_s = I.upload_static(ninv_s);
     I.T.mods = I.mods;
     I.T.logN = logN;
+    I.T.fwdd = I.upload_static(fwdd);
+    I.T.invd = I.upload_static(invd);
+    I.T.qd = I.upload_static(qd);
+    I.T.fp_host = fph.data();
     I.extmap = I.upload_static(I.LT.extmap);
+    I.fps->reg(I.extmap, I.LT.extmap);
     {
         std::vector<int> io(I.P.nall());
         for (size_t i = 0; i < io.size(); ++i) io[i] = (int)i;
         I.iota = I.upload_static(io);
+        I.fps->reg(I.iota, io);
     }
     I.modup_tab = I.upload_static(I.LT.modup);
     I.phinv = I.upload_static(I.LT.phinv);
@@ -546,8 +581,21 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.qlinv_s = I.upload_static(I.LT.qlinv_s);
     I.pmod = I.upload_static(I.LT.pmod);
     I.pinvd = I.upload_static(I.LT.pinvd);
+    // the ModUp forward NTT's limbs (every digit's targets) in any order: FP
+    // primes first, so the launch splits into one FP and one integer run
+    for (size_t ell = 1; ell <= I.P.nq(); ++ell) {
+        const size_t o = I.LT.modup_map_off[ell], c = I.LT.modup_map_cnt[ell];
+        std::vector<std::pair<int, int>> e(c);
+        for (size_t y = 0; y < c; ++y) e[y] = {I.LT.modup_smap[o + y], I.LT.modup_pmap[o + y]};
+        std::stable_partition(e.begin(), e.end(), [&](const std::pair<int, int> &v) { return fph[v.second] != 0; });
+        for (size_t y = 0; y < c; ++y) {
+            I.LT.modup_smap[o + y] = e[y].first;
+            I.LT.modup_pmap[o + y] = e[y].second;
+        }
+    }
     I.modup_smap = I.upload_static(I.LT.modup_smap);
     I.modup_pmap = I.upload_static(I.LT.modup_pmap);
+    I.fps->reg(I.modup_pmap, I.LT.modup_pmap);
     I.pmod_s = I.upload_static(I.LT.pmod_s);
     I.pqlinv = I.upload_static(I.LT.pqlinv);
     I.pqlinv_s = I.upload_static(I.LT.pqlinv_s);
@@ -1846,10 +1894,13 @@ void Engine::ntt_host(u64 *data, int prime_index, int limbs, bool inverse) {
     auto pmm = I.alloc(limbs * sizeof(int));
     HIP_OK(hipMemcpyAsync(pmm->p, pm.data(), limbs * sizeof(int), hipMemcpyHostToDevice, ST));
     HIP_OK(hipMemcpyAsync(d, data, (size_t)limbs * nn * 8, hipMemcpyHostToDevice, ST));
+    const int *pmd = static_cast<int *>(pmm->p);
+    dev::ntt_register_map(pmd, pm.data(), pm.size());  // so the launch splits by prime class
     if (inverse)
-        dev::ntt_inverse(d, limbs, 1, 0, static_cast<int *>(pmm->p), I.T, ST);
+        dev::ntt_inverse(d, limbs, 1, 0, pmd, I.T, ST);
     else
-        dev::ntt_forward(d, limbs, 1, 0, static_cast<int *>(pmm->p), I.T, ST);
+        dev::ntt_forward(d, limbs, 1, 0, pmd, I.T, ST);
+    dev::ntt_unregister_map(pmd);
     HIP_OK(hipMemcpyAsync(data, d, (size_t)limbs * nn * 8, hipMemcpyDeviceToHost, ST));
     HIP_OK(hipStreamSynchronize(ST));
 }
