@@ -39,6 +39,8 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, 'fhe-sorting_amd'))
+# the sharded sort times its partial-sum exchanges (allreduce_ms) only when asked
+os.environ.setdefault('FHE_TIME_COLLECTIVES', '1')
 
 import fhesort as F  # noqa: E402
 

@@ -1204,9 +1204,15 @@ void reducePartial(Engine &cc, const Shard &sh, CtPtr &acc, int slots) {
     if (acc && acc->batch != 1) throw std::invalid_argument("sharded run: a partial must be a single ciphertext");
     // header: presence, level + 1, (level + 1)^2, limbs -- summed over ranks.
     // Every rank sees the same sums, so every rank takes the same branch below.
-    // the exchange's time (bench.py: allreduce_ms beside rank_compute_ms) runs
-    // from a drained stream -- this rank's compute is done -- to the reduced data
-    cc.sync();
+    // The exchange's time (bench.py: allreduce_ms beside rank_compute_ms) runs
+    // from a drained stream -- this rank's compute is done -- to the reduced
+    // data; the two drains that bracket it are taken only when the time is
+    // wanted (FHE_TIME_COLLECTIVES=1, set by bench.py; advisor r4)
+    static const bool timed = [] {
+        const char *e = std::getenv("FHE_TIME_COLLECTIVES");
+        return e && std::atoi(e) != 0;
+    }();
+    if (timed) cc.sync();
     const auto t0 = std::chrono::steady_clock::now();
     auto hdr = cc.alloc_u64(4);
     const u64 l1 = acc ? (u64)(acc->level + 1) : 0;
@@ -1219,9 +1225,11 @@ void reducePartial(Engine &cc, const Shard &sh, CtPtr &acc, int slots) {
     if (acc->limbs != H.limbs) throw std::runtime_error("sharded run: partial limb count differs from the header");
     sh.allreduce(acc->data, 2 * acc->limbs * cc.n());
     cc.reduce_after_allreduce(*acc);
-    cc.sync();
-    cc.ctr.allreduce_ns += (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                               std::chrono::steady_clock::now() - t0).count();
+    if (timed) {
+        cc.sync();
+        cc.ctr.allreduce_ns += (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                   std::chrono::steady_clock::now() - t0).count();
+    }
     cc.ctr.allreduce_calls += 1;
 }
 void DirectSortN::reducePartial(CtPtr &acc, int slots) {
@@ -1420,7 +1428,14 @@ CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext 
     return out;
 }
 
+// Re-encodes every cached mask (the reference's per-use encoding,
+// src/sort_algo.h:341-342, 714-716) for sort() with mask caching off.  Chunks
+// of REFRESH_CHUNK masks: each chunk's new plaintexts replace (and release) old
+// ones before the next chunk is encoded, so the peak is about one chunk above
+// the mask set instead of twice the set (advisor r4).  The other
+// fhe_direct_sort modes (rank only, index check only) keep the cached masks.
 void DirectSortN::refresh_masks() {
+    constexpr size_t REFRESH_CHUNK = 128;
     cc.sync();
     for (auto &e : lane_eng) e->sync();  // nothing of the last sort still reads the old masks
     std::map<int, std::vector<std::tuple<int, int, int, int, int>>> by_slots;
@@ -1429,12 +1444,17 @@ void DirectSortN::refresh_masks() {
         for (auto &kv : mask_cache) by_slots[std::get<1>(kv.first)].push_back(kv.first);
     }
     for (auto &g : by_slots) {
-        std::vector<Engine::MaskSpec> specs;
-        for (auto &key : g.second)
-            specs.push_back(Engine::MaskSpec{std::get<0>(key), std::get<2>(key), std::get<3>(key), std::get<4>(key)});
-        auto pts = cc.encode_masks(specs, g.first, N);  // synchronises the main stream
-        std::lock_guard<std::mutex> lk(mask_mu);
-        for (size_t i = 0; i < pts.size(); ++i) mask_cache[g.second[i]] = pts[i];
+        for (size_t a = 0; a < g.second.size(); a += REFRESH_CHUNK) {
+            const size_t b = std::min(g.second.size(), a + REFRESH_CHUNK);
+            std::vector<Engine::MaskSpec> specs;
+            for (size_t i = a; i < b; ++i) {
+                const auto &key = g.second[i];
+                specs.push_back(Engine::MaskSpec{std::get<0>(key), std::get<2>(key), std::get<3>(key), std::get<4>(key)});
+            }
+            auto pts = cc.encode_masks(specs, g.first, N);  // synchronises the main stream
+            std::lock_guard<std::mutex> lk(mask_mu);
+            for (size_t i = a; i < b; ++i) mask_cache[g.second[i]] = pts[i - a];
+        }
     }
 }
 

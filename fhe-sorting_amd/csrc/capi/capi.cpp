@@ -233,6 +233,7 @@ int fhe_pt_download(fhe_ctx *ctx, const fhe_pt *pt, uint64_t *out) {
     return guard([&] {
         NEED(ctx);
         NEED(pt);
+        NEED(pt->p);
         NEED(out);
         ctx->eng->sync();
         if (hipMemcpy(out, pt->p->data, pt->p->limbs * ctx->eng->n() * 8, hipMemcpyDeviceToHost) != hipSuccess)
@@ -352,7 +353,12 @@ int fhe_compose_rotate_members(fhe_ctx *ctx, const fhe_ct *a, int N, const int32
     return guard([&] {
         NEED(ctx);
         NEED(a);
+        NEED(a->p);
+        NEED(out);
+        if (nrot > 0) NEED(rots);
+        if (nrot < 0 || count < 0) throw std::invalid_argument("compose_rotate_members: negative count");
         if (count != a->p->batch) throw std::invalid_argument("compose_rotate_members: one rotation per member");
+        if (count > 0) NEED(rotations);
         RotationComposerN rc(*ctx->eng, N, std::vector<int>(rots, rots + nrot), (DecomposeAlgo)algo);
         auto m = rc.rotateMembers(*a->p, std::vector<int>(rotations, rotations + count));
         std::vector<const Ciphertext *> v;

@@ -32,7 +32,8 @@ namespace dev {
 namespace {
 
 constexpr int NTB = 256;  // threads per block (row passes, small rings)
-// Wide column passes (FHE_NTT_COL_WIDE, default on): a 256-point column pass
+// Wide column passes (FHE_NTT_COL_WIDE, off by default -- measured slower,
+// DESIGN.md §5 round-4 table): a 256-point column pass
 // runs 64 columns per 1024-thread block, so lane = column and wave = t, the
 // lane's position in its transform: every twiddle of both rounds is then
 // wave-uniform (scalar loads, no VGPRs -- the 16-column blocks held up to 60

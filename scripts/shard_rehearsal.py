@@ -6,6 +6,7 @@ import json, os, sys, time
 import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, 'fhe-sorting_amd'))
+os.environ.setdefault('FHE_TIME_COLLECTIVES', '1')  # allreduce_ms beside the compute
 import fhesort as F
 
 kind = sys.argv[1]

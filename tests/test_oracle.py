@@ -373,3 +373,28 @@ def test_encrypt_ext_lowers_fresh_noise():
     a, b = ctx.encrypt(x, 2048), ctx.encrypt_ext(x, 2048)
     assert a.level == 0 and b.level == 1 and b.info()['scale'] == ctx.delta[1]
     assert np.max(np.abs(ctx.decrypt(b) - x)) * 5 < np.max(np.abs(ctx.decrypt(a) - x))
+
+
+def test_direct_sort_ties_follow_the_plaintext_model():
+    """Verdict r4 item 1: what the reference's DirectSort does on tied inputs
+    (tests/tie_model.py): compare(x, x) = 1/2, so a value of odd multiplicity m
+    lands m times over in its middle slot and an even multiplicity spreads with
+    sinc tails.  The oracle's decryption equals the plaintext model to CKKS
+    precision at N = 8 with the CLI's CompositeSign(4, 3, 3); the output is not
+    the sort of the input."""
+    import tie_model as T
+    N, cfg = 8, (4, 3, 3)
+    rots = O.size_parameters(N)[1]
+    orc = O.Context(12, 39, 50, 60, 3, seed=5)
+    orc.gen_rotation_keys(rots)
+    for x in ([0.5, 0.25, 0.5, 0.75, 0.25, 0.25, 0.1, 0.9], [0.3, 0.3, 0.3, 0.6, 0.6, 0.1, 0.2, 0.2]):
+        x = np.array(x)
+        y = orc.decrypt(orc.direct_sort(orc.encrypt(x, N), N, rots, cfg))[:N]
+        m = T.direct_sort(x, cfg)
+        assert np.max(np.abs(y - m)) < 1e-5
+        assert np.max(np.abs(y - np.sort(x))) > 0.1  # ties: not a sort
+    r = T.ranks([0.5, 0.25, 0.5, 0.75, 0.25, 0.25, 0.1, 0.9], cfg)
+    assert np.allclose(r, [4.5, 2, 4.5, 6, 2, 2, 0, 7], atol=1e-9)
+    # distinct values: the model is the sort
+    x = np.random.default_rng(3).permutation(N) / N
+    assert np.max(np.abs(T.direct_sort(x, cfg) - np.sort(x))) < 1e-9

@@ -2,6 +2,7 @@
 src/sort.h:31-102) on the CPU: the library's header / checksum validation
 against files written by the independent restatement in tests/wire_spec.py,
 the error codes for damaged files, and the client's depth rule."""
+import json
 import os
 
 import numpy as np
@@ -109,6 +110,25 @@ def test_cli_depth_rule():
     assert c.required_depth(128, (4, 3, 3)) == 42
     assert c.cli_rotations(128) == c.MAIN_ROTATIONS
     assert c.cli_rotations(8) == F.size_parameters(8)[1]
+
+
+def test_client_defaults_are_the_reference_config(tmp_path):
+    """Verdict r4 item 1: client.py setup defaults to src/config.json's context
+    (ring 131072, multDepth 44, scale 40, batch 128, main.cpp's rotations) and
+    reads another config file of that format; encrypt --testcase takes the
+    reference's testcase format and divides by 255 (inputOver255)."""
+    c = _client()
+    ref = c.REFERENCE_CONFIG
+    assert (ref['ring_dimension'], ref['mult_depth'], ref['scale_mod_size'], ref['batch_size']) == (131072, 44, 40, 128)
+    assert ref['indexes_for_rotation_key'] == c.MAIN_ROTATIONS and c.load_config(None) == ref
+    assert c.required_depth(128, (4, 3, 3)) <= ref['mult_depth']
+    cfg = tmp_path / 'config.json'
+    cfg.write_text(json.dumps({'mult_depth': 40, 'ring_dimension': 65536, 'scale_mod_size': 50}))
+    assert c.load_config(str(cfg))['ring_dimension'] == 65536
+    tc = tmp_path / 'testcase.json'
+    tc.write_text(json.dumps([{'scheme': 'CKKS', 'runs': [{'input': [{'name': 'input', 'value': [2.34, 245.67]}],
+                                                          'output': []}]}]))
+    assert np.array_equal(c.testcase_values(str(tc)), [2.34, 245.67])
 
 
 def test_cli_binary_fails_like_the_reference(tmp_path):
