@@ -252,6 +252,18 @@ struct KsFold {
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
               hipStream_t st, int members, KsStrides str, KsFold fold = KsFold());
+// ModUp's forward NTT split in two for the relinearisation (ntt.hip): the
+// column pass alone over the mapped limbs (as ntt_forward_mapped), then
+// ntt_row_ks -- the row pass of every digit's target limb fused with the
+// key-switch inner product of ks_inner (no permutation): acc[m][0/1][t] =
+// sum_j NTT_row(ext_j)[t] * key_j (own digit: dntt) (+ the fold on t = ell-1),
+// so ext never returns to HBM in NTT form.  Same words as ntt_forward_mapped +
+// ks_inner.  Members in blocks of 16 (one transform each, one row per block).
+void ntt_forward_mapped_cols(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,
+                             const NttTables &T, hipStream_t st);
+void ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nall, int alpha,
+                int digits, const int *pmap_ext, int members, KsStrides str, KsFold fold, const NttTables &T,
+                hipStream_t st);
 // several key switches in one launch (hoisted rotations by different
 // amounts, or one rotation per member of a batch): member m < count uses key
 // keys[m] and reads ext through perm[m]; strides in `str` (0 = shared input)

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <stdexcept>
 #include <string>
 #include <type_traits>
 #include <utility>
@@ -32,6 +33,17 @@ namespace dev {
 namespace {
 
 constexpr int NTB = 256;  // threads per block (row passes, small rings)
+
+// compile-time dispatch of a small runtime integer (the digit count of ntt_row_ks)
+template <int Lo, int Hi, typename F>
+void dispatch_int(int v, F &&f) {
+    if constexpr (Lo > Hi) {
+        throw std::invalid_argument("unsupported digit count " + std::to_string(v));
+    } else {
+        if (v == Lo) f(std::integral_constant<int, Lo>{});
+        else dispatch_int<Lo + 1, Hi>(v, std::forward<F>(f));
+    }
+}
 // Wide column passes (FHE_NTT_COL_WIDE, off by default -- measured slower,
 // DESIGN.md §5 round-4 table): a 256-point column pass
 // runs 64 columns per 1024-thread block, so lane = column and wave = t, the
@@ -1084,6 +1096,123 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(TWL ? FHE_N
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
     ntt_inv_body<8, 4, false, true, FULL, TWL, FP>(data, seg, pmap, smap, logN, Tb, F);
 }
+// ModUp's forward row pass fused with the key-switch inner product (HMult
+// relinearisation; kernels.hpp ntt_row_ks).  Block: one row (256 points) of
+// one target limb t for 16 members, one 16-lane transform per member, the
+// row's twiddles staged in LDS.  For each digit j the lane group either loads
+// the own-digit limb dntt[t] (NTT form already) or runs the row pass on
+// ext[j][t] (after its column pass), then multiplies by the key rows of digit
+// j and accumulates; acc[m][0][t] and acc[m][1][t] are written once.  The
+// sums are the canonical residues ks_inner computes (integer limbs:
+// mul_barrett + add_mod exactly as k_ks_inner_mc; FP limbs: fp_mulmod terms,
+// one final reduction -- the same residue), so the words are unchanged.
+#ifndef FHE_ROW_KS_WPE
+#define FHE_ROW_KS_WPE 2
+#endif
+template <int D, bool FP, bool FULL>
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FHE_ROW_KS_WPE, 8))) void k_ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
+                                                    int ell, int W, int nall, int alpha, int members,
+                                                    const int *pmap_ext, int logN, NttTables Tb, KsStrides st,
+                                                    KsFold fold, NttFuse Fz) {
+    using TW = TwT<FP>;
+    __shared__ TW twl[256];
+    const size_t n = (size_t)1 << logN;
+    const int t = Fz.limb_of(blockIdx.z);
+    const int pt = __builtin_amdgcn_readfirstlane(pmap_ext[t]);
+    const int tr = threadIdx.x >> 4, tl = threadIdx.x & 15;
+    const int mb = (int)blockIdx.x * 16 + tr;
+    const bool valid = FULL || mb < members;
+    const size_t row = blockIdx.y, rb = row * 256;
+    const Mod md = Tb.mods[pt];
+    const u64 q = md.q, q2 = 2 * q;
+    Ar A{4 * q, (u64)0 - q, 0.0, 0.0};
+    const TW *tw;
+    if constexpr (FP) {
+        tw = Tb.fwdd + (size_t)pt * n;
+        const double2 qd = Tb.qd[pt];
+        A.q = qd.x;
+        A.qi = qd.y;
+    } else {
+        tw = Tb.fwd2 + (size_t)pt * n;
+    }
+    const int S0 = logN - 8;
+    row_twiddles<true>(twl, tw, row, n, S0);
+    __syncthreads();
+    const size_t m = valid ? (size_t)mb : 0;
+    // element r of a lane sits at in-row index row_final_index<true>(tl, r) =
+    // lane part + a compile-time register part
+    const int li = row_final_index<true>(tl, 0);
+#define IDX(r) (li + (row_final_index<true>(0, r)))
+    u64 a0[16], a1[16];
+    const bool folded = fold.d && t == ell - 1;
+    const u64 *fd = fold.d + m * fold.member;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        u64 f0 = 0, f1 = 0;
+        if (folded && valid) {
+            f0 = mul_shoup(fd[rb + IDX(r)], fold.w, fold.ws, q);
+            f1 = mul_shoup(fd[fold.seg + rb + IDX(r)], fold.w, fold.ws, q);
+        }
+        a0[r] = FP ? ubits(fp_in(f0, FP_TWO52)) : f0;
+        a1[r] = FP ? ubits(fp_in(f1, FP_TWO52)) : f1;
+    }
+#pragma unroll 1
+    for (int j = 0; j < D; ++j) {
+        const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
+        u64 x[16];
+        if (t >= lo && t < hi) {  // own digit: the switched polynomial itself (NTT form)
+            const u64 *src = dntt + m * st.d + (size_t)t * n + rb;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const u64 v = valid ? src[IDX(r)] : 0;
+                x[r] = FP ? ubits(fp_in(v, FP_TWO52)) : v;
+            }
+        } else {
+            const u64 *src = ext + m * st.ext + ((size_t)j * W + t) * n + rb;
+            const double fin = FP ? FP_TWO52 + FP_FWD_COL_OUT * A.q : 0.0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const u64 v = valid ? src[tl + 16 * r] : 0;
+                x[r] = FP ? ubits(fp_in(v, fin)) : v;
+            }
+            row_pass_shfl<true, true, FP>(x, tl, row, twl, n, S0, A);
+            if constexpr (!FP) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) x[r] = canon12(x[r], q, q2);
+            }
+        }
+        const u64 *kb = key + (((size_t)j * 2 + 0) * nall + pt) * n + rb;
+        const u64 *ka = key + (((size_t)j * 2 + 1) * nall + pt) * n + rb;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const u64 b = kb[IDX(r)], c = ka[IDX(r)];
+            if constexpr (FP) {
+                const double xv = dbits(x[r]);
+                a0[r] = ubits(dbits(a0[r]) + fp_mulmod(xv, fp_in(b, FP_TWO52), A.q, A.qi));
+                a1[r] = ubits(dbits(a1[r]) + fp_mulmod(xv, fp_in(c, FP_TWO52), A.q, A.qi));
+            } else {
+                a0[r] = add_mod(a0[r], mul_barrett(x[r], b, md), q);
+                a1[r] = add_mod(a1[r], mul_barrett(x[r], c, md), q);
+            }
+        }
+    }
+    if (!valid) return;
+    u64 *o0 = acc + m * st.acc + (size_t)t * n + rb;
+    u64 *o1 = acc + m * st.acc + ((size_t)W + t) * n + rb;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        u64 v0 = a0[r], v1 = a1[r];
+        if constexpr (FP) {  // |a| <= (D 0.51 + 1) q: one reduction, canonical
+            const double r0 = fp_reduce(dbits(v0), A.q, A.qi), r1 = fp_reduce(dbits(v1), A.q, A.qi);
+            v0 = fp_out(r0 < 0.0 ? r0 + A.q : r0, FP_TWO52);
+            v1 = fp_out(r1 < 0.0 ? r1 + A.q : r1, FP_TWO52);
+        }
+        o0[IDX(r)] = v0;
+        o1[IDX(r)] = v1;
+    }
+#undef IDX
+}
+
 // FHE_NTT_TWL (A/B, default 1): the register-only row passes stage a row's
 // twiddles in LDS when the block is one row of 16 segments
 int &row_twl_enabled() {
@@ -1376,6 +1505,62 @@ void ntt_forward_ksfinish(u64 *conv, int limbs, int segs, const NttFuse &F, cons
     const size_t seg = (size_t)limbs << T.logN;
     dispatch<true, true, NTT_PLAIN>(k1, conv, limbs, segs, seg, nullptr, nullptr, T, F, st);
     dispatch<false, true, NTT_KSFINISH>(k2, conv, limbs, segs, seg, nullptr, nullptr, T, F, st);
+}
+
+void ntt_forward_mapped_cols(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,
+                             const NttTables &T, hipStream_t st) {
+    if (count <= 0 || segs <= 0) return;
+    const int k1 = (T.logN + 1) / 2;
+    const NttFuse F;
+    dispatch<true, true, NTT_PLAIN>(k1, data, count, segs, seg, pmap, smap, T, F, st);
+}
+
+void ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nall, int alpha,
+                int digits, const int *pmap_ext, int members, KsStrides str, KsFold fold, const NttTables &T,
+                hipStream_t st) {
+    const int W = ell + K;
+    if (T.logN != 16 && T.logN != 17) throw std::invalid_argument("ntt_row_ks: the row pass is 256 points (rings 2^16, 2^17)");
+    if (digits < 1 || digits > 8) throw std::invalid_argument("ntt_row_ks: 1..8 digits");
+    if (members < 1) return;
+    std::vector<int> pr;
+    const bool known = launch_primes(pmap_ext, W, pr);
+    // the column pass (launch_pass) classed the limbs through the ModUp map; the
+    // row pass here must class them the same way, so the map must be known
+    if (!known && ntt_fp_enabled() && T.fp_host) throw std::invalid_argument("ntt_row_ks: unregistered prime map");
+    const bool full = members % 16 == 0;
+    const dim3 blk(NTB);
+    for (int cls = 0; cls < 2; ++cls) {
+        std::vector<std::pair<int, int>> runs;
+        for (int z = 0; z < W; ++z) {
+            const bool fp = ntt_fp_enabled() && T.fp_host && known && T.fp_host[pr[z]] != 0;
+            if (fp != (cls == 1)) continue;
+            if (!runs.empty() && runs.back().first + runs.back().second == z) ++runs.back().second;
+            else runs.emplace_back(z, 1);
+        }
+        for (size_t r = 0; r < runs.size(); r += 2) {
+            NttFuse Fz;
+            Fz.zs0 = runs[r].first;
+            Fz.zn0 = runs[r].second;
+            Fz.zs1 = r + 1 < runs.size() ? runs[r + 1].first : 0;
+            const int cnt = runs[r].second + (r + 1 < runs.size() ? runs[r + 1].second : 0);
+            const dim3 grid((unsigned)((members + 15) / 16), (unsigned)(1u << (T.logN - 8)), (unsigned)cnt);
+            // ext rows (digits - 1 or digits per target) + own-digit rows + 2 accumulators per member; keys once
+            const double bytes = 8.0 * ((double)members * (digits + 2.0) + 2.0 * digits) * cnt * ((size_t)1 << T.logN);
+            dispatch_int<1, 8>(digits, [&](auto c) {
+                constexpr int DD = decltype(c)::value;
+                auto go = [&](auto fpc, auto fullc) {
+                    constexpr bool FPV = decltype(fpc)::value, FU = decltype(fullc)::value;
+                    launch_clocked(inst_name<DD, FPV, FU>("k_ntt_row_ks"), bytes, k_ntt_row_ks<DD, FPV, FU>, grid, blk,
+                                   st, acc, ext, dntt, key, ell, W, nall, alpha, members, pmap_ext, T.logN, T, str,
+                                   fold, Fz);
+                };
+                if (cls && full) go(std::true_type{}, std::true_type{});
+                else if (cls) go(std::true_type{}, std::false_type{});
+                else if (full) go(std::false_type{}, std::true_type{});
+                else go(std::false_type{}, std::false_type{});
+            });
+        }
+    }
 }
 
 }  // namespace dev

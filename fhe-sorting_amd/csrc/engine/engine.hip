@@ -330,7 +330,18 @@ struct Engine::Impl {
     // ciphertext batch): member m of an input sits at m * stride.
     //
     // ext[m][j][t] (NTT form) for all digits of d[m] ([ell][n], NTT form)
-    std::shared_ptr<DevMem> modup(const u64 *d, size_t ell, int members, size_t d_stride) {
+    // FHE_KS_FUSE (A/B, default 1): the relinearisation runs ModUp's forward row
+    // pass fused with the key-switch inner product (dev::ntt_row_ks)
+    bool ks_fuse(int members) const {
+        static const int on = [] {
+            const char *e = std::getenv("FHE_KS_FUSE");
+            return e ? std::atoi(e) : 1;
+        }();
+        return on && members >= 4 && (P.logN == 16 || P.logN == 17);
+    }
+    // cols_only: the forward NTT's column pass alone (the row pass runs fused
+    // with the key switch, mul_tail)
+    std::shared_ptr<DevMem> modup(const u64 *d, size_t ell, int members, size_t d_stride, bool cols_only = false) {
         Phase phase_("modup");
         const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         const int digits = P.digits_at(ell);
@@ -343,7 +354,11 @@ struct Engine::Impl {
         dev::modup_convert(e, c, (int)ell, P.K, P.alpha, digits, members, ell * nn, es, ext(ell), modup_tab,
                            LT.modup_off[ell].data(), mods, P.logN, st);
         const size_t mo = LT.modup_map_off[ell];
-        dev::ntt_forward_mapped(e, (int)LT.modup_map_cnt[ell], members, es, modup_smap + mo, modup_pmap + mo, T, st);
+        if (cols_only)
+            dev::ntt_forward_mapped_cols(e, (int)LT.modup_map_cnt[ell], members, es, modup_smap + mo, modup_pmap + mo, T,
+                                         st);
+        else
+            dev::ntt_forward_mapped(e, (int)LT.modup_map_cnt[ell], members, es, modup_smap + mo, modup_pmap + mo, T, st);
         return extm;
     }
     // rotation key switch: out[m] (= [2][ell][n]) = ModDown(sum_j ext_j * key_j) + (add[m], 0);
@@ -415,7 +430,8 @@ struct Engine::Impl {
     // here only limb ell-1 and the P limbs leave the NTT domain and one forward
     // NTT of ell-1 limbs per polynomial serves both divisions.
     // d01 [members][2][ell][n], d2 [members][ell][n] (NTT form).
-    void mul_tail(const u64 *e, const u64 *d01, const u64 *d2, size_t ell, int members, u64 *out) {
+    // fused: e is ModUp's output after the column pass only (modup cols_only)
+    void mul_tail(const u64 *e, const u64 *d01, const u64 *d2, size_t ell, int members, u64 *out, bool fused = false) {
         Phase phase_("mul_tail");
         const size_t nn = n(), K = (size_t)P.K, W = ell + K;
         const int digits = P.digits_at(ell);
@@ -432,8 +448,12 @@ struct Engine::Impl {
         fold.member = 2 * ell * nn;
         fold.w = LT.pmod[ell - 1];
         fold.ws = LT.pmod_s[ell - 1];
-        dev::ks_inner(acc, e, d2, static_cast<u64 *>(ks->relin->p), (int)ell, P.K, (int)P.nq(), (int)P.nall(), P.alpha,
-                      digits, nullptr, ext(ell), mods, P.logN, st, members, str, fold);
+        if (fused)
+            dev::ntt_row_ks(acc, e, d2, static_cast<u64 *>(ks->relin->p), (int)ell, P.K, (int)P.nall(), P.alpha, digits,
+                            ext(ell), members, str, fold, T, st);
+        else
+            dev::ks_inner(acc, e, d2, static_cast<u64 *>(ks->relin->p), (int)ell, P.K, (int)P.nq(), (int)P.nall(),
+                          P.alpha, digits, nullptr, ext(ell), mods, P.logN, st, members, str, fold);
         dev::ntt_inverse(acc + (ell - 1) * nn, (int)K + 1, segs, W * nn, ext(ell) + (ell - 1), T, st, /*raw*/ true);
         auto corrm = alloc((size_t)segs * (ell - 1) * nn * 8);
         u64 *corr = static_cast<u64 *>(corrm->p);
@@ -1390,9 +1410,10 @@ CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vec
         const size_t ln = ell * nn;
         dev::ew_add(d01, d01, raw->data, (int)ell, 2 * B, dev::Seg{ln, ln, ln}, MODS, LOGN, ST);
     }
-    auto extm = I.modup(d2, ell, B, ell * nn);
+    const bool fuse = I.ks_fuse(B);
+    auto extm = I.modup(d2, ell, B, ell * nn, fuse);
     auto r = new_ct(a->level + 1, a->slots, I.P.delta[a->level + 1], ell - 1, B);
-    I.mul_tail(static_cast<u64 *>(extm->p), d01, d2, ell, B, r->data);
+    I.mul_tail(static_cast<u64 *>(extm->p), d01, d2, ell, B, r->data, fuse);
     return r;
 }
 CtPtr Engine::mul_add_raw(const Ciphertext &a, const Ciphertext &b, const Ciphertext &raw, const Ciphertext *a_add) {

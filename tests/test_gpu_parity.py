@@ -572,6 +572,20 @@ def test_relinearised_products_large_rings(logN, L):
     for m in range(3):
         same(gpu.member(st, m), orc.mul(xs[m], xs[1]))
     assert np.max(np.abs(gpu.decrypt(gpu.mul(gx[0], gx[1])) - orc.decrypt(orc.mul(xs[0], xs[1])))) < 1e-9
+    # stacks of >= 4 members relinearise through dev::ntt_row_ks (ModUp's row pass
+    # fused with the key-switch inner product; round 5): 16 members (full blocks)
+    # and 20 (a partial block), at the top level and two levels down
+    ys = [orc.encrypt(rng.uniform(-1, 1, 64), 64) for _ in range(20)]
+    gy = [gpu.from_oracle(y) for y in ys]
+    for cnt in (16, 20):
+        st = gpu.mul(gpu.stack(gy[:cnt]), gpu.stack(gy[::-1][:cnt]))
+        for m in (0, 7, cnt - 1):
+            same(gpu.member(st, m), orc.mul(ys[m], ys[::-1][m]))
+    lo = [orc.mul(orc.mul(y, xs[1]), xs[2]) for y in ys[:5]]
+    gl = gpu.stack([gpu.from_oracle(y) for y in lo])
+    st = gpu.mul(gl, gl)
+    for m in range(5):
+        same(gpu.member(st, m), orc.mul(lo[m], lo[m]))
 
 
 def test_config2_direct_sort_full_size_bit_exact():
