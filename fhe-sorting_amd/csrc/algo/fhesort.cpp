@@ -1193,6 +1193,15 @@ ShardHeader checkShardHeader(const u64 h[4]) {
     return ShardHeader{(int)(s1 / present) - 1, (size_t)(limbs / present)};
 }
 
+// algorithm phase of the clocked kernels (bench.py roofline.phases; DirectSort:
+// rank_baby / rank_batches / rank_fold / index_batches / index_fold, MEHP24:
+// its sortFG phases).  Thread-local, so set again inside each lane's work.
+struct AlgoPhase {
+    const char *prev;
+    explicit AlgoPhase(const char *p) : prev(Engine::set_algo_phase(p)) {}
+    ~AlgoPhase() { Engine::set_algo_phase(prev); }
+};
+
 void reducePartial(Engine &cc, const Shard &sh, CtPtr &acc, int slots) {
     // a single rank reduces only when the caller gave it a collective (an
     // RCCL communicator of world 1 still runs the all-reduce)
@@ -1302,8 +1311,11 @@ std::vector<CtPtr> DirectSortN::vecRotsOptMany(Lane L, const std::vector<CtPtr> 
 // accumulation (src/sort_algo.h:474-491) word for word.
 CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConfig &cfg) {
     const SortShape s = rankShape(N, max_batch);
+    std::optional<AlgoPhase> ph;
+    ph.emplace("rank_baby");
     std::vector<CtPtr> baby = babySteps(x, s.np);
     for (auto &b : baby) b->slots = s.num_slots;
+    ph.reset();
     std::vector<int> mine;
     for (int b = 0; b < s.num_batch; ++b)
         if (b % shard_world == shard_rank) mine.push_back(b);
@@ -1313,6 +1325,7 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
     const size_t chunk = (size_t)std::max(1, max_stack);
     auto parts = run_lanes(mine, [&](Lane L, const std::vector<int> &bs) -> CtPtr {
         Engine &E = *L.eng;
+        AlgoPhase lane_ph("rank_batches");
         CtPtr acc;
         for (size_t c0 = 0; c0 < bs.size(); c0 += chunk) {
             std::vector<int> iss(bs.begin() + c0, bs.begin() + std::min(bs.size(), c0 + chunk));
@@ -1335,6 +1348,7 @@ CtPtr DirectSortN::constructRank(const Ciphertext &x, SignFunc f, const SignConf
     cc.sync();  // lane buffers return to their pools only after the main stream read them
     parts.clear();
     reducePartial(rank, s.num_slots);
+    ph.emplace("rank_fold");
     for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)
         rank = cc.add(*rank, *rot.rotate(*rank, s.num_slots / (1 << i)));
     rank->slots = N;
@@ -1394,6 +1408,7 @@ CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext 
     const size_t chunk = (size_t)std::max(1, max_stack);
     auto parts = run_lanes(mine, [&](Lane L, const std::vector<int> &bs) -> CtPtr {
         Engine &E = *L.eng;
+        AlgoPhase lane_ph("index_batches");
         CtPtr acc;
         for (size_t c0 = 0; c0 < bs.size(); c0 += chunk) {
             std::vector<const Plaintext *> chks;
@@ -1422,6 +1437,7 @@ CtPtr DirectSortN::rotationIndexCheckN(const Ciphertext &rank, const Ciphertext 
     cc.sync();
     parts.clear();
     reducePartial(out, s.num_slots);
+    AlgoPhase ph("index_fold");
     for (int i = 1; i < std::log2((double)s.num_partition) + 1; ++i)
         out = cc.add(*out, *rot.rotate(*out, s.num_slots / (1 << i)));
     out->slots = N;
@@ -1629,12 +1645,6 @@ namespace mehp24 {
 
 namespace {
 size_t lg(size_t x) { return (size_t)ceil_log2((long)x); }  // LOG2 (mehp24_utils.h:25)
-// algorithm phase of the clocked kernels (bench.py --workload mehp24: roofline.phases)
-struct AlgoPhase {
-    const char *prev;
-    explicit AlgoPhase(const char *p) : prev(Engine::set_algo_phase(p)) {}
-    ~AlgoPhase() { Engine::set_algo_phase(prev); }
-};
 }  // namespace
 
 namespace utils {

@@ -582,16 +582,33 @@ struct PlainSumArgs {
     const u64 *pt[LIN_MAX];
     int m, accumulate;
     size_t cmember, cpoly;
+    int xcd, segs, cblocks;  // XCD-grouped flat grid (k_mul_plain_sum)
 };
 // grid: x = segment (fastest: the segments that read one plaintext block run
 // back to back while it is still cached: 449 -> 393 us per launch; the L2 fetch
 // bytes stay 1.32x the algorithmic ones, r4_final6), y = coefficient block,
-// z = limb
+// z = limb.  XCD (round 5, A.xcd): the workgroup dispatcher deals consecutive
+// blocks round-robin over the 8 XCDs, so the segments of one plaintext block
+// landed on 8 L2s and each fetched it; with A.xcd the launch is a flat grid of
+// S x T blocks (T = coefficient blocks x limbs, a multiple of 8) whose linear
+// id b runs tile 8 (b / 8 / S) + b % 8, segment (b / 8) % S: every segment of a
+// tile runs on the same XCD, back to back.
 __global__ __launch_bounds__(NT) void k_mul_plain_sum(u64 *out, PlainSumArgs A, size_t seg, const Mod *mods,
                                                       int logN) {
     const size_t n = (size_t)1 << logN;
-    const int l = blockIdx.z, z = blockIdx.x;
-    const size_t k = ((size_t)blockIdx.y * NT + threadIdx.x) * 2;
+    int l, z, cb;
+    if (A.xcd) {
+        const unsigned b = blockIdx.x, j = b >> 3;
+        const unsigned tile = 8 * (j / (unsigned)A.segs) + (b & 7);
+        z = (int)(j % (unsigned)A.segs);
+        cb = (int)(tile % (unsigned)A.cblocks);
+        l = (int)(tile / (unsigned)A.cblocks);
+    } else {
+        l = blockIdx.z;
+        z = blockIdx.x;
+        cb = blockIdx.y;
+    }
+    const size_t k = ((size_t)cb * NT + threadIdx.x) * 2;
     if (k >= n) return;
     const Mod md = mods[l];
     const size_t ln = (size_t)l * n + k;
@@ -1488,8 +1505,22 @@ void ew_mul_plain_sum(u64 *out, const u64 *const *cts, const u64 *const *pts, in
         const double B = 8.0 * ((double)A.m * (cmember ? 2 * members : 2) + A.m + 2.0 * members * (1 + A.accumulate)) *
                          limbs * ((size_t)1 << logN);
         const dim3 g0 = ew_grid(logN, limbs, 2 * members);
-        launch_clocked("k_mul_plain_sum", B, k_mul_plain_sum, dim3(g0.z, g0.x, g0.y), dim3(NT), st, out, A, seg, mods,
-                       logN);
+        // FHE_PS_XCD (A/B, default 1): XCD-grouped flat grid when the tiles divide by 8
+        static const int xcd_env = [] {
+            const char *e = std::getenv("FHE_PS_XCD");
+            return e ? std::atoi(e) : 1;
+        }();
+        const unsigned tiles = g0.x * g0.y;
+        if (xcd_env && tiles % 8 == 0 && (size_t)tiles * g0.z < (1ull << 31)) {
+            A.xcd = 1;
+            A.segs = (int)g0.z;
+            A.cblocks = (int)g0.x;
+            launch_clocked("k_mul_plain_sum", B, k_mul_plain_sum, dim3(tiles * g0.z), dim3(NT), st, out, A, seg, mods,
+                           logN);
+        } else {
+            launch_clocked("k_mul_plain_sum", B, k_mul_plain_sum, dim3(g0.z, g0.x, g0.y), dim3(NT), st, out, A, seg,
+                           mods, logN);
+        }
     }
 }
 void ew_permute(u64 *out, const u64 *in, const uint32_t *perm, int limbs, int segs, Seg S, int logN,

@@ -12,3 +12,4 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_digests.py -x -q --timeout 
 FHE_KS_FUSE=0 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_nofuse.json 2> $O/bench_nofuse.err && \
 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_fuse.json 2> $O/bench_fuse.err && \
 FHE_LIB=fhe-sorting_amd/lib/ab_kswpe3.so timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_fuse3.json 2> $O/bench_fuse3.err
+[ -f $O/bench_fuse3.json ] && FHE_PS_XCD=0 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_psxcd0.json 2> $O/bench_psxcd0.err
