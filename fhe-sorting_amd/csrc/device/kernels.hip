@@ -844,7 +844,7 @@ __global__ __launch_bounds__(NT) void k_ks_inner(u64 *acc, const u64 *ext, const
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.y * NT + threadIdx.x;
     if (k >= n) return;
-    const int t = blockIdx.z;
+    const int t = st.target_of(blockIdx.z);
     const size_t mb = blockIdx.x;
     acc += mb * st.acc;
     ext += mb * st.ext;
@@ -888,7 +888,7 @@ __global__ __launch_bounds__(NT) void k_ks_inner_mc(u64 *acc, const u64 *ext, co
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
-    const int t = blockIdx.y;
+    const int t = st.target_of(blockIdx.y);
     const int m0 = blockIdx.z * MC;
     const int pt = pmap_ext[t];
     const Mod m = mods[pt];
@@ -1622,11 +1622,13 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
 }
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
-              hipStream_t st, int members, KsStrides str, KsFold fold) {
+              hipStream_t st, int members, KsStrides str, KsFold fold, int tcount) {
     (void)nq;
     const int W = ell + K;
+    const int TW = tcount < 0 ? W : tcount;  // targets of this launch
+    if (TW == 0) return;
     // ext (+ own digit) and 2 accumulators per member; the key once
-    const double B = 8.0 * ((double)members * (digits * W + 2.0 * W) + 2.0 * digits * W) * ((size_t)1 << logN);
+    const double B = 8.0 * ((double)members * (digits * TW + 2.0 * TW) + 2.0 * digits * TW) * ((size_t)1 << logN);
     // member groups of MC (FHE_KS_MC=4 for A/B): the key words stay in registers
     // for the MC members of a thread; 8 reads the key half as often as 4
     // (MEHP24 12.74 -> 12.69 s, DirectSort 690.8 -> 689.0 ms, profiles/r3_h)
@@ -1639,7 +1641,7 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
             constexpr int D = decltype(c)::value;
             auto go = [&](auto mcc) {
                 constexpr int MC = decltype(mcc)::value;
-                const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W,
+                const dim3 grid((unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)TW,
                                 (unsigned)((members + MC - 1) / MC));
                 launch_clocked(inst_name<D, MC>("k_ks_inner_mc"), B, k_ks_inner_mc<D, MC>, grid, dim3(NT), st, acc, ext, dntt, key, ell, W,
                                nall, alpha, members, perm, pmap_ext, mods, logN, str, fold);
@@ -1656,7 +1658,7 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
         });
         return;
     }
-    const dim3 grid((unsigned)members, (unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)W);
+    const dim3 grid((unsigned)members, (unsigned)((((size_t)1 << logN) + NT - 1) / NT), (unsigned)TW);
     dispatch_int<1, 8>(digits, [&](auto c) {
         constexpr int D = decltype(c)::value;
         launch_clocked(inst_name<D>("k_ks_inner"), B, k_ks_inner<D>, grid, dim3(NT), st, acc, ext, dntt, key, ell, W, nall, alpha,

@@ -8,6 +8,8 @@
 //     the limbs are not Q primes 0..ell-1 (extended Q u P basis).
 #pragma once
 #include <string>
+#include <utility>
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <cstddef>
@@ -242,6 +244,10 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
 // acc0/acc1 [W][n] per member: sum_j ext_j * key_j   (own-digit limbs read from dntt)
 struct KsStrides {
     size_t acc = 0, ext = 0, d = 0;  // member strides of acc [2][W][n], ext, dntt
+    // target runs (ks_inner with a target subset): grid target z is target
+    // zs0 + z for z < zn0, else zs1 + z - zn0 (default: every target)
+    int zs0 = 0, zn0 = 1 << 30, zs1 = 0;
+    __host__ __device__ int target_of(int z) const { return z < zn0 ? zs0 + z : zs1 + (z - zn0); }
 };
 // optional HMult fold: limb ell-1 of the accumulators starts at w * d[k], w * d[seg + k]
 struct KsFold {
@@ -249,9 +255,10 @@ struct KsFold {
     size_t seg = 0, member = 0;
     u64 w = 0, ws = 0;       // P mod q_{ell-1} and its Shoup companion
 };
+// (tcount >= 0: only tcount targets, through str's target runs)
 void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nq, int nall,
               int alpha, int digits, const uint32_t *perm, const int *pmap_ext, const Mod *mods, int logN,
-              hipStream_t st, int members, KsStrides str, KsFold fold = KsFold());
+              hipStream_t st, int members, KsStrides str, KsFold fold = KsFold(), int tcount = -1);
 // ModUp's forward NTT split in two for the relinearisation (ntt.hip): the
 // column pass alone over the mapped limbs (as ntt_forward_mapped), then
 // ntt_row_ks -- the row pass of every digit's target limb fused with the
@@ -261,9 +268,18 @@ void ks_inner(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell
 // ks_inner.  Members in blocks of 16 (one transform each, one row per block).
 void ntt_forward_mapped_cols(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,
                              const NttTables &T, hipStream_t st);
+// fp_only: the targets of integer-class primes are left to the caller (their
+// row pass: ntt_forward_mapped_rows; their inner product: ks_inner over the
+// integer runs, ntt_class_runs) -- measured faster there
 void ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nall, int alpha,
                 int digits, const int *pmap_ext, int members, KsStrides str, KsFold fold, const NttTables &T,
-                hipStream_t st);
+                hipStream_t st, bool fp_only = false);
+// the row pass alone over mapped limbs (second half of ntt_forward_mapped)
+void ntt_forward_mapped_rows(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,
+                             const NttTables &T, hipStream_t st);
+// the limbs z < count of a prime map (pmap, registered; null = identity) whose
+// class is FP (fp = true) or integer, as runs (start, length)
+std::vector<std::pair<int, int>> ntt_class_runs(const int *pmap, int count, bool fp, const NttTables &T);
 // several key switches in one launch (hoisted rotations by different
 // amounts, or one rotation per member of a batch): member m < count uses key
 // keys[m] and reads ext through perm[m]; strides in `str` (0 = shared input)

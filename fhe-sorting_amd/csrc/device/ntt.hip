@@ -1515,28 +1515,44 @@ void ntt_forward_mapped_cols(u64 *data, int count, int segs, size_t seg, const i
     dispatch<true, true, NTT_PLAIN>(k1, data, count, segs, seg, pmap, smap, T, F, st);
 }
 
+void ntt_forward_mapped_rows(u64 *data, int count, int segs, size_t seg, const int *smap, const int *pmap,
+                             const NttTables &T, hipStream_t st) {
+    if (count <= 0 || segs <= 0) return;
+    const int k2 = T.logN - (T.logN + 1) / 2;
+    const NttFuse F;
+    dispatch<false, true, NTT_PLAIN>(k2, data, count, segs, seg, pmap, smap, T, F, st);
+}
+
+std::vector<std::pair<int, int>> ntt_class_runs(const int *pmap, int count, bool fp, const NttTables &T) {
+    std::vector<int> pr;
+    const bool known = launch_primes(pmap, count, pr);
+    std::vector<std::pair<int, int>> runs;
+    for (int z = 0; z < count; ++z) {
+        const bool f = ntt_fp_enabled() && T.fp_host && known && T.fp_host[pr[z]] != 0;
+        if (f != fp) continue;
+        if (!runs.empty() && runs.back().first + runs.back().second == z) ++runs.back().second;
+        else runs.emplace_back(z, 1);
+    }
+    return runs;
+}
+
 void ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int ell, int K, int nall, int alpha,
                 int digits, const int *pmap_ext, int members, KsStrides str, KsFold fold, const NttTables &T,
-                hipStream_t st) {
+                hipStream_t st, bool fp_only) {
     const int W = ell + K;
     if (T.logN != 16 && T.logN != 17) throw std::invalid_argument("ntt_row_ks: the row pass is 256 points (rings 2^16, 2^17)");
     if (digits < 1 || digits > 8) throw std::invalid_argument("ntt_row_ks: 1..8 digits");
     if (members < 1) return;
     std::vector<int> pr;
     const bool known = launch_primes(pmap_ext, W, pr);
+    (void)pr;
     // the column pass (launch_pass) classed the limbs through the ModUp map; the
     // row pass here must class them the same way, so the map must be known
     if (!known && ntt_fp_enabled() && T.fp_host) throw std::invalid_argument("ntt_row_ks: unregistered prime map");
     const bool full = members % 16 == 0;
     const dim3 blk(NTB);
-    for (int cls = 0; cls < 2; ++cls) {
-        std::vector<std::pair<int, int>> runs;
-        for (int z = 0; z < W; ++z) {
-            const bool fp = ntt_fp_enabled() && T.fp_host && known && T.fp_host[pr[z]] != 0;
-            if (fp != (cls == 1)) continue;
-            if (!runs.empty() && runs.back().first + runs.back().second == z) ++runs.back().second;
-            else runs.emplace_back(z, 1);
-        }
+    for (int cls = fp_only ? 1 : 0; cls < 2; ++cls) {
+        const std::vector<std::pair<int, int>> runs = ntt_class_runs(pmap_ext, W, cls == 1, T);
         for (size_t r = 0; r < runs.size(); r += 2) {
             NttFuse Fz;
             Fz.zs0 = runs[r].first;

@@ -330,9 +330,9 @@ struct Engine::Impl {
     // ciphertext batch): member m of an input sits at m * stride.
     //
     // ext[m][j][t] (NTT form) for all digits of d[m] ([ell][n], NTT form)
-    // FHE_KS_FUSE (A/B, default 0 until measured on the GPU): the relinearisation
-    // runs ModUp's forward row pass fused with the key-switch inner product
-    // (dev::ntt_row_ks)
+    // FHE_KS_FUSE (A/B; default 0 until the GPU suite ran it): the relinearisation runs ModUp's forward row
+    // pass fused with the key-switch inner product for the FP-class targets
+    // (dev::ntt_row_ks; integer targets keep the row pass + ks_inner)
     bool ks_fuse(int members) const {
         static const int on = [] {
             const char *e = std::getenv("FHE_KS_FUSE");
@@ -355,10 +355,16 @@ struct Engine::Impl {
         dev::modup_convert(e, c, (int)ell, P.K, P.alpha, digits, members, ell * nn, es, ext(ell), modup_tab,
                            LT.modup_off[ell].data(), mods, P.logN, st);
         const size_t mo = LT.modup_map_off[ell];
-        if (cols_only)
-            dev::ntt_forward_mapped_cols(e, (int)LT.modup_map_cnt[ell], members, es, modup_smap + mo, modup_pmap + mo, T,
-                                         st);
-        else
+        if (cols_only) {
+            // the column pass for every limb; the row pass here only for the
+            // integer-class primes (the FP targets' row pass runs fused with the
+            // inner product, mul_tail)
+            const int cnt = (int)LT.modup_map_cnt[ell];
+            dev::ntt_forward_mapped_cols(e, cnt, members, es, modup_smap + mo, modup_pmap + mo, T, st);
+            for (auto &r : dev::ntt_class_runs(modup_pmap + mo, cnt, false, T))
+                dev::ntt_forward_mapped_rows(e, r.second, members, es, modup_smap + mo + r.first,
+                                             modup_pmap + mo + r.first, T, st);
+        } else
             dev::ntt_forward_mapped(e, (int)LT.modup_map_cnt[ell], members, es, modup_smap + mo, modup_pmap + mo, T, st);
         return extm;
     }
@@ -449,10 +455,22 @@ struct Engine::Impl {
         fold.member = 2 * ell * nn;
         fold.w = LT.pmod[ell - 1];
         fold.ws = LT.pmod_s[ell - 1];
-        if (fused)
+        if (fused) {
+            // FP targets: row pass + inner product fused; integer targets (q_0 and
+            // the special primes): their row pass ran in modup, ks_inner here
             dev::ntt_row_ks(acc, e, d2, static_cast<u64 *>(ks->relin->p), (int)ell, P.K, (int)P.nall(), P.alpha, digits,
-                            ext(ell), members, str, fold, T, st);
-        else
+                            ext(ell), members, str, fold, T, st, /*fp_only*/ true);
+            const auto runs = dev::ntt_class_runs(ext(ell), (int)W, false, T);
+            for (size_t r = 0; r < runs.size(); r += 2) {
+                dev::KsStrides s2 = str;
+                s2.zs0 = runs[r].first;
+                s2.zn0 = runs[r].second;
+                s2.zs1 = r + 1 < runs.size() ? runs[r + 1].first : 0;
+                const int cnt = runs[r].second + (r + 1 < runs.size() ? runs[r + 1].second : 0);
+                dev::ks_inner(acc, e, d2, static_cast<u64 *>(ks->relin->p), (int)ell, P.K, (int)P.nq(), (int)P.nall(),
+                              P.alpha, digits, nullptr, ext(ell), mods, P.logN, st, members, s2, fold, cnt);
+            }
+        } else
             dev::ks_inner(acc, e, d2, static_cast<u64 *>(ks->relin->p), (int)ell, P.K, (int)P.nq(), (int)P.nall(),
                           P.alpha, digits, nullptr, ext(ell), mods, P.logN, st, members, str, fold);
         dev::ntt_inverse(acc + (ell - 1) * nn, (int)K + 1, segs, W * nn, ext(ell) + (ell - 1), T, st, /*raw*/ true);
