@@ -330,13 +330,13 @@ struct Engine::Impl {
     // ciphertext batch): member m of an input sits at m * stride.
     //
     // ext[m][j][t] (NTT form) for all digits of d[m] ([ell][n], NTT form)
-    // FHE_KS_FUSE (A/B; default 0 until the GPU suite ran it): the relinearisation runs ModUp's forward row
+    // FHE_KS_FUSE (A/B, default 1; 548.2 -> 537.8 ms, profiles/r5_g): the relinearisation runs ModUp's forward row
     // pass fused with the key-switch inner product for the FP-class targets
     // (dev::ntt_row_ks; integer targets keep the row pass + ks_inner)
     bool ks_fuse(int members) const {
         static const int on = [] {
             const char *e = std::getenv("FHE_KS_FUSE");
-            return e ? std::atoi(e) : 0;
+            return e ? std::atoi(e) : 1;
         }();
         return on && members >= 4 && (P.logN == 16 || P.logN == 17);
     }
