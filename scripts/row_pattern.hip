@@ -28,14 +28,14 @@ typedef unsigned long long v2u __attribute__((ext_vector_type(2)));
 template <bool NT>
 __global__ __launch_bounds__(256) void k_flat16(u64 *a, const u64 *src) {
     const size_t base = ((size_t)blockIdx.x * 16) * 512 + 2 * threadIdx.x;
-    v2u x[8];
+    v2u x[16];  // 256 lanes x 16 B x 16 = the block's 8192 words
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < 16; ++r) {
         const v2u *p = reinterpret_cast<const v2u *>(src + base + r * 512);
         x[r] = NT ? __builtin_nontemporal_load(p) : *p;
     }
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < 16; ++r) {
         v2u *p = reinterpret_cast<v2u *>(a + base + r * 512);
         v2u v = x[r];
         v.x += 1;
