@@ -468,6 +468,24 @@ __device__ __forceinline__ void row_twiddles(TW *twl, const TW *tw, size_t row, 
     const int j = e - twl_off<FWD>(S);
     twl[e] = FWD ? tw[((size_t)1 << (S0 + S)) + (row << S) + j] : tw[(n >> (S + 1)) + (row << (7 - S)) + j];
 }
+// the tables of R consecutive rows row0 .. row0 + R - 1 (R <= TWL_ROWS), row r
+// at twl + 256 r: a block whose 16 transforms are 16 / R segments x R rows
+// (launch_pass: lsegb >= 2) reads each row's twiddles from HBM / L2 once
+constexpr int TWL_ROWS = 4;
+template <bool FWD, class TW>
+__device__ __forceinline__ void row_twiddles_multi(TW *twl, const TW *tw, size_t row0, int R, size_t n, int S0) {
+    const size_t rows = n >> 8;
+    for (int e = threadIdx.x; e < 255 * R; e += blockDim.x) {
+        const int r = e / 255, f = e - 255 * r;
+        if (row0 + (size_t)r >= rows) break;  // (grids cover whole rows; never taken)
+        int S = 0;
+        while (S < 7 && f >= twl_off<FWD>(S + 1)) ++S;
+        const int j = f - twl_off<FWD>(S);
+        const size_t row = row0 + (size_t)r;
+        twl[256 * r + f] =
+            FWD ? tw[((size_t)1 << (S0 + S)) + (row << S) + j] : tw[(n >> (S + 1)) + (row << (7 - S)) + j];
+    }
+}
 template <bool FWD, int S, bool TWL, bool FP>
 __device__ __forceinline__ void row_stage(u64 *x, int t, size_t row, const TwT<FP> *tw, size_t n, int S0,
                                           const Ar &A) {
@@ -708,11 +726,13 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
         }
     };
     if constexpr (SH) {
-        if constexpr (TWL) {  // every transform of the block is row blockIdx.y
-            __shared__ TW twl[256];
-            row_twiddles<true>(twl, tw, tid_global, n, S0);
+        if constexpr (TWL) {  // the block's rows blockIdx.y R .. + R - 1, R = 16 >> lsegb <= TWL_ROWS
+            __shared__ TW twl[TWL_ROWS * 256];
+            const int R = 16 >> F.lsegb;
+            const size_t row0 = (size_t)blockIdx.y * R;
+            row_twiddles_multi<true>(twl, tw, row0, R, n, S0);
             __syncthreads();
-            row_pass_shfl<true, true, FP>(x, t, tid_global, twl, n, S0, A);
+            row_pass_shfl<true, true, FP>(x, t, tid_global, twl + 256 * (int)(tid_global - row0), n, S0, A);
         } else {
             row_pass_shfl<true, false, FP>(x, t, tid_global, tw, n, S0, A);
         }
@@ -913,11 +933,13 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
             x[2 * m] = FP ? ubits(fp_in(v.x, fin)) : v.x;
             x[2 * m + 1] = FP ? ubits(fp_in(v.y, fin)) : v.y;
         }
-        if constexpr (TWL) {  // every transform of the block is row blockIdx.y
-            __shared__ TW twl[256];
-            row_twiddles<false>(twl, tw, tid_global, n, 0);
+        if constexpr (TWL) {  // the block's rows blockIdx.y R .. + R - 1, R = 16 >> lsegb <= TWL_ROWS
+            __shared__ TW twl[TWL_ROWS * 256];
+            const int R = 16 >> F.lsegb;
+            const size_t row0 = (size_t)blockIdx.y * R;
+            row_twiddles_multi<false>(twl, tw, row0, R, n, 0);
             __syncthreads();
-            row_pass_shfl<false, true, FP>(x, t, tid_global, twl, n, 0, A);
+            row_pass_shfl<false, true, FP>(x, t, tid_global, twl + 256 * (int)(tid_global - row0), n, 0, A);
         } else {
             row_pass_shfl<false, false, FP>(x, t, tid_global, tw, n, 0, A);
         }
@@ -1097,9 +1119,10 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(TWL ? FHE_N
     ntt_inv_body<8, 4, false, true, FULL, TWL, FP>(data, seg, pmap, smap, logN, Tb, F);
 }
 // ModUp's forward row pass fused with the key-switch inner product (HMult
-// relinearisation; kernels.hpp ntt_row_ks).  Block: one row (256 points) of
-// one target limb t for 16 members, one 16-lane transform per member, the
-// row's twiddles staged in LDS.  For each digit j the lane group either loads
+// relinearisation; kernels.hpp ntt_row_ks).  Block: 16 transforms of one
+// target limb t = 2^lmb members x 16 / 2^lmb rows (2^lmb = 16 for wide
+// batches; 4 or 8 when a sharded rank holds fewer members, so no lane idles),
+// one 16-lane transform each, the rows' twiddles staged in LDS.  For each digit j the lane group either loads
 // the own-digit limb dntt[t] (NTT form already) or runs the row pass on
 // ext[j][t] (after its column pass), then multiplies by the key rows of digit
 // j and accumulates; acc[m][0][t] and acc[m][1][t] are written once.  The
@@ -1113,16 +1136,17 @@ template <int D, bool FP, bool FULL>
 __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FHE_ROW_KS_WPE, 8))) void k_ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
                                                     int ell, int W, int nall, int alpha, int members,
                                                     const int *pmap_ext, int logN, NttTables Tb, KsStrides st,
-                                                    KsFold fold, NttFuse Fz) {
+                                                    KsFold fold, NttFuse Fz, int lmb) {
     using TW = TwT<FP>;
-    __shared__ TW twl[256];
+    __shared__ TW twl[TWL_ROWS * 256];
     const size_t n = (size_t)1 << logN;
     const int t = Fz.limb_of(blockIdx.z);
     const int pt = __builtin_amdgcn_readfirstlane(pmap_ext[t]);
     const int tr = threadIdx.x >> 4, tl = threadIdx.x & 15;
-    const int mb = (int)blockIdx.x * 16 + tr;
+    const int R = 16 >> lmb;  // rows per block
+    const int mb = ((int)blockIdx.x << lmb) + (tr & ((1 << lmb) - 1));
     const bool valid = FULL || mb < members;
-    const size_t row = blockIdx.y, rb = row * 256;
+    const size_t row0 = (size_t)blockIdx.y * R, row = row0 + (tr >> lmb), rb = row * 256;
     const Mod md = Tb.mods[pt];
     const u64 q = md.q, q2 = 2 * q;
     Ar A{4 * q, (u64)0 - q, 0.0, 0.0};
@@ -1136,8 +1160,9 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FHE_ROW_KS_
         tw = Tb.fwd2 + (size_t)pt * n;
     }
     const int S0 = logN - 8;
-    row_twiddles<true>(twl, tw, row, n, S0);
+    row_twiddles_multi<true>(twl, tw, row0, R, n, S0);
     __syncthreads();
+    const TW *twr = twl + 256 * (tr >> lmb);
     const size_t m = valid ? (size_t)mb : 0;
     // element r of a lane sits at in-row index row_final_index<true>(tl, r) =
     // lane part + a compile-time register part
@@ -1175,7 +1200,7 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FHE_ROW_KS_
                 const u64 v = valid ? src[tl + 16 * r] : 0;
                 x[r] = FP ? ubits(fp_in(v, fin)) : v;
             }
-            row_pass_shfl<true, true, FP>(x, tl, row, twl, n, S0, A);
+            row_pass_shfl<true, true, FP>(x, tl, row, twr, n, S0, A);
             if constexpr (!FP) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) x[r] = canon12(x[r], q, q2);
@@ -1272,7 +1297,8 @@ void launch_pass_one(u64 *data, int limbs, int segs, size_t seg, const int *pmap
                 dim3(NTHR));
 #define FHE_NTT_LAUNCH(K, FF) \
     hipExtLaunchKernelGGL((K), grid, dim3(NTHR), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
-    const bool twl = sh && Fs.lsegb == 4 && row_twl_enabled() != 0;
+    // staged row twiddles when a block holds at most TWL_ROWS rows (>= 4 segments)
+    const bool twl = sh && (16 >> Fs.lsegb) <= TWL_ROWS && row_twl_enabled() != 0;
     if (FWD && sh) {
         if (full && twl) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, true, FP>), Fs);
         else if (full) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, false, FP>), Fs);
@@ -1549,7 +1575,10 @@ void ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int e
     // the column pass (launch_pass) classed the limbs through the ModUp map; the
     // row pass here must class them the same way, so the map must be known
     if (!known && ntt_fp_enabled() && T.fp_host) throw std::invalid_argument("ntt_row_ks: unregistered prime map");
-    const bool full = members % 16 == 0;
+    // 2^lmb members per block (16 / 2^lmb rows): the largest power of two <= members, 4..16
+    int lmb = 4;
+    while (lmb > 2 && (1 << lmb) > members) --lmb;
+    const bool full = members % (1 << lmb) == 0;
     const dim3 blk(NTB);
     for (int cls = fp_only ? 1 : 0; cls < 2; ++cls) {
         const std::vector<std::pair<int, int>> runs = ntt_class_runs(pmap_ext, W, cls == 1, T);
@@ -1559,7 +1588,8 @@ void ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int e
             Fz.zn0 = runs[r].second;
             Fz.zs1 = r + 1 < runs.size() ? runs[r + 1].first : 0;
             const int cnt = runs[r].second + (r + 1 < runs.size() ? runs[r + 1].second : 0);
-            const dim3 grid((unsigned)((members + 15) / 16), (unsigned)(1u << (T.logN - 8)), (unsigned)cnt);
+            const dim3 grid((unsigned)((members + (1 << lmb) - 1) >> lmb), (unsigned)((1u << (T.logN - 8)) >> (4 - lmb)),
+                            (unsigned)cnt);
             // ext rows (digits - 1 or digits per target) + own-digit rows + 2 accumulators per member; keys once
             const double bytes = 8.0 * ((double)members * (digits + 2.0) + 2.0 * digits) * cnt * ((size_t)1 << T.logN);
             dispatch_int<1, 8>(digits, [&](auto c) {
@@ -1568,7 +1598,7 @@ void ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key, int e
                     constexpr bool FPV = decltype(fpc)::value, FU = decltype(fullc)::value;
                     launch_clocked(inst_name<DD, FPV, FU>("k_ntt_row_ks"), bytes, k_ntt_row_ks<DD, FPV, FU>, grid, blk,
                                    st, acc, ext, dntt, key, ell, W, nall, alpha, members, pmap_ext, T.logN, T, str,
-                                   fold, Fz);
+                                   fold, Fz, lmb);
                 };
                 if (cls && full) go(std::true_type{}, std::true_type{});
                 else if (cls) go(std::true_type{}, std::false_type{});

@@ -573,11 +573,13 @@ def test_relinearised_products_large_rings(logN, L):
         same(gpu.member(st, m), orc.mul(xs[m], xs[1]))
     assert np.max(np.abs(gpu.decrypt(gpu.mul(gx[0], gx[1])) - orc.decrypt(orc.mul(xs[0], xs[1])))) < 1e-9
     # stacks of >= 4 members relinearise through dev::ntt_row_ks (ModUp's row pass
-    # fused with the key-switch inner product; round 5): 16 members (full blocks)
-    # and 20 (a partial block), at the top level and two levels down
+    # fused with the key-switch inner product; round 5): 16 members (full blocks),
+    # 20 (a partial block), 8 (8 members x 2 rows per block) and 5 two levels
+    # down (4 members x 4 rows per block, partial); the narrow ciphertext ops of
+    # those batches stage 2-4 rows of twiddles per block
     ys = [orc.encrypt(rng.uniform(-1, 1, 64), 64) for _ in range(20)]
     gy = [gpu.from_oracle(y) for y in ys]
-    for cnt in (16, 20):
+    for cnt in (16, 20, 8):  # 16 members per block (full, partial); 8 per block x 2 rows
         st = gpu.mul(gpu.stack(gy[:cnt]), gpu.stack(gy[::-1][:cnt]))
         for m in (0, 7, cnt - 1):
             same(gpu.member(st, m), orc.mul(ys[m], ys[::-1][m]))
