@@ -1376,6 +1376,39 @@ bool launch_primes(const int *pmap, int limbs, std::vector<int> &out) {
     for (int z = 0; z < limbs; ++z) out[z] = it->second[off + z];
     return true;
 }
+// FHE_NTT_AUX (A/B, default 0 -- measured slower: 539.1 / 540.9 ms without,
+// 548.6 / 548.2 ms with, profiles/r5_j; the event fork / join costs more than the
+// overlap gains): a pass split into an FP and an integer launch
+// whose smaller launch covers at most AUX_MAX_LIMBS limbs (q_0 beside the 40-bit
+// limbs: one limb of a 1/40 share that alone would half-fill the chip for its
+// whole latency) runs the small one on an auxiliary stream, forked from and
+// joined back into the caller's stream by events, so it overlaps the big one.
+// Both launches touch disjoint limbs; everything after the pass waits for both.
+constexpr int AUX_MAX_LIMBS = 2;
+int &ntt_aux_enabled() {
+    static int v = [] {
+        const char *e = std::getenv("FHE_NTT_AUX");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+struct AuxStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+AuxStream *aux_for(hipStream_t st) {  // one per caller stream (lanes are threads with streams of their own)
+    static std::mutex mu;
+    static std::map<hipStream_t, AuxStream> m;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = m.find(st);
+    if (it != m.end()) return &it->second;
+    AuxStream a;
+    if (hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&a.join, hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    return &m.emplace(st, a).first->second;
+}
 // One launch per class (integer / FP), each over the class's limbs as at most
 // two contiguous runs (NttFuse::limb_of); more runs take more launches.  A
 // launch whose limb map is unknown on the host stays one integer launch.
@@ -1387,6 +1420,12 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
         launch_pass_one<PB, EB, COLS, FWD, MODE, false>(data, limbs, segs, seg, pmap, smap, T, F, st);
         return;
     }
+    struct Piece {
+        bool fp;
+        NttFuse G;
+        int cnt;
+    };
+    std::vector<Piece> pieces;
     for (int cls = 0; cls < 2; ++cls) {
         std::vector<std::pair<int, int>> runs;  // (start, length)
         for (int z = 0; z < limbs; ++z) {
@@ -1400,10 +1439,30 @@ void launch_pass(u64 *data, int limbs, int segs, size_t seg, const int *pmap, co
             G.zn0 = runs[r].second;
             G.zs1 = r + 1 < runs.size() ? runs[r + 1].first : 0;
             const int cnt = runs[r].second + (r + 1 < runs.size() ? runs[r + 1].second : 0);
-            if (cls) launch_pass_one<PB, EB, COLS, FWD, MODE, true>(data, cnt, segs, seg, pmap, smap, T, G, st);
-            else launch_pass_one<PB, EB, COLS, FWD, MODE, false>(data, cnt, segs, seg, pmap, smap, T, G, st);
+            pieces.push_back(Piece{cls == 1, G, cnt});
         }
     }
+    auto go = [&](const Piece &p, hipStream_t s) {
+        if (p.fp) launch_pass_one<PB, EB, COLS, FWD, MODE, true>(data, p.cnt, segs, seg, pmap, smap, T, p.G, s);
+        else launch_pass_one<PB, EB, COLS, FWD, MODE, false>(data, p.cnt, segs, seg, pmap, smap, T, p.G, s);
+    };
+    AuxStream *aux = nullptr;
+    // (not under the live clock: it books each launch's own span, so the
+    // roofline sort keeps one kernel at a time)
+    if (pieces.size() == 2 && ntt_aux_enabled() && !launch_clock() &&
+        std::min(pieces[0].cnt, pieces[1].cnt) <= AUX_MAX_LIMBS)
+        aux = aux_for(st);
+    if (!aux) {
+        for (auto &p : pieces) go(p, st);
+        return;
+    }
+    const int small = pieces[0].cnt <= pieces[1].cnt ? 0 : 1;
+    (void)hipEventRecord(aux->fork, st);
+    (void)hipStreamWaitEvent(aux->s, aux->fork, 0);
+    go(pieces[small], aux->s);
+    (void)hipEventRecord(aux->join, aux->s);
+    go(pieces[1 - small], st);
+    (void)hipStreamWaitEvent(st, aux->join, 0);
 }
 
 // pass bits -> (PB, EB): EB = ceil(PB / 2)
