@@ -113,6 +113,11 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
 #ifndef FHE_NTT_COL_SCALAR
 #define FHE_NTT_COL_SCALAR 1
 #endif
+// FP row passes with fused epilogues: load the epilogue operands before the
+// butterflies (1, as the integer passes) or in the store loop (0: fewer VGPRs)
+#ifndef FHE_NTT_FP_EPI_PRE
+#define FHE_NTT_FP_EPI_PRE 1
+#endif
 typedef const __attribute__((address_space(4))) u64 const_u64_t;
 __device__ __forceinline__ ulonglong2 scalar_tw(const ulonglong2 *p, size_t i) {
     const const_u64_t *q = (const const_u64_t *)p + 2 * i;
@@ -663,8 +668,10 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // accumulators and d) are loaded now, so the loads overlap the butterflies
     // instead of stalling the store loop (the tile's LDS bounds occupancy, the
     // extra VGPRs do not)
-    constexpr bool EPI_X = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL || MODE == NTT_KSFINISH);
-    constexpr bool EPI_D = !COLS && (MODE == NTT_MULTAIL || MODE == NTT_KSFINISH);
+    // (FP rows: FHE_NTT_FP_EPI_PRE=0 loads them in the store loop instead -- A/B)
+    constexpr bool EPI_X = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL || MODE == NTT_KSFINISH) &&
+                           (!FP || FHE_NTT_FP_EPI_PRE);
+    constexpr bool EPI_D = !COLS && (MODE == NTT_MULTAIL || MODE == NTT_KSFINISH) && (!FP || FHE_NTT_FP_EPI_PRE);
     // key-switch finish: only c0 segments (even z) take the added polynomial
     const bool has_d = MODE == NTT_KSFINISH ? (F.d != nullptr && !(zseg & 1)) : true;
     const size_t d_base = MODE == NTT_KSFINISH ? (size_t)(zseg >> 1) * F.seg_d : (size_t)zseg * F.seg_d;
@@ -717,9 +724,10 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
             const u64 o = shoup_fold(tt, c1, c1s, nq);
             F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
         } else if (MODE == NTT_KSFINISH) {  // (acc - v) P^-1 + d, acc + 12q - v < 13q
-            const u64 acc = ex[EPI_X ? r : 0];
+            const u64 acc = EPI_X ? ex[EPI_X ? r : 0] : F.x[z * F.seg_x + lo + idx];
             u64 o = shoup_fold(acc + 3 * q4 - v, c1, c1s, nq);
-            o = (o >= q ? o - q : o) + ed[EPI_D ? r : 0];  // d = 0 on c1 segments
+            const u64 dv = EPI_D ? ed[EPI_D ? r : 0] : (has_d ? F.d[d_base + lo + idx] : 0);
+            o = (o >= q ? o - q : o) + dv;  // d = 0 on c1 segments
             F.out[z * F.seg_out + lo + idx] = o >= q ? o - q : o;
         } else {
             a[tid_global * LEN + idx] = canon12(v, q, q2);
