@@ -36,6 +36,17 @@ int ceil_log2(long x) {
 void trim_zeros(std::vector<double> &a) {
     while (a.size() > 1 && a.back() == 0.0) a.pop_back();
 }
+// leaves per linear-sum pass: every leaf of a pass shares one read of the baby
+// steps (dev::LEAF_G = 32 per leaf-sum launch; FHE_PS_CHUNK for A/B timing,
+// 16 = the round-4 passes)
+size_t ps_chunk() {
+    static const size_t v = [] {
+        const char *e = std::getenv("FHE_PS_CHUNK");
+        const int c = e ? std::atoi(e) : 16;
+        return (size_t)std::min(32, std::max(1, c));
+    }();
+    return v;
+}
 
 // Levels OpenFHE's EvalChebyshevSeriesPS consumes for a degree-d series: the
 // reference's multDepth tables (src/sort_algo.h:87-201) budget these, and its
@@ -170,13 +181,9 @@ struct PSEval {
     void evaluate_chunk(size_t first) {
         const int target = leaves[first].target;
         const bool raw = leaves[first].raw;
-        // up to 16 leaves per linear-sum pass (one read of the baby steps for all
-        // of them; FHE_PS_CHUNK for A/B timing)
-        static const size_t max_chunk = [] {
-            const char *e = std::getenv("FHE_PS_CHUNK");
-            const int v = e ? std::atoi(e) : 16;
-            return (size_t)std::min(16, std::max(1, v));
-        }();
+        // up to ps_chunk() leaves per linear-sum pass (one read of the baby steps
+        // for all of them)
+        const size_t max_chunk = ps_chunk();
         std::vector<size_t> chunk;
         for (size_t i = first; i < leaves.size() && chunk.size() < max_chunk; ++i)
             if (leaves[i].target == target && leaves[i].raw == raw && !ready.count(i) && has_terms(leaves[i].a))
@@ -534,12 +541,13 @@ struct PSOpenFHE {
         for (int j = 1; j < m; ++j) t = twice_prod(*t, *T2[j], T2[0].get(), -1.0);
         return t;
     }
-    // leaves sharing (target, raw) are evaluated up to 16 per linear-sum pass
-    // (the leaf-sum kernel's outputs; any grouping gives the same words)
+    // leaves sharing (target, raw) are evaluated up to ps_chunk() per linear-sum
+    // pass (the leaf-sum kernel's outputs; any grouping gives the same words)
     void evaluate_chunk(size_t first) {
         const OFLeaf &L0 = P->leaves[first];
         std::vector<size_t> chunk;
-        for (size_t i = first; i < P->leaves.size() && chunk.size() < 16; ++i)
+        const size_t max_chunk = ps_chunk();
+        for (size_t i = first; i < P->leaves.size() && chunk.size() < max_chunk; ++i)
             if (P->leaves[i].mm == L0.mm && P->leaves[i].raw == L0.raw && !ready.count(i)) chunk.push_back(i);
         std::vector<int> idx;
         for (size_t c : chunk)

@@ -399,6 +399,30 @@ __device__ __forceinline__ u64 combine_rows(const v4i (&v)[4], const Mod &m) {
     a.hi = (u64)(L[0] >> 63) + (u64)(L[1] >> 32) + c + (u64)L[2] + ((u64)L[3] << 32) + (1ull << 62);
     return reduce128(a, m);
 }
+// combine_rows plus a (< 2q), canonical, with one two-term Shoup step for the
+// 128-bit value lo + 2^64 hi: lo * 1 - floor(lo w1s / 2^64) q and hi r64 -
+// floor(hi r64s / 2^64) q are each in [0, 2q) (w1s = floor(2^64 / q)), so
+// r = lo + hi r64 - (both quotients) q + a lies in [0, 6q) (< 2^64: q < 2^61)
+// and three conditional subtractions finish it.  Same residue as
+// add_mod(combine_rows(v), a) (round 5: about half its instructions).
+__device__ __forceinline__ u64 combine_rows_add(const v4i (&v)[4], const Mod &m, u64 w1s, u64 a) {
+    int64_t L[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+        const int32_t p = v[kk][0] + (v[kk][1] << 8), q = v[kk][2] + (v[kk][3] << 8);
+        L[kk] = (int64_t)p + ((int64_t)q << 16);
+    }
+    const u64 lo = (u64)L[0] + ((u64)L[1] << 32);
+    const u64 c = lo < (u64)L[0];
+    const u64 hi = (u64)(L[0] >> 63) + (u64)(L[1] >> 32) + c + (u64)L[2] + ((u64)L[3] << 32) + (1ull << 62);
+    u64 r = lo + hi * m.r64 - (mulhi(lo, w1s) + mulhi(hi, m.r64s)) * m.q + a;
+    const u64 q2 = 2 * m.q, q4 = 4 * m.q;
+    r = r >= q4 ? r - q4 : r;
+    r = r >= q2 ? r - q2 : r;
+    return r >= m.q ? r - m.q : r;
+}
+// floor(2^64 / q) from the Barrett constant floor(2^2k / q) (k >= 32)
+__device__ __forceinline__ u64 shoup_one(const Mod &m) { return m.mu >> (2 * m.k - 64); }
 // the per-output constant C0 * sum_i c_i - 2^126 mod q
 __device__ __forceinline__ u64 sums_constant(u64 csum, const Mod &m) {
     const u64 b126 = mul_shoup(reduce64(1ull << 62, m), m.r64, m.r64s, m.q);
@@ -449,6 +473,12 @@ __device__ __forceinline__ v4i bytes_of(u64 y0, u64 y1) {
     return v4i{(int)(uint32_t)y0, (int)(uint32_t)(y0 >> 32), (int)(uint32_t)y1, (int)(uint32_t)(y1 >> 32)};
 }
 
+// k-slot order (hi x, hi y, lo x, lo y) of k_leaf_sums_mfma's fragments
+__device__ __forceinline__ v4i bytes_hilo(u64 y0, u64 y1) {
+    return v4i{(int)(uint32_t)(y0 >> 32), (int)(uint32_t)(y1 >> 32), (int)(uint32_t)y0, (int)(uint32_t)y1};
+}
+typedef int v16i __attribute__((ext_vector_type(16)));
+
 // Coefficients per block of the leaf sums: wide launches take 4096 (round 3:
 // 2238-2245 us against 2303-2305 us at 1024 per launch, profiles/r3_mfma); narrow
 // ones (one ciphertext: the bootstrap's series) halve it until the grid has
@@ -483,7 +513,6 @@ template <int KS, int NG>
 __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(FHE_LF_WPE, 8))) void k_leaf_sums_mfma(LeafArgs A, size_t seg, const Mod *mods, int logN,
                                                           int chunk) {
     __shared__ u64 etab[4 * NG][8 * KS];  // byte-reversed balanced digits of each constant
-    __shared__ u64 cval[4 * NG][8 * KS];
     __shared__ u64 corr[4 * NG];
     __shared__ const u64 *xptr[8 * KS];
     __shared__ size_t xoff[8 * KS];
@@ -492,10 +521,10 @@ __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(FHE_LF_WP
     const int l = blockIdx.y;
     const Mod md = mods[l];
     const int tid = threadIdx.x;
-    for (int p = tid; p < 4 * NG * 8 * KS; p += LF_NT) {
+    const int ngr = (A.G + 3) >> 2;  // groups of four outputs in this launch (<= NG)
+    for (int p = tid; p < 4 * ngr * 8 * KS; p += LF_NT) {
         const int t = p / (8 * KS), i = p % (8 * KS);
         const u64 c = (t < A.G && i < A.m) ? smod(A.K[t * A.m + i], A.sh[t * A.m + i], md) : 0;
-        cval[t][i] = c;
         etab[t][i] = __builtin_bswap64(balanced_digits(c));
     }
     if (tid < 8 * KS) {  // padding sources read source 0 (their constants are zero)
@@ -504,15 +533,18 @@ __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(FHE_LF_WP
         xoff[tid] = (size_t)blockIdx.z * A.xseg[i] + (size_t)l * n;
     }
     __syncthreads();
-    if (tid < 4 * NG) {
+    if (tid < 4 * ngr) {
         optr[tid] = tid < A.G ? A.out[tid] : nullptr;
         u64 s = 0;
-        for (int i = 0; i < A.m; ++i) s = add_mod(s, cval[tid][i], md.q);
+        if (tid < A.G)
+            for (int i = 0; i < A.m; ++i) s = add_mod(s, smod(A.K[tid * A.m + i], A.sh[tid * A.m + i], md), md.q);
         corr[tid] = sums_constant(s, md);
     }
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
     const int ta = (lane & 15) >> 2, rr = lane & 3;  // A row: output ta of the group, shift 4 kk + rr
+    const uint32_t ab = 3 - rr;                            // window byte offset (see the products below)
+    const u64 w1s = shoup_one(md);
     const size_t oo_l = (size_t)blockIdx.z * seg + (size_t)l * n;
     for (size_t nb = (size_t)blockIdx.x * chunk + wave * 16 * LF_NC; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
          nb += LF_NT / 4 * LF_NC) {
@@ -524,35 +556,37 @@ __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(FHE_LF_WP
             const gu64 *p0 = to_global(xptr[i0]) + xoff[i0] + nb + col;
             const gu64 *p1 = to_global(xptr[i0 + 1]) + xoff[i0 + 1] + nb + col;
 #pragma unroll
-            for (int c = 0; c < LF_NC; ++c) bf[c][ks] = bytes_of(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
+            for (int c = 0; c < LF_NC; ++c) bf[c][ks] = bytes_hilo(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
         }
 #pragma unroll 1
-        for (int grp = 0; grp < NG; ++grp) {
+        for (int grp = 0; grp < ngr; ++grp) {
             const int t = 4 * grp + lg;
             u64 *o = optr[t < A.G ? t : 0] + oo_l + nb + col;
             v4i acc[LF_NC][4];
 #pragma unroll
-            for (int c = 0; c < LF_NC; ++c)
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk) acc[c][kk] = v4i{0, 0, 0, 0};
-#pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
                 const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(&etab[4 * grp + ta][8 * ks + 2 * lg]);
+                // shift_window(e, s), s = 4 kk + rr, is bytes 15 - s .. 22 - s of the
+                // 24-byte string 0^8 e 0^8: its dwords are byte-aligned extracts at
+                // offset 3 - rr, and the four row blocks share three of them per source
+                // ((lo, hi) = kk 0: (P, 0), 1: (Q, P), 2: (R, Q), 3: (0, R)).  With the
+                // k slots of a lane in the order (hi x, hi y, lo x, lo y) -- bf the same
+                // -- the fragment of row block kk is dwords 2 kk .. 2 kk + 3 of
+                // 0 0 Px Py Qx Qy Rx Ry 0 0, so the four share registers
+                const uint32_t x0 = (uint32_t)e.x, x1 = (uint32_t)(e.x >> 32);
+                const uint32_t y0 = (uint32_t)e.y, y1 = (uint32_t)(e.y >> 32);
+                const v16i sq = {0, 0, (int)__builtin_amdgcn_alignbyte(0u, x1, ab), (int)__builtin_amdgcn_alignbyte(0u, y1, ab),
+                                 (int)__builtin_amdgcn_alignbyte(x1, x0, ab), (int)__builtin_amdgcn_alignbyte(y1, y0, ab),
+                                 (int)__builtin_amdgcn_alignbyte(x0, 0u, ab), (int)__builtin_amdgcn_alignbyte(y0, 0u, ab),
+                                 0, 0, 0, 0, 0, 0, 0, 0};
+                const v4i af[4] = {__builtin_shufflevector(sq, sq, 0, 1, 2, 3), __builtin_shufflevector(sq, sq, 2, 3, 4, 5),
+                                   __builtin_shufflevector(sq, sq, 4, 5, 6, 7), __builtin_shufflevector(sq, sq, 6, 7, 8, 9)};
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk) {
-                    const int s = 4 * kk + rr;  // shift_window(e, s) of both sources
-                    u64 w0, w1;
-                    if (kk < 2) {
-                        w0 = e.x >> (8 * (7 - s));
-                        w1 = e.y >> (8 * (7 - s));
-                    } else {
-                        w0 = s == 15 ? 0 : e.x << (8 * (s - 7));
-                        w1 = s == 15 ? 0 : e.y << (8 * (s - 7));
-                    }
-                    const v4i af = bytes_of(w0, w1);
 #pragma unroll
-                    for (int c = 0; c < LF_NC; ++c)
-                        acc[c][kk] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[c][ks], acc[c][kk], 0, 0, 0);
+                    for (int c = 0; c < LF_NC; ++c)  // (first step: zero accumulator operand, an inline constant)
+                        acc[c][kk] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[kk], bf[c][ks],
+                                                                          ks ? acc[c][kk] : v4i{0, 0, 0, 0}, 0, 0, 0);
                 }
                 // one source step's windows at a time (hoisting every step's
                 // fragments ahead spilled the one-group instantiations)
@@ -568,7 +602,7 @@ __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(FHE_LF_WP
                 }
                 const u64 cr = corr[t];
 #pragma unroll
-                for (int c = 0; c < LF_NC; ++c) o[16 * c] = add_mod(add_mod(combine_rows(acc[c], md), cr, md.q), prev[c], md.q);
+                for (int c = 0; c < LF_NC; ++c) o[16 * c] = combine_rows_add(acc[c], md, w1s, cr + prev[c]);
             }
         }
     }
@@ -1425,7 +1459,7 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
                          int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st,
                          const uint8_t *sh, const int64_t *dK, const uint8_t *dsh) {
     if (limbs <= 0 || segs <= 0 || G <= 0 || m <= 0) return;
-    if (G > LEAF_G) throw std::invalid_argument("ew_linear_sum_multi: at most 16 outputs per call");
+    if (G > LEAF_G) throw std::invalid_argument("ew_linear_sum_multi: at most LEAF_G outputs per call");
     const size_t n = (size_t)1 << logN;
     if (linear_sums_on_mfma(logN) && dK && dsh && m <= LEAF_M) {
         // one pass: every series the sorts evaluate has k <= 52 baby steps (more
@@ -1446,9 +1480,11 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
             size_t ch = std::min<size_t>(LS_CH_MAX, n);
             while (ch > 256 && (n / ch) * (size_t)limbs * (size_t)segs < 2048) ch /= 2;
             const dim3 grid((unsigned)((n + ch - 1) / ch), (unsigned)limbs, (unsigned)segs);
+            // NG: the LDS table's groups of four outputs, the launch's rounded up to 1, 2, 4, 8
+            const int ngc = (G + 3) / 4 <= 1 ? 1 : (G + 3) / 4 <= 2 ? 2 : (G + 3) / 4 <= 4 ? 3 : 4;
             dispatch_int<1, 8>((A.m + 7) / 8, [&](auto ks) {
-                dispatch_int<1, 4>((G + 3) / 4, [&](auto ng) {
-                    constexpr int KS = decltype(ks)::value, NG = decltype(ng)::value;
+                dispatch_int<1, 4>(ngc, [&](auto ng) {
+                    constexpr int KS = decltype(ks)::value, NG = 1 << (decltype(ng)::value - 1);
                     launch_clocked(inst_name<KS, NG>("k_leaf_sums_mfma"), B, k_leaf_sums_mfma<KS, NG>, grid, dim3(LF_NT),
                                    st, A, seg, mods, logN, (int)ch);
                 });

@@ -190,14 +190,14 @@ void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *
 void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int limbs, int segs, size_t seg,
                    size_t xseg, const Mod *mods, int logN, hipStream_t st, bool accumulate = false,
                    const uint8_t *sh = nullptr);
-// outs[g] = sum_i (K[g*m + i] 2^sh[g*m + i] mod q_l) * x_i for g < G <= 16 (the
+// outs[g] = sum_i (K[g*m + i] 2^sh[g*m + i] mod q_l) * x_i for g < G <= 32 (the
 // Paterson-Stockmeyer leaves of one level; x_i: [segs][limbs][n] with segment
 // stride xseg[i]; outs: stride seg).  On the matrix cores (set_mfma_sums bit 1)
-// one pass reads every input once for up to 16 outputs and 64 inputs; the
+// one pass reads every input once for up to 32 outputs and 64 inputs; the
 // constants then come from the device copies dK / dsh of K / sh ([G][m]).  The
 // VALU kernel (mask bit clear, no device copies, or m > 64) takes passes of
 // <= 10 outputs x 32 inputs from the host arrays.
-constexpr int LEAF_G = 16, LEAF_M = 64;
+constexpr int LEAF_G = 32, LEAF_M = 64;
 void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,
                          int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st,
                          const uint8_t *sh, const int64_t *dK, const uint8_t *dsh);

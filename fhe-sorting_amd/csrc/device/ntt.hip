@@ -473,22 +473,33 @@ __device__ __forceinline__ void row_twiddles(TW *twl, const TW *tw, size_t row, 
     const int j = e - twl_off<FWD>(S);
     twl[e] = FWD ? tw[((size_t)1 << (S0 + S)) + (row << S) + j] : tw[(n >> (S + 1)) + (row << (7 - S)) + j];
 }
-// the tables of R consecutive rows row0 .. row0 + R - 1 (R <= TWL_ROWS), row r
-// at twl + 256 r: a block whose 16 transforms are 16 / R segments x R rows
-// (launch_pass: lsegb >= 2) reads each row's twiddles from HBM / L2 once
+// the tables of R consecutive rows row0 .. row0 + R - 1, row r at twl + 256 r:
+// a block whose 16 transforms are 16 / R segments x R rows reads each row's
+// twiddles from HBM / L2 once.  Thread f < 255 copies entry f of every row (its
+// stage and offset computed once; R <= 16 independent loads, then the stores).
+// The row-pass kernels take the table in dynamic LDS sized for their R
+// (launch_pass_one); the fused relinearisation's R <= TWL_ROWS is static.
 constexpr int TWL_ROWS = 4;
 template <bool FWD, class TW>
 __device__ __forceinline__ void row_twiddles_multi(TW *twl, const TW *tw, size_t row0, int R, size_t n, int S0) {
+    const int f = threadIdx.x;  // blockDim 256
+    if (f >= 255) return;
     const size_t rows = n >> 8;
-    for (int e = threadIdx.x; e < 255 * R; e += blockDim.x) {
-        const int r = e / 255, f = e - 255 * r;
-        if (row0 + (size_t)r >= rows) break;  // (grids cover whole rows; never taken)
-        int S = 0;
-        while (S < 7 && f >= twl_off<FWD>(S + 1)) ++S;
-        const int j = f - twl_off<FWD>(S);
-        const size_t row = row0 + (size_t)r;
-        twl[256 * r + f] =
-            FWD ? tw[((size_t)1 << (S0 + S)) + (row << S) + j] : tw[(n >> (S + 1)) + (row << (7 - S)) + j];
+    int S = 0;
+    while (S < 7 && f >= twl_off<FWD>(S + 1)) ++S;
+    const int j = f - twl_off<FWD>(S);
+    const size_t step = FWD ? ((size_t)1 << S) : ((size_t)1 << (7 - S));
+    const TW *src = (FWD ? tw + ((size_t)1 << (S0 + S)) : tw + (n >> (S + 1))) + row0 * step + j;
+    const size_t rmax = rows - 1 - row0;  // (grids cover whole rows; the clamp keeps small rings in bounds)
+#pragma unroll
+    for (int r0 = 0; r0 < 16; r0 += 4) {
+        if (r0 >= R) break;
+        TW v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = src[min((size_t)(r0 + k), rmax) * step];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (r0 + k < R && (size_t)(r0 + k) <= rmax) twl[256 * (r0 + k) + f] = v[k];
     }
 }
 template <bool FWD, int S, bool TWL, bool FP>
@@ -734,8 +745,9 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
         }
     };
     if constexpr (SH) {
-        if constexpr (TWL) {  // the block's rows blockIdx.y R .. + R - 1, R = 16 >> lsegb <= TWL_ROWS
-            __shared__ TW twl[TWL_ROWS * 256];
+        if constexpr (TWL) {  // the block's rows blockIdx.y R .. + R - 1, R = 16 >> lsegb (dynamic LDS, R x 256)
+            extern __shared__ __attribute__((aligned(16))) unsigned char row_twl_lds[];
+            TW *const twl = reinterpret_cast<TW *>(row_twl_lds);
             const int R = 16 >> F.lsegb;
             const size_t row0 = (size_t)blockIdx.y * R;
             row_twiddles_multi<true>(twl, tw, row0, R, n, S0);
@@ -941,8 +953,9 @@ __device__ __forceinline__ void ntt_inv_body(u64 *data, size_t seg, const int *p
             x[2 * m] = FP ? ubits(fp_in(v.x, fin)) : v.x;
             x[2 * m + 1] = FP ? ubits(fp_in(v.y, fin)) : v.y;
         }
-        if constexpr (TWL) {  // the block's rows blockIdx.y R .. + R - 1, R = 16 >> lsegb <= TWL_ROWS
-            __shared__ TW twl[TWL_ROWS * 256];
+        if constexpr (TWL) {  // the block's rows blockIdx.y R .. + R - 1, R = 16 >> lsegb (dynamic LDS, R x 256)
+            extern __shared__ __attribute__((aligned(16))) unsigned char row_twl_lds[];
+            TW *const twl = reinterpret_cast<TW *>(row_twl_lds);
             const int R = 16 >> F.lsegb;
             const size_t row0 = (size_t)blockIdx.y * R;
             row_twiddles_multi<false>(twl, tw, row0, R, n, 0);
@@ -1140,8 +1153,12 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(TWL ? FHE_N
 #ifndef FHE_ROW_KS_WPE
 #define FHE_ROW_KS_WPE 2
 #endif
+// D = 1 (no accumulation across digits): 4 waves per SIMD
+#ifndef FHE_ROW_KS_WPE1
+#define FHE_ROW_KS_WPE1 4
+#endif
 template <int D, bool FP, bool FULL>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FHE_ROW_KS_WPE, 8))) void k_ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(D == 1 ? FHE_ROW_KS_WPE1 : FHE_ROW_KS_WPE, 8))) void k_ntt_row_ks(u64 *acc, const u64 *ext, const u64 *dntt, const u64 *key,
                                                     int ell, int W, int nall, int alpha, int members,
                                                     const int *pmap_ext, int logN, NttTables Tb, KsStrides st,
                                                     KsFold fold, NttFuse Fz, int lmb) {
@@ -1176,23 +1193,11 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FHE_ROW_KS_
     // lane part + a compile-time register part
     const int li = row_final_index<true>(tl, 0);
 #define IDX(r) (li + (row_final_index<true>(0, r)))
-    u64 a0[16], a1[16];
     const bool folded = fold.d && t == ell - 1;
     const u64 *fd = fold.d + m * fold.member;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        u64 f0 = 0, f1 = 0;
-        if (folded && valid) {
-            f0 = mul_shoup(fd[rb + IDX(r)], fold.w, fold.ws, q);
-            f1 = mul_shoup(fd[fold.seg + rb + IDX(r)], fold.w, fold.ws, q);
-        }
-        a0[r] = FP ? ubits(fp_in(f0, FP_TWO52)) : f0;
-        a1[r] = FP ? ubits(fp_in(f1, FP_TWO52)) : f1;
-    }
-#pragma unroll 1
-    for (int j = 0; j < D; ++j) {
+    // x = digit j's row of the target limb in NTT form (own digit: dntt itself)
+    auto digit_row = [&](int j, u64(&x)[16]) {
         const int lo = j * alpha, hi = min((j + 1) * alpha, ell);
-        u64 x[16];
         if (t >= lo && t < hi) {  // own digit: the switched polynomial itself (NTT form)
             const u64 *src = dntt + m * st.d + (size_t)t * n + rb;
 #pragma unroll
@@ -1214,6 +1219,9 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FHE_ROW_KS_
                 for (int r = 0; r < 16; ++r) x[r] = canon12(x[r], q, q2);
             }
         }
+    };
+    // a += x * key_j
+    auto mac = [&](int j, const u64(&x)[16], u64(&a0)[16], u64(&a1)[16]) {
         const u64 *kb = key + (((size_t)j * 2 + 0) * nall + pt) * n + rb;
         const u64 *ka = key + (((size_t)j * 2 + 1) * nall + pt) * n + rb;
 #pragma unroll
@@ -1228,20 +1236,70 @@ __global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FHE_ROW_KS_
                 a1[r] = add_mod(a1[r], mul_barrett(x[r], c, md), q);
             }
         }
-    }
-    if (!valid) return;
+    };
+    // the folded (dropped) limb's term, scaled
+    auto fold_of = [&](int r, u64 &f0, u64 &f1) {
+        f0 = f1 = 0;
+        if (folded && valid) {
+            f0 = mul_shoup(fd[rb + IDX(r)], fold.w, fold.ws, q);
+            f1 = mul_shoup(fd[fold.seg + rb + IDX(r)], fold.w, fold.ws, q);
+        }
+    };
     u64 *o0 = acc + m * st.acc + (size_t)t * n + rb;
     u64 *o1 = acc + m * st.acc + ((size_t)W + t) * n + rb;
+    // canonical store of one accumulator value
+    auto fin = [&](u64 v) -> u64 {
+        if constexpr (FP) {  // |a| <= (D 0.51 + 1) q: one reduction, canonical
+            const double r0 = fp_reduce(dbits(v), A.q, A.qi);
+            return fp_out(r0 < 0.0 ? r0 + A.q : r0, FP_TWO52);
+        } else {
+            return v;
+        }
+    };
+    if constexpr (D == 1) {  // one digit: each value stored as it is made (no accumulator arrays)
+        u64 x[16];
+        digit_row(0, x);
+        const u64 *kb = key + (size_t)pt * n + rb;
+        const u64 *ka = key + ((size_t)nall + pt) * n + rb;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            u64 f0, f1, v0, v1;
+            fold_of(r, f0, f1);
+            const u64 b = kb[IDX(r)], c = ka[IDX(r)];
+            if constexpr (FP) {
+                const double xv = dbits(x[r]);
+                v0 = ubits(fp_in(f0, FP_TWO52) + fp_mulmod(xv, fp_in(b, FP_TWO52), A.q, A.qi));
+                v1 = ubits(fp_in(f1, FP_TWO52) + fp_mulmod(xv, fp_in(c, FP_TWO52), A.q, A.qi));
+            } else {
+                v0 = add_mod(f0, mul_barrett(x[r], b, md), q);
+                v1 = add_mod(f1, mul_barrett(x[r], c, md), q);
+            }
+            if (valid) {
+                o0[IDX(r)] = fin(v0);
+                o1[IDX(r)] = fin(v1);
+            }
+        }
+        return;
+    }
+    u64 a0[16], a1[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        u64 v0 = a0[r], v1 = a1[r];
-        if constexpr (FP) {  // |a| <= (D 0.51 + 1) q: one reduction, canonical
-            const double r0 = fp_reduce(dbits(v0), A.q, A.qi), r1 = fp_reduce(dbits(v1), A.q, A.qi);
-            v0 = fp_out(r0 < 0.0 ? r0 + A.q : r0, FP_TWO52);
-            v1 = fp_out(r1 < 0.0 ? r1 + A.q : r1, FP_TWO52);
-        }
-        o0[IDX(r)] = v0;
-        o1[IDX(r)] = v1;
+        u64 f0, f1;
+        fold_of(r, f0, f1);
+        a0[r] = FP ? ubits(fp_in(f0, FP_TWO52)) : f0;
+        a1[r] = FP ? ubits(fp_in(f1, FP_TWO52)) : f1;
+    }
+#pragma unroll 1
+    for (int j = 0; j < D; ++j) {
+        u64 x[16];
+        digit_row(j, x);
+        mac(j, x, a0, a1);
+    }
+    if (!valid) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        o0[IDX(r)] = fin(a0[r]);
+        o1[IDX(r)] = fin(a1[r]);
     }
 #undef IDX
 }
@@ -1252,6 +1310,19 @@ int &row_twl_enabled() {
     static int v = [] {
         const char *e = std::getenv("FHE_NTT_TWL");
         return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
+// FHE_NTT_TWL_ROWS (A/B, default 4): most rows per block whose twiddles are
+// staged in LDS -- blocks of >= 4 segments.  Staging the 8 / 16 rows of the
+// one- and two-segment blocks too (32 / 64 KB of dynamic LDS) measured slower:
+// k-way 2845 ms at 4, 2883 at 8, 2978 at 16; the N=1024 sort 538.1 / 538.2 at
+// 4 against 539.7 / 543.8 at 16; MEHP24 11.24 s against 11.26 s (profiles/r5_m)
+int &row_twl_rows() {
+    static int v = [] {
+        const char *e = std::getenv("FHE_NTT_TWL_ROWS");
+        return e ? std::atoi(e) : 4;
     }();
     return v;
 }
@@ -1303,10 +1374,13 @@ void launch_pass_one(u64 *data, int limbs, int segs, size_t seg, const int *pmap
     const int slot = clk ? clk->events(e0, e1) : -1;
     note_launch(FWD ? (COLS ? "k_ntt_fwd(col)" : "k_ntt_fwd(row)") : (COLS ? "k_ntt_inv(col)" : "k_ntt_inv(row)"), grid,
                 dim3(NTHR));
+    // staged row twiddles (dynamic LDS: the block's 16 >> lsegb rows x 256 entries)
+    // when a block holds at most row_twl_rows() rows
+    const int rows_blk = 16 >> Fs.lsegb;
+    const bool twl = sh && rows_blk <= row_twl_rows() && row_twl_enabled() != 0;
+    const unsigned lds_dyn = twl ? (unsigned)(rows_blk * 256 * (FP ? sizeof(double) : sizeof(TwT<false>))) : 0u;
 #define FHE_NTT_LAUNCH(K, FF) \
-    hipExtLaunchKernelGGL((K), grid, dim3(NTHR), 0, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
-    // staged row twiddles when a block holds at most TWL_ROWS rows (>= 4 segments)
-    const bool twl = sh && (16 >> Fs.lsegb) <= TWL_ROWS && row_twl_enabled() != 0;
+    hipExtLaunchKernelGGL((K), grid, dim3(NTHR), lds_dyn, st, e0, e1, 0, data, seg, pmap, smap, T.logN, T, FF)
     if (FWD && sh) {
         if (full && twl) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, true, FP>), Fs);
         else if (full) FHE_NTT_LAUNCH((k_ntt_fwd_row<MODE, true, false, FP>), Fs);

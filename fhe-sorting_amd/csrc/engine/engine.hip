@@ -1783,7 +1783,7 @@ std::vector<CtPtr> Engine::linear_sums_to(const std::vector<const Ciphertext *> 
         xseg[i] = xs[i]->limbs * nn;
     }
     std::vector<CtPtr> outs;
-    // passes of at most 16 outputs (the kernel's limit), balanced: 18 -> 9 + 9
+    // passes of at most LEAF_G = 32 outputs (the kernel's limit), balanced: 36 -> 18 + 18
     const size_t passes = (c.size() + dev::LEAF_G - 1) / dev::LEAF_G, per = (c.size() + passes - 1) / passes;
     const bool mfma = dev::linear_sums_on_mfma(LOGN) && m <= (size_t)dev::LEAF_M;
     for (size_t g0 = 0; g0 < c.size(); g0 += per) {
