@@ -38,11 +38,12 @@ void trim_zeros(std::vector<double> &a) {
 }
 // leaves per linear-sum pass: every leaf of a pass shares one read of the baby
 // steps (dev::LEAF_G = 32 per leaf-sum launch; FHE_PS_CHUNK for A/B timing,
-// 16 = the round-4 passes)
+// 16 = the round-4 passes: sort 543.1 / 546.8 -> 538.2 / 537.9 ms with the window
+// kernel, profiles/r5_o; with the folded kernel 536.3 -> 523.2, profiles/r5_p)
 size_t ps_chunk() {
     static const size_t v = [] {
         const char *e = std::getenv("FHE_PS_CHUNK");
-        const int c = e ? std::atoi(e) : 16;
+        const int c = e ? std::atoi(e) : 32;
         return (size_t)std::min(32, std::max(1, c));
     }();
     return v;

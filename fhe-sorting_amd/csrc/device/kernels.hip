@@ -505,7 +505,10 @@ struct LeafArgs {
     const uint8_t *sh;      // device [G][m]
     int m, G, accumulate;
 };
-constexpr int LF_NC = 2, LF_NT = 256;
+#ifndef FHE_LF_NC  // 16-coefficient column tiles per wave sharing one set of windows (A/B: -DFHE_LF_NC=4)
+#define FHE_LF_NC 2
+#endif
+constexpr int LF_NC = FHE_LF_NC, LF_NT = 256;
 #ifndef FHE_LF_WPE  // waves per SIMD asked of the compiler (A/B: -DFHE_LF_WPE=4)
 #define FHE_LF_WPE 3
 #endif
@@ -603,6 +606,126 @@ __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(FHE_LF_WP
                 const u64 cr = corr[t];
 #pragma unroll
                 for (int c = 0; c < LF_NC; ++c) o[16 * c] = combine_rows_add(acc[c], md, w1s, cr + prev[c]);
+            }
+        }
+    }
+}
+
+// Folded-constant leaf sums (round 5, FHE_LEAF_FOLD): the byte shifts move into
+// the constants.  With d_{t,i,a} = 256^a c_{t,i} mod q and y_i = sum_a u_{i,a} 256^a,
+//   out_t = sum_{i,a} u_{i,a} d_{t,i,a}  (mod q),
+// and d = sum_b e_b(d) 256^b in balanced digits, so the M index runs over
+// (output, digit b < 8) -- two 16-row blocks per group of four outputs instead of
+// four, half the MFMAs -- and the A fragment of (t, b) over k = (i, a) is the byte
+// string e_b(d_{t,i,0..7}): a table lookup, no windows.  The block builds the table
+// once ([group][row block][source step][lane] x 16 B, 14 KB per group at 56 sources)
+// and keeps it in LDS; every wave streams four 16-coefficient column tiles per
+// step with its B fragments in registers, so an A fragment read serves four MFMAs.
+// Rows: |v_b| < 448 * 2^14, so V = L0 + 2^32 L1 (L = four rows, < 2^47) -- one
+// 128-bit fold (combine_rows_add's two-term Shoup step, bias 2^126) per output.
+// Byte 0..6 of y are read as signed (u - 128), so out = V + 128 sum_{i, a<7} d.
+// Same residues as k_leaf_sums_mfma (exact integer sums, canonical results).
+constexpr int LFF_NT = 512, LFF_NC = 4;
+typedef int v8i __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ u64 fold_rows2(const v4i &r0, const v4i &r1, const Mod &m, u64 w1s, u64 a) {
+    const int32_t p0 = r0[0] + (r0[1] << 8), q0 = r0[2] + (r0[3] << 8);
+    const int32_t p1 = r1[0] + (r1[1] << 8), q1 = r1[2] + (r1[3] << 8);
+    const int64_t L0 = (int64_t)p0 + ((int64_t)q0 << 16), L1 = (int64_t)p1 + ((int64_t)q1 << 16);
+    const u64 lo = (u64)L0 + ((u64)L1 << 32);
+    const u64 c = lo < (u64)L0;
+    const u64 hi = (u64)(L0 >> 63) + (u64)(L1 >> 32) + c + (1ull << 62);
+    u64 r = lo + hi * m.r64 - (mulhi(lo, w1s) + mulhi(hi, m.r64s)) * m.q + a;
+    const u64 q2 = 2 * m.q, q4 = 4 * m.q;
+    r = r >= q4 ? r - q4 : r;
+    r = r >= q2 ? r - q2 : r;
+    return r >= m.q ? r - m.q : r;
+}
+template <int KS, int NG>
+__global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_leaf_sums_fold(
+    LeafArgs A, size_t seg, const Mod *mods, int logN, int chunk) {
+    __shared__ v4i afr[NG * 2 * KS * 64];       // A fragments, 1 KB per (group, row block, step)
+    __shared__ u64 psum[4 * NG][8 * KS];         // sum_{a<7} d_{t,i,a} mod q per (t, i)
+    __shared__ u64 corr[4 * NG];
+    __shared__ const u64 *xptr[8 * KS];
+    __shared__ size_t xoff[8 * KS];
+    __shared__ u64 *optr[4 * NG];
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const Mod md = mods[l];
+    const int tid = threadIdx.x;
+    const int ngr = (A.G + 3) >> 2;
+    {
+        u64 *const img = reinterpret_cast<u64 *>(afr);
+        for (int p = tid; p < 4 * ngr * 8 * KS; p += LFF_NT) {
+            const int t = p / (8 * KS), i = p % (8 * KS);
+            u64 d = (t < A.G && i < A.m) ? smod(A.K[t * A.m + i], A.sh[t * A.m + i], md) : 0;
+            u64 dig[8], s7 = 0;
+#pragma unroll
+            for (int a = 0; a < 8; ++a) {
+                dig[a] = balanced_digits(d);  // byte b = e_b(d_{t,i,a})
+                if (a < 7) s7 = add_mod(s7, d, md.q);
+                d = mul_barrett(d, 256, md);  // (q > 256)
+            }
+            psum[t][i] = s7;
+            const int grp = t >> 2, ta = t & 3, ks = i >> 3, lgi = (i & 7) >> 1, half = i & 1;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                u64 e = 0;
+#pragma unroll
+                for (int a = 0; a < 8; ++a) e |= ((dig[a] >> (8 * b)) & 255) << (8 * a);
+                const int lane = 16 * lgi + 4 * ta + (b & 3);
+                img[2 * (((grp * 2 + (b >> 2)) * KS + ks) * 64 + lane) + half] = e;
+            }
+        }
+    }
+    if (tid < 8 * KS) {  // padding sources read source 0 (their constants are zero)
+        const int i = tid < A.m ? tid : 0;
+        xptr[tid] = A.x[i];
+        xoff[tid] = (size_t)blockIdx.z * A.xseg[i] + (size_t)l * n;
+    }
+    __syncthreads();
+    if (tid < 4 * ngr) {
+        optr[tid] = tid < A.G ? A.out[tid] : nullptr;
+        u64 s = 0;
+        for (int i = 0; i < A.m; ++i) s = add_mod(s, psum[tid][i], md.q);
+        // + 128 sum d (the signed bytes) - 2^126 (fold_rows2's bias)
+        const u64 b126 = mul_shoup(reduce64(1ull << 62, md), md.r64, md.r64s, md.q);
+        corr[tid] = sub_mod(mul_barrett(s, 128, md), b126, md.q);
+    }
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
+    const u64 w1s = shoup_one(md);
+    const size_t oo_l = (size_t)blockIdx.z * seg + (size_t)l * n;
+    for (size_t nb = (size_t)blockIdx.x * chunk + wave * 16 * LFF_NC; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
+         nb += LFF_NT / 4 * LFF_NC) {
+        v4i bf[LFF_NC][KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int i0 = 8 * ks + 2 * lg;
+            const gu64 *p0 = to_global(xptr[i0]) + xoff[i0] + nb + col;
+            const gu64 *p1 = to_global(xptr[i0 + 1]) + xoff[i0 + 1] + nb + col;
+#pragma unroll
+            for (int c = 0; c < LFF_NC; ++c) bf[c][ks] = bytes_of(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
+        }
+#pragma unroll 1
+        for (int grp = 0; grp < ngr; ++grp) {
+            const int t = 4 * grp + lg;
+            v4i acc[LFF_NC][2];
+            const v4i *ag = afr + (size_t)grp * 2 * KS * 64 + lane;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const v4i a0 = ag[ks * 64], a1 = ag[(KS + ks) * 64];
+#pragma unroll
+                for (int c = 0; c < LFF_NC; ++c) {
+                    acc[c][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[c][ks], ks ? acc[c][0] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                    acc[c][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[c][ks], ks ? acc[c][1] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                }
+            }
+            if (t < A.G) {
+                u64 *o = optr[t] + oo_l + nb + col;
+                const u64 cr = corr[t];
+#pragma unroll
+                for (int c = 0; c < LFF_NC; ++c) o[16 * c] = fold_rows2(acc[c][0], acc[c][1], md, w1s, cr);  // (never accumulating)
             }
         }
     }
@@ -1454,6 +1577,17 @@ void ew_linear_sum(u64 *out, const u64 *const *xs, const int64_t *K, int m, int 
         if (m == 0) break;
     }
 }
+// FHE_LEAF_FOLD (A/B, default 1): the folded-constant leaf-sum kernel
+// (k_leaf_sums_fold) for rings >= 2^10; 0 keeps the window kernel.  Measured with
+// 32-leaf passes: leaf launch 8428 -> 6881 us, sort 531.5 / 531.5 -> 523.2 / 523.1
+// ms (profiles/r5_p)
+int leaf_fold_enabled() {
+    static const int v = [] {
+        const char *e = std::getenv("FHE_LEAF_FOLD");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
 bool linear_sums_on_mfma(int logN) { return use_mfma_sums(MF_LIN) && logN >= 8; }
 void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const size_t *xseg, const int64_t *K, int m,
                          int limbs, int segs, size_t seg, const Mod *mods, int logN, hipStream_t st,
@@ -1482,6 +1616,19 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
             const dim3 grid((unsigned)((n + ch - 1) / ch), (unsigned)limbs, (unsigned)segs);
             // NG: the LDS table's groups of four outputs, the launch's rounded up to 1, 2, 4, 8
             const int ngc = (G + 3) / 4 <= 1 ? 1 : (G + 3) / 4 <= 2 ? 2 : (G + 3) / 4 <= 4 ? 3 : 4;
+            if (leaf_fold_enabled() && n >= 2 * (size_t)LFF_NT) {
+                size_t chf = std::min<size_t>(LS_CH_MAX, n);
+                while (chf > 2 * (size_t)LFF_NT && (n / chf) * (size_t)limbs * (size_t)segs < 1024) chf /= 2;
+                const dim3 gridf((unsigned)((n + chf - 1) / chf), (unsigned)limbs, (unsigned)segs);
+                dispatch_int<1, 8>((A.m + 7) / 8, [&](auto ks) {
+                    dispatch_int<1, 4>(ngc, [&](auto ng) {
+                        constexpr int KS = decltype(ks)::value, NG = 1 << (decltype(ng)::value - 1);
+                        launch_clocked(inst_name<KS, NG>("k_leaf_sums_fold"), B, k_leaf_sums_fold<KS, NG>, gridf,
+                                       dim3(LFF_NT), st, A, seg, mods, logN, (int)chf);
+                    });
+                });
+                return;
+            }
             dispatch_int<1, 8>((A.m + 7) / 8, [&](auto ks) {
                 dispatch_int<1, 4>(ngc, [&](auto ng) {
                     constexpr int KS = decltype(ks)::value, NG = 1 << (decltype(ng)::value - 1);

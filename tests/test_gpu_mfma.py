@@ -111,7 +111,7 @@ def test_ring16_products_mfma():
 
 
 def test_leaf_sums_4096_blocks_ring16_stack32():
-    """k_leaf_sums_mfma at the width the bench runs it: ring 2^16 and a
+    """k_leaf_sums_mfma (or k_leaf_sums_fold) at the width the bench runs it: ring 2^16 and a
     32-member stack (64 segments), so the launches take the 4096-coefficient
     blocks (kernels.hip ew_linear_sum_multi: n / 4096 x limbs x segments >= 2048),
     passes of more than 8 baby steps (KS >= 2) and more than 4 leaves (NG >= 2):
@@ -130,7 +130,7 @@ def test_leaf_sums_4096_blocks_ring16_stack32():
     with F.KernelClock(gpu) as clk:
         out = gpu.cheb(st, c)
     shapes = [tuple(int(v) for v in k.split('<')[1].rstrip('>').split(','))
-              for k in clk.stats if k.startswith('k_leaf_sums_mfma<')]
+              for k in clk.stats if k.startswith(('k_leaf_sums_mfma<', 'k_leaf_sums_fold<'))]
     assert any(ks >= 2 and ng >= 2 for ks, ng in shapes), f'leaf-sum launches: {sorted(clk.stats)}'
     ref = [orc.cheb(x, c) for x in xs]
     for m in range(32):
