@@ -227,6 +227,64 @@ __global__ __launch_bounds__(NT) void k_tensor(u64 *d01, u64 *d2, const u64 *a, 
     st2(d01 + z * 2 * ln_all + ln_all + o, e1);
     st2(d2 + z * ln_all + o, e2);
 }
+// k_tensor with mul_add's summands folded into (d0, d1) (round 5): d_p of member z
+// += sum_i (K_i 2^sh_i mod q_l) x_i[2 z + p] -- the same lazy 128-bit sum and one
+// reduction as k_linear_sum accumulating into d01 after the tensor, so the words
+// are unchanged, without that pass's re-read and re-write of d01 (4 of its
+// 2 (M + 2) limb-units per member).  M <= TL_MAX summands of one limb count.
+constexpr int TL_MAX = 4;
+struct TensorLin {
+    const u64 *x[TL_MAX];
+    int64_t K[TL_MAX];
+    uint8_t sh[TL_MAX];
+    size_t xseg;  // segment stride of the summands (segment 2 member + poly)
+};
+template <int M>
+__global__ __launch_bounds__(NT) void k_tensor_lin(u64 *d01, u64 *d2, const u64 *a, const u64 *b, size_t ln_all,
+                                                   size_t sa, size_t sb, const u64 *a2, size_t sa2, TensorLin L,
+                                                   const Mod *mods, int logN) {
+    __shared__ u64 w[TL_MAX];
+    const size_t n = (size_t)1 << logN;
+    const int l = blockIdx.y;
+    const Mod m = mods[l];
+    if ((int)threadIdx.x < M) w[threadIdx.x] = smod(L.K[threadIdx.x], L.sh[threadIdx.x], m);
+    __syncthreads();
+    const size_t k = ((size_t)blockIdx.x * NT + threadIdx.x) * 2;
+    if (k >= n) return;
+    const size_t z = blockIdx.z, o = (size_t)l * n + k;
+    const u64 *A = a + z * sa, *Bp = b + z * sb;
+    ulonglong2 a0 = ld2(A + o), a1 = ld2(A + ln_all + o);
+    if (a2) {
+        const u64 *A2 = a2 + z * sa2;
+        const ulonglong2 c0 = ld2(A2 + o), c1 = ld2(A2 + ln_all + o);
+        a0 = make_ulonglong2(add_mod(a0.x, c0.x, m.q), add_mod(a0.y, c0.y, m.q));
+        a1 = make_ulonglong2(add_mod(a1.x, c1.x, m.q), add_mod(a1.y, c1.y, m.q));
+    }
+    const ulonglong2 b0 = ld2(Bp + o), b1 = ld2(Bp + ln_all + o);
+    ulonglong2 xs[2][M];  // the summands' loads issued with the operands'
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int i = 0; i < M; ++i) xs[p][i] = ld2(L.x[i] + (2 * z + p) * L.xseg + o);
+    Acc128 r[2][2];
+    r[0][0].lo = mul_barrett(a0.x, b0.x, m);
+    r[0][1].lo = mul_barrett(a0.y, b0.y, m);
+    r[1][0].lo = add_mod(mul_barrett(a0.x, b1.x, m), mul_barrett(a1.x, b0.x, m), m.q);
+    r[1][1].lo = add_mod(mul_barrett(a0.y, b1.y, m), mul_barrett(a1.y, b0.y, m), m.q);
+    ulonglong2 e2;
+    e2.x = mul_barrett(a1.x, b1.x, m);
+    e2.y = mul_barrett(a1.y, b1.y, m);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            mac128(r[p][0], xs[p][i].x, w[i]);
+            mac128(r[p][1], xs[p][i].y, w[i]);
+        }
+        st2(d01 + z * 2 * ln_all + p * ln_all + o, make_ulonglong2(reduce128(r[p][0], m), reduce128(r[p][1], m)));
+    }
+    st2(d2 + z * ln_all + o, e2);
+}
 // out [2][limbs][n] = sum over members of in [members][2][limbs][n]
 __global__ __launch_bounds__(NT) void k_sum_members(u64 *out, const u64 *in, int members, size_t ln_all,
                                                     const Mod *mods, int logN) {
@@ -1552,6 +1610,27 @@ void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int mem
     const double B = 8.0 * (5.0 * members + 2.0 * (sb ? members : 1) + (a2 ? 2.0 * members : 0.0)) * ln_all;
     launch_clocked("k_tensor", B, k_tensor, ew_grid(logN, limbs, members), dim3(NT), st, d01, d2, a, b, ln_all, sa, sb,
                    a2, sa2, mods, logN);
+}
+bool ew_tensor_lin(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int members, size_t sa, size_t sb,
+                   const u64 *const *xs, const int64_t *K, const uint8_t *sh, int m, size_t xseg, const Mod *mods,
+                   int logN, hipStream_t st, const u64 *a2, size_t sa2) {
+    if (m < 1 || m > TL_MAX || limbs <= 0 || members <= 0) return false;
+    const size_t ln_all = (size_t)limbs << logN;
+    TensorLin L{};
+    for (int i = 0; i < m; ++i) {
+        L.x[i] = xs[i];
+        L.K[i] = K[i];
+        L.sh[i] = sh ? sh[i] : 0;
+    }
+    L.xseg = xseg;
+    const double B = 8.0 * (5.0 * members + 2.0 * (sb ? members : 1) + (a2 ? 2.0 * members : 0.0) + 2.0 * m * members) *
+                     ln_all;
+    dispatch_int<1, TL_MAX>(m, [&](auto mm) {
+        constexpr int MM = decltype(mm)::value;
+        launch_clocked(inst_name<MM>("k_tensor_lin"), B, k_tensor_lin<MM>, ew_grid(logN, limbs, members), dim3(NT), st,
+                       d01, d2, a, b, ln_all, sa, sb, a2, sa2, L, mods, logN);
+    });
+    return true;
 }
 void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st) {
     if (limbs <= 0 || members <= 0) return;

@@ -184,6 +184,12 @@ void ew_mul_plain(u64 *out, const u64 *a, const u64 *p, int limbs, int segs, Seg
 // (a member m at m * sa, b member at m * sb; sb = 0 broadcasts one ciphertext)
 void ew_tensor(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int members, size_t sa, size_t sb,
                const Mod *mods, int logN, hipStream_t st, const u64 *a2 = nullptr, size_t sa2 = 0);
+// ew_tensor with d_p += sum_i (K_i 2^sh_i mod q) x_i[2 member + p] (x_i segment
+// stride xseg) for 1 <= m <= 4 summands; false (nothing launched) otherwise.
+// Word-identical to ew_tensor then ew_linear_sum(d01, ..., accumulate).
+bool ew_tensor_lin(u64 *d01, u64 *d2, const u64 *a, const u64 *b, int limbs, int members, size_t sa, size_t sb,
+                   const u64 *const *xs, const int64_t *K, const uint8_t *sh, int m, size_t xseg, const Mod *mods,
+                   int logN, hipStream_t st, const u64 *a2 = nullptr, size_t sa2 = 0);
 // out [2][limbs][n] = sum_m in [m][2][limbs][n]
 void ew_sum_members(u64 *out, const u64 *in, int members, int limbs, const Mod *mods, int logN, hipStream_t st);
 // out (+)= sum_i (K_i 2^sh_i mod q_l) * x_i   (x_i: [segs][limbs][n], common segment stride; sh may be null)

@@ -1370,6 +1370,15 @@ CtPtr Engine::mul_plain_sum(const std::vector<const Ciphertext *> &a, const std:
     return r;
 }
 
+// FHE_TENSOR_LIN (A/B, default 1): mul_add's summands folded into the tensor pass
+static bool tensor_lin_enabled() {
+    static const int on = [] {
+        const char *e = std::getenv("FHE_TENSOR_LIN");
+        return e ? std::atoi(e) : 1;
+    }();
+    return on != 0;
+}
+
 // ct x ct with relinearisation and rescale.  b may be a single ciphertext
 // multiplied into every member of a (broadcast).
 CtPtr Engine::mul(const Ciphertext &a0, const Ciphertext &b0) { return mul_add(a0, b0, {}, {}); }
@@ -1397,10 +1406,37 @@ CtPtr Engine::mul_add(const Ciphertext &a0, const Ciphertext &b0, const std::vec
     count_bytes(6.0 * ell + ks_units(ell) + 2.0 * ell * xs.size(), B);
     auto d01m = I.alloc((size_t)B * 2 * ell * nn * 8), d2m = I.alloc((size_t)B * ell * nn * 8);
     u64 *d01 = static_cast<u64 *>(d01m->p), *d2 = static_cast<u64 *>(d2m->p);
-    dev::ew_tensor(d01, d2, a->data, b->data, (int)ell, B, 2 * ell * nn, b->batch == 1 ? 0 : 2 * ell * nn, MODS,
-                   LOGN, ST, a_add ? a_add->data : nullptr, 2 * ell * nn);
     if (a_add) count_bytes(6.0 * ell, B);  // the add it replaces
-    if (!xs.empty()) {
+    // the summands folded into the tensor pass (k_tensor_lin) when they share a
+    // limb count and are at most four: no second pass over d01
+    bool fused_lin = false;
+    if (!xs.empty() && xs.size() <= 4 && tensor_lin_enabled()) {
+        const int target = a->level + 1;
+        const u64 qd = I.P.primes[I.P.L - target + 1];
+        std::vector<const u64 *> x;
+        std::vector<int64_t> k;
+        std::vector<uint8_t> sh;
+        bool one = true;
+        for (size_t i = 0; i < xs.size(); ++i) {
+            if (xs[i]->level > a->level) throw std::invalid_argument("mul_add: summand level too high");
+            if (xs[i]->batch != B) throw std::invalid_argument("mul_add: batch size mismatch");
+            one = one && xs[i]->limbs == xs[0]->limbs;
+            const host::SConst K = host::const_to_target(cs[i], I.P.delta[target], qd, xs[i]->scale);
+            x.push_back(xs[i]->data);
+            k.push_back(K.k);
+            sh.push_back((uint8_t)K.sh);
+        }
+        if (one)
+            fused_lin = dev::ew_tensor_lin(d01, d2, a->data, b->data, (int)ell, B, 2 * ell * nn,
+                                           b->batch == 1 ? 0 : 2 * ell * nn, x.data(), k.data(), sh.data(),
+                                           (int)x.size(), xs[0]->limbs * nn, MODS, LOGN, ST,
+                                           a_add ? a_add->data : nullptr, 2 * ell * nn);
+        if (fused_lin) ctr.constmult += xs.size() * B;
+    }
+    if (!fused_lin)
+        dev::ew_tensor(d01, d2, a->data, b->data, (int)ell, B, 2 * ell * nn, b->batch == 1 ? 0 : 2 * ell * nn, MODS,
+                       LOGN, ST, a_add ? a_add->data : nullptr, 2 * ell * nn);
+    if (!xs.empty() && !fused_lin) {
         const int target = a->level + 1;
         const u64 qd = I.P.primes[I.P.L - target + 1];
         struct Group {
