@@ -698,12 +698,31 @@ __device__ __forceinline__ u64 fold_rows2(const v4i &r0, const v4i &r1, const Mo
     r = r >= q2 ? r - q2 : r;
     return r >= m.q ? r - m.q : r;
 }
+// fold_rows2 for a prime q < 2^41 in fp64 (exact): 2^32 mod q = 2^32, so with
+// L0, L1 exact doubles (|L| < 2^47) b = L1 2^32 is exact, h = rint(b / q) is
+// within one of the true quotient and r1 = fma(-h, q, b) = b - h q exactly
+// (|r1| < 1.5 q); t = r1 + L0 + a is an exact integer below 2^49, and one more
+// rint / fma leaves (-q/2, q/2].  The same canonical residue as fold_rows2 (whose
+// 2^126 bias the caller's constant a does not carry here).
+constexpr u64 FOLD_FP_QMAX = 1ull << 41;
+__device__ __forceinline__ u64 fold_rows2_fp(const v4i &r0, const v4i &r1, double q, double qi, u64 a) {
+    const int32_t p0 = r0[0] + (r0[1] << 8), q0 = r0[2] + (r0[3] << 8);
+    const int32_t p1 = r1[0] + (r1[1] << 8), q1 = r1[2] + (r1[3] << 8);
+    const double L0 = (double)p0 + (double)q0 * 65536.0, L1 = (double)p1 + (double)q1 * 65536.0;  // exact
+    const double b = L1 * 4294967296.0;
+    const double h = __builtin_rint(b * qi);
+    const double t = __builtin_fma(-h, q, b) + L0 + (double)a;
+    const double h2 = __builtin_rint(t * qi);
+    double r = __builtin_fma(-h2, q, t);
+    r = r < 0.0 ? r + q : r;
+    return (u64)__double_as_longlong(r + 4503599627370496.0) ^ 0x4330000000000000ull;  // r in [0, q) < 2^52
+}
 template <int KS, int NG>
 __global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_leaf_sums_fold(
     LeafArgs A, size_t seg, const Mod *mods, int logN, int chunk) {
     __shared__ v4i afr[NG * 2 * KS * 64];       // A fragments, 1 KB per (group, row block, step)
     __shared__ u64 psum[4 * NG][8 * KS];         // sum_{a<7} d_{t,i,a} mod q per (t, i)
-    __shared__ u64 corr[4 * NG];
+    __shared__ u64 corr[4 * NG], cfp[4 * NG];
     __shared__ const u64 *xptr[8 * KS];
     __shared__ size_t xoff[8 * KS];
     __shared__ u64 *optr[4 * NG];
@@ -749,10 +768,13 @@ __global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) 
         // + 128 sum d (the signed bytes) - 2^126 (fold_rows2's bias)
         const u64 b126 = mul_shoup(reduce64(1ull << 62, md), md.r64, md.r64s, md.q);
         corr[tid] = sub_mod(mul_barrett(s, 128, md), b126, md.q);
+        cfp[tid] = mul_barrett(s, 128, md);  // (the fp64 epilogue has no bias)
     }
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
     const u64 w1s = shoup_one(md);
+    const bool fpq = md.q < FOLD_FP_QMAX;  // (uniform: one prime per block)
+    const double qd = (double)md.q, qid = 1.0 / qd;
     const size_t oo_l = (size_t)blockIdx.z * seg + (size_t)l * n;
     for (size_t nb = (size_t)blockIdx.x * chunk + wave * 16 * LFF_NC; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
          nb += LFF_NT / 4 * LFF_NC) {
@@ -781,9 +803,15 @@ __global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) 
             }
             if (t < A.G) {
                 u64 *o = optr[t] + oo_l + nb + col;
-                const u64 cr = corr[t];
+                if (fpq) {
+                    const u64 cr = cfp[t];
 #pragma unroll
-                for (int c = 0; c < LFF_NC; ++c) o[16 * c] = fold_rows2(acc[c][0], acc[c][1], md, w1s, cr);  // (never accumulating)
+                    for (int c = 0; c < LFF_NC; ++c) o[16 * c] = fold_rows2_fp(acc[c][0], acc[c][1], qd, qid, cr);
+                } else {
+                    const u64 cr = corr[t];
+#pragma unroll
+                    for (int c = 0; c < LFF_NC; ++c) o[16 * c] = fold_rows2(acc[c][0], acc[c][1], md, w1s, cr);  // (never accumulating)
+                }
             }
         }
     }
@@ -1039,6 +1067,135 @@ __global__ __launch_bounds__(NT) void k_modup_mfma(u64 *__restrict__ ext, const 
             u64 *o = ext + ((size_t)j * W + t) * n + nb + col;
 #pragma unroll
             for (int c = 0; c < 4; ++c) o[16 * c] = add_mod(combine_rows(acc[c], mt), cr, mt.q);
+        }
+    }
+}
+
+// ModUp basis conversion with folded constants (round 5, FHE_MODUP_FOLD; the
+// leaf sums' k_leaf_sums_fold scheme): with d_{t,i,a} = 256^a qhat[t][i] mod q_t,
+// ext_t = sum_{i,a} u_{i,a} d_{t,i,a} over the bytes u of y_i = [x_i qhinv_i]_{q_i},
+// so the rows are (target, balanced digit b of d) and the A fragments are a table
+// built once per block in LDS (targets [blockIdx.y * gpc groups of four, + gpc)),
+// while the B fragments (the scaled source residues of four 16-coefficient tiles
+// per wave) stay in registers across every target group.  One 128-bit fold per
+// output with the target's own modulus.  Same residues as k_modup_convert.
+// grid: x = n / chunk, y = target-group chunks, z = member * digits + digit.
+constexpr int MUF_NT = 512;
+// target groups per block: the LDS table holds 2 KS KB per group (<= ~110 KB)
+__host__ __device__ constexpr int muf_gpc(int ks) { return ks <= 3 ? 16 : 48 / ks; }
+template <int KS>
+__global__ __launch_bounds__(MUF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_modup_fold(
+    u64 *__restrict__ ext, const u64 *__restrict__ coef, int W, int ell, ModUpArgs A, const int *pmap_ext,
+    const Mod *mods, int logN, int gpc, int chunk) {
+    constexpr int GPC = muf_gpc(KS);
+    __shared__ v4i afr[GPC * 2 * KS * 64];
+    __shared__ u64 psum[4 * GPC][8 * KS];
+    __shared__ Mod tm[4 * GPC];
+    __shared__ double tqi[4 * GPC];  // 1 / q_t (the fp64 epilogue)
+    __shared__ u64 corr[4 * GPC], cfp[4 * GPC];
+    const size_t n = (size_t)1 << logN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
+    const int j = (int)(blockIdx.z % (unsigned)A.digits);
+    const size_t mb = blockIdx.z / (unsigned)A.digits;
+    coef += mb * A.coef_stride;
+    ext += mb * A.ext_stride;
+    const int lo = A.lo[j], hi = A.hi[j], na = hi - lo, T = W - na;
+    const int g0 = blockIdx.y * gpc, ng = min((T + 3) / 4 - g0, gpc);  // this block's groups
+    const u64 *qh = A.qhat[j];
+    {
+        u64 *const img = reinterpret_cast<u64 *>(afr);
+        for (int p = tid; p < 4 * ng * 8 * KS; p += MUF_NT) {
+            const int tl = p / (8 * KS), i = p % (8 * KS), tau = 4 * g0 + tl;
+            const int t = tau < lo ? tau : tau + na;
+            u64 d = 0;
+            Mod mt{};
+            if (tau < T) {
+                mt = mods[pmap_ext[t]];
+                if (i < na) d = qh[(size_t)t * A.qstride + i];
+            }
+            u64 dig[8], s7 = 0;
+#pragma unroll
+            for (int a = 0; a < 8; ++a) {
+                dig[a] = balanced_digits(d);
+                if (tau < T) {
+                    if (a < 7) s7 = add_mod(s7, d, mt.q);
+                    d = mul_barrett(d, 256, mt);
+                }
+            }
+            psum[tl][i] = s7;
+            const int grp = tl >> 2, ta = tl & 3, ks = i >> 3, lgi = (i & 7) >> 1, half = i & 1;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                u64 e = 0;
+#pragma unroll
+                for (int a = 0; a < 8; ++a) e |= ((dig[a] >> (8 * b)) & 255) << (8 * a);
+                img[2 * (((grp * 2 + (b >> 2)) * KS + ks) * 64 + 16 * lgi + 4 * ta + (b & 3)) + half] = e;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 4 * ng) {
+        const int tau = 4 * g0 + tid;
+        if (tau < T) {
+            const Mod mt = mods[pmap_ext[tau < lo ? tau : tau + na]];
+            u64 s = 0;
+            for (int i = 0; i < na; ++i) s = add_mod(s, psum[tid][i], mt.q);
+            const u64 b126 = mul_shoup(reduce64(1ull << 62, mt), mt.r64, mt.r64s, mt.q);
+            tm[tid] = mt;
+            tqi[tid] = 1.0 / (double)mt.q;
+            corr[tid] = sub_mod(mul_barrett(s, 128, mt), b126, mt.q);
+            cfp[tid] = mul_barrett(s, 128, mt);
+        }
+    }
+    __syncthreads();
+    for (size_t nb = (size_t)blockIdx.x * chunk + wave * 64; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
+         nb += MUF_NT) {
+        // B fragments: scaled source residues of sources 8 ks + 2 lg, +1
+        v4i bf[4][KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            u64 y[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                // padding sources (i >= na) read the digit's last limb: zero constants
+                const int i = min(8 * ks + 2 * lg + h, na - 1);
+                const u64 w = A.qhinv[j][i], wp = A.qhinv_s[j][i], q = mods[lo + i].q;
+                const u64 *src = coef + (size_t)(lo + i) * n + nb + col;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) y[h][c] = mul_shoup(src[16 * c], w, wp, q) ^ XMASK;
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) bf[c][ks] = bytes_of(y[0][c], y[1][c]);
+        }
+#pragma unroll 1
+        for (int grp = 0; grp < ng; ++grp) {
+            v4i acc[4][2];
+            const v4i *ag = afr + (size_t)grp * 2 * KS * 64 + lane;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const v4i a0 = ag[ks * 64], a1 = ag[(KS + ks) * 64];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    acc[c][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[c][ks], ks ? acc[c][0] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                    acc[c][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[c][ks], ks ? acc[c][1] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                }
+            }
+            const int tl = 4 * grp + lg, tau = 4 * g0 + tl;
+            if (tau < T) {
+                const int t = tau < lo ? tau : tau + na;
+                const Mod mt = tm[tl];
+                u64 *o = ext + ((size_t)j * W + t) * n + nb + col;
+                if (mt.q < FOLD_FP_QMAX) {
+                    const double qd = (double)mt.q, qid = tqi[tl];
+                    const u64 cr = cfp[tl];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[16 * c] = fold_rows2_fp(acc[c][0], acc[c][1], qd, qid, cr);
+                } else {
+                    const u64 w1s = shoup_one(mt), cr = corr[tl];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[16 * c] = fold_rows2(acc[c][0], acc[c][1], mt, w1s, cr);
+                }
+            }
         }
     }
 }
@@ -1541,6 +1698,170 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_mfma(u64 *__restrict__ c
         }
     }
 }
+// Fused ModDown + rescale conversion with folded constants (round 5,
+// FHE_MODDOWN_FOLD; the k_modup_fold scheme).  Sources: the K scaled special
+// residues with constants phat[t][i], and one more, the signed P-term
+// lv = centred(y) - count (+ 2^61 so it is a positive value below 2^62) with
+// constant pmod[t] -- so the whole output is one sum of products:
+//   corr_t = sum_i yk_i phat[t][i] + lv pmod[t]  (mod q_t),
+// the same residue as k_moddown_rescale_convert.  The per-coefficient part (yk,
+// the centred count, the last limb's conversion, y) is computed by the lane
+// that owns the coefficient and handed to its column's lanes by __shfl.
+// grid: x = n / chunk, y = target-group chunks, z = segment.
+constexpr int MDF_NT = 512;
+template <int KS, int KT>
+__global__ __launch_bounds__(MDF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_moddown_rescale_fold(
+    u64 *__restrict__ corr_out, const u64 *__restrict__ acc, int ell, int nq, size_t seg_acc, size_t seg_corr,
+    const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv, const u64 *pinv_s, const u64 *pmod,
+    const double *pinvd, const u64 *ninv, const u64 *ninv_s, const Mod *mods, int logN, int gpc, int chunk) {
+    static_assert(8 * KS >= KT + 1, "K special sources + the P term");
+    constexpr int GPC = muf_gpc(KS);
+    __shared__ v4i afr[GPC * 2 * KS * 64];
+    __shared__ u64 psum[4 * GPC][8 * KS];
+    __shared__ Mod tm[4 * GPC];
+    __shared__ double tqi[4 * GPC];  // 1 / q_t (the fp64 epilogue)
+    __shared__ u64 corr[4 * GPC], cfp[4 * GPC];
+    const size_t n = (size_t)1 << logN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
+    const int last = ell - 1, T = last;
+    const u64 *src = acc + (size_t)blockIdx.z * seg_acc + (size_t)last * n;
+    u64 *dst = corr_out + (size_t)blockIdx.z * seg_corr;
+    const int g0 = blockIdx.y * gpc, ng = min((T + 3) / 4 - g0, gpc);
+    {
+        u64 *const img = reinterpret_cast<u64 *>(afr);
+        for (int p = tid; p < 4 * ng * 8 * KS; p += MDF_NT) {
+            const int tl = p / (8 * KS), i = p % (8 * KS), t = 4 * g0 + tl;
+            u64 d = 0;
+            Mod mt{};
+            if (t < T) {
+                mt = mods[t];
+                d = i < KT ? phat[(size_t)t * KT + i] : i == KT ? pmod[t] : 0;
+            }
+            u64 dig[8], s7 = 0;
+#pragma unroll
+            for (int a = 0; a < 8; ++a) {
+                dig[a] = balanced_digits(d);
+                if (t < T) {
+                    if (a < 7) s7 = add_mod(s7, d, mt.q);
+                    d = mul_barrett(d, 256, mt);
+                }
+            }
+            psum[tl][i] = s7;
+            const int grp = tl >> 2, ta = tl & 3, ks = i >> 3, lgi = (i & 7) >> 1, half = i & 1;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                u64 e = 0;
+#pragma unroll
+                for (int a = 0; a < 8; ++a) e |= ((dig[a] >> (8 * b)) & 255) << (8 * a);
+                img[2 * (((grp * 2 + (b >> 2)) * KS + ks) * 64 + 16 * lgi + 4 * ta + (b & 3)) + half] = e;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 4 * ng) {
+        const int t = 4 * g0 + tid;
+        if (t < T) {
+            const Mod mt = mods[t];
+            u64 s = 0;
+            for (int i = 0; i <= KT; ++i) s = add_mod(s, psum[tid][i], mt.q);
+            // + 128 sum d (signed bytes) - 2^61 pmod (the P term's offset) - 2^126 (bias)
+            const u64 b126 = mul_shoup(reduce64(1ull << 62, mt), mt.r64, mt.r64s, mt.q);
+            const u64 off = mul_barrett(reduce64(1ull << 61, mt), pmod[t], mt);
+            tm[tid] = mt;
+            tqi[tid] = 1.0 / (double)mt.q;
+            corr[tid] = sub_mod(sub_mod(mul_barrett(s, 128, mt), b126, mt.q), off, mt.q);
+            cfp[tid] = sub_mod(mul_barrett(s, 128, mt), off, mt.q);
+        }
+    }
+    __syncthreads();
+    const Mod ml = mods[last];
+    const u64 ql = ml.q;
+    for (size_t nb = (size_t)blockIdx.x * chunk + wave * 64; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
+         nb += MDF_NT) {
+        // per-coefficient part, coefficient nb + lane: the P term's source value
+        u64 pv;
+        {
+            const size_t k = nb + lane;
+            u64 yk[KT];
+            Split30 v[KT];
+#pragma unroll
+            for (int i = 0; i < KT; ++i) {
+                yk[i] = mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+                v[i] = split30(yk[i]);
+            }
+            const u64 cntv = centre_count<KT>(yk, pinvd);
+            Acc4 cacc;
+            Acc128 cr;
+#pragma unroll
+            for (int kk = 0; kk < KT; ++kk) {
+                mac4(cacc, v[kk], split30(phat[(size_t)last * KT + kk]));
+                spill4<KT + 1>(cr, cacc, kk);
+            }
+            mac4(cacc, split30(cntv), split30(ql - pmod[last]));
+            fold4(cr, cacc);
+            const u64 cl = reduce128(cr, ml);
+            const u64 xl = mul_shoup(src[k], ninv[last], ninv_s[last], ql);
+            const u64 y = mul_shoup(sub_mod(xl, cl, ql), pinv[last], pinv_s[last], ql);
+            // centred y - count, offset by 2^61: |centred y| <= q_last / 2 < 2^60,
+            // count < K, so 0 < pv < 2^62 (its top byte < 64, a positive signed byte)
+            const int64_t yc = y > (ql >> 1) ? (int64_t)y - (int64_t)ql : (int64_t)y;
+            pv = (u64)(yc - (int64_t)cntv + (int64_t)(1ull << 61));
+        }
+        u64 pvc[4];  // the P term of column tile c, coefficient nb + 16 c + col
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pvc[c] = __shfl(pv, 16 * c + col);
+        // B fragments: the scaled special residues (sources i < KT) and the P term (i = KT)
+        v4i bf[4][KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            u64 yy[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 8 * ks + 2 * lg + h;
+                if (i < KT) {
+                    const u64 w = phinv[i], wp = phinv_s[i], q = mods[nq + i].q;
+                    const u64 *sp = src + (size_t)(1 + i) * n + nb + col;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) yy[h][c] = mul_shoup(sp[16 * c], w, wp, q) ^ XMASK;
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) yy[h][c] = (i == KT ? pvc[c] : 0) ^ XMASK;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) bf[c][ks] = bytes_of(yy[0][c], yy[1][c]);
+        }
+#pragma unroll 1
+        for (int grp = 0; grp < ng; ++grp) {
+            v4i a4[4][2];
+            const v4i *ag = afr + (size_t)grp * 2 * KS * 64 + lane;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const v4i a0 = ag[ks * 64], a1 = ag[(KS + ks) * 64];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    a4[c][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[c][ks], ks ? a4[c][0] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                    a4[c][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[c][ks], ks ? a4[c][1] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                }
+            }
+            const int tl = 4 * grp + lg, t = 4 * g0 + tl;
+            if (t < T) {
+                const Mod mt = tm[tl];
+                u64 *o = dst + (size_t)t * n + nb + col;
+                if (mt.q < FOLD_FP_QMAX) {
+                    const double qd = (double)mt.q, qid = tqi[tl];
+                    const u64 cr = cfp[tl];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[16 * c] = fold_rows2_fp(a4[c][0], a4[c][1], qd, qid, cr);
+                } else {
+                    const u64 w1s = shoup_one(mt), cr = corr[tl];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) o[16 * c] = fold_rows2(a4[c][0], a4[c][1], mt, w1s, cr);
+                }
+            }
+        }
+    }
+}
 inline dim3 ew_grid(int logN, int limbs, int segs) {
     const size_t n = (size_t)1 << logN;
     return dim3((unsigned)((n / 2 + NT - 1) / NT), (unsigned)limbs, (unsigned)segs);
@@ -1818,6 +2139,18 @@ void ew_reduce(u64 *x, int limbs, int segs, size_t seg, const Mod *mods, int log
     hipLaunchKernelGGL(k_reduce, ew_grid(logN, limbs, segs), dim3(NT), 0, st, x, Seg{seg, seg, 0}, mods, logN);
 }
 
+// FHE_MODUP_FOLD (A/B): the folded-constant MFMA ModUp conversion (k_modup_fold):
+// 0 off, 1 always, N >= 2 launches of >= N (member, digit) pairs; default -1:
+// digits of more than 16 sources (MEHP24's alpha = 22: 11.08 -> 10.80 s; at the
+// N=1024 sort's alpha = 14 it ties the VALU kernel, 154.6 vs 158.2 us avg;
+// profiles/r5_s, r5_u)
+int modup_fold_enabled() {
+    static const int v = [] {
+        const char *e = std::getenv("FHE_MODUP_FOLD");
+        return e ? std::atoi(e) : -1;
+    }();
+    return v;
+}
 void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
                    size_t coef_stride, size_t ext_stride, const int *pmap_ext, const u64 *tabs,
                    const size_t *tab_off, const Mod *mods, int logN, hipStream_t st) {
@@ -1844,6 +2177,24 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
     const size_t n = (size_t)1 << logN;
     auto launch = [&](int nd, int at, const ModUpArgs &Ar, u64 *ext0) {
         const double B = 8.0 * members * (double)((size_t)nd * W) * (double)n;  // sources in + targets out
+        const int mf = modup_fold_enabled();
+        const bool fold = mf < 0 ? at > 16 : mf == 1 || (mf >= 2 && nd * members >= mf);
+        if (fold && n >= (size_t)MUF_NT && at <= 32) {  // (KS <= 4: no spills)
+            // every target group of a digit in one block when they fit the LDS table
+            // (muf_gpc groups of four), else chunks over grid.y; coefficient chunks
+            // of up to 4096 per block, smaller while the grid has < 2048 blocks
+            const int ngt = (W - at + 3) / 4;
+            dispatch_int<1, 4>((at + 7) / 8, [&](auto c) {
+                constexpr int KS = decltype(c)::value;
+                const int chunks = (ngt + muf_gpc(KS) - 1) / muf_gpc(KS), gpc = (ngt + chunks - 1) / chunks;
+                size_t ch = std::min<size_t>(4096, n);
+                while (ch > (size_t)MUF_NT && (n / ch) * (size_t)chunks * (size_t)(nd * members) < 2048) ch /= 2;
+                launch_clocked(inst_name<KS>("k_modup_fold"), B, k_modup_fold<KS>,
+                               dim3((unsigned)(n / ch), (unsigned)chunks, (unsigned)(nd * members)), dim3(MUF_NT), st,
+                               ext0, coef, W, ell, Ar, pmap_ext, mods, logN, gpc, (int)ch);
+            });
+            return;
+        }
         if (use_mfma_sums(MF_MODUP) && n >= 256) {
             // groups of four targets, chunked over grid.y when the launch is narrow
             const int ngt = (W - at + 3) / 4;
@@ -1991,6 +2342,16 @@ void ew_permute_multi(u64 *out, const u64 *in, const KsKeys &keys, int limbs, in
     if (count > KS_MAXKEYS) throw std::invalid_argument("ew_permute_multi: too many keys");
     hipLaunchKernelGGL(k_permute_mk, pt_grid(logN, limbs, count), dim3(NT), 0, st, out, in, keys, S, logN);
 }
+// FHE_MODDOWN_FOLD (A/B, default 0): the folded-constant MFMA ModDown+rescale
+// conversion -- measured slower at K = 10 (346 vs 276 us, the N=1024 sort
+// 522.8 -> 528.7 ms) and no gain at MEHP24's K = 16 (profiles/r5_t, r5_u)
+int moddown_fold_enabled() {
+    static const int v = [] {
+        const char *e = std::getenv("FHE_MODDOWN_FOLD");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                              const u64 *pinv_s, const u64 *pmod, const double *pinvd, const u64 *ninv,
@@ -1998,6 +2359,22 @@ void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, 
     if (ell <= 1) return;
     const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
     const size_t n = (size_t)1 << logN;
+    // FHE_MODDOWN_FOLD = 1: always; N >= 2: launches of >= N segments
+    const int mdf = moddown_fold_enabled();
+    if (mdf && (mdf == 1 || segs >= mdf) && n >= (size_t)MDF_NT && K + 1 <= 32) {
+        const int ngt = (ell - 1 + 3) / 4;
+        dispatch_int<1, 16>(K, [&](auto c) {
+            constexpr int KT = decltype(c)::value, KS = (KT + 1 + 7) / 8;
+            const int chunks = (ngt + muf_gpc(KS) - 1) / muf_gpc(KS), gpc = (ngt + chunks - 1) / chunks;
+            size_t ch = std::min<size_t>(4096, n);
+            while (ch > (size_t)MDF_NT && (n / ch) * (size_t)chunks * (size_t)segs < 2048) ch /= 2;
+            launch_clocked(inst_name<KS, KT>("k_moddown_rescale_fold"), B, k_moddown_rescale_fold<KS, KT>,
+                           dim3((unsigned)(n / ch), (unsigned)chunks, (unsigned)segs), dim3(MDF_NT), st, corr, acc, ell,
+                           nq, seg_acc, seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, pinvd, ninv, ninv_s, mods,
+                           logN, gpc, (int)ch);
+        });
+        return;
+    }
     if (use_mfma_sums(MF_MODDOWN) && n >= 256 && pmod_s) {
         const int ngt = (ell - 1 + 3) / 4;
         const size_t base = n / 256 * (size_t)segs;
