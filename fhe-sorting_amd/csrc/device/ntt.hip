@@ -1129,8 +1129,12 @@ __global__ __launch_bounds__((nthreads<PB, COLS>())) __attribute__((amdgpu_waves
 #ifndef FHE_NTT_FP_ROW_WPE
 #define FHE_NTT_FP_ROW_WPE 1
 #endif
+// the FP rescale rows alone (A/B: -DFHE_NTT_FP_RESCALE_WPE=n)
+#ifndef FHE_NTT_FP_RESCALE_WPE
+#define FHE_NTT_FP_RESCALE_WPE FHE_NTT_FP_ROW_WPE
+#endif
 template <int MODE, bool FULL, bool TWL, bool FP>
-__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FP ? FHE_NTT_FP_ROW_WPE : TWL ? FHE_NTT_ROW_WPE : 1, 8))) void k_ntt_fwd_row(
+__global__ __launch_bounds__(NTB) __attribute__((amdgpu_waves_per_eu(FP ? (MODE == NTT_RESCALE ? FHE_NTT_FP_RESCALE_WPE : FHE_NTT_FP_ROW_WPE) : TWL ? FHE_NTT_ROW_WPE : 1, 8))) void k_ntt_fwd_row(
     u64 *data, size_t seg, const int *pmap, const int *smap, int logN, NttTables Tb, NttFuse F) {
     ntt_fwd_body<8, 4, false, MODE, true, FULL, TWL, FP>(data, seg, pmap, smap, logN, Tb, F);
 }
