@@ -310,3 +310,33 @@ def test_committed_counter_tables_match_the_built_library(tmp_path, monkeypatch)
     monkeypatch.setattr(m, 'REPO', str(tmp_path))
     t, src = m.load_table('pmc_x.json')
     assert t is None and 'stale' in src
+
+
+def test_committed_tables_cover_the_profiled_kernels():
+    """Every kernel of the closing profile's sort-only trace that takes >= 1% of the
+    sort (profiles/r5_final3/region_kernel_stats.csv) has a row in the committed
+    instruction-mix table (profiles/valu_mix.json, the roofline's VALU pricing) and
+    in the SQ counter table, so the bench line's valu_frac / limiter are defined for
+    the kernels that matter -- the round's new kernels (k_leaf_sums_fold,
+    k_tensor_lin, k_modup_fold) included."""
+    import csv
+    import re
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stats = os.path.join(repo, 'profiles', 'r5_final3', 'region_kernel_stats.csv')
+    if not os.path.exists(stats):
+        pytest.skip('no closing profile committed')
+    rows = list(csv.DictReader(open(stats)))
+    total = sum(float(r['TotalDurationNs']) for r in rows)
+    mix = json.load(open(os.path.join(repo, 'profiles', 'valu_mix.json')))
+    sq = json.load(open(os.path.join(repo, 'profiles', 'pmc_sq.json')))
+    missing = []
+    for r in rows:
+        if float(r['TotalDurationNs']) < 0.01 * total:
+            continue
+        m = re.search(r'(k_[a-z0-9_]+(<[^>]*>)?)\(', r['Name'])
+        name = m.group(1) if m else r['Name']
+        if name not in mix or name not in sq:
+            missing.append(name)
+    assert not missing, missing
+    assert any(k.startswith('k_leaf_sums_fold<') for k in mix)
+    assert any(k.startswith('k_tensor_lin<') for k in mix)
