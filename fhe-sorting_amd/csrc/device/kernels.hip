@@ -717,6 +717,67 @@ __device__ __forceinline__ u64 fold_rows2_fp(const v4i &r0, const v4i &r1, doubl
     r = r < 0.0 ? r + q : r;
     return (u64)__double_as_longlong(r + 4503599627370496.0) ^ 0x4330000000000000ull;  // r in [0, q) < 2^52
 }
+// fp64 conversion outputs of NTG (1, 2 or 4) targets for the NT coefficients of a
+// block (NT / 64 per lane), from the sources' (yh, yl) pairs in LDS (ys[s][x]):
+//   H = sum_s yh h(c'_s) + yl h(c_s),  L = cst + sum_s yh l(c'_s) + yl l(c_s),
+//   out = 2^20 H + L mod q  (two rint / fma reductions; MID: one exact reduction
+// of H and L halfway).  Sources outermost: a source's 4 NTG constants are scalar
+// loads that serve 4 NTG (NT / 64) FMAs per lane, and one ds_read_b128 of a
+// coefficient's (yh, yl) serves 4 NTG of them, so neither the scalar cache nor the
+// LDS bounds the FMAs.  Canonical residues.
+struct FpTargets {
+    const double *c[4];   // rows [S][4]
+    const double *tq[4];  // {cst, q, 1 / q, flag}
+    u64 *o[4];            // the block's first output coefficient of each target
+};
+template <int S, int MID, int NTG>
+__device__ __forceinline__ void fp_targets(const double2 (*ys)[NT], int lane, const FpTargets &F) {
+    constexpr int G = NT / 64;
+    double H[NTG][G], L[NTG][G], q[NTG], qi[NTG];
+#pragma unroll
+    for (int t = 0; t < NTG; ++t) {
+        q[t] = F.tq[t][1];
+        qi[t] = F.tq[t][2];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            H[t][g] = 0.0;
+            L[t][g] = F.tq[t][0];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        double c[NTG][4];
+#pragma unroll
+        for (int t = 0; t < NTG; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) c[t][e] = F.c[t][4 * s + e];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const double2 y = ys[s][64 * g + lane];
+#pragma unroll
+            for (int t = 0; t < NTG; ++t) {
+                H[t][g] = __builtin_fma(y.x, c[t][0], H[t][g]);
+                H[t][g] = __builtin_fma(y.y, c[t][1], H[t][g]);
+                L[t][g] = __builtin_fma(y.x, c[t][2], L[t][g]);
+                L[t][g] = __builtin_fma(y.y, c[t][3], L[t][g]);
+                if (MID && s == (S + 1) / 2 - 1) {
+                    H[t][g] = __builtin_fma(-__builtin_rint(H[t][g] * qi[t]), q[t], H[t][g]);
+                    L[t][g] = __builtin_fma(-__builtin_rint(L[t][g] * qi[t]), q[t], L[t][g]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NTG; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const double b = H[t][g] * 1048576.0;  // 2^20 H, exact
+            const double tt = __builtin_fma(-__builtin_rint(b * qi[t]), q[t], b) + L[t][g];
+            double r = __builtin_fma(-__builtin_rint(tt * qi[t]), q[t], tt);
+            r = r < 0.0 ? r + q[t] : r;
+            F.o[t][64 * g + lane] = (u64)__double_as_longlong(r + 4503599627370496.0) ^ 0x4330000000000000ull;
+        }
+}
 template <int KS, int NG>
 __global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_leaf_sums_fold(
     LeafArgs A, size_t seg, const Mod *mods, int logN, int chunk) {
@@ -953,6 +1014,8 @@ struct ModUpArgs {
     int lo[8], hi[8];
     int digits, qstride;
     size_t coef_stride, ext_stride;
+    // fp64 rows per digit (host::LevelTables modup_fp): [W][qstride][4], then [W][4]
+    const double *fpc[8], *fpq[8];
 };
 
 // grid: x = n / NT, y = target chunks of tch (conv_chunk), z = member * digits + digit.
@@ -991,6 +1054,88 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
         }
         fold4(r, acc);
         ext[((size_t)j * W + t) * n + k] = reduce128(r, mt);
+    }
+}
+
+// The same in exact fp64 for the targets below 2^41 (round 6; the scheme of
+// k_moddown_rescale_fp, whose fp_target it shares): source i enters as
+// yh = (y >> 30) - oh_i, yl = (y & (2^30 - 1)) - 2^29 with oh = 2^29 for a prime
+// >= 2^41 (q_0) and 0 for the 40-bit primes (|yh| < 2^11), so a target costs
+// 4 AT fp64 FMAs against two accumulators plus the two-step reduction; the
+// integer targets (the special primes, q_0; flag tq[3]) rebuild y from (yh, yl)
+// and keep the 128-bit sums.  Block: 256 coefficients; the scaled sources are
+// computed once into LDS, then wave w takes targets w, w + 4, ... with the
+// constants scalar-loaded once per wave (4 coefficients per lane).  Same
+// canonical residues.  grid: x = n / 256, y = target chunks, z = member * digits + digit.
+template <int AT, int MID>
+__global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u64 *__restrict__ coef, int W, int ell, ModUpArgs A,
+                                                 const int *pmap_ext, const Mod *mods, int logN, int tch) {
+    __shared__ double2 ys[AT][NT];
+    const size_t n = (size_t)1 << logN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const size_t k0 = (size_t)blockIdx.x * NT;  // (n is a multiple of NT)
+    const int j = (int)(blockIdx.z % (unsigned)A.digits);
+    const size_t mb = blockIdx.z / (unsigned)A.digits;
+    coef += mb * A.coef_stride;
+    ext += mb * A.ext_stride;
+    const int lo = A.lo[j], hi = A.hi[j];
+#pragma unroll
+    for (int i = 0; i < AT; ++i) {
+        const int src = min(lo + i, ell - 1);
+        const u64 qs = mods[src].q;
+        const int oh = qs >= FOLD_FP_QMAX ? (1 << 29) : 0;
+        const u64 yv = mul_shoup(coef[(size_t)src * n + k0 + tid], A.qhinv[j][i], A.qhinv_s[j][i], qs);
+        ys[i][tid] = make_double2((double)((int)(uint32_t)(yv >> 30) - oh),
+                                  (double)((int)((uint32_t)yv & (uint32_t)MASK30) - (1 << 29)));
+    }
+    __syncthreads();
+    const u64 *qh = A.qhat[j];
+    const double *fc = A.fpc[j], *fq = A.fpq[j];
+    u64 *eo = ext + (size_t)j * W * n + k0;
+    // an integer target (the special primes, q_0): the 128-bit sums over y rebuilt from (yh, yl)
+    auto int_target = [&](int t) {
+        const Mod mt = mods[pmap_ext[t]];
+#pragma unroll 1
+        for (int g = 0; g < NT / 64; ++g) {
+            const int x = 64 * g + lane;
+            Acc4 acc;
+            Acc128 r;
+#pragma unroll
+            for (int i = 0; i < AT; ++i) {
+                const int oh = mods[min(lo + i, ell - 1)].q >= FOLD_FP_QMAX ? (1 << 29) : 0;
+                const double2 y = ys[i][x];
+                const u64 yv = ((u64)((int)y.x + oh) << 30) + (u64)((int)y.y + (1 << 29));
+                mac4(acc, split30(yv), split30(qh[(size_t)t * A.qstride + i]));
+                spill4<AT>(r, acc, i);
+            }
+            fold4(r, acc);
+            eo[(size_t)t * n + x] = reduce128(r, mt);
+        }
+    };
+    // this block's targets, own digit skipped (tau -> t); wave w: pairs w, w + 4, ...
+    const int na = hi - lo, T = W - na;
+    const int tau0 = blockIdx.y * tch, tau1 = min(tau0 + tch, T);
+    for (int ta = tau0 + 2 * wave; ta < tau1; ta += 2 * (NT / 64)) {
+        const bool hasb = ta + 1 < tau1;
+        const int t0 = ta < lo ? ta : ta + na, t1 = ta + 1 < lo ? ta + 1 : ta + 1 + na;
+        const bool int0 = fq[(size_t)t0 * 4 + 3] != 0.0, int1 = hasb && fq[(size_t)t1 * 4 + 3] != 0.0;
+        if (hasb && !int0 && !int1) {
+            const FpTargets F{{fc + (size_t)t0 * A.qstride * 4, fc + (size_t)t1 * A.qstride * 4},
+                              {fq + (size_t)t0 * 4, fq + (size_t)t1 * 4},
+                              {eo + (size_t)t0 * n, eo + (size_t)t1 * n}};
+            fp_targets<AT, MID, 2>(ys, lane, F);
+            continue;
+        }
+        for (int u = 0; u <= (hasb ? 1 : 0); ++u) {
+            const int t = u ? t1 : t0;
+            if (fq[(size_t)t * 4 + 3] != 0.0) {
+                int_target(t);
+            } else {
+                const FpTargets F{{fc + (size_t)t * A.qstride * 4, nullptr}, {fq + (size_t)t * 4, nullptr},
+                                  {eo + (size_t)t * n, nullptr}};
+                fp_targets<AT, MID, 1>(ys, lane, F);
+            }
+        }
     }
 }
 
@@ -1584,6 +1729,147 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_convert(u64 *__restrict_
     }
 }
 
+// The same in exact fp64 for the targets q_i < 2^41 (round 6; the integer
+// targets -- q_0 -- keep the 128-bit sums above).  Each source enters as two
+// exact doubles, y_k = yh 2^30 + yl + off_k with |yh|, |yl| <= 2^29 (the K
+// scaled special residues; off = 2^59 + 2^29) or yh = pv >> 30, yl its low 30
+// bits (the P term pv = centred(y) - count, |pv| < 2^40 + K), and one target is
+//   H = sum_k yh h(c'_k) + yl h(c_k),  L = cst + sum_k yh l(c'_k) + yl l(c_k)
+// (c' = 2^30 c mod q_i centred, split at 2^20 with |l| <= 2^19: every product
+// is below 2^49 and the host checks that every partial sum stays below 2^53,
+// hostmath.cpp fp_conv_row), so each term is one exact FMA and
+// corr_i = 2^20 H + L mod q_i takes two rint / fma reductions: 4 (K+1) fp64
+// FMAs + 8 fp64 operations per output where the 128-bit form issues 4 (K+1)
+// v_mad_u64_u32 + its fold and reduce128.  MID: one exact reduction of H and L
+// halfway.  Same canonical residues as k_moddown_rescale_convert.
+// the per-coefficient part: sources of coefficient k as (yh, yl) doubles
+template <int KT>
+__device__ __forceinline__ void md_sources(const u64 *src, size_t k, size_t n, int nq, int last, const u64 *phinv,
+                                           const u64 *phinv_s, const u64 *phat, const u64 *pinv, const u64 *pinv_s,
+                                           const u64 *pmod, const double *pinvd, const u64 *ninv, const u64 *ninv_s,
+                                           const Mod *mods, double (&yh)[KT + 1], double (&yl)[KT + 1]) {
+    u64 yk[KT];
+#pragma unroll
+    for (int i = 0; i < KT; ++i) {
+        yk[i] = mul_shoup(src[(size_t)(1 + i) * n + k], phinv[i], phinv_s[i], mods[nq + i].q);
+        yh[i] = (double)((int)(uint32_t)(yk[i] >> 30) - (1 << 29));
+        yl[i] = (double)((int)((uint32_t)yk[i] & (uint32_t)MASK30) - (1 << 29));
+    }
+    const u64 cntv = centre_count<KT>(yk, pinvd);
+    const Mod ml = mods[last];
+    const u64 ql = ml.q;
+    Acc4 cacc;
+    Acc128 cr;
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+        mac4(cacc, split30(yk[kk]), split30(phat[(size_t)last * KT + kk]));
+        spill4<KT + 1>(cr, cacc, kk);
+    }
+    mac4(cacc, split30(cntv), split30(ql - pmod[last]));
+    fold4(cr, cacc);
+    const u64 cl = reduce128(cr, ml);
+    const u64 xl = mul_shoup(src[k], ninv[last], ninv_s[last], ql);
+    const u64 y = mul_shoup(sub_mod(xl, cl, ql), pinv[last], pinv_s[last], ql);
+    const int64_t pv = (y > (ql >> 1) ? (int64_t)y - (int64_t)ql : (int64_t)y) - (int64_t)cntv;
+    const int64_t ph = pv >> 30;
+    yh[KT] = (double)ph;
+    yl[KT] = (double)(int)(pv - ph * ((int64_t)1 << 30));
+}
+// Block: 256 coefficients.  Phase 1: thread x computes coefficient x's sources
+// (md_sources, once per coefficient) into LDS ([2 (K+1)][256] doubles).  Phase 2:
+// wave w takes the targets i0 + w, i0 + w + 4, ...; a target's constants are
+// scalar-loaded once per wave and serve its 256 coefficients (4 per lane, read
+// back from LDS with conflict-free ds_read_b64), so the scalar traffic per FMA is
+// a quarter of a thread-per-coefficient loop's and the table never has to stay in
+// the scalar cache.  grid: x = n / 256, y = target chunks of tch, z = segment.
+template <int KT, int MID, int TPI>
+__global__ __launch_bounds__(NT) void k_moddown_rescale_fp(u64 *__restrict__ corr, const u64 *__restrict__ acc, int ell, int nq,
+                                                           size_t seg_acc, size_t seg_corr, const u64 *phinv,
+                                                           const u64 *phinv_s, const u64 *phat, const u64 *pinv,
+                                                           const u64 *pinv_s, const u64 *pmod, const double *pinvd,
+                                                           const u64 *ninv, const u64 *ninv_s, const Mod *mods,
+                                                           const double *__restrict__ fpc, const double *__restrict__ fpq,
+                                                           int logN, int tch) {
+    __shared__ double2 ys[KT + 1][NT];
+    const size_t n = (size_t)1 << logN;
+    // (readfirstlane: the compiler then knows the wave index, so each target's
+    // constants go through scalar loads)
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const size_t k0 = (size_t)blockIdx.x * NT;  // (n is a multiple of NT)
+    const int last = ell - 1;
+    const u64 *src = acc + (size_t)blockIdx.z * seg_acc + (size_t)last * n;
+    u64 *dst = corr + (size_t)blockIdx.z * seg_corr + k0;
+    {
+        double yh[KT + 1], yl[KT + 1];
+        md_sources<KT>(src, k0 + tid, n, nq, last, phinv, phinv_s, phat, pinv, pinv_s, pmod, pinvd, ninv, ninv_s, mods,
+                       yh, yl);
+#pragma unroll
+        for (int s = 0; s <= KT; ++s) ys[s][tid] = make_double2(yh[s], yl[s]);
+    }
+    __syncthreads();
+    // an integer target (host flag: q_i >= 2^41): the 128-bit sums over y rebuilt from (yh, yl)
+    auto int_target = [&](int i) {
+        const Mod mi = mods[i];
+#pragma unroll 1
+        for (int g = 0; g < NT / 64; ++g) {
+            const int x = 64 * g + lane;
+            const double2 yp = ys[KT][x];
+            const int64_t pv = (int64_t)yp.x * ((int64_t)1 << 30) + (int64_t)yp.y;
+            const u64 lv = pv < 0 ? mi.q - (u64)(-pv) : (u64)pv;  // |pv| < 2^41 <= q_i
+            Acc4 a4;
+            Acc128 r;
+            mac4(a4, split30(lv), split30(pmod[i]));
+#pragma unroll
+            for (int kk = 0; kk < KT; ++kk) {
+                const double2 y = ys[kk][x];
+                const u64 yv = ((u64)((int)y.x + (1 << 29)) << 30) + (u64)((int)y.y + (1 << 29));
+                mac4(a4, split30(yv), split30(phat[(size_t)i * KT + kk]));
+                spill4<KT + 1>(r, a4, kk + 1);
+            }
+            fold4(r, a4);
+            dst[(size_t)i * n + x] = reduce128(r, mi);
+        }
+    };
+    // wave w: target groups w, w + 4, ... of TPI targets of this block's chunk; a
+    // group holding q_0 (the one integer target of a 40-bit context) or cut short
+    // by the chunk's end runs as integer targets, pairs and singles
+    const int i0 = blockIdx.y * tch, i1 = min(i0 + tch, last);
+    auto is_int = [&](int i) { return fpq[(size_t)i * 4 + 3] != 0.0; };
+    auto fpt = [&](int i, int u, FpTargets &F) {
+        F.c[u] = fpc + (size_t)i * (KT + 1) * 4;
+        F.tq[u] = fpq + (size_t)i * 4;
+        F.o[u] = dst + (size_t)i * n;
+    };
+    for (int ia = i0 + TPI * wave; ia < i1; ia += TPI * (NT / 64)) {
+        const int cnt = min(TPI, i1 - ia);
+        bool anyint = false;
+        for (int u = 0; u < cnt; ++u) anyint |= is_int(ia + u);
+        if (cnt == TPI && !anyint) {
+            FpTargets F{};
+            for (int u = 0; u < TPI; ++u) fpt(ia + u, u, F);
+            fp_targets<KT + 1, MID, TPI>(ys, lane, F);
+            continue;
+        }
+        for (int i = ia; i < ia + cnt;) {
+            if (is_int(i)) {
+                int_target(i);
+                ++i;
+            } else if (i + 1 < ia + cnt && !is_int(i + 1)) {
+                FpTargets F{};
+                fpt(i, 0, F);
+                fpt(i + 1, 1, F);
+                fp_targets<KT + 1, MID, 2>(ys, lane, F);
+                i += 2;
+            } else {
+                FpTargets F{};
+                fpt(i, 0, F);
+                fp_targets<KT + 1, MID, 1>(ys, lane, F);
+                ++i;
+            }
+        }
+    }
+}
+
 // The same on MFMA: the K-source conversion of the special limbs to the ell-1
 // remaining Q limbs runs as the i8 sums of products (c_{i,k} = phat[i][k]); the
 // per-coefficient part (scaled special residues, the centred count, the last
@@ -2151,9 +2437,19 @@ int modup_fold_enabled() {
     }();
     return v;
 }
+// FHE_MODUP_FP (A/B): 0 = the 128-bit kernel only, N >= 1 = the fp64 kernel for
+// digits of at least N sources (default 0: measured slower, profiles/r6_c)
+int modup_fp_min_sources() {
+    static const int v = [] {
+        const char *e = std::getenv("FHE_MODUP_FP");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
 void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
                    size_t coef_stride, size_t ext_stride, const int *pmap_ext, const u64 *tabs,
-                   const size_t *tab_off, const Mod *mods, int logN, hipStream_t st) {
+                   const size_t *tab_off, const Mod *mods, int logN, hipStream_t st, const double *fptab,
+                   const size_t *fp_off, int fpmid) {
     const int W = ell + K;
     ModUpArgs A{};
     for (int j = 0; j < digits; ++j) {
@@ -2163,7 +2459,12 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
         A.qhat[j] = base + 2 * alpha;
         A.lo[j] = j * alpha;
         A.hi[j] = std::min((j + 1) * alpha, ell);
+        if (fptab && fp_off) {
+            A.fpc[j] = fptab + fp_off[j];
+            A.fpq[j] = fptab + fp_off[j] + (size_t)W * alpha * 4;
+        }
     }
+    const bool fp0 = fptab && fp_off && fpmid >= 0 && modup_fp_min_sources() > 0 && ((size_t)1 << logN) % NT == 0;
     A.digits = digits;
     A.qstride = alpha;
     A.coef_stride = coef_stride;
@@ -2177,6 +2478,7 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
     const size_t n = (size_t)1 << logN;
     auto launch = [&](int nd, int at, const ModUpArgs &Ar, u64 *ext0) {
         const double B = 8.0 * members * (double)((size_t)nd * W) * (double)n;  // sources in + targets out
+        const bool fp = fp0 && at >= modup_fp_min_sources();
         const int mf = modup_fold_enabled();
         const bool fold = mf < 0 ? at > 16 : mf == 1 || (mf >= 2 && nd * members >= mf);
         if (fold && n >= (size_t)MUF_NT && at <= 32) {  // (KS <= 4: no spills)
@@ -2211,9 +2513,17 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
         }
         dispatch_int<1, 24>(at, [&](auto c) {
             constexpr int AT = decltype(c)::value;
-            const int tch = conv_chunk(logN, W, nd * members);
-            launch_clocked(inst_name<AT>("k_modup_convert"), B, k_modup_convert<AT>, pt_grid(logN, (W + tch - 1) / tch, nd * members),
-                           dim3(NT), st, ext0, coef, W, ell, Ar, pmap_ext, mods, logN, tch);
+            const int tch = conv_chunk(logN, fp ? W - at : W, nd * members);  // (fp: chunks of the non-own targets)
+            const dim3 g = pt_grid(logN, ((fp ? W - at : W) + tch - 1) / tch, nd * members);
+            if (fp && fpmid == 0)
+                launch_clocked(inst_name<AT, 0>("k_modup_fp"), B, k_modup_fp<AT, 0>, g, dim3(NT), st, ext0, coef, W, ell,
+                               Ar, pmap_ext, mods, logN, tch);
+            else if (fp)
+                launch_clocked(inst_name<AT, 1>("k_modup_fp"), B, k_modup_fp<AT, 1>, g, dim3(NT), st, ext0, coef, W, ell,
+                               Ar, pmap_ext, mods, logN, tch);
+            else
+                launch_clocked(inst_name<AT>("k_modup_convert"), B, k_modup_convert<AT>, g, dim3(NT), st, ext0, coef, W,
+                               ell, Ar, pmap_ext, mods, logN, tch);
         });
     };
     if (full > 0) {
@@ -2230,6 +2540,8 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
         Al.qhat[0] = A.qhat[j];
         Al.lo[0] = A.lo[j];
         Al.hi[0] = A.hi[j];
+        Al.fpc[0] = A.fpc[j];
+        Al.fpq[0] = A.fpq[j];
         launch(1, last, Al, ext + (size_t)j * W * n);
     }
 }
@@ -2352,10 +2664,29 @@ int moddown_fold_enabled() {
     }();
     return v;
 }
+// FHE_MODDOWN_FP (A/B): 0 = the 128-bit kernel only, N >= 1 = the fp64 kernel for
+// conversions of at least N targets (default 16: below that the per-coefficient
+// part and the integer target q_0 outweigh the cheaper sums, profiles/r6_e)
+// FHE_CONV_TPI (A/B, 2 or 4): targets per work item of the fp64 ModDown kernel
+int conv_tpi() {
+    static const int v = [] {
+        const char *e = std::getenv("FHE_CONV_TPI");
+        return e && std::atoi(e) == 4 ? 4 : 2;
+    }();
+    return v;
+}
+int moddown_fp_min_targets() {
+    static const int v = [] {
+        const char *e = std::getenv("FHE_MODDOWN_FP");
+        return e ? std::atoi(e) : 16;
+    }();
+    return v;
+}
 void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, size_t seg_acc, size_t seg_corr,
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                              const u64 *pinv_s, const u64 *pmod, const double *pinvd, const u64 *ninv,
-                             const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st, const u64 *pmod_s) {
+                             const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st, const u64 *pmod_s,
+                             const double *fpc, const double *fpq, int fpmid) {
     if (ell <= 1) return;
     const double B = 8.0 * segs * (double)(K + 1 + ell - 1) * ((size_t)1 << logN);
     const size_t n = (size_t)1 << logN;
@@ -2386,6 +2717,28 @@ void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, 
                            dim3((unsigned)(n / 256), (unsigned)((ngt + gpc - 1) / gpc), (unsigned)segs), dim3(NT), st,
                            corr, acc, ell, nq, seg_acc, seg_corr, phinv, phinv_s, phat, pinv, pinv_s, pmod, pmod_s,
                            pinvd, ninv, ninv_s, mods, logN, gpc);
+        });
+        return;
+    }
+    if (fpc && fpq && fpmid >= 0 && (moddown_fp_min_targets() > 0 && ell - 1 >= moddown_fp_min_targets()) && n % NT == 0) {
+        dispatch_int<1, 16>(K, [&](auto c) {
+            constexpr int KT = decltype(c)::value;
+            const int tch = conv_chunk(logN, ell - 1, segs);
+            const dim3 g((unsigned)(n / NT), (unsigned)((ell - 1 + tch - 1) / tch), (unsigned)segs);
+            auto go = [&](auto mid, auto tpi) {
+                constexpr int MI = decltype(mid)::value, TP = decltype(tpi)::value;
+                launch_clocked(inst_name<KT, MI, TP>("k_moddown_rescale_fp"), B, k_moddown_rescale_fp<KT, MI, TP>, g,
+                               dim3(NT), st, corr, acc, ell, nq, seg_acc, seg_corr, phinv, phinv_s, phat, pinv, pinv_s,
+                               pmod, pinvd, ninv, ninv_s, mods, fpc, fpq, logN, tch);
+            };
+            using I0 = std::integral_constant<int, 0>;
+            using I1 = std::integral_constant<int, 1>;
+            using I2 = std::integral_constant<int, 2>;
+            using I4 = std::integral_constant<int, 4>;
+            if (conv_tpi() == 4)
+                fpmid == 0 ? go(I0{}, I4{}) : go(I1{}, I4{});
+            else
+                fpmid == 0 ? go(I0{}, I2{}) : go(I1{}, I2{});
         });
         return;
     }

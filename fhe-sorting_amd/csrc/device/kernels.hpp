@@ -246,7 +246,9 @@ int set_mfma_sums(int mask);
 void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int digits, int members,
                    size_t coef_stride, size_t ext_stride, const int *pmap_ext,
                    const u64 *tabs /* packed, see engine */, const size_t *tab_off, const Mod *mods, int logN,
-                   hipStream_t st);
+                   hipStream_t st,
+                   // given (host::LevelTables modup_fp*, fpmid >= 0): the fp64 kernel
+                   const double *fptab = nullptr, const size_t *fp_off = nullptr, int fpmid = -1);
 // acc0/acc1 [W][n] per member: sum_j ext_j * key_j   (own-digit limbs read from dntt)
 struct KsStrides {
     size_t acc = 0, ext = 0, d = 0;  // member strides of acc [2][W][n], ext, dntt
@@ -329,7 +331,9 @@ void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, 
                              int segs, const u64 *phinv, const u64 *phinv_s, const u64 *phat, const u64 *pinv,
                              const u64 *pinv_s, const u64 *pmod, const double *pinvd, const u64 *ninv,
                              const u64 *ninv_s, const Mod *mods, int logN, hipStream_t st,
-                             const u64 *pmod_s = nullptr);  // given: the MFMA kernel
+                             const u64 *pmod_s = nullptr,  // given: the MFMA kernel
+                             // given (host::LevelTables mdfp_*, fpmid >= 0): the fp64 kernel
+                             const double *fpc = nullptr, const double *fpq = nullptr, int fpmid = -1);
 // conv[s][i][k] = (sum_k' y_k' phat[i][k'] - v P) mod q_i for i < ell, y_k' =
 // pc[s][k'] * phinv_k' (pc: unscaled inverse NTT, phinv carries n^-1),
 // v = round(sum_k' y_k' pinvd_k'): the centred Conv_{P->q_i}

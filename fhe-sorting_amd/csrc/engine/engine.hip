@@ -178,6 +178,8 @@ struct Engine::Impl {
     u64 *qlinv = nullptr, *qlinv_s = nullptr;
     u64 *pmod = nullptr, *pmod_s = nullptr, *pqlinv = nullptr, *pqlinv_s = nullptr;
     double *pinvd = nullptr;
+    double *mdfp_c = nullptr, *mdfp_q = nullptr;  // fp64 ModDown + rescale rows (LevelTables)
+    double *modup_fp = nullptr;  // fp64 ModUp rows (LevelTables modup_fp)
     int *modup_smap = nullptr, *modup_pmap = nullptr;
     // the NTT's host-side class table (T.fp_host points into it) and the prime
     // maps registered with the NTT launcher; shared with forks, released (maps
@@ -353,7 +355,8 @@ struct Engine::Impl {
         auto extm = alloc((size_t)members * es * 8);
         u64 *e = static_cast<u64 *>(extm->p);
         dev::modup_convert(e, c, (int)ell, P.K, P.alpha, digits, members, ell * nn, es, ext(ell), modup_tab,
-                           LT.modup_off[ell].data(), mods, P.logN, st);
+                           LT.modup_off[ell].data(), mods, P.logN, st, modup_fp, LT.modup_fp_off[ell].data(),
+                           LT.modup_fp_mid);
         const size_t mo = LT.modup_map_off[ell];
         if (cols_only) {
             // the column pass for every limb; the row pass here only for the
@@ -478,7 +481,7 @@ struct Engine::Impl {
         u64 *corr = static_cast<u64 *>(corrm->p);
         dev::moddown_rescale_convert(corr, acc, (int)ell, P.K, (int)P.nq(), W * nn, (ell - 1) * nn, segs, phinv,
                                      phinv_s, phat, pinv, pinv_s, pmod, pinvd, T.ninv, T.ninv_s, mods, P.logN, st,
-                                     pmod_s);
+                                     pmod_s, mdfp_c, mdfp_q, LT.mdfp_mid);
         // forward NTT of corr whose row pass finishes (acc + d P - corr) (P q_last)^-1 into `out`
         dev::NttFuse F;
         F.out = out;
@@ -620,6 +623,9 @@ Engine::Engine(int logN, int L, int scale_bits, int first_bits, int dnum, int de
     I.qlinv_s = I.upload_static(I.LT.qlinv_s);
     I.pmod = I.upload_static(I.LT.pmod);
     I.pinvd = I.upload_static(I.LT.pinvd);
+    I.mdfp_c = I.upload_static(I.LT.mdfp_c);
+    I.mdfp_q = I.upload_static(I.LT.mdfp_q);
+    I.modup_fp = I.upload_static(I.LT.modup_fp);
     // the ModUp forward NTT's limbs (every digit's targets) in any order: FP
     // primes first, so the launch splits into one FP and one integer run
     for (size_t ell = 1; ell <= I.P.nq(); ++ell) {
@@ -2209,12 +2215,41 @@ void Engine::time_kernel(const std::string &name, size_t ell, int iters, double 
                 dev::ntt_inverse(e, (int)W, digits, W * nn, I.ext(ell), I.T, ST);
         };
         bytes = (row ? 2.0 : 4.0) * (double)(W * digits) * B;
+    } else if (name == "moddown_rescale32") {  // the HMult tail's conversion over 32 members (64 segments)
+        const int segs = 64;
+        auto bm = I.alloc((size_t)segs * W * nn * 8), cm = I.alloc((size_t)segs * ell * nn * 8);
+        u64 *a = static_cast<u64 *>(bm->p), *corr = static_cast<u64 *>(cm->p);
+        HIP_OK(hipMemsetAsync(a, 0x33, (size_t)segs * W * nn * 8, ST));
+        dev::ew_reduce(a, (int)W, segs, W * nn, MODS, LOGN, ST);  // residues below every limb's prime
+        em = bm;  // keep alive
+        dm = cm;
+        launch = [&, a, corr] {
+            dev::moddown_rescale_convert(corr, a, (int)ell, (int)K, (int)I.P.nq(), W * nn, (ell - 1) * nn, segs, I.phinv,
+                                         I.phinv_s, I.phat, I.pinv, I.pinv_s, I.pmod, I.pinvd, I.T.ninv, I.T.ninv_s,
+                                         MODS, LOGN, ST, I.pmod_s, I.mdfp_c, I.mdfp_q, I.LT.mdfp_mid);
+        };
+        bytes = (double)segs * (K + 1 + ell - 1) * B;
     } else if (name == "modup_convert") {
         launch = [&] {
             dev::modup_convert(e, d, (int)ell, (int)K, I.P.alpha, digits, 1, ell * nn, (size_t)digits * W * nn,
-                               I.ext(ell), I.modup_tab, I.LT.modup_off[ell].data(), MODS, LOGN, ST);
+                               I.ext(ell), I.modup_tab, I.LT.modup_off[ell].data(), MODS, LOGN, ST, I.modup_fp,
+                               I.LT.modup_fp_off[ell].data(), I.LT.modup_fp_mid);
         };
         bytes = (double)(ell + (size_t)digits * W - ell) * B;
+    } else if (name == "modup32") {  // ModUp's conversion over 32 members
+        const int mem = 32;
+        auto cm = I.alloc((size_t)mem * ell * nn * 8), xm = I.alloc((size_t)mem * digits * W * nn * 8);
+        u64 *c = static_cast<u64 *>(cm->p), *x = static_cast<u64 *>(xm->p);
+        HIP_OK(hipMemsetAsync(c, 0x44, (size_t)mem * ell * nn * 8, ST));
+        dev::ew_reduce(c, (int)ell, mem, ell * nn, MODS, LOGN, ST);
+        em = xm;  // keep alive
+        dm = cm;
+        launch = [&, c, x] {
+            dev::modup_convert(x, c, (int)ell, (int)K, I.P.alpha, digits, mem, ell * nn, (size_t)digits * W * nn,
+                               I.ext(ell), I.modup_tab, I.LT.modup_off[ell].data(), MODS, LOGN, ST, I.modup_fp,
+                               I.LT.modup_fp_off[ell].data(), I.LT.modup_fp_mid);
+        };
+        bytes = (double)mem * (ell + (size_t)digits * W - ell) * B;
     } else {
         throw std::invalid_argument("time_kernel: unknown kernel " + name);
     }

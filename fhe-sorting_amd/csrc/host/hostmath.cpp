@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <complex>
 #include <mutex>
 #include <set>
@@ -438,6 +439,54 @@ Entropy Entropy::from_seed(u64 seed) {
 Prng::Prng(const Entropy &e, u64 tag, bool pub)
     : use_cc(e.secure && !pub), sm(e.secure ? e.seed_a : e.seed, tag), cc(e.key, tag) {}
 
+// ---------------------------------------------- fp64 sums of products --
+// One target row of an fp64 basis conversion (kernels.hip k_moddown_rescale_fp).
+// The kernel feeds source k as two exact doubles with y_k = yh 2^30 + yl + off_k,
+// |yh| <= yh_max, |yl| <= yl_max, and accumulates
+//   H = sum_k yh h(c'_k) + yl h(c_k),  L = cst + sum_k yh l(c'_k) + yl l(c_k),
+// so sum_k y_k c_k = 2^20 H + L (mod q) with c' = 2^30 c mod q: every product
+// and partial sum is an integer the FMA represents exactly while the bounds
+// below stay under 2^53.  Returns the split class: 0 = whole sums fit, 1 = fit
+// with one exact reduction (mod q) after source (S + 1) / 2 - 1, -1 = neither.
+struct FpSrc {
+    u64 yh_max, yl_max, off;
+};
+static int fp_conv_row(const std::vector<u64> &c, u64 q, const std::vector<FpSrc> &src, double *row, double *tq) {
+    const Modulus m(q);
+    const size_t S = c.size();
+    auto cen = [q](u64 x) { return x > q / 2 ? (i64)x - (i64)q : (i64)x; };
+    auto split = [](i64 v, i64 &h, i64 &l) {
+        h = (v + (1 << 19)) >> 20;  // round to nearest: l in [-2^19, 2^19)
+        l = v - h * ((i64)1 << 20);
+    };
+    const u64 two30 = ((u64)1 << 30) % q;
+    u64 cst = 0, bh[2] = {0, 0}, bl[2] = {0, 0};
+    const size_t half = (S + 1) / 2;
+    for (size_t k = 0; k < S; ++k) {
+        i64 hp, lp, h, l;
+        split(cen(mulmod(c[k] % q, two30, m)), hp, lp);
+        split(cen(c[k] % q), h, l);
+        row[4 * k + 0] = (double)hp;
+        row[4 * k + 1] = (double)h;
+        row[4 * k + 2] = (double)lp;
+        row[4 * k + 3] = (double)l;
+        const int p = k < half ? 0 : 1;
+        bh[p] += src[k].yh_max * (u64)std::llabs(hp) + src[k].yl_max * (u64)std::llabs(h);
+        bl[p] += src[k].yh_max * (u64)std::llabs(lp) + src[k].yl_max * (u64)std::llabs(l);
+        cst = (cst + mulmod(src[k].off % q, c[k] % q, m)) % q;
+    }
+    tq[0] = (double)cst;
+    tq[1] = (double)q;
+    tq[2] = 1.0 / (double)q;
+    tq[3] = 0.0;
+    const u64 lim = (u64)1 << 53;
+    // the final reduction adds L to a remainder below q; a halfway reduction
+    // leaves |H|, |L| <= q
+    if (bh[0] + bh[1] < lim && cst + bl[0] + bl[1] + 2 * q < lim) return 0;
+    if (bh[0] < lim && cst + bl[0] < lim && q + bh[1] < lim && 3 * q + bl[1] < lim) return 1;
+    return -1;
+}
+
 // ---------------------------------------------------------- level tables --
 LevelTables make_level_tables(const Params &P) {
     LevelTables T;
@@ -468,6 +517,8 @@ LevelTables make_level_tables(const Params &P) {
         T.modup_map_cnt[ell] = T.modup_smap.size() - T.modup_map_off[ell];
     }
     T.modup_off.assign(nq + 1, {});
+    T.modup_fp_off.assign(nq + 1, {});
+    int fp_cls = -2;  // worst fp64 class over the rows (-2: none yet)
     for (size_t ell = 1; ell <= nq; ++ell) {
         const size_t W = ell + K;
         const size_t digits = (ell + alpha - 1) / alpha;
@@ -500,8 +551,35 @@ LevelTables make_level_tables(const Params &P) {
             T.modup.insert(T.modup.end(), qhinv.begin(), qhinv.end());
             T.modup.insert(T.modup.end(), qhinv_s.begin(), qhinv_s.end());
             T.modup.insert(T.modup.end(), qhat.begin(), qhat.end());
+            // fp64 rows: source i (< 2^60) enters as yh = (y >> 30) - oh, yl =
+            // (y & (2^30 - 1)) - 2^29 with oh = 2^29 for a prime >= 2^41 (q_0), else 0
+            // (y < 2^41: |yh| < 2^11); padding sources have zero constants
+            std::vector<FpSrc> src(hi - lo);
+            for (size_t i = lo; i < hi; ++i) {
+                const bool big = P.primes[i] >= ((u64)1 << 41);
+                src[i - lo] = FpSrc{big ? (u64)1 << 29 : (u64)1 << 11, (u64)1 << 29,
+                                    (big ? (u64)1 << 59 : 0) + ((u64)1 << 29)};
+            }
+            const size_t fo = T.modup_fp.size();
+            T.modup_fp_off[ell].push_back(fo);
+            T.modup_fp.resize(fo + W * alpha * 4 + W * 4, 0.0);
+            for (size_t t = 0; t < W; ++t) {
+                if (t >= lo && t < hi) continue;
+                const size_t pt = t < ell ? t : nq + (t - ell);
+                if (P.primes[pt] >= ((u64)1 << 41)) {  // integer targets keep the 128-bit sums (flag 1)
+                    T.modup_fp[fo + W * alpha * 4 + t * 4 + 3] = 1.0;
+                    continue;
+                }
+                // the digit's hi - lo sources (a partial last digit launches with that
+                // many, so the halfway split falls where the kernel's does)
+                std::vector<u64> c(qhat.begin() + t * alpha, qhat.begin() + t * alpha + (hi - lo));
+                const int r = fp_conv_row(c, P.primes[pt], src, &T.modup_fp[fo + t * alpha * 4],
+                                          &T.modup_fp[fo + W * alpha * 4 + t * 4]);
+                fp_cls = (r < 0 || fp_cls == -1) ? -1 : std::max(fp_cls, r);
+            }
         }
     }
+    T.modup_fp_mid = fp_cls == -2 ? -1 : fp_cls;
     // ModDown
     T.phinv.resize(K);
     T.phinv_s.resize(K);
@@ -534,6 +612,29 @@ LevelTables make_level_tables(const Params &P) {
         T.pinv_s[i] = shoup(T.pinv[i], mi.q);
         T.pmod[i] = Pm;
         T.pmod_s[i] = shoup(Pm, mi.q);
+    }
+    // fp64 ModDown + rescale rows: the K scaled special residues y_k < 2^60 enter
+    // as yh = (y >> 30) - 2^29, yl = (y & (2^30 - 1)) - 2^29 (off = 2^59 + 2^29);
+    // the P term pv = centred(y_last) - count (|pv| < 2^40 + K) as pv >> 30 and
+    // its low 30 bits
+    {
+        std::vector<FpSrc> src(K + 1, FpSrc{(u64)1 << 29, (u64)1 << 29, ((u64)1 << 59) + ((u64)1 << 29)});
+        src[K] = FpSrc{(u64)1 << 11, (u64)1 << 30, 0};
+        T.mdfp_c.assign(nq * (K + 1) * 4, 0.0);
+        T.mdfp_q.assign(nq * 4, 0.0);
+        int cls = -2;  // worst class over the fp targets (-2: none yet)
+        for (size_t i = 0; i < nq; ++i) {
+            if (P.primes[i] >= ((u64)1 << 41)) {  // integer targets keep the 128-bit sums (flag 1)
+                T.mdfp_q[i * 4 + 3] = 1.0;
+                continue;
+            }
+            std::vector<u64> c(K + 1);
+            for (size_t k = 0; k < K; ++k) c[k] = T.phat[i * K + k];
+            c[K] = T.pmod[i];
+            const int r = fp_conv_row(c, P.primes[i], src, &T.mdfp_c[i * (K + 1) * 4], &T.mdfp_q[i * 4]);
+            cls = (r < 0 || cls == -1) ? -1 : std::max(cls, r);
+        }
+        T.mdfp_mid = cls == -2 ? -1 : cls;
     }
     // Rescale
     T.qlinv.assign((nq + 1) * nq, 0);

@@ -148,12 +148,30 @@ struct LevelTables {
     // qhinv and phinv include n^-1 (their inputs come from unscaled inverse NTTs)
     std::vector<u64> modup;             // packed
     std::vector<std::vector<size_t>> modup_off;  // [ell][digit] offset into modup
+    // fp64 form of the ModUp conversion (kernels.hip k_modup_fp), per ell and
+    // digit: rows [W][alpha][4] of {h(c'), h(c), l(c'), l(c)} (c = qhat[t][i], zero
+    // for the integer targets and the padding sources), then [W][4] {cst, q, 1/q, 0}
+    // ({0, 0, 0, 1} for an integer target)
+    // (the mdfp_* scheme below); modup_fp_mid as mdfp_mid over every row
+    std::vector<double> modup_fp;
+    std::vector<std::vector<size_t>> modup_fp_off;  // [ell][digit] offset into modup_fp
+    int modup_fp_mid = -1;
     // ModDown (level independent)
     std::vector<u64> phinv, phinv_s;    // [K]
     std::vector<u64> phat;              // [nq][K]
     std::vector<u64> pinv, pinv_s;      // [nq]
     std::vector<u64> pmod, pmod_s;      // [nq]  P mod q_i
     std::vector<double> pinvd;          // [K]   1 / p_k (ModDown's centring count)
+    // fp64 form of the fused ModDown + rescale conversion (kernels.hip
+    // k_moddown_rescale_fp; DESIGN.md §5 "fp64 conversions"): per target i with
+    // q_i < 2^41, for each source k (the K special residues, then the P term)
+    // {h(c'), h(c), l(c'), l(c)} with c = phat[i][k] (pmod[i] for the P term),
+    // c' = 2^30 c mod q_i, both centred and split v = h 2^20 + l, |l| <= 2^19;
+    // mdfp_q[i] = {sum_k off_k c_k mod q_i, q_i, 1 / q_i, 0} ({0, 0, 0, 1}: an integer
+    // target, q_i >= 2^41, which keeps the 128-bit sums).  mdfp_mid: 0 = the
+    // sums fit 2^53 whole, 1 = with one reduction halfway, -1 = not usable
+    std::vector<double> mdfp_c, mdfp_q;  // [nq][K+1][4], [nq][4]
+    int mdfp_mid = -1;
     // fused ModDown + rescale (HMult tail): pqlinv[ell][i] = (P q_{ell-1})^{-1} mod q_i
     std::vector<u64> pqlinv, pqlinv_s;  // [nq+1][nq]
     // Rescale, per ell: qlinv[ell][i] = q_{ell-1}^{-1} mod q_i
