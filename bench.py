@@ -347,22 +347,29 @@ def valu_fraction(sq, mix, keys, avg_s):
 
 
 def achievable_hbm_frac():
-    """The HBM rate an in-place read + write stream reaches with no arithmetic, as
-    a fraction of the 8 TB/s peak: the best 8-B-per-lane in-place pattern of
-    scripts/row_pattern.hip on one MI355X (profiles/r5_rates/row_pattern.jsonl;
-    the NTT passes and element-wise kernels read and write [segs][limbs][n] in
-    place).  0.786 (the guide's float4 copy, 6.29 TB/s) when absent."""
-    path = os.path.join(REPO, 'profiles', 'r5_rates', 'row_pattern.jsonl')
+    """The best HBM rate a plain copy reaches on an MI355X, as a fraction of the
+    8 TB/s peak: the fastest pattern of scripts/row_pattern.hip over both of its
+    passes (round 6, profiles/r6_rates/row_pattern*.jsonl) -- the guide's
+    grid-stride 16-B copy with 4-8 loads in flight per thread (5.94 TB/s = 0.742
+    in the first pass, 0.68 in the second on the same box a second later; the
+    guide's own figure is 6.29 TB/s = 0.786), the in-place and the NTT passes' own
+    block shapes (0.72 and 0.71 in the first pass).  0.786 when the files are
+    absent."""
+    rows = []
+    for name in ('row_pattern.jsonl', 'row_pattern_2.jsonl'):
+        try:
+            rows += [json.loads(l) for l in open(os.path.join(REPO, 'profiles', 'r6_rates', name)) if l.strip()]
+        except (OSError, ValueError):
+            pass
     try:
-        rows = [json.loads(l) for l in open(path) if l.strip()]
-        return max(r['frac'] for r in rows if r['pattern'] in ('flat', 'seg16', 'row16', 'seg16x3', 'row16x3'))
-    except (OSError, ValueError, KeyError):
+        return max(r['frac'] for r in rows)
+    except (ValueError, KeyError):
         return 0.786
 
 
 def limiter_of(name, frac, vf, waves=None, hbm_ach=None):
-    """What bounds the kernel: 'hbm' at >= 0.85 of the achievable in-place HBM
-    rate (achievable_hbm_frac(), whatever the kernel); 'valu' at >= 0.85 of the
+    """What bounds the kernel: 'hbm' at >= 0.85 of the best measured copy rate
+    (achievable_hbm_frac(), whatever the kernel); 'valu' at >= 0.85 of the
     measured VALU throughput (whatever its waits); 'memory latency' when the SQ
     pass puts >= 0.3 of its wave cycles in s_waitcnt, at least its issue
     stalls; else 'issue latency (W waves/SIMD)': dependent-instruction stalls at

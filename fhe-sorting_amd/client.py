@@ -46,6 +46,21 @@ def cli_rotations(N):
     return list(MAIN_ROTATIONS) if N == 128 else F.size_parameters(N)[1]
 
 
+def setup_rotations(N, conf):
+    """The rotation keys `setup` generates: the config's indexes_for_rotation_key
+    for N = 128 (src/main.cpp's context), else bin/fhesort's set for N -- always
+    including every rotation bin/fhesort uses (sort_cli.cpp), so a config with a
+    different list cannot leave the CLI without a key at sort time (advisor r5).
+    Returns (rotations, the CLI rotations the config lacked)."""
+    need = cli_rotations(N)
+    if N == 128 and conf.get('indexes_for_rotation_key'):
+        rots = [int(r) for r in conf['indexes_for_rotation_key']]
+        have = set(rots)
+        added = [r for r in need if r not in have]
+        return rots + added, added
+    return list(need), []
+
+
 def table_sign_config(N):
     """DirectSortTest's CompositeSign per N (tests/DirectSortTest.cpp:104-112),
     the configuration getSizeParameters' depth is sized for."""
@@ -96,9 +111,10 @@ def setup(a):
         raise SystemExit(f'depth {depth} < {need} needed by DirectSort<{a.n}> with CompositeSign{cfg}')
     os.makedirs(a.dir, exist_ok=True)
     ctx = F.Context(log_n, depth, scale_bits, 60, 3, seed=a.seed, device=a.device)
-    rots = cli_rotations(a.n)
-    if a.n == 128 and conf.get('indexes_for_rotation_key'):
-        rots = [int(r) for r in conf['indexes_for_rotation_key']]
+    rots, added = setup_rotations(a.n, conf)
+    if added:
+        print(f'setup: the config\'s indexes_for_rotation_key lacks {len(added)} rotation(s) bin/fhesort uses '
+              f'for N = {a.n} ({added[:8]}{"..." if len(added) > 8 else ""}); their keys are generated too')
     ctx.gen_rotation_keys(rots)
     ctx.serialize(_path(a.dir, 'cc'))
     ctx.serialize_public_key(_path(a.dir, 'pub'))

@@ -18,6 +18,7 @@
 
 #include <cstdlib>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -1436,16 +1437,24 @@ int &ntt_fp_enabled() {
     }();
     return v;
 }
-// host copies of the device prime maps (ntt_register_map), by device address
+// host copies of the device prime maps (ntt_register_map), by device address;
+// `gen` counts (un)registrations so the per-thread lookup cache below can tell
+// when its entries went stale
 struct MapRegistry {
     std::mutex mu;
     std::map<const int *, std::vector<int>> maps;
+    std::atomic<unsigned long> gen{0};
 };
 MapRegistry &map_registry() {
     static MapRegistry r;
     return r;
 }
-// the prime of each limb of a launch, if its map is known on the host
+// the prime of each limb of a launch, if its map is known on the host.  Every
+// pass of every transform asks this (several times per HMult), so the answers
+// are cached per thread by (map, limbs) -- no lock, search or copy on a hit
+// (advisor r5); the cache empties itself when a map is (un)registered.  Both
+// passes of one transform (the column pass here, the fused row pass in
+// ntt_row_ks) ask the same registry, so they classify every limb alike.
 bool launch_primes(const int *pmap, int limbs, std::vector<int> &out) {
     out.resize(limbs);
     if (!pmap) {
@@ -1453,14 +1462,40 @@ bool launch_primes(const int *pmap, int limbs, std::vector<int> &out) {
         return true;
     }
     MapRegistry &R = map_registry();
-    std::lock_guard<std::mutex> lk(R.mu);
-    auto it = R.maps.upper_bound(pmap);
-    if (it == R.maps.begin()) return false;
-    --it;
-    const size_t off = (size_t)(pmap - it->first);
-    if (off + (size_t)limbs > it->second.size()) return false;
-    for (int z = 0; z < limbs; ++z) out[z] = it->second[off + z];
-    return true;
+    struct Entry {
+        const int *pmap;
+        int limbs;
+        bool known;
+        std::vector<int> primes;
+    };
+    static thread_local std::vector<Entry> cache;
+    static thread_local unsigned long cache_gen = ~0ul;
+    const unsigned long g = R.gen.load(std::memory_order_acquire);
+    if (g != cache_gen) {
+        cache.clear();
+        cache_gen = g;
+    }
+    for (const Entry &e : cache)
+        if (e.pmap == pmap && e.limbs == limbs) {
+            if (e.known) out = e.primes;
+            return e.known;
+        }
+    bool known = false;
+    {
+        std::lock_guard<std::mutex> lk(R.mu);
+        auto it = R.maps.upper_bound(pmap);
+        if (it != R.maps.begin()) {
+            --it;
+            const size_t off = (size_t)(pmap - it->first);
+            if (off + (size_t)limbs <= it->second.size()) {
+                for (int z = 0; z < limbs; ++z) out[z] = it->second[off + z];
+                known = true;
+            }
+        }
+    }
+    if (cache.size() >= 256) cache.clear();
+    cache.push_back(Entry{pmap, limbs, known, known ? out : std::vector<int>{}});
+    return known;
 }
 // FHE_NTT_AUX (A/B, default 0 -- measured slower: 539.1 / 540.9 ms without,
 // 548.6 / 548.2 ms with, profiles/r5_j; the event fork / join costs more than the
@@ -1574,11 +1609,13 @@ void ntt_register_map(const int *dev, const int *host, size_t count) {
     MapRegistry &R = map_registry();
     std::lock_guard<std::mutex> lk(R.mu);
     R.maps[dev].assign(host, host + count);
+    R.gen.fetch_add(1, std::memory_order_release);
 }
 void ntt_unregister_map(const int *dev) {
     MapRegistry &R = map_registry();
     std::lock_guard<std::mutex> lk(R.mu);
     R.maps.erase(dev);
+    R.gen.fetch_add(1, std::memory_order_release);
 }
 bool ntt_fp_prime(u64 q) { return (q >> FP_QBITS) == 0; }
 

@@ -7,6 +7,11 @@
 //   row16  : 16 consecutive rows of ONE segment per block (32 KB contiguous);
 //   seg16x3: seg16 plus two more read streams (the HMult-tail epilogue's
 //            accumulator and d operands) -> 3 reads + 1 write per element.
+// Round 6 (verdict r5 item 3): the guide's float4-copy shape as well --
+//   copy16_gs<U>: out-of-place 16-B copy, grid-stride loop, U loads in flight
+//                 per thread before the dependent stores (grids of 2..16 blocks
+//                 per CU), and its in-place twin (read + write of one buffer);
+// every pattern is timed over 100 launches (was 10).
 // Build: hipcc --offload-arch=gfx950 -O3 row_pattern.hip -o row_pattern
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -99,6 +104,29 @@ __global__ __launch_bounds__(256) void k_row16x3(u64 *a, const u64 *b, const u64
     for (int r = 0; r < 16; ++r) a[off + t + 16 * r] = x[r] + y[r] + z[r];
 }
 
+// grid-stride 16-B copy: each thread issues U loads, then U stores, per trip
+template <int U>
+__global__ __launch_bounds__(256) void k_copy16_gs(v2u *dst, const v2u *src, size_t n16) {
+    const size_t stride = (size_t)gridDim.x * 256 * U;
+    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < n16; base += stride) {
+        v2u x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * 256;
+            x[u] = i < n16 ? src[i] : v2u{0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * 256;
+            if (i < n16) {
+                v2u v = x[u];
+                v.x += 1;
+                dst[i] = v;
+            }
+        }
+    }
+}
+
 template <typename F>
 void run(const char *name, F launch, double bytes) {
     hipEvent_t e0, e1;
@@ -106,7 +134,7 @@ void run(const char *name, F launch, double bytes) {
     (void)hipEventCreate(&e1);
     launch();
     (void)hipEventRecord(e0);
-    const int it = 10;
+    const int it = 100;
     for (int i = 0; i < it; ++i) launch();
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
@@ -137,5 +165,16 @@ int main() {
     run("row16", [&] { k_row16<<<dim3(segs, 16, limbs), 256>>>(a, seg); }, B2);
     run("seg16x3", [&] { k_seg16x3<<<dim3(segs / 16, 256, limbs), 256>>>(a, b, c, seg); }, B4);
     run("row16x3", [&] { k_row16x3<<<dim3(segs, 16, limbs), 256>>>(a, b, c, seg); }, B4);
+    const size_t n16 = total / 2;
+    char nm[64];
+    for (int bpc : {2, 4, 8, 16}) {
+        const unsigned g = 256u * bpc;
+        snprintf(nm, sizeof nm, "copy16_gs4_b%d", bpc);
+        run(nm, [&] { k_copy16_gs<4><<<g, 256>>>((v2u *)a, (const v2u *)b, n16); }, B2);
+        snprintf(nm, sizeof nm, "copy16_gs8_b%d", bpc);
+        run(nm, [&] { k_copy16_gs<8><<<g, 256>>>((v2u *)a, (const v2u *)b, n16); }, B2);
+        snprintf(nm, sizeof nm, "inplace16_gs8_b%d", bpc);
+        run(nm, [&] { k_copy16_gs<8><<<g, 256>>>((v2u *)a, (const v2u *)a, n16); }, B2);
+    }
     return 0;
 }

@@ -288,12 +288,32 @@ def test_bench_limiter_rule():
     assert 0.5 < m.achievable_hbm_frac() <= 1.0
 
 
-def test_committed_counter_tables_match_the_built_library(tmp_path, monkeypatch):
+def test_bench_hbm_ceiling_is_the_best_measured_copy():
+    """roofline.hbm_achievable_frac (verdict r5 item 3) is the fastest pattern of
+    the committed probe (profiles/r6_rates: the guide's grid-stride 16-B copy,
+    100 launches per pattern, two passes), not the best 8-B in-place pattern; the
+    headline's 'hbm' label needs >= 0.85 of it."""
+    m = _bench_module()
+    rows = []
+    for name in ('row_pattern.jsonl', 'row_pattern_2.jsonl'):
+        with open(os.path.join(os.path.dirname(BENCH), 'profiles', 'r6_rates', name)) as f:
+            rows += [json.loads(l) for l in f if l.strip()]
+    assert any(r['pattern'].startswith('copy16_gs') for r in rows)
+    best = max(r['frac'] for r in rows)
+    assert m.achievable_hbm_frac() == best
+    assert best >= max(r['frac'] for r in rows if r['pattern'].startswith('copy16_gs'))
+    assert m.limiter_of('k', 0.84 * best, {'valu_frac': 0.2, 'wave_cycle_split': {'waitcnt': 0.1, 'issue_stall': 0.5}},
+                        3) == 'issue latency (3 waves/SIMD)'
+    assert m.limiter_of('k', 0.86 * best, {}) == 'hbm'
+
+
+def test_counter_tables_are_refused_for_another_library(tmp_path, monkeypatch):
     """The PMC / SQ tables in profiles/ carry the SHA-256 of the library they were
     collected on; bench.py reports their traffic and VALU figures only for that
-    library.  The committed tables must match the in-tree build (a source change
-    to the engine without a new closing profile fails here), and a table stamped
-    with another hash is refused with the reason."""
+    library.  A committed table that does not match the in-tree build only WARNS
+    here (measurement provenance, not correctness: bench.py then reports those
+    figures as null until the next closing profile; FHE_STRICT_TABLES=1 makes it
+    fail), and a table stamped with another hash is refused with the reason."""
     m = _bench_module()
     stale = []
     if os.path.exists(m.F.LIB_PATH):
@@ -303,8 +323,11 @@ def test_committed_counter_tables_match_the_built_library(tmp_path, monkeypatch)
             if t is None:  # measurement provenance, not correctness (advisor r4): say so, do not fail
                 stale.append(src)
     if stale:
-        warnings.warn('committed counter tables do not match the in-tree library (bench.py reports their '
-                      'figures as null until the next closing profile): ' + '; '.join(stale))
+        msg = ('committed counter tables do not match the in-tree library (bench.py reports their '
+               'figures as null until the next closing profile): ' + '; '.join(stale))
+        if os.environ.get('FHE_STRICT_TABLES') == '1':
+            pytest.fail(msg)
+        warnings.warn(msg)
     (tmp_path / 'profiles').mkdir()
     (tmp_path / 'profiles' / 'pmc_x.json').write_text(json.dumps({'_meta': {'lib_sha256': '0' * 64}, 'k_add': {}}))
     monkeypatch.setattr(m, 'REPO', str(tmp_path))

@@ -580,12 +580,16 @@ def test_relinearised_products_large_rings(logN, L):
     ys = [orc.encrypt(rng.uniform(-1, 1, 64), 64) for _ in range(20)]
     gy = [gpu.from_oracle(y) for y in ys]
     for cnt in (16, 20, 8):  # 16 members per block (full, partial); 8 per block x 2 rows
-        st = gpu.mul(gpu.stack(gy[:cnt]), gpu.stack(gy[::-1][:cnt]))
+        with F.KernelClock(gpu) as clk:  # (advisor r5: the fused kernel must be the one that ran)
+            st = gpu.mul(gpu.stack(gy[:cnt]), gpu.stack(gy[::-1][:cnt]))
+        assert any(k.startswith('k_ntt_row_ks') for k in clk.stats), sorted(clk.stats)
         for m in (0, 7, cnt - 1):
             same(gpu.member(st, m), orc.mul(ys[m], ys[::-1][m]))
     lo = [orc.mul(orc.mul(y, xs[1]), xs[2]) for y in ys[:5]]
     gl = gpu.stack([gpu.from_oracle(y) for y in lo])
-    st = gpu.mul(gl, gl)
+    with F.KernelClock(gpu) as clk:
+        st = gpu.mul(gl, gl)
+    assert any(k.startswith('k_ntt_row_ks') for k in clk.stats), sorted(clk.stats)
     for m in range(5):
         same(gpu.member(st, m), orc.mul(lo[m], lo[m]))
 

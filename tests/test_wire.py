@@ -112,6 +112,21 @@ def test_cli_depth_rule():
     assert c.cli_rotations(8) == F.size_parameters(8)[1]
 
 
+def test_setup_rotations_cover_the_cli():
+    """advisor r5: `setup --config X` keys X's indexes_for_rotation_key for N = 128,
+    plus every rotation bin/fhesort uses that X lacks (the CLI's set is fixed,
+    sort_cli.cpp), so the sort never meets a missing key."""
+    c = _client()
+    rots, added = c.setup_rotations(128, {'indexes_for_rotation_key': c.MAIN_ROTATIONS})
+    assert rots == list(c.MAIN_ROTATIONS) and added == []
+    short = list(c.MAIN_ROTATIONS)[:5] + [12345]
+    rots, added = c.setup_rotations(128, {'indexes_for_rotation_key': short})
+    assert set(c.MAIN_ROTATIONS) <= set(rots) and 12345 in rots
+    assert added == [r for r in c.MAIN_ROTATIONS if r not in short]
+    rots, added = c.setup_rotations(8, {'indexes_for_rotation_key': [1]})
+    assert rots == c.cli_rotations(8) and added == []
+
+
 def test_client_defaults_are_the_reference_config(tmp_path):
     """Verdict r4 item 1: client.py setup defaults to src/config.json's context
     (ring 131072, multDepth 44, scale 40, batch 128, main.cpp's rotations) and
