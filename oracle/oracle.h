@@ -184,6 +184,10 @@ class Context {
     // Paterson-Stockmeyer split of cheb_series_ps: 1 = OpenFHE's (default),
     // 0 = the power-of-two split
     int ps_split = 1;
+    // 1: OpenFHE's ApproxModDown -- the plain fast base conversion, which floors
+    // x / P with a 0..K overshoot (no centring count); 0: this build's exact centred
+    // ModDown.  Oracle only: what the departure costs (verdict r5 item 7)
+    int moddown_floor = 0;
 
     void keygen();
     void gen_rotation_keys(const std::vector<int> &rot);

@@ -64,6 +64,12 @@ int orc_set_ps_split(void *c, int split) {
     return 0;
 }
 
+// ModDown form: 1 = OpenFHE's flooring fast conversion, 0 = the exact centred one
+int orc_set_moddown_floor(void *c, int floor) {
+    if (floor != 0 && floor != 1) return -1;
+    static_cast<Context *>(c)->moddown_floor = floor;
+    return 0;
+}
 int orc_params(void *c, uint64_t *primes, int *nq, int *K, int *alpha, double *delta) {
     auto *cc = static_cast<Context *>(c);
     if (primes) std::memcpy(primes, cc->P.primes.data(), cc->P.primes.size() * 8);

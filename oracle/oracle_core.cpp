@@ -941,7 +941,7 @@ void Context::moddown(const u64 *in, size_t ell, u64 *out) const {
                 acc = mod_add(acc, mod_mul(pc[k * n + c] % mi.q, phat[k], mi), mi.q);
                 t = t + (double)pc[k * n + c] * (1.0 / (double)P.primes[nq + k]);
             }
-            const u64 v = (u64)(t + 0.5);
+            const u64 v = moddown_floor ? 0 : (u64)(t + 0.5);
             conv[c] = mod_sub(acc, mod_mul(v, Pq, mi), mi.q);
         }
         ntt_forward(conv.data(), tab[i], n);

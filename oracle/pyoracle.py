@@ -34,6 +34,7 @@ def lib():
             'orc_ctx_new': (vp, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64]),
             'orc_ctx_free': (None, [vp]),
             'orc_set_ps_split': (C.c_int, [vp, C.c_int]),
+            'orc_set_moddown_floor': (C.c_int, [vp, C.c_int]),
             'orc_cheb_ps_depth': (C.c_int, [C.c_int, C.c_int]),
             'orc_params': (C.c_int, [vp, u64p, ip, ip, ip, dp]),
             'orc_keygen': (C.c_int, [vp]),
@@ -257,6 +258,12 @@ class Context:
         if lib().orc_set_ps_split(self.h, int(split)) != 0:
             raise ValueError('ps split must be 0 or 1')
         self.ps_split = int(split)
+
+    def set_moddown_floor(self, floor):
+        """1: OpenFHE's ApproxModDown (the flooring fast base conversion); 0: the
+        exact centred ModDown this build specifies (the default)"""
+        if lib().orc_set_moddown_floor(self.h, int(floor)) != 0:
+            raise ValueError('moddown floor must be 0 or 1')
 
     # keys -------------------------------------------------------------
     def keygen(self):
