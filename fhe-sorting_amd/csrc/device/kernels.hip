@@ -1024,8 +1024,11 @@ struct ModUpArgs {
 // size): the source loop is straight-line; a shorter last digit reads a
 // clamped limb times a zero constant.
 template <int AT>
+// tbeg: the first target (0, or ell: the special-prime targets only, beside a
+// k_modup_fp launch that takes the Q targets)
 __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, const u64 *__restrict__ coef, int W, int ell, ModUpArgs A,
-                                                      const int *pmap_ext, const Mod *mods, int logN, int tch) {
+                                                      const int *pmap_ext, const Mod *mods, int logN, int tch,
+                                                      int tbeg) {
     const size_t n = (size_t)1 << logN;
     const size_t k = (size_t)blockIdx.x * NT + threadIdx.x;
     if (k >= n) return;
@@ -1034,7 +1037,7 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
     coef += mb * A.coef_stride;
     ext += mb * A.ext_stride;
     const int lo = A.lo[j], hi = A.hi[j];
-    const int t0 = blockIdx.y * tch;
+    const int t0 = tbeg + blockIdx.y * tch;
     Split30 y[AT];
 #pragma unroll
     for (int i = 0; i < AT; ++i) {
@@ -1068,8 +1071,10 @@ __global__ __launch_bounds__(NT) void k_modup_convert(u64 *__restrict__ ext, con
 // constants scalar-loaded once per wave (4 coefficients per lane).  Same
 // canonical residues.  grid: x = n / 256, y = target chunks, z = member * digits + digit.
 template <int AT, int MID>
+// qonly: the Q targets (t < ell) only; the special primes run in k_modup_convert
+// (tbeg = ell) beside it
 __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u64 *__restrict__ coef, int W, int ell, ModUpArgs A,
-                                                 const int *pmap_ext, const Mod *mods, int logN, int tch) {
+                                                 const int *pmap_ext, const Mod *mods, int logN, int tch, int qonly) {
     __shared__ double2 ys[AT][NT];
     const size_t n = (size_t)1 << logN;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1113,7 +1118,7 @@ __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u6
         }
     };
     // this block's targets, own digit skipped (tau -> t); wave w: pairs w, w + 4, ...
-    const int na = hi - lo, T = W - na;
+    const int na = hi - lo, T = (qonly ? ell : W) - na;
     const int tau0 = blockIdx.y * tch, tau1 = min(tau0 + tch, T);
     for (int ta = tau0 + 2 * wave; ta < tau1; ta += 2 * (NT / 64)) {
         const bool hasb = ta + 1 < tau1;
@@ -2513,17 +2518,32 @@ void modup_convert(u64 *ext, const u64 *coef, int ell, int K, int alpha, int dig
         }
         dispatch_int<1, 24>(at, [&](auto c) {
             constexpr int AT = decltype(c)::value;
-            const int tch = conv_chunk(logN, fp ? W - at : W, nd * members);  // (fp: chunks of the non-own targets)
-            const dim3 g = pt_grid(logN, ((fp ? W - at : W) + tch - 1) / tch, nd * members);
-            if (fp && fpmid == 0)
-                launch_clocked(inst_name<AT, 0>("k_modup_fp"), B, k_modup_fp<AT, 0>, g, dim3(NT), st, ext0, coef, W, ell,
-                               Ar, pmap_ext, mods, logN, tch);
-            else if (fp)
-                launch_clocked(inst_name<AT, 1>("k_modup_fp"), B, k_modup_fp<AT, 1>, g, dim3(NT), st, ext0, coef, W, ell,
-                               Ar, pmap_ext, mods, logN, tch);
-            else
-                launch_clocked(inst_name<AT>("k_modup_convert"), B, k_modup_convert<AT>, g, dim3(NT), st, ext0, coef, W,
-                               ell, Ar, pmap_ext, mods, logN, tch);
+            if (!fp) {
+                const int tch = conv_chunk(logN, W, nd * members);
+                launch_clocked(inst_name<AT>("k_modup_convert"), B, k_modup_convert<AT>,
+                               pt_grid(logN, (W + tch - 1) / tch, nd * members), dim3(NT), st, ext0, coef, W, ell, Ar,
+                               pmap_ext, mods, logN, tch, 0);
+                return;
+            }
+            // the fp64 kernel takes the Q targets (q_0 through its integer path), the
+            // 128-bit kernel the K special primes beside it (each reads the sources)
+            const int Tq = ell - at, Kt = W - ell;
+            const double Bq = 8.0 * members * (double)nd * (at + Tq) * (double)n;
+            const double Bk = 8.0 * members * (double)nd * (at + Kt) * (double)n;
+            const int tq = conv_chunk(logN, Tq, nd * members);
+            const dim3 gq = pt_grid(logN, (Tq + tq - 1) / tq, nd * members);
+            if (Tq > 0) {
+                if (fpmid == 0)
+                    launch_clocked(inst_name<AT, 0>("k_modup_fp"), Bq, k_modup_fp<AT, 0>, gq, dim3(NT), st, ext0, coef, W,
+                                   ell, Ar, pmap_ext, mods, logN, tq, 1);
+                else
+                    launch_clocked(inst_name<AT, 1>("k_modup_fp"), Bq, k_modup_fp<AT, 1>, gq, dim3(NT), st, ext0, coef, W,
+                                   ell, Ar, pmap_ext, mods, logN, tq, 1);
+            }
+            const int tk = conv_chunk(logN, Kt, nd * members);
+            launch_clocked(inst_name<AT>("k_modup_convert"), Bk, k_modup_convert<AT>,
+                           pt_grid(logN, (Kt + tk - 1) / tk, nd * members), dim3(NT), st, ext0, coef, W, ell, Ar,
+                           pmap_ext, mods, logN, tk, ell);
         });
     };
     if (full > 0) {
