@@ -337,15 +337,15 @@ def test_counter_tables_are_refused_for_another_library(tmp_path, monkeypatch):
 
 def test_committed_tables_cover_the_profiled_kernels():
     """Every kernel of the closing profile's sort-only trace that takes >= 1% of the
-    sort (profiles/r5_final3/region_kernel_stats.csv) has a row in the committed
+    sort (profiles/r6_final/region_kernel_stats.csv) has a row in the committed
     instruction-mix table (profiles/valu_mix.json, the roofline's VALU pricing) and
     in the SQ counter table, so the bench line's valu_frac / limiter are defined for
-    the kernels that matter -- the round's new kernels (k_leaf_sums_fold,
-    k_tensor_lin, k_modup_fold) included."""
+    the kernels that matter -- the newer kernels (k_leaf_sums_fold, k_tensor_lin,
+    k_modup_fold, round 6's k_moddown_rescale_fp) included."""
     import csv
     import re
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    stats = os.path.join(repo, 'profiles', 'r5_final3', 'region_kernel_stats.csv')
+    stats = os.path.join(repo, 'profiles', 'r6_final', 'region_kernel_stats.csv')
     if not os.path.exists(stats):
         pytest.skip('no closing profile committed')
     rows = list(csv.DictReader(open(stats)))
@@ -363,3 +363,4 @@ def test_committed_tables_cover_the_profiled_kernels():
     assert not missing, missing
     assert any(k.startswith('k_leaf_sums_fold<') for k in mix)
     assert any(k.startswith('k_tensor_lin<') for k in mix)
+    assert any(k.startswith('k_moddown_rescale_fp<') for k in mix) and any(k.startswith('k_moddown_rescale_fp<') for k in sq)
