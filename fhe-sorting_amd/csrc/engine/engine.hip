@@ -340,7 +340,24 @@ struct Engine::Impl {
             const char *e = std::getenv("FHE_KS_FUSE");
             return e ? std::atoi(e) : 1;
         }();
-        return on && members >= 4 && (P.logN == 16 || P.logN == 17);
+        // FHE_KS_FUSE_MIN (A/B): the fewest members a fused launch takes (default 4)
+        static const int min_members = [] {
+            const char *e = std::getenv("FHE_KS_FUSE_MIN");
+            return e ? std::max(1, std::atoi(e)) : 4;
+        }();
+        return on && members >= min_members && (P.logN == 16 || P.logN == 17);
+    }
+    // FHE_KS_FUSE_INT (A/B, default 1; round 6, verdict r5 item 2): the integer-class
+    // targets (q_0, the special primes) through the fused kernel too -- ModUp then
+    // runs no row pass at all and ks_inner none: sort 516.5 / 517.3 -> 509.9 / 510.6 ms
+    // (profiles/r6_ab/ks_fuse_int_ab.jsonl); round 5 had measured the fused integer
+    // launch per target against the FP one, not against the row pass + ks_inner it replaces
+    static bool ks_fuse_int() {
+        static const bool on = [] {
+            const char *e = std::getenv("FHE_KS_FUSE_INT");
+            return e ? std::atoi(e) != 0 : true;
+        }();
+        return on;
     }
     // cols_only: the forward NTT's column pass alone (the row pass runs fused
     // with the key switch, mul_tail)
@@ -364,6 +381,7 @@ struct Engine::Impl {
             // inner product, mul_tail)
             const int cnt = (int)LT.modup_map_cnt[ell];
             dev::ntt_forward_mapped_cols(e, cnt, members, es, modup_smap + mo, modup_pmap + mo, T, st);
+            if (!ks_fuse_int())
             for (auto &r : dev::ntt_class_runs(modup_pmap + mo, cnt, false, T))
                 dev::ntt_forward_mapped_rows(e, r.second, members, es, modup_smap + mo + r.first,
                                              modup_pmap + mo + r.first, T, st);
@@ -462,8 +480,9 @@ struct Engine::Impl {
             // FP targets: row pass + inner product fused; integer targets (q_0 and
             // the special primes): their row pass ran in modup, ks_inner here
             dev::ntt_row_ks(acc, e, d2, static_cast<u64 *>(ks->relin->p), (int)ell, P.K, (int)P.nall(), P.alpha, digits,
-                            ext(ell), members, str, fold, T, st, /*fp_only*/ true);
-            const auto runs = dev::ntt_class_runs(ext(ell), (int)W, false, T);
+                            ext(ell), members, str, fold, T, st, /*fp_only*/ !ks_fuse_int());
+            const auto runs = ks_fuse_int() ? std::vector<std::pair<int, int>>{}
+                                            : dev::ntt_class_runs(ext(ell), (int)W, false, T);
             for (size_t r = 0; r < runs.size(); r += 2) {
                 dev::KsStrides s2 = str;
                 s2.zs0 = runs[r].first;
