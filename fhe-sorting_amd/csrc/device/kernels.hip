@@ -730,8 +730,12 @@ struct FpTargets {
     const double *tq[4];  // {cst, q, 1 / q, flag}
     u64 *o[4];            // the block's first output coefficient of each target
 };
-template <int S, int MID, int NTG>
-__device__ __forceinline__ void fp_targets(const double2 (*ys)[NT], int lane, const FpTargets &F) {
+// (YS: double2, or int2 -- the sources' (yh, yl) as int32 in half the LDS, converted
+// on the read, FHE_MDFP_I32)
+__device__ __forceinline__ double2 fp_src(const double2 &v) { return v; }
+__device__ __forceinline__ double2 fp_src(const int2 &v) { return make_double2((double)v.x, (double)v.y); }
+template <int S, int MID, int NTG, typename YS>
+__device__ __forceinline__ void fp_targets(const YS (*ys)[NT], int lane, const FpTargets &F) {
     constexpr int G = NT / 64;
     double H[NTG][G], L[NTG][G], q[NTG], qi[NTG];
 #pragma unroll
@@ -753,7 +757,7 @@ __device__ __forceinline__ void fp_targets(const double2 (*ys)[NT], int lane, co
             for (int e = 0; e < 4; ++e) c[t][e] = F.c[t][4 * s + e];
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const double2 y = ys[s][64 * g + lane];
+            const double2 y = fp_src(ys[s][64 * g + lane]);
 #pragma unroll
             for (int t = 0; t < NTG; ++t) {
                 H[t][g] = __builtin_fma(y.x, c[t][0], H[t][g]);
@@ -1128,7 +1132,7 @@ __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u6
             const FpTargets F{{fc + (size_t)t0 * A.qstride * 4, fc + (size_t)t1 * A.qstride * 4},
                               {fq + (size_t)t0 * 4, fq + (size_t)t1 * 4},
                               {eo + (size_t)t0 * n, eo + (size_t)t1 * n}};
-            fp_targets<AT, MID, 2>(ys, lane, F);
+            fp_targets<AT, MID, 2, double2>(ys, lane, F);
             continue;
         }
         for (int u = 0; u <= (hasb ? 1 : 0); ++u) {
@@ -1138,7 +1142,7 @@ __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u6
             } else {
                 const FpTargets F{{fc + (size_t)t * A.qstride * 4, nullptr}, {fq + (size_t)t * 4, nullptr},
                                   {eo + (size_t)t * n, nullptr}};
-                fp_targets<AT, MID, 1>(ys, lane, F);
+                fp_targets<AT, MID, 1, double2>(ys, lane, F);
             }
         }
     }
@@ -1781,13 +1785,14 @@ __device__ __forceinline__ void md_sources(const u64 *src, size_t k, size_t n, i
     yl[KT] = (double)(int)(pv - ph * ((int64_t)1 << 30));
 }
 // Block: 256 coefficients.  Phase 1: thread x computes coefficient x's sources
-// (md_sources, once per coefficient) into LDS ([2 (K+1)][256] doubles).  Phase 2:
+// (md_sources, once per coefficient) into LDS ([K+1][256] (yh, yl) pairs: int32 by
+// default, I32 = 0 doubles; |yh|, |yl| <= 2^30, exact either way).  Phase 2:
 // wave w takes the targets i0 + w, i0 + w + 4, ...; a target's constants are
 // scalar-loaded once per wave and serve its 256 coefficients (4 per lane, read
 // back from LDS with conflict-free ds_read_b64), so the scalar traffic per FMA is
 // a quarter of a thread-per-coefficient loop's and the table never has to stay in
 // the scalar cache.  grid: x = n / 256, y = target chunks of tch, z = segment.
-template <int KT, int MID, int TPI>
+template <int KT, int MID, int TPI, int I32>
 __global__ __launch_bounds__(NT) void k_moddown_rescale_fp(u64 *__restrict__ corr, const u64 *__restrict__ acc, int ell, int nq,
                                                            size_t seg_acc, size_t seg_corr, const u64 *phinv,
                                                            const u64 *phinv_s, const u64 *phat, const u64 *pinv,
@@ -1795,7 +1800,8 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_fp(u64 *__restrict__ cor
                                                            const u64 *ninv, const u64 *ninv_s, const Mod *mods,
                                                            const double *__restrict__ fpc, const double *__restrict__ fpq,
                                                            int logN, int tch) {
-    __shared__ double2 ys[KT + 1][NT];
+    using YS = std::conditional_t<I32 != 0, int2, double2>;
+    __shared__ YS ys[KT + 1][NT];
     const size_t n = (size_t)1 << logN;
     // (readfirstlane: the compiler then knows the wave index, so each target's
     // constants go through scalar loads)
@@ -1809,7 +1815,12 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_fp(u64 *__restrict__ cor
         md_sources<KT>(src, k0 + tid, n, nq, last, phinv, phinv_s, phat, pinv, pinv_s, pmod, pinvd, ninv, ninv_s, mods,
                        yh, yl);
 #pragma unroll
-        for (int s = 0; s <= KT; ++s) ys[s][tid] = make_double2(yh[s], yl[s]);
+        for (int s = 0; s <= KT; ++s) {
+            if constexpr (I32)
+                ys[s][tid] = make_int2((int)yh[s], (int)yl[s]);
+            else
+                ys[s][tid] = make_double2(yh[s], yl[s]);
+        }
     }
     __syncthreads();
     // an integer target (host flag: q_i >= 2^41): the 128-bit sums over y rebuilt from (yh, yl)
@@ -1818,7 +1829,7 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_fp(u64 *__restrict__ cor
 #pragma unroll 1
         for (int g = 0; g < NT / 64; ++g) {
             const int x = 64 * g + lane;
-            const double2 yp = ys[KT][x];
+            const double2 yp = fp_src(ys[KT][x]);
             const int64_t pv = (int64_t)yp.x * ((int64_t)1 << 30) + (int64_t)yp.y;
             const u64 lv = pv < 0 ? mi.q - (u64)(-pv) : (u64)pv;  // |pv| < 2^41 <= q_i
             Acc4 a4;
@@ -1826,7 +1837,7 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_fp(u64 *__restrict__ cor
             mac4(a4, split30(lv), split30(pmod[i]));
 #pragma unroll
             for (int kk = 0; kk < KT; ++kk) {
-                const double2 y = ys[kk][x];
+                const double2 y = fp_src(ys[kk][x]);
                 const u64 yv = ((u64)((int)y.x + (1 << 29)) << 30) + (u64)((int)y.y + (1 << 29));
                 mac4(a4, split30(yv), split30(phat[(size_t)i * KT + kk]));
                 spill4<KT + 1>(r, a4, kk + 1);
@@ -1852,7 +1863,7 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_fp(u64 *__restrict__ cor
         if (cnt == TPI && !anyint) {
             FpTargets F{};
             for (int u = 0; u < TPI; ++u) fpt(ia + u, u, F);
-            fp_targets<KT + 1, MID, TPI>(ys, lane, F);
+            fp_targets<KT + 1, MID, TPI, YS>(ys, lane, F);
             continue;
         }
         for (int i = ia; i < ia + cnt;) {
@@ -1863,12 +1874,12 @@ __global__ __launch_bounds__(NT) void k_moddown_rescale_fp(u64 *__restrict__ cor
                 FpTargets F{};
                 fpt(i, 0, F);
                 fpt(i + 1, 1, F);
-                fp_targets<KT + 1, MID, 2>(ys, lane, F);
+                fp_targets<KT + 1, MID, 2, YS>(ys, lane, F);
                 i += 2;
             } else {
                 FpTargets F{};
                 fpt(i, 0, F);
-                fp_targets<KT + 1, MID, 1>(ys, lane, F);
+                fp_targets<KT + 1, MID, 1, YS>(ys, lane, F);
                 ++i;
             }
         }
@@ -2687,6 +2698,17 @@ int moddown_fold_enabled() {
 // FHE_MODDOWN_FP (A/B): 0 = the 128-bit kernel only, N >= 1 = the fp64 kernel for
 // conversions of at least N targets (default 16: below that the per-coefficient
 // part and the integer target q_0 outweigh the cheaper sums, profiles/r6_e)
+// FHE_MDFP_I32 (default 1; 0: A/B): the fp64 ModDown kernel's sources as int32
+// (yh, yl) pairs in LDS -- half the LDS of double pairs, 56 / 83 VGPRs and 7 / 4
+// waves per SIMD at K = 10 / 16 against 91 / 136 and 3 / 2 (MEHP24 -3.2%,
+// profiles/r6_ab/mdfp_i32_ab.jsonl)
+int mdfp_i32() {
+    static const int v = [] {
+        const char *e = std::getenv("FHE_MDFP_I32");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
 // FHE_CONV_TPI (A/B, 2 or 4): targets per work item of the fp64 ModDown kernel
 int conv_tpi() {
     static const int v = [] {
@@ -2747,9 +2769,14 @@ void moddown_rescale_convert(u64 *corr, const u64 *acc, int ell, int K, int nq, 
             const dim3 g((unsigned)(n / NT), (unsigned)((ell - 1 + tch - 1) / tch), (unsigned)segs);
             auto go = [&](auto mid, auto tpi) {
                 constexpr int MI = decltype(mid)::value, TP = decltype(tpi)::value;
-                launch_clocked(inst_name<KT, MI, TP>("k_moddown_rescale_fp"), B, k_moddown_rescale_fp<KT, MI, TP>, g,
-                               dim3(NT), st, corr, acc, ell, nq, seg_acc, seg_corr, phinv, phinv_s, phat, pinv, pinv_s,
-                               pmod, pinvd, ninv, ninv_s, mods, fpc, fpq, logN, tch);
+                if (mdfp_i32())
+                    launch_clocked(inst_name<KT, MI, TP, 1>("k_moddown_rescale_fp"), B, k_moddown_rescale_fp<KT, MI, TP, 1>, g,
+                                   dim3(NT), st, corr, acc, ell, nq, seg_acc, seg_corr, phinv, phinv_s, phat, pinv, pinv_s,
+                                   pmod, pinvd, ninv, ninv_s, mods, fpc, fpq, logN, tch);
+                else
+                    launch_clocked(inst_name<KT, MI, TP, 0>("k_moddown_rescale_fp"), B, k_moddown_rescale_fp<KT, MI, TP, 0>, g,
+                                   dim3(NT), st, corr, acc, ell, nq, seg_acc, seg_corr, phinv, phinv_s, phat, pinv, pinv_s,
+                                   pmod, pinvd, ninv, ninv_s, mods, fpc, fpq, logN, tch);
             };
             using I0 = std::integral_constant<int, 0>;
             using I1 = std::integral_constant<int, 1>;
