@@ -1079,7 +1079,7 @@ template <int AT, int MID>
 // (tbeg = ell) beside it
 __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u64 *__restrict__ coef, int W, int ell, ModUpArgs A,
                                                  const int *pmap_ext, const Mod *mods, int logN, int tch, int qonly) {
-    __shared__ double2 ys[AT][NT];
+    __shared__ int2 ys[AT][NT];  // (yh, yl) as int32 (|yh|, |yl| <= 2^29)
     const size_t n = (size_t)1 << logN;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const size_t k0 = (size_t)blockIdx.x * NT;  // (n is a multiple of NT)
@@ -1094,8 +1094,7 @@ __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u6
         const u64 qs = mods[src].q;
         const int oh = qs >= FOLD_FP_QMAX ? (1 << 29) : 0;
         const u64 yv = mul_shoup(coef[(size_t)src * n + k0 + tid], A.qhinv[j][i], A.qhinv_s[j][i], qs);
-        ys[i][tid] = make_double2((double)((int)(uint32_t)(yv >> 30) - oh),
-                                  (double)((int)((uint32_t)yv & (uint32_t)MASK30) - (1 << 29)));
+        ys[i][tid] = make_int2((int)(uint32_t)(yv >> 30) - oh, (int)((uint32_t)yv & (uint32_t)MASK30) - (1 << 29));
     }
     __syncthreads();
     const u64 *qh = A.qhat[j];
@@ -1112,8 +1111,8 @@ __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u6
 #pragma unroll
             for (int i = 0; i < AT; ++i) {
                 const int oh = mods[min(lo + i, ell - 1)].q >= FOLD_FP_QMAX ? (1 << 29) : 0;
-                const double2 y = ys[i][x];
-                const u64 yv = ((u64)((int)y.x + oh) << 30) + (u64)((int)y.y + (1 << 29));
+                const int2 y = ys[i][x];
+                const u64 yv = ((u64)(y.x + oh) << 30) + (u64)(y.y + (1 << 29));
                 mac4(acc, split30(yv), split30(qh[(size_t)t * A.qstride + i]));
                 spill4<AT>(r, acc, i);
             }
@@ -1132,7 +1131,7 @@ __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u6
             const FpTargets F{{fc + (size_t)t0 * A.qstride * 4, fc + (size_t)t1 * A.qstride * 4},
                               {fq + (size_t)t0 * 4, fq + (size_t)t1 * 4},
                               {eo + (size_t)t0 * n, eo + (size_t)t1 * n}};
-            fp_targets<AT, MID, 2, double2>(ys, lane, F);
+            fp_targets<AT, MID, 2, int2>(ys, lane, F);
             continue;
         }
         for (int u = 0; u <= (hasb ? 1 : 0); ++u) {
@@ -1142,7 +1141,7 @@ __global__ __launch_bounds__(NT) void k_modup_fp(u64 *__restrict__ ext, const u6
             } else {
                 const FpTargets F{{fc + (size_t)t * A.qstride * 4, nullptr}, {fq + (size_t)t * 4, nullptr},
                                   {eo + (size_t)t * n, nullptr}};
-                fp_targets<AT, MID, 1, double2>(ys, lane, F);
+                fp_targets<AT, MID, 1, int2>(ys, lane, F);
             }
         }
     }
@@ -2695,9 +2694,6 @@ int moddown_fold_enabled() {
     }();
     return v;
 }
-// FHE_MODDOWN_FP (A/B): 0 = the 128-bit kernel only, N >= 1 = the fp64 kernel for
-// conversions of at least N targets (default 16: below that the per-coefficient
-// part and the integer target q_0 outweigh the cheaper sums, profiles/r6_e)
 // FHE_MDFP_I32 (default 1; 0: A/B): the fp64 ModDown kernel's sources as int32
 // (yh, yl) pairs in LDS -- half the LDS of double pairs, 56 / 83 VGPRs and 7 / 4
 // waves per SIMD at K = 10 / 16 against 91 / 136 and 3 / 2 (MEHP24 -3.2%,
@@ -2717,10 +2713,14 @@ int conv_tpi() {
     }();
     return v;
 }
+// FHE_MODDOWN_FP (A/B): 0 = the 128-bit kernel only, N >= 1 = the fp64 kernel for
+// conversions of at least N targets (default 1, every conversion whose bounds
+// hold: with the int32 sources the fp64 kernel wins at every size down to 6
+// targets, profiles/r6_ab/mdfp_min_ab.jsonl; with double sources it lost below 16)
 int moddown_fp_min_targets() {
     static const int v = [] {
         const char *e = std::getenv("FHE_MODDOWN_FP");
-        return e ? std::atoi(e) : 16;
+        return e ? std::atoi(e) : 1;
     }();
     return v;
 }
