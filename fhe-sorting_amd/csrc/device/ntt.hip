@@ -119,6 +119,10 @@ __device__ __forceinline__ int lds_at(int tr, int idx) {
 #ifndef FHE_NTT_FP_EPI_PRE
 #define FHE_NTT_FP_EPI_PRE 1
 #endif
+// the same for the HMult-tail / key-switch-finish rows alone (A/B: -DFHE_NTT_FP_EPI_PRE_MT=n)
+#ifndef FHE_NTT_FP_EPI_PRE_MT
+#define FHE_NTT_FP_EPI_PRE_MT FHE_NTT_FP_EPI_PRE
+#endif
 typedef const __attribute__((address_space(4))) u64 const_u64_t;
 __device__ __forceinline__ ulonglong2 scalar_tw(const ulonglong2 *p, size_t i) {
     const const_u64_t *q = (const const_u64_t *)p + 2 * i;
@@ -681,9 +685,10 @@ __device__ __forceinline__ void ntt_fwd_body(u64 *data, size_t seg, const int *p
     // instead of stalling the store loop (the tile's LDS bounds occupancy, the
     // extra VGPRs do not)
     // (FP rows: FHE_NTT_FP_EPI_PRE=0 loads them in the store loop instead -- A/B)
+    constexpr bool EPI_PRE = MODE == NTT_RESCALE ? FHE_NTT_FP_EPI_PRE : FHE_NTT_FP_EPI_PRE_MT;
     constexpr bool EPI_X = !COLS && (MODE == NTT_RESCALE || MODE == NTT_MULTAIL || MODE == NTT_KSFINISH) &&
-                           (!FP || FHE_NTT_FP_EPI_PRE);
-    constexpr bool EPI_D = !COLS && (MODE == NTT_MULTAIL || MODE == NTT_KSFINISH) && (!FP || FHE_NTT_FP_EPI_PRE);
+                           (!FP || EPI_PRE);
+    constexpr bool EPI_D = !COLS && (MODE == NTT_MULTAIL || MODE == NTT_KSFINISH) && (!FP || EPI_PRE);
     // key-switch finish: only c0 segments (even z) take the added polynomial
     const bool has_d = MODE == NTT_KSFINISH ? (F.d != nullptr && !(zseg & 1)) : true;
     const size_t d_base = MODE == NTT_KSFINISH ? (size_t)(zseg >> 1) * F.seg_d : (size_t)zseg * F.seg_d;
