@@ -562,6 +562,7 @@ struct LeafArgs {
     const int64_t *K;       // device [G][m]
     const uint8_t *sh;      // device [G][m]
     int m, G, accumulate;
+    int six;  // k_leaf_sums_fold: the FP primes' six-digit rows (FHE_LEAF_SIX)
 };
 #ifndef FHE_LF_NC  // 16-coefficient column tiles per wave sharing one set of windows (A/B: -DFHE_LF_NC=4)
 #define FHE_LF_NC 2
@@ -684,6 +685,14 @@ __global__ __launch_bounds__(LF_NT) __attribute__((amdgpu_waves_per_eu(FHE_LF_WP
 // Byte 0..6 of y are read as signed (u - 128), so out = V + 128 sum_{i, a<7} d.
 // Same residues as k_leaf_sums_mfma (exact integer sums, canonical results).
 constexpr int LFF_NT = 512, LFF_NC = 4;
+// FHE_LEAF_SIX (A/B, default 1): the FP-class primes' six-digit row layout below
+inline bool leaf_six_enabled_host() {
+    static const bool v = [] {
+        const char *e = std::getenv("FHE_LEAF_SIX");
+        return !e || std::atoi(e) != 0;
+    }();
+    return v;
+}
 typedef int v8i __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ u64 fold_rows2(const v4i &r0, const v4i &r1, const Mod &m, u64 w1s, u64 a) {
     const int32_t p0 = r0[0] + (r0[1] << 8), q0 = r0[2] + (r0[3] << 8);
@@ -796,9 +805,16 @@ __global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) 
     const Mod md = mods[l];
     const int tid = threadIdx.x;
     const int ngr = (A.G + 3) >> 2;
+    // a prime below 2^41 (FP class; uniform: one prime per block) has d < 2^41, so
+    // its balanced digits 6 and 7 are zero: with NG >= 2 a pair of groups then takes
+    // three row blocks instead of four -- each group's digits 0-3, and one block of
+    // both groups' digits 4-5 (row 4 ta + 2 g + b - 4) -- a quarter fewer MFMAs
+    const bool fpq = md.q < FOLD_FP_QMAX;
+    const bool six = NG >= 2 && KS <= 7 && fpq && A.six;  // (KS = 8: the third accumulator spills)
+    const int ngt = six ? (ngr + 1) & ~1 : ngr;  // table groups (whole pairs)
     {
         u64 *const img = reinterpret_cast<u64 *>(afr);
-        for (int p = tid; p < 4 * ngr * 8 * KS; p += LFF_NT) {
+        for (int p = tid; p < 4 * ngt * 8 * KS; p += LFF_NT) {
             const int t = p / (8 * KS), i = p % (8 * KS);
             u64 d = (t < A.G && i < A.m) ? smod(A.K[t * A.m + i], A.sh[t * A.m + i], md) : 0;
             u64 dig[8], s7 = 0;
@@ -810,6 +826,19 @@ __global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) 
             }
             psum[t][i] = s7;
             const int grp = t >> 2, ta = t & 3, ks = i >> 3, lgi = (i & 7) >> 1, half = i & 1;
+            if (six) {
+                const int pr = grp >> 1, g = grp & 1;
+#pragma unroll
+                for (int b = 0; b < 6; ++b) {
+                    u64 e = 0;
+#pragma unroll
+                    for (int a = 0; a < 8; ++a) e |= ((dig[a] >> (8 * b)) & 255) << (8 * a);
+                    const int blk = b < 4 ? 3 * pr + g : 3 * pr + 2;
+                    const int row = b < 4 ? 4 * ta + b : 4 * ta + 2 * g + (b - 4);
+                    img[2 * ((blk * KS + ks) * 64 + 16 * lgi + row) + half] = e;
+                }
+                continue;
+            }
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
                 u64 e = 0;
@@ -838,7 +867,6 @@ __global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) 
     __syncthreads();
     const int lane = tid & 63, wave = tid >> 6, col = lane & 15, lg = lane >> 4;
     const u64 w1s = shoup_one(md);
-    const bool fpq = md.q < FOLD_FP_QMAX;  // (uniform: one prime per block)
     const double qd = (double)md.q, qid = 1.0 / qd;
     const size_t oo_l = (size_t)blockIdx.z * seg + (size_t)l * n;
     for (size_t nb = (size_t)blockIdx.x * chunk + wave * 16 * LFF_NC; nb < (size_t)(blockIdx.x + 1) * chunk && nb < n;
@@ -851,6 +879,37 @@ __global__ __launch_bounds__(LFF_NT) __attribute__((amdgpu_waves_per_eu(2, 8))) 
             const gu64 *p1 = to_global(xptr[i0 + 1]) + xoff[i0 + 1] + nb + col;
 #pragma unroll
             for (int c = 0; c < LFF_NC; ++c) bf[c][ks] = bytes_of(p0[16 * c] ^ XMASK, p1[16 * c] ^ XMASK);
+        }
+        if constexpr (NG >= 2 && KS <= 7) {
+            if (six) {
+#pragma unroll 1
+                for (int pr = 0; pr < ngt >> 1; ++pr) {
+                    v4i acc[LFF_NC][3];
+                    const v4i *ag = afr + (size_t)pr * 3 * KS * 64 + lane;
+#pragma unroll
+                    for (int ks = 0; ks < KS; ++ks) {
+                        const v4i a0 = ag[ks * 64], a1 = ag[(KS + ks) * 64], a2 = ag[(2 * KS + ks) * 64];
+#pragma unroll
+                        for (int c = 0; c < LFF_NC; ++c) {
+                            acc[c][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[c][ks], ks ? acc[c][0] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                            acc[c][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[c][ks], ks ? acc[c][1] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                            acc[c][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, bf[c][ks], ks ? acc[c][2] : v4i{0, 0, 0, 0}, 0, 0, 0);
+                        }
+                    }
+#pragma unroll
+                    for (int g = 0; g < 2; ++g) {
+                        const int t = 8 * pr + 4 * g + lg;
+                        if (t < A.G) {
+                            u64 *o = optr[t] + oo_l + nb + col;
+                            const u64 cr = cfp[t];
+#pragma unroll
+                            for (int c = 0; c < LFF_NC; ++c)
+                                o[16 * c] = fold_rows2_fp(acc[c][g], v4i{acc[c][2][2 * g], acc[c][2][2 * g + 1], 0, 0}, qd, qid, cr);
+                        }
+                    }
+                }
+                continue;
+            }
         }
 #pragma unroll 1
         for (int grp = 0; grp < ngr; ++grp) {
@@ -2305,6 +2364,7 @@ void ew_linear_sum_multi(u64 *const *outs, int G, const u64 *const *xs, const si
             A.G = G;
             A.accumulate = 0;
             for (int g = 0; g < G; ++g) A.out[g] = outs[g];
+            A.six = leaf_six_enabled_host();
             for (int i = 0; i < A.m; ++i) {
                 A.x[i] = xs[i];
                 A.xseg[i] = (uint32_t)xseg[i];
